@@ -1,0 +1,231 @@
+"""CPU restatement (plain torch fp32) of the reference hot path. TEST INFRASTRUCTURE ONLY — see oracle/__init__.py.
+
+Parity status: PINNED. tests/test_oracle_golden.py checks every function below against the golden vectors that
+tests/golden/gen_golden.py produced by importing /root/reference in the build container.
+
+Parameters are passed as a dict keyed exactly like the reference state_dict (e.g. ``layer1.0.conv1.weight``).
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+# --------------------------------------------------------------------------------------------------- A1
+def ws_weight(w: torch.Tensor) -> torch.Tensor:
+    """Weight standardisation, unet3D.py:21-26: per output channel mean over (Cin,k,k,k), unbiased variance
+    of the centred weight, ``+1e-12`` inside the sqrt."""
+    mean = w.mean(dim=1, keepdim=True).mean(dim=2, keepdim=True).mean(dim=3, keepdim=True).mean(dim=4, keepdim=True)
+    wc = w - mean
+    std = torch.sqrt(torch.var(wc.reshape(w.shape[0], -1), dim=1) + 1e-12).reshape(-1, 1, 1, 1, 1)
+    return wc / std
+
+
+def conv(x, w, stride=1, bias=None, ws=True):
+    """unet3D.py:27 / conv3x3x3 :30-35 — pad = k//2 (1 for 3^3, 0 for 1^3)."""
+    k = w.shape[2]
+    return F.conv3d(x, ws_weight(w) if ws else w, bias, stride, k // 2)
+
+
+# --------------------------------------------------------------------------------------------- A4 / A5
+def gn_relu(x, groups, gamma, beta):
+    """nn.GroupNorm(G, C) (eps 1e-5, biased variance) then ReLU — unet3D.py:44-47."""
+    return F.relu(F.group_norm(x, groups, gamma, beta, 1e-5))
+
+
+# ------------------------------------------------------------------------------------------------- A3
+def block(P, pre, x, stride, groups, ws=True):
+    """NoBottleneck.forward, unet3D.py:56-73; downsample = GN -> ReLU -> 1^3 conv stride s (_make_layer :1666-1686)."""
+    out = conv(gn_relu(x, groups, P[pre + "gn1.weight"], P[pre + "gn1.bias"]), P[pre + "conv1.weight"], stride, ws=ws)
+    out = conv(gn_relu(out, groups, P[pre + "gn2.weight"], P[pre + "gn2.bias"]), P[pre + "conv2.weight"], 1, ws=ws)
+    if pre + "downsample.0.weight" in P:
+        res = conv(gn_relu(x, groups, P[pre + "downsample.0.weight"], P[pre + "downsample.0.bias"]),
+                   P[pre + "downsample.2.weight"], stride, ws=ws)
+    else:
+        res = x
+    return out + res
+
+
+def layer(P, name, x, nblocks, stride, groups, ws=True):
+    for b in range(nblocks):
+        x = block(P, f"{name}.{b}.", x, stride if b == 0 else 1, groups, ws)
+    return x
+
+
+def upsample2x(x):
+    """nn.Upsample(scale_factor=2, mode='trilinear') (align_corners=False), unet3D.py:1646."""
+    return F.interpolate(x, scale_factor=2, mode="trilinear")
+
+
+# ------------------------------------------------------------------------------------------------- A7
+def trunk(P, x, layers=(1, 2, 2, 2, 2), groups=16, fusion_groups=16, ws=True, conv0=False):
+    """Encoder/decoder trunk shared by unet3D_baseline.forward :663-711, unet3D.forward :1734-1784 and
+    unet3D_g.forward :1568-1615. Returns (decoder output x1, bottleneck after fusionConv)."""
+    if conv0:
+        x = conv(x, P["conv0.weight"], 2, ws=ws)
+    x = conv(x, P["conv1.weight"], 1, ws=ws)
+    skips = []
+    for i, name in enumerate(["layer0", "layer1", "layer2", "layer3", "layer4"]):
+        x = layer(P, name, x, layers[i], 1 if i == 0 else 2, groups, ws)
+        skips.append(x)
+    x = conv(gn_relu(x, fusion_groups, P["fusionConv.0.weight"], P["fusionConv.0.bias"]), P["fusionConv.2.weight"], 1,
+             ws=ws)
+    bott = x
+    for name, skip in zip(["x8_resb", "x4_resb", "x2_resb", "x1_resb"], [skips[3], skips[2], skips[1], skips[0]]):
+        x = upsample2x(x) + skip
+        x = layer(P, name, x, 1, 1, groups, ws)
+    return x, bott
+
+
+def precls(P, x, groups):
+    """precls_conv = GN -> ReLU -> Conv3d 1^3 with bias, unet3D.py:629-633 / :1653-1657."""
+    return F.conv3d(gn_relu(x, groups, P["precls_conv.0.weight"], P["precls_conv.0.bias"]),
+                    P["precls_conv.2.weight"], P["precls_conv.2.bias"])
+
+
+def baseline_forward(P, x, ws=True):
+    """unet3D_baseline(layers=[1,2,2,2,2], num_classes, weight_std).forward, unet3D.py:663-718."""
+    y, _ = trunk(P, x, ws=ws)
+    return precls(P, y, 16)
+
+
+def unet3d_g_forward(P, x, init_filter=8, layers=(1, 1, 1, 1, 1), ws=True):
+    """unet3D_g.forward, unet3D.py:1568-1623: stride-2 conv0, GN(4) blocks, GN(init/2) fusion, GN(init/4) precls,
+    final x2 trilinear upsample of the logits."""
+    y, _ = trunk(P, x, layers=layers, groups=4, fusion_groups=init_filter // 2, ws=ws, conv0=True)
+    return upsample2x(precls(P, y, init_filter // 4))
+
+
+def unet3d_dyn_forward(P, x, task_id, ws=True):
+    """UNet3D(num_classes, weight_std) = unet3D([1,2,2,2,2]) with the DynConv 8,8,2 head, unet3D.py:1734-1811."""
+    y, bott = trunk(P, x, ws=ws)
+    N = x.shape[0]
+    onehot = F.one_hot(task_id.long(), 7).float().reshape(N, 7, 1, 1, 1)          # encoding_task :1688-1693
+    feat = gn_relu(bott, 16, P["GAP.0.weight"], P["GAP.0.bias"]).mean(dim=(2, 3, 4), keepdim=True)  # GAP :1659-1663
+    params = F.conv3d(torch.cat([feat, onehot], 1), P["controller.weight"], P["controller.bias"]).reshape(N, -1)
+    head = precls(P, y, 16)                                                           # N x 8 x D x H x W
+    D, H, W = head.shape[2:]
+    h = head.reshape(1, -1, D, H, W)
+    wn, bn = [64, 64, 16], [8, 8, 2]                                                  # :1790-1798
+    splits = list(torch.split_with_sizes(params, wn + bn, dim=1))                    # parse_dynamic_params :1695-1718
+    ws_, bs_ = splits[:3], splits[3:]
+    for l in range(3):
+        co = 8 if l < 2 else 2
+        h = F.conv3d(h, ws_[l].reshape(N * co, -1, 1, 1, 1), bs_[l].reshape(N * co), groups=N)  # heads_forward :1720
+        if l < 2:
+            h = F.relu(h)
+    return h.reshape(-1, 2, D, H, W)
+
+
+# ------------------------------------------------------------------------------------------- A10 / A11
+def edice_partial(inputs, target, mask=None, soft_max=True, uce=True):
+    """EDiceLoss_partial.forward, loss_partial.py:71-99 with DiceLoss :10-57.
+
+    Quirks kept: only ``mask[0]`` weights the whole batch; dice summed over all samples+voxels per class;
+    loss divided by C (not sum of weights); BCE = torch BCELoss (mean over S*V, log clamped at -100)."""
+    C = inputs.shape[1]
+    p = torch.softmax(inputs, 1) if soft_max else torch.sigmoid(inputs)
+    if mask is None:
+        mask = [torch.ones(C) for _ in range(inputs.shape[0])]
+    w = mask[0]
+    loss = 0.0
+    for i in range(C):
+        t = (target == i).float()
+        s = p[:, i]
+        inter = torch.sum(s * t)
+        y_sum = torch.sum(t * t)
+        z_sum = torch.sum(s * s)
+        d = 1 - (2 * inter + 1e-5) / (z_sum + y_sum + 1e-5)
+        loss = loss + d * w[i]
+    loss = loss / C
+    if uce:
+        ce = 0.0
+        for l in range(C):
+            ce = ce + F.binary_cross_entropy(p[:, l].float(), (target == l).float()) * w[l]
+        loss = loss + ce
+    return loss
+
+
+# ------------------------------------------------------------------------------------------------- A14
+def get_dice(preds, labels, num_class=13):
+    """evaluate_amos.py:92-154 (atlas=None branch): argmax of softmax; per class l=1..num_class per-sample
+    dice 2*sum(P*T)/(sum P + sum T + 1), sensitivity sum(P*T)/(sum T + 1), precision sum(P*T)/(sum P + 1),
+    each averaged over samples. Returns three float64 numpy arrays."""
+    am = torch.argmax(torch.softmax(preds, 1), 1)
+    S = preds.shape[0]
+    dices, senc, spec = [], [], []
+    for l in range(1, num_class + 1):
+        P = (am == l).reshape(S, -1).double()
+        T = (labels == l).reshape(S, -1).double()
+        num = (P * T).sum(1)
+        dices.append((2 * num / (P.sum(1) + T.sum(1) + 1)).mean().item())
+        senc.append((num / (T.sum(1) + 1)).mean().item())
+        spec.append((num / (P.sum(1) + 1)).mean().item())
+    return np.array(dices), np.array(senc), np.array(spec)
+
+
+# ---------------------------------------------------------------------------------------------- next f1
+def gaussian_map(patch_size, sigma_scale=1.0 / 8):
+    """_get_gaussian, evaluate_amos.py:184-197: scipy gaussian_filter (truncate 4.0, mode constant) of a centred
+    delta = separable product of normalised 1-D kernels; scaled to max 1; zeros replaced by the min non-zero."""
+    axes = []
+    for n in patch_size:
+        sigma = n * sigma_scale
+        radius = int(4.0 * sigma + 0.5)
+        xs = np.arange(-radius, radius + 1, dtype=np.float64)
+        k = np.exp(-0.5 * (xs / sigma) ** 2)
+        k /= k.sum()
+        c = n // 2
+        prof = np.zeros(n)
+        for i in range(n):
+            d = i - c
+            if -radius <= d <= radius:
+                prof[i] = k[d + radius]
+        axes.append(prof)
+    g = axes[0][:, None, None] * axes[1][None, :, None] * axes[2][None, None, :]
+    g = g / g.max()
+    g = g.astype(np.float32)
+    g[g == 0] = g[g != 0].min()
+    return g
+
+
+def params_from_module_dict(sd):
+    return {k: v.detach().float().cpu() for k, v in sd.items()}
+
+
+def state_shapes_baseline(num_classes=16, in_channel=1, init_filter=32, layers=(1, 2, 2, 2, 2), groups_ds=True,
+                          conv0=False, dyn=False):
+    """Ordered (key, shape) list of the reference state_dict for unet3D_baseline / unet3D / unet3D_g."""
+    f = init_filter
+    out = []
+    if conv0:
+        out.append(("conv0.weight", (f, in_channel, 3, 3, 3)))
+        out.append(("conv1.weight", (f, f, 3, 3, 3)))
+    else:
+        out.append(("conv1.weight", (f, in_channel, 3, 3, 3)))
+
+    def blk(pre, cin, cout, ds):
+        o = [(pre + "gn1.weight", (cin,)), (pre + "gn1.bias", (cin,)), (pre + "conv1.weight", (cout, cin, 3, 3, 3)),
+             (pre + "gn2.weight", (cout,)), (pre + "gn2.bias", (cout,)), (pre + "conv2.weight", (cout, cout, 3, 3, 3))]
+        if ds:
+            o += [(pre + "downsample.0.weight", (cin,)), (pre + "downsample.0.bias", (cin,)),
+                  (pre + "downsample.2.weight", (cout, cin, 1, 1, 1))]
+        return o
+
+    chans = [(f, f), (f, 2 * f), (2 * f, 4 * f), (4 * f, 8 * f), (8 * f, 8 * f)]
+    for i, (ci, co) in enumerate(chans):
+        for b in range(layers[i]):
+            cin = ci if b == 0 else co
+            out += blk(f"layer{i}.{b}.", cin, co, b == 0 and (i > 0 or ci != co))
+    out += [("fusionConv.0.weight", (8 * f,)), ("fusionConv.0.bias", (8 * f,)),
+            ("fusionConv.2.weight", (8 * f, 8 * f, 1, 1, 1))]
+    for name, ci, co in [("x8_resb", 8 * f, 4 * f), ("x4_resb", 4 * f, 2 * f), ("x2_resb", 2 * f, f), ("x1_resb", f, f)]:
+        out += blk(f"{name}.0.", ci, co, ci != co)
+    ncls = 8 if dyn else num_classes
+    out += [("precls_conv.0.weight", (f,)), ("precls_conv.0.bias", (f,)),
+            ("precls_conv.2.weight", (ncls, f, 1, 1, 1)), ("precls_conv.2.bias", (ncls,))]
+    if dyn:
+        out += [("GAP.0.weight", (256,)), ("GAP.0.bias", (256,)), ("controller.weight", (162, 263, 1, 1, 1)),
+                ("controller.bias", (162,))]
+    return out

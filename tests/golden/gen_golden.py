@@ -1,0 +1,269 @@
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE in this container.
+
+TEST INFRASTRUCTURE. Run here only (the reference does not exist on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+
+Everything it writes is data (inputs + expected outputs) in small .npz files; weights are not stored,
+only the seed of oracle/weights_recipe.py. The reference is imported read-only from /root/reference with
+the shims SURVEY.md §8c lists (no source of it is copied anywhere):
+  * ``unet3D.unet3D.encoding_task``: the original moves the one-hot to ``.cuda()`` (unet3D.py:1688-1693);
+    the shim builds the identical one-hot on the CPU.
+  * ``loss_partial.autocast``: imported name is commented out (loss_partial.py:4, used :90); fp32 CPU
+    ``autocast(enabled=False)`` is a no-op, so a nullcontext is semantically identical.
+  * empty stub modules for ``cv2``, ``tensorboardX``, ``SimpleITK``, ``nibabel`` (not installed, unused by
+    the functions exercised).
+"""
+import contextlib
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+from weights_recipe import apply_recipe, input_volume, label_volume  # noqa: E402
+
+for name in ("cv2", "tensorboardX", "SimpleITK", "nibabel"):
+    m = types.ModuleType(name)
+    if name == "tensorboardX":
+        m.SummaryWriter = object
+    sys.modules.setdefault(name, m)
+sys.path.insert(0, REF)
+
+import unet3D as R  # noqa: E402
+from loss_functions import loss_partial as RLP  # noqa: E402
+import evaluate_amos as REV  # noqa: E402
+
+R.unet3D.encoding_task = lambda self, t: F.one_hot(t.long(), 7).float()
+RLP.autocast = lambda enabled=False: contextlib.nullcontext()
+
+torch.set_num_threads(8)
+torch.manual_seed(0)
+OUT = HERE
+SAMPLE_N = 4096
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print(f"wrote {name}: {os.path.getsize(path) / 1024:.1f} KiB")
+
+
+def grad_summary(model, n_sample=16):
+    """Per-parameter grad L2 norm + grads at recipe-seeded flat indices (key order = state_dict)."""
+    names, norms, idx_all, val_all = [], [], [], []
+    for i, (k, p) in enumerate(model.named_parameters()):
+        g = p.grad.detach().reshape(-1).double()
+        rng = np.random.default_rng([1234, i])
+        idx = rng.integers(0, g.numel(), size=n_sample)
+        names.append(k)
+        norms.append(g.norm().item())
+        idx_all.append(idx)
+        val_all.append(g[torch.from_numpy(idx)].numpy())
+    return np.array(names), np.array(norms), np.stack(idx_all), np.stack(val_all)
+
+
+def dice_arrays(preds, labels, num_class):
+    dices, senc, spec, am = REV.get_dice(preds, labels, 1, num_class=num_class)
+    return (np.array([float(d) for d in dices]), np.array([float(s) for s in senc]),
+            np.array([float(s) for s in spec]))
+
+
+def g1():
+    m = R.UNet3D(num_classes=2, weight_std=True)
+    apply_recipe(m, seed=0)
+    m.eval()
+    x = torch.from_numpy(input_volume((1, 1, 32, 32, 32), seed=1))
+    task = torch.tensor([0])
+    with torch.no_grad():
+        logits = m(x, task)
+    lab = torch.from_numpy(label_volume((1, 1, 32, 32, 32), 2, seed=2))
+    d, se, sp = dice_arrays(logits, lab, 1)
+    # backward through the dynamic head with a fixed upstream gradient
+    m.train()
+    x2 = torch.from_numpy(input_volume((2, 1, 32, 32, 32), seed=3))
+    task2 = torch.tensor([0, 5])
+    out = m(x2, task2)
+    up = torch.from_numpy(input_volume(tuple(out.shape), seed=4))
+    (out * up).sum().backward()
+    names, norms, gidx, gval = grad_summary(m)
+    save("g1_unet3d_dyn_32.npz", x=x.numpy(), task_id=task.numpy(), logits=logits.numpy(), labels=lab.numpy(),
+         dice=d, senc=se, spec=sp, x2=x2.numpy(), task_id2=task2.numpy(), logits2=out.detach().numpy(),
+         up2=up.numpy(), gnames=names, gnorm=norms, gidx=gidx, gval=gval)
+
+
+def g2():
+    m = R.unet3D_g([1, 1, 1, 1, 1], num_classes=2, weight_std=True, init_filter=8, in_channel=1)
+    apply_recipe(m, seed=0)
+    m.eval()
+    x = torch.from_numpy(input_volume((1, 1, 32, 32, 32), seed=5))
+    with torch.no_grad():
+        logits = m(x)
+    lab = torch.from_numpy(label_volume((1, 1, 32, 32, 32), 2, seed=6))
+    d, se, sp = dice_arrays(logits, lab, 1)
+    # the refiner configuration of train_amos_atlas_final.py:120 (init_filter 24, 2 input channels)
+    r = R.unet3D_g([1, 1, 1, 1, 1], num_classes=2, weight_std=True, init_filter=24, in_channel=2)
+    apply_recipe(r, seed=0)
+    r.train()
+    xr = torch.from_numpy(input_volume((1, 2, 32, 32, 32), seed=7))
+    outr = r(xr)
+    up = torch.from_numpy(input_volume(tuple(outr.shape), seed=8))
+    (outr * up).sum().backward()
+    names, norms, gidx, gval = grad_summary(r)
+    save("g2_unet3d_g_32.npz", x=x.numpy(), logits=logits.numpy(), labels=lab.numpy(), dice=d, senc=se, spec=sp,
+         xr=xr.numpy(), logits_r=outr.detach().numpy(), up_r=up.numpy(), gnames=names, gnorm=norms,
+         gidx=gidx, gval=gval)
+
+
+def loss_cases(C, S, spatial, seed):
+    rng = np.random.default_rng([seed, 99])
+    m_a = (rng.random(C) < 0.6).astype(np.int64)
+    m_a[1] = 1
+    m_b = np.zeros(C, dtype=np.int64)
+    m_c1 = (rng.random(C) < 0.5).astype(np.int64)
+    return {"a": [torch.from_numpy(m_a)], "zero": [torch.from_numpy(m_b)],
+            "persample": [torch.from_numpy(m_a), torch.from_numpy(m_c1)]}
+
+
+def g3():
+    C = 16
+    m = R.unet3D_baseline([1, 2, 2, 2, 2], num_classes=C, weight_std=True)
+    apply_recipe(m, seed=0)
+    m.train()
+    x = torch.from_numpy(input_volume((2, 1, 16, 16, 16), seed=9, kind="ct"))
+    lab = torch.from_numpy(label_volume((2, 1, 16, 16, 16), C, seed=10))
+    masks = loss_cases(C, 2, (16, 16, 16), seed=11)
+    logits, _, _ = m(x)
+    edice = RLP.EDiceLoss_partial(C)
+    losses = {}
+    for k, mk in masks.items():
+        losses[k] = float(edice(logits.detach(), lab.squeeze(1), mask=mk, soft_max=True))
+    lg = logits.detach().clone().requires_grad_(True)
+    la = edice(lg, lab.squeeze(1), mask=masks["a"], soft_max=True)
+    la.backward()
+    dlogits = lg.grad.numpy()
+    m.zero_grad()
+    loss = edice(logits, lab.squeeze(1), mask=masks["a"], soft_max=True)
+    loss.backward()
+    names, norms, gidx, gval = grad_summary(m)
+    save("g3_baseline16_16.npz", x=x.numpy(), labels=lab.numpy(), logits=logits.detach().numpy(),
+         mask_a=masks["a"][0].numpy(), mask_zero=masks["zero"][0].numpy(), mask_ps1=masks["persample"][1].numpy(),
+         loss_a=losses["a"], loss_zero=losses["zero"], loss_persample=losses["persample"], dlogits=dlogits,
+         gnames=names, gnorm=norms, gidx=gidx, gval=gval)
+
+
+def g3b():
+    """2x1x32^3 baseline16 logits sampled at seeded voxels (full tensor would be 4 MB)."""
+    C = 16
+    m = R.unet3D_baseline([1, 2, 2, 2, 2], num_classes=C, weight_std=True)
+    apply_recipe(m, seed=0)
+    m.eval()
+    x = torch.from_numpy(input_volume((2, 1, 32, 32, 32), seed=12, kind="ct"))
+    with torch.no_grad():
+        logits = m(x)
+    flat = logits.permute(0, 2, 3, 4, 1).reshape(-1, C)
+    rng = np.random.default_rng([13, 13])
+    vidx = rng.integers(0, flat.shape[0], size=SAMPLE_N)
+    lab = torch.from_numpy(label_volume((2, 1, 32, 32, 32), C, seed=14))
+    d, se, sp = dice_arrays(logits, lab, C - 1)
+    save("g3b_baseline16_32.npz", x=x.numpy(), vidx=vidx, logits_s=flat[torch.from_numpy(vidx)].numpy(),
+         mean=logits.mean((0, 2, 3, 4)).numpy(), std=logits.std((0, 2, 3, 4)).numpy(),
+         amin=logits.amin((0, 2, 3, 4)).numpy(), amax=logits.amax((0, 2, 3, 4)).numpy(),
+         labels=lab.numpy(), dice=d, senc=se, spec=sp)
+
+
+def g4():
+    """Per-op known-answer vectors at small shapes."""
+    out = {}
+    torch.manual_seed(0)
+    for tag, (cin, cout, k, s, sp) in {"c3s1": (32, 32, 3, 1, 8), "c3s2": (32, 64, 3, 2, 8), "c1s2": (32, 64, 1, 2, 8),
+                                       "c3s1b": (64, 32, 3, 1, 6), "c1s1": (64, 32, 1, 1, 6)}.items():
+        conv = R.conv3x3x3(cin, cout, kernel_size=(k, k, k), stride=(s, s, s), padding=k // 2, weight_std=True)
+        apply_recipe(conv, seed=1)
+        x = torch.from_numpy(input_volume((2, cin, sp, sp, sp), seed=20)).requires_grad_(True)
+        y = conv(x)
+        up = torch.from_numpy(input_volume(tuple(y.shape), seed=21))
+        (y * up).sum().backward()
+        out[f"{tag}_x"] = x.detach().numpy()
+        out[f"{tag}_y"] = y.detach().numpy()
+        out[f"{tag}_up"] = up.numpy()
+        out[f"{tag}_dx"] = x.grad.numpy()
+        out[f"{tag}_dw"] = conv.weight.grad.numpy()
+        out[f"{tag}_w"] = conv.weight.detach().numpy()
+    # GroupNorm(16, 32) + ReLU
+    gn = torch.nn.GroupNorm(16, 32)
+    apply_recipe(gn, seed=2)
+    x = (torch.from_numpy(input_volume((2, 32, 6, 7, 8), seed=22)) * 3 + 1.5).requires_grad_(True)
+    y = F.relu(gn(x))
+    up = torch.from_numpy(input_volume(tuple(y.shape), seed=23))
+    (y * up).sum().backward()
+    out.update(gn_x=x.detach().numpy(), gn_y=y.detach().numpy(), gn_up=up.numpy(), gn_dx=x.grad.numpy(),
+               gn_dgamma=gn.weight.grad.numpy(), gn_dbeta=gn.bias.grad.numpy(), gn_gamma=gn.weight.detach().numpy(),
+               gn_beta=gn.bias.detach().numpy())
+    # trilinear x2 (align_corners=False) on odd sizes
+    upm = torch.nn.Upsample(scale_factor=2, mode="trilinear")
+    x = torch.from_numpy(input_volume((2, 8, 5, 6, 7), seed=24)).requires_grad_(True)
+    y = upm(x)
+    up = torch.from_numpy(input_volume(tuple(y.shape), seed=25))
+    (y * up).sum().backward()
+    out.update(up_x=x.detach().numpy(), up_y=y.detach().numpy(), up_up=up.numpy(), up_dx=x.grad.numpy())
+    # partial Dice + BCE, C = 14 and 16
+    for C in (14, 16):
+        lg = (torch.from_numpy(input_volume((2, C, 8, 8, 8), seed=30 + C)) * 2).requires_grad_(True)
+        lab = torch.from_numpy(label_volume((2, 8, 8, 8), C, seed=31 + C))
+        rng = np.random.default_rng([32, C])
+        mk = (rng.random(15 if C == 14 else C) < 0.6).astype(np.int64)
+        loss = RLP.EDiceLoss_partial(C)(lg, lab, mask=[torch.from_numpy(mk)], soft_max=True)
+        loss.backward()
+        d, se, sp = dice_arrays(lg.detach(), lab.unsqueeze(1), C - 1)
+        out.update({f"loss{C}_logits": lg.detach().numpy(), f"loss{C}_labels": lab.numpy(), f"loss{C}_mask": mk,
+                    f"loss{C}_value": float(loss), f"loss{C}_dlogits": lg.grad.numpy(),
+                    f"loss{C}_dice": d, f"loss{C}_senc": se, f"loss{C}_spec": sp})
+    # soft_max=False (sigmoid) and uce=False variants, C = 14
+    lg = out["loss14_logits"]
+    lab = torch.from_numpy(out["loss14_labels"])
+    for tag, kw in {"sig": dict(soft_max=False), "nouce": dict(uce=False)}.items():
+        t = torch.from_numpy(lg).clone().requires_grad_(True)
+        loss = RLP.EDiceLoss_partial(14)(t, lab, mask=[torch.from_numpy(out["loss14_mask"])], **kw)
+        loss.backward()
+        out[f"loss14{tag}_value"] = float(loss)
+        out[f"loss14{tag}_dlogits"] = t.grad.numpy()
+    save("g4_ops.npz", **out)
+
+
+def g5():
+    """Full-size 96^3 single-sample forward: summary + sampled voxels."""
+    C = 16
+    m = R.unet3D_baseline([1, 2, 2, 2, 2], num_classes=C, weight_std=True)
+    apply_recipe(m, seed=0)
+    m.eval()
+    x = torch.from_numpy(input_volume((1, 1, 96, 96, 96), seed=40, kind="ct"))
+    with torch.no_grad():
+        logits = m(x)
+    flat = logits.permute(0, 2, 3, 4, 1).reshape(-1, C)
+    rng = np.random.default_rng([41, 41])
+    vidx = rng.integers(0, flat.shape[0], size=SAMPLE_N)
+    save("g5_baseline16_96.npz", vidx=vidx, logits_s=flat[torch.from_numpy(vidx)].numpy(),
+         mean=logits.mean((0, 2, 3, 4)).numpy(), std=logits.std((0, 2, 3, 4)).numpy(),
+         amin=logits.amin((0, 2, 3, 4)).numpy(), amax=logits.amax((0, 2, 3, 4)).numpy())
+
+
+def g6():
+    """Gaussian importance map of predict_sliding (evaluate_amos.py:184-197) for the 64x192x192 tile."""
+    g = REV._get_gaussian((64, 192, 192), sigma_scale=1.0 / 8)
+    rng = np.random.default_rng([42, 42])
+    pts = np.stack([rng.integers(0, s, size=SAMPLE_N) for s in g.shape], 1)
+    save("g6_gaussian.npz", line_d=g[:, 96, 96], line_h=g[32, :, 96], line_w=g[32, 96, :], corner=g[0, 0, 0],
+         gmin=g.min(), gmax=g.max(), pts=pts, vals=g[pts[:, 0], pts[:, 1], pts[:, 2]])
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6"]
+    for w in which:
+        globals()[w]()

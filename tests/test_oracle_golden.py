@@ -1,0 +1,158 @@
+"""Pin the CPU oracle (oracle/ref_cpu.py) against the golden vectors generated from the reference itself."""
+import numpy as np
+import torch
+
+from conftest import golden
+from oracle import ref_cpu as O
+from oracle.weights_recipe import recipe_state_dict
+
+torch.set_num_threads(min(8, torch.get_num_threads()))
+
+
+def P(shapes):
+    return {k: torch.from_numpy(v) for k, v in recipe_state_dict(shapes, seed=0).items()}
+
+
+def test_state_dict_order_matches_reference():
+    g = golden("g3_baseline16_16.npz")
+    keys = [k for k, _ in O.state_shapes_baseline(16)]
+    assert list(g["gnames"]) == keys
+    g = golden("g1_unet3d_dyn_32.npz")
+    keys = [k for k, _ in O.state_shapes_baseline(dyn=True)]
+    assert list(g["gnames"]) == keys
+    g = golden("g2_unet3d_g_32.npz")
+    keys = [k for k, _ in O.state_shapes_baseline(2, in_channel=2, init_filter=24, layers=(1,) * 5, conv0=True)]
+    assert list(g["gnames"]) == keys
+
+
+def test_g1_unet3d_dynconv_forward_and_dice():
+    g = golden("g1_unet3d_dyn_32.npz")
+    params = P(O.state_shapes_baseline(dyn=True))
+    with torch.no_grad():
+        y = O.unet3d_dyn_forward(params, torch.from_numpy(g["x"]), torch.from_numpy(g["task_id"]))
+    assert np.abs(y.numpy() - g["logits"]).max() < 1e-4
+    d, se, sp = O.get_dice(y, torch.from_numpy(g["labels"]), 1)
+    np.testing.assert_allclose(d, g["dice"], atol=1e-6)
+    np.testing.assert_allclose(se, g["senc"], atol=1e-6)
+    np.testing.assert_allclose(sp, g["spec"], atol=1e-6)
+
+
+def test_g1_unet3d_dynconv_backward():
+    g = golden("g1_unet3d_dyn_32.npz")
+    params = {k: v.requires_grad_(True) for k, v in P(O.state_shapes_baseline(dyn=True)).items()}
+    y = O.unet3d_dyn_forward(params, torch.from_numpy(g["x2"]), torch.from_numpy(g["task_id2"]))
+    assert np.abs(y.detach().numpy() - g["logits2"]).max() < 1e-4
+    (y * torch.from_numpy(g["up2"])).sum().backward()
+    for i, k in enumerate(g["gnames"]):
+        gr = params[k].grad.reshape(-1).double()
+        np.testing.assert_allclose(gr.norm().item(), g["gnorm"][i], rtol=1e-3, atol=1e-6)
+        np.testing.assert_allclose(gr[torch.from_numpy(g["gidx"][i])].numpy(), g["gval"][i], rtol=2e-3,
+                                   atol=2e-5 * max(1.0, g["gnorm"][i]))
+
+
+def test_g2_unet3d_g():
+    g = golden("g2_unet3d_g_32.npz")
+    params = P(O.state_shapes_baseline(2, in_channel=1, init_filter=8, layers=(1,) * 5, conv0=True))
+    with torch.no_grad():
+        y = O.unet3d_g_forward(params, torch.from_numpy(g["x"]), init_filter=8)
+    assert np.abs(y.numpy() - g["logits"]).max() < 1e-4
+    d, _, _ = O.get_dice(y, torch.from_numpy(g["labels"]), 1)
+    np.testing.assert_allclose(d, g["dice"], atol=1e-6)
+    params = {k: v.requires_grad_(True) for k, v in
+              P(O.state_shapes_baseline(2, in_channel=2, init_filter=24, layers=(1,) * 5, conv0=True)).items()}
+    y = O.unet3d_g_forward(params, torch.from_numpy(g["xr"]), init_filter=24)
+    assert np.abs(y.detach().numpy() - g["logits_r"]).max() < 1e-4
+    (y * torch.from_numpy(g["up_r"])).sum().backward()
+    for i, k in enumerate(g["gnames"]):
+        np.testing.assert_allclose(params[k].grad.double().norm().item(), g["gnorm"][i], rtol=1e-3, atol=1e-6)
+
+
+def test_g3_baseline_forward_loss_grads():
+    g = golden("g3_baseline16_16.npz")
+    params = {k: v.requires_grad_(True) for k, v in P(O.state_shapes_baseline(16)).items()}
+    y = O.baseline_forward(params, torch.from_numpy(g["x"]))
+    assert np.abs(y.detach().numpy() - g["logits"]).max() < 1e-4
+    lab = torch.from_numpy(g["labels"]).squeeze(1)
+    ma = torch.from_numpy(g["mask_a"])
+    for key, mask in [("loss_a", [ma]), ("loss_zero", [torch.from_numpy(g["mask_zero"])]),
+                      ("loss_persample", [ma, torch.from_numpy(g["mask_ps1"])])]:
+        v = O.edice_partial(y.detach(), lab, mask=mask)
+        np.testing.assert_allclose(float(v), float(g[key]), rtol=1e-5, atol=1e-6)
+    lg = y.detach().clone().requires_grad_(True)
+    O.edice_partial(lg, lab, mask=[ma]).backward()
+    np.testing.assert_allclose(lg.grad.numpy(), g["dlogits"], rtol=1e-4, atol=1e-9)
+    O.edice_partial(y, lab, mask=[ma]).backward()
+    for i, k in enumerate(g["gnames"]):
+        gr = params[k].grad.reshape(-1).double()
+        np.testing.assert_allclose(gr.norm().item(), g["gnorm"][i], rtol=1e-3, atol=1e-9)
+
+
+def test_g3b_g5_sampled_logits():
+    for name, shape in [("g3b_baseline16_32.npz", None), ("g5_baseline16_96.npz", (1, 1, 96, 96, 96))]:
+        g = golden(name)
+        params = P(O.state_shapes_baseline(16))
+        if shape is None:
+            x = torch.from_numpy(g["x"])
+        else:
+            from oracle.weights_recipe import input_volume
+            x = torch.from_numpy(input_volume(shape, seed=40, kind="ct"))
+        with torch.no_grad():
+            y = O.baseline_forward(params, x)
+        flat = y.permute(0, 2, 3, 4, 1).reshape(-1, 16)[torch.from_numpy(g["vidx"])]
+        assert np.abs(flat.numpy() - g["logits_s"]).max() < 1e-4
+        np.testing.assert_allclose(y.mean((0, 2, 3, 4)).numpy(), g["mean"], atol=1e-5)
+        if "dice" in g:
+            d, _, _ = O.get_dice(y, torch.from_numpy(g["labels"]), 15)
+            np.testing.assert_allclose(d, g["dice"], atol=1e-6)
+
+
+def test_g4_ops():
+    g = golden("g4_ops.npz")
+    for tag, s in [("c3s1", 1), ("c3s2", 2), ("c1s2", 2), ("c3s1b", 1), ("c1s1", 1)]:
+        x = torch.from_numpy(g[f"{tag}_x"]).requires_grad_(True)
+        w = torch.from_numpy(g[f"{tag}_w"]).requires_grad_(True)
+        y = O.conv(x, w, s)
+        np.testing.assert_allclose(y.detach().numpy(), g[f"{tag}_y"], atol=1e-4)
+        (y * torch.from_numpy(g[f"{tag}_up"])).sum().backward()
+        np.testing.assert_allclose(x.grad.numpy(), g[f"{tag}_dx"], atol=1e-4)
+        np.testing.assert_allclose(w.grad.numpy(), g[f"{tag}_dw"], atol=1e-3, rtol=1e-4)
+    x = torch.from_numpy(g["gn_x"]).requires_grad_(True)
+    ga = torch.from_numpy(g["gn_gamma"]).requires_grad_(True)
+    be = torch.from_numpy(g["gn_beta"]).requires_grad_(True)
+    y = O.gn_relu(x, 16, ga, be)
+    np.testing.assert_allclose(y.detach().numpy(), g["gn_y"], atol=1e-5)
+    (y * torch.from_numpy(g["gn_up"])).sum().backward()
+    np.testing.assert_allclose(x.grad.numpy(), g["gn_dx"], atol=1e-5)
+    np.testing.assert_allclose(ga.grad.numpy(), g["gn_dgamma"], atol=1e-4)
+    np.testing.assert_allclose(be.grad.numpy(), g["gn_dbeta"], atol=1e-4)
+    x = torch.from_numpy(g["up_x"]).requires_grad_(True)
+    y = O.upsample2x(x)
+    np.testing.assert_allclose(y.detach().numpy(), g["up_y"], atol=1e-6)
+    (y * torch.from_numpy(g["up_up"])).sum().backward()
+    np.testing.assert_allclose(x.grad.numpy(), g["up_dx"], atol=1e-5)
+    for C in (14, 16):
+        lg = torch.from_numpy(g[f"loss{C}_logits"]).requires_grad_(True)
+        lab = torch.from_numpy(g[f"loss{C}_labels"])
+        v = O.edice_partial(lg, lab, mask=[torch.from_numpy(g[f"loss{C}_mask"])])
+        np.testing.assert_allclose(float(v), float(g[f"loss{C}_value"]), rtol=1e-5)
+        v.backward()
+        np.testing.assert_allclose(lg.grad.numpy(), g[f"loss{C}_dlogits"], rtol=1e-4, atol=1e-9)
+        d, se, sp = O.get_dice(lg.detach(), lab.unsqueeze(1), C - 1)
+        np.testing.assert_allclose(d, g[f"loss{C}_dice"], atol=1e-6)
+    for tag, kw in {"sig": dict(soft_max=False), "nouce": dict(uce=False)}.items():
+        lg = torch.from_numpy(g["loss14_logits"]).requires_grad_(True)
+        v = O.edice_partial(lg, torch.from_numpy(g["loss14_labels"]), mask=[torch.from_numpy(g["loss14_mask"])], **kw)
+        np.testing.assert_allclose(float(v), float(g[f"loss14{tag}_value"]), rtol=1e-5)
+        v.backward()
+        np.testing.assert_allclose(lg.grad.numpy(), g[f"loss14{tag}_dlogits"], rtol=1e-4, atol=1e-9)
+
+
+def test_g6_gaussian():
+    g = golden("g6_gaussian.npz")
+    m = O.gaussian_map((64, 192, 192))
+    np.testing.assert_allclose(m[:, 96, 96], g["line_d"], rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(m[32, :, 96], g["line_h"], rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(m[32, 96, :], g["line_w"], rtol=1e-5, atol=1e-12)
+    pts = g["pts"]
+    np.testing.assert_allclose(m[pts[:, 0], pts[:, 1], pts[:, 2]], g["vals"], rtol=1e-4, atol=1e-12)
+    np.testing.assert_allclose(m.min(), g["gmin"], rtol=1e-4)
