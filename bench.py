@@ -1,0 +1,185 @@
+"""Benchmark: train voxels/s at 96^3 patch on 1..8 MI355X (BASELINE.json metric), one process per GPU.
+
+Workload (BASELINE.json configs[1]; configs[2] at N=8): the reference's 16-organ trunk unet3D_baseline([1,2,2,2,2],
+16, weight_std=True), batch 2x1x96^3 per GPU, bf16 activations (fp32 master weights, fp32 accumulation),
+synthetic CT-like volumes, random-init weights. One step = forward + EDiceLoss_partial(16) (uce) + backward
+(gradient all-reduce over RCCL inside the backward when N > 1) + SGD(momentum 0.9, wd 1e-4).
+
+Prints ONE JSON line on rank 0. `roofline` is the dominant kernel (the 32->32 3^3 conv at 96^3, 50.9% of
+forward FLOPs) timed with HIP events on the stream it is launched on; `cpu_baseline` times the oracle
+(plain-PyTorch fp32 restatement) on this host's cores on a bounded sample (one 1x96^3 training step).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "multimodal-pl_amd"), REPO]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+VOX96 = 96 ** 3
+STEP_GFLOP_PER_SAMPLE = 1152.733  # fwd + dgrad + wgrad conv FLOPs per 96^3 sample (C=16)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=2, help="patches per GPU")
+    p.add_argument("--patch", type=int, default=96)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--no-roofline", action="store_true")
+    return p.parse_args()
+
+
+def synthetic(batch, patch, device, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    hu = torch.rand((batch, 1, patch, patch, patch), generator=g) * 2000 - 1000
+    x = (hu.clamp(-325, 325) / 325).to(device)            # CT normalisation, MOTSDataset.py:171-182
+    lab = torch.randint(0, 16, (batch, 1, patch, patch, patch), generator=g).float().to(device)
+    mask = (torch.rand(16, generator=g) < 0.6).long()
+    mask[1] = 1
+    return x, lab, mask
+
+
+def dominant_kernel_roofline(device, batch, patch, reps=20):
+    """Time the 32->32 3^3 stride-1 conv (GN+ReLU prologue, residual epilogue) at patch^3, bf16, as launched
+    in the trunk, with HIP events on torch's current stream (the stream libu3d launches on)."""
+    from u3d import ops
+    x = torch.randn((batch, patch, patch, patch, 32), device=device).to(torch.bfloat16)
+    w = torch.randn(32, 32, 3, 3, 3, device=device)
+    pf, _, _ = ops.wstd_fwd(w, torch.bfloat16, True, need_dgrad=False)
+    st = ops.gn_stats(x, 16)
+    ga = torch.ones(32, device=device)
+    be = torch.zeros(32, device=device)
+    for _ in range(3):
+        y = ops.conv_fwd(x, pf, 32, 3, 1, (st, ga, be, 16), residual=x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        y = ops.conv_fwd(x, pf, 32, 3, 1, (st, ga, be, 16), residual=x)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flops = 2.0 * batch * patch ** 3 * 27 * 32 * 32
+    achieved = flops / (ms * 1e-3) / 1e12
+    del y
+    return {"kernel": "igemm_kernel<bf16,bf16,128,32> (conv 32->32 3^3 s1 @%d^3, GN+ReLU prologue, residual)" % patch,
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None, "avg_launch_ms": round(ms, 4),
+            "flop_per_launch": flops}
+
+
+def cpu_baseline(patch):
+    """Oracle (plain PyTorch fp32 CPU restatement) timed on one 1x1xpatch^3 training step on this host."""
+    from oracle import ref_cpu as O
+    from oracle.weights_recipe import recipe_state_dict
+    ncpu = len(os.sched_getaffinity(0))
+    torch.set_num_threads(max(1, min(ncpu, 32)))
+    P = {k: torch.from_numpy(v).requires_grad_(True) for k, v in recipe_state_dict(O.state_shapes_baseline(16)).items()}
+    x, lab, mask = synthetic(1, patch, "cpu", 7)
+
+    def step(xx, ll):
+        y = O.baseline_forward(P, xx)
+        loss = O.edice_partial(y, ll.squeeze(1), mask=[mask])
+        loss.backward()
+        return loss
+
+    xs, ls, _ = synthetic(1, 32, "cpu", 8)
+    step(xs, ls)  # warm-up (small)
+    t0 = time.perf_counter()
+    step(x, lab)
+    dt = time.perf_counter() - t0
+    return {"value": round(patch ** 3 / dt, 1), "unit": "voxels/s", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"1 training step (fwd+EDiceLoss_partial+bwd, fp32) at 1x1x{patch}^3, "
+                                      f"{dt:.2f} s, oracle/ref_cpu.py"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+
+    import unet3D
+    from loss_functions.loss_partial import EDiceLoss_partial
+    from u3d.ddp import U3DDataParallel
+
+    torch.manual_seed(0)
+    model = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=16, weight_std=True).to(device).train()
+    net = U3DDataParallel(model) if world > 1 else model
+    opt = torch.optim.SGD(model.parameters(), lr=5e-4, momentum=0.9, weight_decay=1e-4)
+    crit = EDiceLoss_partial(16)
+    x, lab, mask = synthetic(a.batch, a.patch, device, 1000 + rank)
+    target = lab.squeeze(1)
+    amp = a.dtype == "bf16"
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            logits, _, _ = net(x)
+        loss = crit(logits, target, mask=[mask])
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    ms = dt / a.steps * 1e3
+    vox = world * a.batch * a.patch ** 3 * a.steps / dt
+
+    roof = None
+    cpu = None
+    if rank == 0 and not a.no_roofline:
+        roof = dominant_kernel_roofline(device, a.batch, a.patch)
+        step_gflop = STEP_GFLOP_PER_SAMPLE * a.batch * (a.patch / 96) ** 3
+        roof["step_mfma_frac"] = round(step_gflop / (ms * 1e-3) / 1e3 / PEAK_BF16_TFLOPS, 4)
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(a.patch)
+    if rank == 0:
+        out = {
+            "metric": "train voxels/sec at 96^3 patch, 1/2/4/8 MI355X; fwd+bwd step ms",
+            "value": round(vox, 1), "unit": "voxels/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": a.dtype, "data": "synthetic (CT-normalised random volumes, random labels, random-init weights)",
+            "config": {"workload": "unet3D_baseline([1,2,2,2,2],16,weight_std) fwd+EDiceLoss_partial+bwd+SGD",
+                       "model": "unet3D_baseline-16", "global_batch": world * a.batch, "seq_len": a.patch ** 3,
+                       "patch": [a.patch] * 3, "parallelism": f"dp{world}"},
+            "loss": round(float(loss), 6),
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,145 @@
+/*
+ * libu3d — C ABI of the MI355X-native (gfx950 / CDNA4) 3D U-Net segmentation path.
+ *
+ * Drop-in boundary (SURVEY.md §8b row B'). The reference (TThuraya/multimodal-PL) is pure Python +
+ * PyTorch; every entry point below replaces one ATen op (or fused group of ops) that the reference's
+ * Python reaches, cited as reference file:line. Callers are the autograd Functions in
+ * multimodal-pl_amd/u3d/ (loaded with ctypes); nothing here knows about torch.
+ *
+ * Conventions
+ *  - Activations are NDHWC ("channels-last-3d"), element type `dtype` (U3D_F32 or U3D_BF16), fp32 math.
+ *    Logits / loss inputs are fp32 NDHWC. Model input volumes are fp32 NCDHW (as the reference gets them).
+ *  - Packed conv weights are [k^3][cout_p][cin_p] (forward) / [k^3][cin_p][cout_p] (data-grad) with
+ *    cout_p = round_up(cout, 32), cin_p = round_up(cin, 32), zero padded.
+ *  - GroupNorm statistics are float [n][groups][2] = (mean, rstd).
+ *  - Every call is asynchronous on `stream` (a hipStream_t; pass torch's current stream). Buffers are
+ *    caller-owned; the library never allocates device memory. Workspace sizes come from *_workspace().
+ *  - Return 0 on success, else U3D_EINVAL / U3D_EUNSUPPORTED / U3D_EHIP with a thread-local message in
+ *    u3d_last_error().
+ */
+#ifndef U3D_H_
+#define U3D_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define U3D_OK 0
+#define U3D_EINVAL 1
+#define U3D_EUNSUPPORTED 2
+#define U3D_EHIP 3
+
+#define U3D_F32 0
+#define U3D_BF16 1
+
+typedef void* u3d_stream_t; /* hipStream_t */
+
+const char* u3d_last_error(void);
+int u3d_abi_version(void);
+
+/* ---------------------------------------------------------------- weight standardisation (A1)
+ * Replaces Conv3d.forward's weight.mean(...)/torch.var/div, unet3D.py:21-26, and packs the weight for
+ * the implicit-GEMM kernels. standardize=0 packs only (nn.Conv3d of precls_conv, unet3D.py:633). */
+int u3d_wstd_fwd(int dtype, const float* w, int cout, int cin, int ksize, int standardize, void* wpk_fwd,
+                 void* wpk_dgrad, float* wstats, u3d_stream_t stream);
+/* Backward of the above: sums `nsplit` wgrad partial slabs [nsplit][k^3][cout_p][cin_p] (IN PLACE into
+ * slab 0) and maps dW_hat -> dW [cout][cin][k^3] through the standardisation (unet3D.py:22-26 autograd). */
+int u3d_wstd_bwd(float* dwpk_partials, int nsplit, const float* w, const float* wstats, int cout, int cin,
+                 int ksize, int standardize, float* dw, int accumulate, u3d_stream_t stream);
+
+/* ---------------------------------------------------------------- 3-D convolution (A1-A3, A7)
+ * F.conv3d(relu(group_norm(x)), W_hat, bias, stride, pad=k//2) (unet3D.py:27, 44-53, 1640-1657) as one
+ * MFMA implicit GEMM: M = output voxels, N = cout, K = k^3 * cin. If gn_stats != NULL the GroupNorm
+ * apply + ReLU runs in the operand prologue (zero padding stays zero). residual (same layout as y) is
+ * added in the epilogue (NoBottleneck `out + residual`, unet3D.py:71); bias (fp32 [cout]) too.
+ * y_f32 != 0 writes fp32 output (logit head) whatever dtype is. ksize in {1,3}; stride in {1,2};
+ * cin % 8 == 0 (use u3d_stem_fwd for cin <= 4). */
+int u3d_conv_fwd(int dtype, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                 int ksize, int stride, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
+                 int gn_groups, const void* residual, const float* bias, void* y, int y_f32,
+                 u3d_stream_t stream);
+/* Data gradient: dA = conv_transpose(dy, W_hat) into dA [n][d][h][w][cin] (overwritten), where (d,h,w)
+ * is the forward INPUT grid. Stride-2 layers run as 8 parity-class dense sub-convolutions. */
+int u3d_conv_dgrad(int dtype, const void* dy, int n, int cout, const void* wpk_dgrad, int cin, int d, int h,
+                   int w, int ksize, int stride, void* dx, u3d_stream_t stream);
+/* Weight gradient partial slabs: partials[s][t][co][ci] = sum over voxel split s of dy * A, with
+ * A = relu(gn(x)) recomputed in the prologue (same gn_* as the forward call). */
+int u3d_conv_wgrad_splits(int n, int cin, int d, int h, int w, int cout, int ksize, int stride);
+int u3d_conv_wgrad(int dtype, const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout,
+                   int ksize, int stride, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
+                   int gn_groups, float* partials, int nsplit, u3d_stream_t stream);
+
+/* Stem conv with cin <= 4 (conv1 1->32, unet3D.py:1632; conv0 2->f stride 2, :1514): fp32 NCDHW input,
+ * direct VALU conv (K = 27*cin is too short for MFMA), NDHWC output. */
+int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                 int stride, void* y, u3d_stream_t stream);
+int u3d_stem_wgrad_splits(int n, int d, int h, int w, int stride);
+int u3d_stem_wgrad(int dtype, const void* dy, const float* x, int n, int cin, int d, int h, int w, int cout,
+                   int stride, float* partials, int nsplit, u3d_stream_t stream);
+
+/* ---------------------------------------------------------------- GroupNorm (A4) statistics / backward
+ * nn.GroupNorm(G, C) statistics (biased variance, eps 1e-5): stats[n][g] = (mean, 1/sqrt(var+eps)).
+ * Deterministic: per-block shifted partial sums in fp32, combined in fp64 in fixed order. */
+long long u3d_gn_workspace_bytes(int n, int c, long long v);
+int u3d_gn_stats(int dtype, const void* x, int n, int c, long long v, int groups, float* stats, float* ws,
+                 u3d_stream_t stream);
+/* Backward of relu(group_norm(x)) given dA (grad wrt the ReLU output): dx (+)= ..., dgamma/dbeta (+)= ... */
+int u3d_gn_bwd(int dtype, const void* da, const void* x, int n, int c, long long v, int groups,
+               const float* stats, const float* gamma, const float* beta, void* dx, int accumulate,
+               float* dgamma, float* dbeta, int accumulate_params, float* ws, u3d_stream_t stream);
+
+/* ---------------------------------------------------------------- trilinear x2 upsample + skip (A6)
+ * nn.Upsample(scale_factor=2, mode='trilinear') (align_corners=False) then `+ skip`
+ * (unet3D.py:1646, 1764-1783). x [n][d][h][w][c] -> y [n][2d][2h][2w][c]; skip nullable. */
+int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
+                       u3d_stream_t stream);
+int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d, int h, int w, void* dx, int accumulate,
+                       u3d_stream_t stream);
+
+/* ---------------------------------------------------------------- small elementwise / reductions */
+int u3d_add_inplace(int dtype, void* y, const void* x, long long numel, u3d_stream_t stream);
+/* y[r][c] = c < cin ? x[r][c] : 0, c < cout, converted between U3D_F32 / U3D_BF16 (fp32 logit gradients ->
+ * the head's GEMM operand, channel-padded to a multiple of 8) */
+int u3d_cast(int dtype_in, const void* x, int dtype_out, void* y, long long rows, int cin, int cout,
+             u3d_stream_t stream);
+/* out[c] (+)= sum over rows of x[row][c] (conv bias gradient), fp64 combine */
+int u3d_channel_sum(int dtype, const void* x, long long rows, int c, float* out, int accumulate, float* ws,
+                    u3d_stream_t stream);
+long long u3d_channel_sum_workspace_bytes(long long rows, int c);
+
+/* ---------------------------------------------------------------- partial-label Dice + BCE (A10, A11, A13)
+ * EDiceLoss_partial(C)(logits, target, mask=[w], soft_max, uce), loss_partial.py:71-99 / DiceLoss :10-57.
+ * logits fp32 [S][V][C] (NDHWC), labels fp32 [S][V] (integer-valued), weights fp32 [C] (= mask[0][:C]).
+ * sums (fp64 [C][4]) = per class (sum p*t, sum p^2, sum t, sum BCE) over the whole batch; loss fp32[1]. */
+long long u3d_loss_workspace_bytes(int S, long long V, int C);
+int u3d_partial_loss_fwd(const float* logits, const float* labels, int S, long long V, int C, int softmax,
+                         const float* weights, int uce, double* sums, float* loss, float* ws, u3d_stream_t stream);
+/* dlogits (dtype_out, [S][V][C]) = d loss / d logits * grad_out[0] (device scalar) */
+int u3d_partial_loss_bwd(int dtype_out, const float* logits, const float* labels, int S, long long V, int C,
+                         int softmax, const float* weights, int uce, const double* sums, const float* grad_out,
+                         void* dlogits, u3d_stream_t stream);
+
+/* ---------------------------------------------------------------- hard Dice metric (A14)
+ * get_dice(preds, labels, t_id, atlas=None, num_class), evaluate_amos.py:128-154 with dice_score :92-102:
+ * argmax(softmax(logits)) per voxel; counts[s][l-1] = (sum P*T, sum P, sum T) for l = 1..num_class, and
+ * metrics[l-1] = (dice, sensitivity, precision) averaged over samples in fp32 like the reference. */
+int u3d_dice_metric(const float* logits, const float* labels, int S, long long V, int C, int num_class,
+                    long long* counts, float* metrics, long long* argmax /* nullable, [S][V] */,
+                    u3d_stream_t stream);
+
+/* ---------------------------------------------------------------- DynConv 8,8,2 head of UNet3D (A8, A9)
+ * GAP (unet3D.py:1659-1663): out[n][c] = mean_v relu(group_norm(x))[n][v][c] */
+int u3d_gn_relu_mean(int dtype, const void* x, int n, int c, long long v, int groups, const float* stats,
+                     const float* gamma, const float* beta, float* out, u3d_stream_t stream);
+/* controller (unet3D.py:1664, 1753-1759): params[n] = W cat(feat[n], onehot(task[n], kt)) + b, W [m][kf+kt] */
+int u3d_dyn_controller(const float* feat, int n, int kf, const long long* task, int kt, const float* w,
+                       const float* b, int m, float* params, u3d_stream_t stream);
+/* heads_forward (unet3D.py:1720-1732, 1788-1804): h fp32 [n][v][8] -> out fp32 [n][v][2] */
+int u3d_dynhead_fwd(const float* h, const float* params, int n, long long v, float* out, u3d_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* U3D_H_ */

@@ -1,0 +1,114 @@
+// Shared device helpers for libu3d (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <algorithm>
+#include <string>
+
+#include "../../include/u3d.h"
+
+namespace u3d {
+
+// ------------------------------------------------------------------------------------------ errors
+void set_error(const std::string& msg);
+int fail(int code, const char* fmt, ...);
+int check_launch(const char* what);
+
+#define U3D_REQUIRE(cond, ...)                                  \
+  do {                                                          \
+    if (!(cond)) return ::u3d::fail(U3D_EINVAL, __VA_ARGS__);   \
+  } while (0)
+#define U3D_HIP(expr)                                                               \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess)                                                           \
+      return ::u3d::fail(U3D_EHIP, "%s: %s", #expr, hipGetErrorString(e_));         \
+  } while (0)
+
+// ------------------------------------------------------------------------------------- bf16 / f32
+typedef uint16_t bf16;  // bf16 stored as its bit pattern
+
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(bf16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float v) {
+  __hip_bfloat16 h = __float2bfloat16(v);  // RNE, v_cvt_pk_bf16_f32 on gfx950
+  return *reinterpret_cast<bf16*>(&h);
+}
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+// 16-byte vector of T: 8 bf16 or 4 f32.
+template <typename T> struct Vec16 { static constexpr int N = 16 / sizeof(T); };
+
+template <typename T>
+__device__ __forceinline__ void load16(const T* p, float (&v)[Vec16<T>::N]) {
+  u32x4 r = *reinterpret_cast<const u32x4*>(p);
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(r[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(r[i] << 16);
+      v[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store16(T* p, const float (&v)[Vec16<T>::N]) {
+  u32x4 r;
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = __float_as_uint(v[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      r[i] = (uint32_t)from_f<bf16>(v[2 * i]) | ((uint32_t)from_f<bf16>(v[2 * i + 1]) << 16);
+  }
+  *reinterpret_cast<u32x4*>(p) = r;
+}
+
+// N-wide load/store: 16-B vector when N fills 16 bytes, scalar otherwise (odd channel counts).
+template <typename T, int N>
+__device__ __forceinline__ void loadv(const T* p, float (&v)[N]) {
+  if constexpr (N * sizeof(T) == 16) {
+    load16<T>(p, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = to_f(p[i]);
+  }
+}
+template <typename T, int N>
+__device__ __forceinline__ void storev(T* p, const float (&v)[N]) {
+  if constexpr (N * sizeof(T) == 16) {
+    store16<T>(p, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = from_f<T>(v[i]);
+  }
+}
+
+// -------------------------------------------------------------------------------- wave reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+}  // namespace u3d

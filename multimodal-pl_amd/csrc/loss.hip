@@ -1,0 +1,259 @@
+// Partial-label soft Dice + per-class BCE (EDiceLoss_partial, reference loss_partial.py:59-99 with
+// DiceLoss :10-57) and the hard Dice metric of evaluate_amos.py:92-154, on NDHWC fp32 logits.
+//
+// Forward is one pass over the logits producing per-class sums (sum p*t, sum p^2, sum t, sum BCE) for
+// the whole batch (the reference sums every sample together, :24-36), combined in fp64; the scalar loss
+// is formed on the device (no host sync: the reference's per-class .item() at :55 is dropped).
+// Backward is one elementwise pass: dL/dp from the sums, then the softmax (or sigmoid) Jacobian.
+#include "common.h"
+
+namespace u3d {
+
+constexpr int LT = 256;
+constexpr int CMAX = 32;
+
+__device__ __forceinline__ void probs(const float* __restrict__ lg, int C, int softmax, float (&p)[CMAX]) {
+  if (softmax) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) m = fmaxf(m, lg[c]);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        p[c] = expf(lg[c] - m);
+        s += p[c];
+      }
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) p[c] = p[c] / s;
+  } else if (softmax == 0) {
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) p[c] = 1.f / (1.f + expf(-lg[c]));
+  } else {  // 2: inputs are already probabilities (DiceLoss called directly, loss_partial.py:38)
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) p[c] = lg[c];
+  }
+}
+
+// torch BCELoss element: (t - 1) * max(log1p(-p), -100) - t * max(log(p), -100)
+__device__ __forceinline__ float bce_elem(float p, float t) {
+  return (t - 1.f) * fmaxf(log1pf(-p), -100.f) - t * fmaxf(logf(p), -100.f);
+}
+
+__global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
+                                                         long long nvox, int C, int softmax, int uce,
+                                                         float* __restrict__ ws) {
+  __shared__ float red[LT / 64][4 * CMAX];
+  float acc[4][CMAX];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) acc[k][c] = 0.f;
+  for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < nvox; v += (long long)gridDim.x * LT) {
+    float p[CMAX];
+    probs(lg + v * C, C, softmax, p);
+    const float t = lab[v];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        const float tc = (t == (float)c) ? 1.f : 0.f;
+        acc[0][c] = fmaf(p[c], tc, acc[0][c]);
+        acc[1][c] = fmaf(p[c], p[c], acc[1][c]);
+        acc[2][c] += tc;
+        if (uce) acc[3][c] += bce_elem(p[c], tc);
+      }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        float s = wave_sum(acc[k][c]);
+        if (lane == 0) red[wave][k * CMAX + c] = s;
+      }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 4 * C; i += LT) {
+    const int k = i / C, c = i % C;
+    float s = 0.f;
+    for (int w = 0; w < LT / 64; ++w) s += red[w][k * CMAX + c];
+    ws[(long long)blockIdx.x * 4 * C + k * C + c] = s;
+  }
+}
+
+__global__ __launch_bounds__(LT) void loss_final_kernel(const float* __restrict__ ws, int nblk, int C,
+                                                       const float* __restrict__ wt, int uce, double count,
+                                                       double* __restrict__ sums, float* __restrict__ loss) {
+  __shared__ double s[4 * CMAX];
+  for (int i = threadIdx.x; i < 4 * C; i += LT) {
+    double a = 0;
+    for (int b = 0; b < nblk; ++b) a += ws[(long long)b * 4 * C + i];
+    s[i] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double dice = 0, ce = 0;
+    for (int c = 0; c < C; ++c) {
+      const double I = s[c], Z = s[C + c], Y = s[2 * C + c], B = s[3 * C + c];
+      sums[c * 4 + 0] = I;
+      sums[c * 4 + 1] = Z;
+      sums[c * 4 + 2] = Y;
+      sums[c * 4 + 3] = B;
+      const float d = 1.f - (float)((2.0 * I + 1e-5) / (Z + Y + 1e-5));
+      dice += (double)d * wt[c];
+      ce += (double)(float)(B / count) * wt[c];
+    }
+    double l = dice / C;
+    if (uce) l += ce;
+    loss[0] = (float)l;
+  }
+}
+
+template <typename TO>
+__global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
+                                                     long long nvox, int C, int softmax, int uce,
+                                                     const float* __restrict__ wt, const double* __restrict__ sums,
+                                                     const float* __restrict__ gout, double count, TO* __restrict__ dl) {
+  __shared__ float kd_a[CMAX], kd_b[CMAX], kb[CMAX];
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    const double I = sums[c * 4], Z = sums[c * 4 + 1], Y = sums[c * 4 + 2];
+    const double num = 2.0 * I + 1e-5, den = Z + Y + 1e-5;
+    const double scale = (double)wt[c] / C * gout[0];
+    // d(1 - num/den)/dp = -(2 t den - num * 2 p) / den^2  =  t * a + p * b
+    kd_a[c] = (float)(-2.0 / den * scale);
+    kd_b[c] = (float)(2.0 * num / (den * den) * scale);
+    kb[c] = uce ? (float)((double)wt[c] / count * gout[0]) : 0.f;
+  }
+  __syncthreads();
+  for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < nvox; v += (long long)gridDim.x * LT) {
+    float p[CMAX], g[CMAX];
+    probs(lg + v * C, C, softmax, p);
+    const float t = lab[v];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        const float tc = (t == (float)c) ? 1.f : 0.f;
+        float gc = fmaf(tc, kd_a[c], p[c] * kd_b[c]);
+        if (uce) gc += kb[c] * (p[c] - tc) / fmaxf((1.f - p[c]) * p[c], 1e-12f);
+        g[c] = gc;
+        dot = fmaf(gc, p[c], dot);
+      }
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+      if (c < C) {
+        const float r = softmax == 1 ? p[c] * (g[c] - dot) : softmax == 0 ? g[c] * (1.f - p[c]) * p[c] : g[c];
+        dl[v * C + c] = from_f<TO>(r);
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------- Dice metric
+__global__ __launch_bounds__(LT) void dice_count_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
+                                                       long long V, int C, int ncls,
+                                                       unsigned long long* __restrict__ cnt,
+                                                       long long* __restrict__ amap) {
+  __shared__ unsigned int h[3 * CMAX];
+  for (int i = threadIdx.x; i < 3 * CMAX; i += LT) h[i] = 0;
+  __syncthreads();
+  const int s = blockIdx.y;
+  const float* base = lg + (long long)s * V * C;
+  for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < V; v += (long long)gridDim.x * LT) {
+    float p[CMAX];
+    probs(base + v * C, C, 1, p);
+    int am = 0;
+    float best = p[0];
+#pragma unroll
+    for (int c = 1; c < CMAX; ++c)
+      if (c < C && p[c] > best) {
+        best = p[c];
+        am = c;
+      }
+    if (amap) amap[(long long)s * V + v] = am;
+    const float t = lab[(long long)s * V + v];
+    const int ti = (t >= 1.f && t <= (float)ncls && t == floorf(t)) ? (int)t : 0;
+    if (am >= 1 && am <= ncls) atomicAdd(&h[(am - 1) * 3 + 1], 1u);
+    if (ti >= 1) atomicAdd(&h[(ti - 1) * 3 + 2], 1u);
+    if (am >= 1 && am <= ncls && am == ti) atomicAdd(&h[(am - 1) * 3 + 0], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * ncls; i += LT)
+    if (h[i]) atomicAdd(&cnt[(long long)s * 3 * ncls + i], (unsigned long long)h[i]);
+}
+
+__global__ void dice_final_kernel(const unsigned long long* __restrict__ cnt, int S, int ncls, float* __restrict__ m) {
+  const int l = threadIdx.x;
+  if (l >= ncls) return;
+  float sd = 0.f, ss = 0.f, sp = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const unsigned long long* c = cnt + ((long long)s * ncls + l) * 3;
+    const float num = (float)c[0], P = (float)c[1], T = (float)c[2];
+    sd += (float)(2 * c[0]) / (float)(c[1] + c[2] + 1);
+    ss += num / (float)(c[2] + 1);
+    sp += num / (float)(c[1] + 1);
+    (void)P;
+    (void)T;
+  }
+  m[l * 3 + 0] = sd / (float)S;
+  m[l * 3 + 1] = ss / (float)S;
+  m[l * 3 + 2] = sp / (float)S;
+}
+
+static int loss_blocks(long long nvox) { return (int)std::min<long long>(1024, std::max<long long>(1, (nvox + LT - 1) / LT)); }
+
+}  // namespace u3d
+
+using namespace u3d;
+
+extern "C" long long u3d_loss_workspace_bytes(int S, long long V, int C) {
+  return (long long)loss_blocks((long long)S * V) * 4 * C * 4;
+}
+
+extern "C" int u3d_partial_loss_fwd(const float* logits, const float* labels, int S, long long V, int C, int softmax,
+                                    const float* weights, int uce, double* sums, float* loss, float* ws,
+                                    u3d_stream_t stream) {
+  U3D_REQUIRE(logits && labels && weights && sums && loss && ws, "partial_loss_fwd: null pointer");
+  U3D_REQUIRE(C >= 1 && C <= CMAX && S >= 1 && V >= 1, "partial_loss_fwd: C=%d unsupported (max %d)", C, CMAX);
+  hipStream_t s = (hipStream_t)stream;
+  const long long nvox = (long long)S * V;
+  const int nb = loss_blocks(nvox);
+  hipLaunchKernelGGL(loss_partial_kernel, dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, ws);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(LT), 0, s, ws, nb, C, weights, uce, (double)nvox, sums, loss);
+  return check_launch("partial_loss_fwd");
+}
+
+extern "C" int u3d_partial_loss_bwd(int dtype_out, const float* logits, const float* labels, int S, long long V, int C,
+                                    int softmax, const float* weights, int uce, const double* sums,
+                                    const float* grad_out, void* dlogits, u3d_stream_t stream) {
+  U3D_REQUIRE(logits && labels && weights && sums && grad_out && dlogits, "partial_loss_bwd: null pointer");
+  U3D_REQUIRE(C >= 1 && C <= CMAX, "partial_loss_bwd: C=%d unsupported", C);
+  hipStream_t s = (hipStream_t)stream;
+  const long long nvox = (long long)S * V;
+  const int nb = (int)std::min<long long>(8192, (nvox + LT - 1) / LT);
+  if (dtype_out == U3D_BF16)
+    hipLaunchKernelGGL(loss_bwd_kernel<bf16>, dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, weights,
+                       sums, grad_out, (double)nvox, (bf16*)dlogits);
+  else
+    hipLaunchKernelGGL(loss_bwd_kernel<float>, dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, weights,
+                       sums, grad_out, (double)nvox, (float*)dlogits);
+  return check_launch("partial_loss_bwd");
+}
+
+extern "C" int u3d_dice_metric(const float* logits, const float* labels, int S, long long V, int C, int num_class,
+                               long long* counts, float* metrics, long long* argmax, u3d_stream_t stream) {
+  U3D_REQUIRE(logits && labels && counts && metrics, "dice_metric: null pointer");
+  U3D_REQUIRE(C >= 1 && C <= CMAX && num_class >= 1 && num_class <= CMAX && S >= 1, "dice_metric: bad sizes");
+  hipStream_t s = (hipStream_t)stream;
+  U3D_HIP(hipMemsetAsync(counts, 0, (size_t)S * num_class * 3 * 8, s));
+  const int nb = (int)std::min<long long>(1024, (V + LT - 1) / LT);
+  hipLaunchKernelGGL(dice_count_kernel, dim3(nb, S), dim3(LT), 0, s, logits, labels, V, C, num_class,
+                     (unsigned long long*)counts, argmax);
+  hipLaunchKernelGGL(dice_final_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)counts, S, num_class,
+                     metrics);
+  return check_launch("dice_metric");
+}

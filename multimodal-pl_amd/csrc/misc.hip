@@ -1,0 +1,138 @@
+// Small elementwise / reduction helpers of the U-Net path.
+//   u3d_add_inplace  — gradient accumulation y += x (the reference's implicit autograd accumulation for
+//                      tensors with several consumers, e.g. block inputs feeding residual + conv paths).
+//   u3d_channel_sum  — conv bias gradient sum_v dy[v][c] (precls_conv bias, unet3D.py:633).
+#include "common.h"
+
+namespace u3d {
+
+template <typename T>
+__global__ __launch_bounds__(256) void add_kernel(T* __restrict__ y, const T* __restrict__ x, long long nvec) {
+  constexpr int VEC = 16 / sizeof(T);
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
+    float a[VEC], b[VEC];
+    load16<T>(y + i * VEC, a);
+    load16<T>(x + i * VEC, b);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) a[e] += b[e];
+    store16<T>(y + i * VEC, a);
+  }
+}
+
+template <typename T>
+__global__ void add_tail_kernel(T* __restrict__ y, const T* __restrict__ x, long long start, long long n) {
+  long long i = start + blockIdx.x * 256LL + threadIdx.x;
+  if (i < n) y[i] = from_f<T>(to_f(y[i]) + to_f(x[i]));
+}
+
+// per-block per-channel partial sums: thread (row lane, channel) strided
+template <typename T>
+__global__ __launch_bounds__(256) void chsum_partial(const T* __restrict__ x, long long rows, int c, int rpb,
+                                                    float* __restrict__ ws) {
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  const int lanes = 256 / c;  // c <= 256
+  const int ch = tid % c, rl = tid / c;
+  float s = 0.f;
+  if (rl < lanes) {
+    const long long r0 = (long long)blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+    for (long long r = r0 + rl; r < r1; r += lanes) s += to_f(x[r * c + ch]);
+  }
+  red[tid] = s;
+  __syncthreads();
+  if (tid < c) {
+    float t = 0.f;
+    for (int l = 0; l < lanes; ++l) t += red[l * c + tid];
+    ws[(long long)blockIdx.x * c + tid] = t;
+  }
+}
+
+__global__ void chsum_final(const float* __restrict__ ws, int nblk, int c, float* __restrict__ out, int accum) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  double s = 0;
+  for (int b = 0; b < nblk; ++b) s += ws[(long long)b * c + ch];
+  out[ch] = (accum ? out[ch] : 0.f) + (float)s;
+}
+
+static int chsum_blocks(long long rows, int c, int* rpb) {
+  const int lanes = 256 / c;
+  long long want = std::max<long long>(lanes * 4, (rows + 1023) / 1024);
+  *rpb = (int)want;
+  return (int)((rows + want - 1) / want);
+}
+
+}  // namespace u3d
+
+using namespace u3d;
+
+extern "C" int u3d_add_inplace(int dtype, void* y, const void* x, long long numel, u3d_stream_t stream) {
+  U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "add_inplace: bad dtype");
+  U3D_REQUIRE(y && x && numel >= 0, "add_inplace: bad args");
+  if (numel == 0) return U3D_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int vec = dtype == U3D_BF16 ? 8 : 4;
+  const long long nvec = numel / vec, tail = nvec * vec;
+  if (nvec) {
+    const int nb = (int)std::min<long long>(8192, (nvec + 255) / 256);
+    if (dtype == U3D_BF16) hipLaunchKernelGGL(add_kernel<bf16>, dim3(nb), dim3(256), 0, s, (bf16*)y, (const bf16*)x, nvec);
+    else hipLaunchKernelGGL(add_kernel<float>, dim3(nb), dim3(256), 0, s, (float*)y, (const float*)x, nvec);
+  }
+  if (tail < numel) {
+    if (dtype == U3D_BF16) hipLaunchKernelGGL(add_tail_kernel<bf16>, dim3(1), dim3(256), 0, s, (bf16*)y, (const bf16*)x, tail, numel);
+    else hipLaunchKernelGGL(add_tail_kernel<float>, dim3(1), dim3(256), 0, s, (float*)y, (const float*)x, tail, numel);
+  }
+  return check_launch("add_kernel");
+}
+
+extern "C" long long u3d_channel_sum_workspace_bytes(long long rows, int c) {
+  int rpb;
+  return (long long)chsum_blocks(rows, c, &rpb) * c * 4;
+}
+
+extern "C" int u3d_channel_sum(int dtype, const void* x, long long rows, int c, float* out, int accumulate, float* ws,
+                               u3d_stream_t stream) {
+  U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "channel_sum: bad dtype");
+  U3D_REQUIRE(x && out && ws && rows > 0 && c >= 1 && c <= 256, "channel_sum: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  int rpb;
+  const int nb = chsum_blocks(rows, c, &rpb);
+  if (dtype == U3D_BF16) hipLaunchKernelGGL(chsum_partial<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)x, rows, c, rpb, ws);
+  else hipLaunchKernelGGL(chsum_partial<float>, dim3(nb), dim3(256), 0, s, (const float*)x, rows, c, rpb, ws);
+  hipLaunchKernelGGL(chsum_final, dim3((c + 63) / 64), dim3(64), 0, s, ws, nb, c, out, accumulate);
+  return check_launch("channel_sum");
+}
+
+namespace u3d {
+// y[r][c] = c < cin ? x[r][c] : 0 for c < cout (dtype conversion + zero channel padding)
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long long rows, int cin,
+                                                  int cout) {
+  const long long n = rows * cout;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long r = i / cout;
+    const int c = (int)(i - r * cout);
+    y[i] = from_f<TO>(c < cin ? to_f(x[r * cin + c]) : 0.f);
+  }
+}
+}  // namespace u3d
+
+extern "C" int u3d_cast(int dtype_in, const void* x, int dtype_out, void* y, long long rows, int cin, int cout,
+                        u3d_stream_t stream) {
+  U3D_REQUIRE((dtype_in == U3D_F32 || dtype_in == U3D_BF16) && (dtype_out == U3D_F32 || dtype_out == U3D_BF16),
+              "cast: bad dtype");
+  U3D_REQUIRE(x && y && rows >= 0 && cin >= 1 && cout >= cin, "cast: bad args");
+  const long long numel = rows * cout;
+  if (numel == 0) return U3D_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)std::min<long long>(8192, (numel + 255) / 256);
+  if (dtype_in == U3D_F32 && dtype_out == U3D_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(nb), dim3(256), 0, s, (const float*)x, (bf16*)y, rows, cin, cout);
+  else if (dtype_in == U3D_BF16 && dtype_out == U3D_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(nb), dim3(256), 0, s, (const bf16*)x, (float*)y, rows, cin, cout);
+  else if (dtype_in == U3D_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(nb), dim3(256), 0, s, (const float*)x, (float*)y, rows, cin, cout);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(nb), dim3(256), 0, s, (const bf16*)x, (bf16*)y, rows, cin, cout);
+  return check_launch("cast_kernel");
+}

@@ -1,0 +1,161 @@
+// Trilinear x2 upsampling (align_corners=False) fused with the decoder skip addition, and its backward.
+// Reference: self.upsamplex2 = nn.Upsample(scale_factor=2, mode='trilinear') (unet3D.py:1646) followed by
+// `x = x + skip{3,2,1,0}` (unet3D.py:1764-1783); also the logit upsample of unet3D_g (:1621).
+// Source index per dim (PyTorch area_pixel_compute_source_index, scale 1/2):
+//   src = max(0, (o + 0.5) * 0.5 - 0.5); i0 = floor(src); i1 = i0 + (i0 < n-1); l1 = src - i0; l0 = 1 - l1.
+#include "common.h"
+
+namespace u3d {
+
+struct Lerp {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ Lerp lerp_of(int o, int n) {
+  float src = fmaxf(0.f, (o + 0.5f) * 0.5f - 0.5f);
+  int i0 = (int)src;
+  Lerp L;
+  L.i0 = i0;
+  L.i1 = i0 + (i0 < n - 1 ? 1 : 0);
+  L.l1 = src - (float)i0;
+  L.l0 = 1.f - L.l1;
+  return L;
+}
+
+// weight of output o onto input i along one dim (0 if o does not read i)
+__device__ __forceinline__ float wt_of(int o, int i, int n) {
+  Lerp L = lerp_of(o, n);
+  float w = 0.f;
+  if (L.i0 == i) w += L.l0;
+  if (L.i1 == i) w += L.l1;
+  return w;
+}
+
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void up_fwd_kernel(const T* __restrict__ x, const T* __restrict__ skip,
+                                                    T* __restrict__ y, int n, int c, int d, int h, int w) {
+  const int chn = c / VEC, D = 2 * d, H = 2 * h, W = 2 * w;
+  const long long total = (long long)n * D * H * W * chn;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(i % chn);
+    long long t = i / chn;
+    const int ow = (int)(t % W); t /= W;
+    const int oh = (int)(t % H); t /= H;
+    const int od = (int)(t % D);
+    const int nn = (int)(t / D);
+    const Lerp Ld = lerp_of(od, d), Lh = lerp_of(oh, h), Lw = lerp_of(ow, w);
+    const T* xb = x + (long long)nn * d * h * w * c + j * VEC;
+    auto at = [&](int a, int b, int e, float (&v)[VEC]) { loadv<T, VEC>(xb + (((long long)a * h + b) * w + e) * c, v); };
+    float v000[VEC], v001[VEC], v010[VEC], v011[VEC], v100[VEC], v101[VEC], v110[VEC], v111[VEC];
+    at(Ld.i0, Lh.i0, Lw.i0, v000); at(Ld.i0, Lh.i0, Lw.i1, v001);
+    at(Ld.i0, Lh.i1, Lw.i0, v010); at(Ld.i0, Lh.i1, Lw.i1, v011);
+    at(Ld.i1, Lh.i0, Lw.i0, v100); at(Ld.i1, Lh.i0, Lw.i1, v101);
+    at(Ld.i1, Lh.i1, Lw.i0, v110); at(Ld.i1, Lh.i1, Lw.i1, v111);
+    float o[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e)  // PyTorch CPU nesting order: t0*(h0*(w0*a + w1*b) + h1*(...)) + t1*(...)
+      o[e] = Ld.l0 * (Lh.l0 * (Lw.l0 * v000[e] + Lw.l1 * v001[e]) + Lh.l1 * (Lw.l0 * v010[e] + Lw.l1 * v011[e])) +
+             Ld.l1 * (Lh.l0 * (Lw.l0 * v100[e] + Lw.l1 * v101[e]) + Lh.l1 * (Lw.l0 * v110[e] + Lw.l1 * v111[e]));
+    const long long off = i * VEC;
+    if (skip) {
+      float sv[VEC];
+      loadv<T, VEC>(skip + off, sv);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) o[e] += sv[e];
+    }
+    storev<T, VEC>(y + off, o);
+  }
+}
+
+// gather form of the adjoint: input i collects outputs {2i-1, 2i, 2i+1, 2i+2} per dim
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void up_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, int c, int d,
+                                                    int h, int w, int accum) {
+  const int chn = c / VEC, D = 2 * d, H = 2 * h, W = 2 * w;
+  const long long total = (long long)n * d * h * w * chn;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(i % chn);
+    long long t = i / chn;
+    const int iw = (int)(t % w); t /= w;
+    const int ih = (int)(t % h); t /= h;
+    const int id = (int)(t % d);
+    const int nn = (int)(t / d);
+    int od_[4], oh_[4], ow_[4];
+    float wd[4], wh[4], ww[4];
+    int cd = 0, ch = 0, cw = 0;
+    for (int k = -1; k <= 2; ++k) {
+      int o = 2 * id + k;
+      if (o >= 0 && o < D) { float q = wt_of(o, id, d); if (q != 0.f) { od_[cd] = o; wd[cd++] = q; } }
+      o = 2 * ih + k;
+      if (o >= 0 && o < H) { float q = wt_of(o, ih, h); if (q != 0.f) { oh_[ch] = o; wh[ch++] = q; } }
+      o = 2 * iw + k;
+      if (o >= 0 && o < W) { float q = wt_of(o, iw, w); if (q != 0.f) { ow_[cw] = o; ww[cw++] = q; } }
+    }
+    float acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+    const T* yb = dy + (long long)nn * D * H * W * c + j * VEC;
+    for (int a = 0; a < cd; ++a)
+      for (int b = 0; b < ch; ++b)
+        for (int q = 0; q < cw; ++q) {
+          float v[VEC];
+          loadv<T, VEC>(yb + (((long long)od_[a] * H + oh_[b]) * W + ow_[q]) * c, v);
+          const float wgt = wd[a] * wh[b] * ww[q];
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[e] = fmaf(wgt, v[e], acc[e]);
+        }
+    const long long off = i * VEC;
+    if (accum) {
+      float o[VEC];
+      loadv<T, VEC>(dx + off, o);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[e] += o[e];
+    }
+    storev<T, VEC>(dx + off, acc);
+  }
+}
+
+}  // namespace u3d
+
+using namespace u3d;
+
+static int grid_for(long long total) { return (int)std::min<long long>(8192, std::max<long long>(1, (total + 255) / 256)); }
+
+extern "C" int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
+                                  u3d_stream_t stream) {
+  U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "upsample: bad dtype");
+  U3D_REQUIRE(x && y && n > 0 && c > 0 && d > 0 && h > 0 && w > 0, "upsample: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  const int vec = dtype == U3D_BF16 ? 8 : 4;
+  const bool vect = c % vec == 0;
+  const long long total = (long long)n * 8 * d * h * w * (vect ? c / vec : c);
+  const dim3 gr(grid_for(total)), bl(256);
+  if (dtype == U3D_BF16) {
+    if (vect) hipLaunchKernelGGL((up_fwd_kernel<bf16, 8>), gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w);
+    else hipLaunchKernelGGL((up_fwd_kernel<bf16, 1>), gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w);
+  } else {
+    if (vect) hipLaunchKernelGGL((up_fwd_kernel<float, 4>), gr, bl, 0, s, (const float*)x, (const float*)skip, (float*)y, n, c, d, h, w);
+    else hipLaunchKernelGGL((up_fwd_kernel<float, 1>), gr, bl, 0, s, (const float*)x, (const float*)skip, (float*)y, n, c, d, h, w);
+  }
+  return check_launch("up_fwd_kernel");
+}
+
+extern "C" int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d, int h, int w, void* dx, int accumulate,
+                                  u3d_stream_t stream) {
+  U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "upsample_bwd: bad dtype");
+  U3D_REQUIRE(dy && dx && n > 0 && c > 0 && d > 0 && h > 0 && w > 0, "upsample_bwd: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  const int vec = dtype == U3D_BF16 ? 8 : 4;
+  const bool vect = c % vec == 0;
+  const long long total = (long long)n * d * h * w * (vect ? c / vec : c);
+  const dim3 gr(grid_for(total)), bl(256);
+  if (dtype == U3D_BF16) {
+    if (vect) hipLaunchKernelGGL((up_bwd_kernel<bf16, 8>), gr, bl, 0, s, (const bf16*)dy, (bf16*)dx, n, c, d, h, w, accumulate);
+    else hipLaunchKernelGGL((up_bwd_kernel<bf16, 1>), gr, bl, 0, s, (const bf16*)dy, (bf16*)dx, n, c, d, h, w, accumulate);
+  } else {
+    if (vect) hipLaunchKernelGGL((up_bwd_kernel<float, 4>), gr, bl, 0, s, (const float*)dy, (float*)dx, n, c, d, h, w, accumulate);
+    else hipLaunchKernelGGL((up_bwd_kernel<float, 1>), gr, bl, 0, s, (const float*)dy, (float*)dx, n, c, d, h, w, accumulate);
+  }
+  return check_launch("up_bwd_kernel");
+}

@@ -1,0 +1,85 @@
+"""ctypes binding of libu3d.so (include/u3d.h). No fallback: if the library is missing or the tensors are
+not on a ROCm device, calls raise."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libu3d.so")
+
+F32, BF16 = 0, 1
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_longlong
+
+# name -> argtypes (restype int unless noted)
+_SIGS = {
+    "u3d_abi_version": [],
+    "u3d_wstd_fwd": [I, P, I, I, I, I, P, P, P, P],
+    "u3d_wstd_bwd": [P, I, P, P, I, I, I, I, P, I, P],
+    "u3d_conv_fwd": [I, P, I, I, I, I, I, P, I, I, I, P, P, P, I, P, P, P, I, P],
+    "u3d_conv_dgrad": [I, P, I, I, P, I, I, I, I, I, I, P, P],
+    "u3d_conv_wgrad_splits": [I, I, I, I, I, I, I, I],
+    "u3d_conv_wgrad": [I, P, P, I, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
+    "u3d_stem_fwd": [I, P, I, I, I, I, I, P, I, I, P, P],
+    "u3d_stem_wgrad_splits": [I, I, I, I, I],
+    "u3d_stem_wgrad": [I, P, P, I, I, I, I, I, I, I, P, I, P],
+    "u3d_gn_workspace_bytes": [I, I, L],
+    "u3d_gn_stats": [I, P, I, I, L, I, P, P, P],
+    "u3d_gn_bwd": [I, P, P, I, I, L, I, P, P, P, P, I, P, P, I, P, P],
+    "u3d_upsample2x_add": [I, P, I, I, I, I, I, P, P, P],
+    "u3d_upsample2x_bwd": [I, P, I, I, I, I, I, P, I, P],
+    "u3d_add_inplace": [I, P, P, L, P],
+    "u3d_channel_sum": [I, P, L, I, P, I, P, P],
+    "u3d_channel_sum_workspace_bytes": [L, I],
+    "u3d_cast": [I, P, I, P, L, I, I, P],
+    "u3d_loss_workspace_bytes": [I, L, I],
+    "u3d_partial_loss_fwd": [P, P, I, L, I, I, P, I, P, P, P, P],
+    "u3d_partial_loss_bwd": [I, P, P, I, L, I, I, P, I, P, P, P, P],
+    "u3d_dice_metric": [P, P, I, L, I, I, P, P, P, P],
+    "u3d_gn_relu_mean": [I, P, I, I, L, I, P, P, P, P, P],
+    "u3d_dyn_controller": [P, I, I, P, I, P, P, I, P, P],
+    "u3d_dynhead_fwd": [P, P, I, L, P, P],
+}
+_RESTYPE = {"u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L}
+
+_lib = None
+
+
+class U3DError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libu3d.so once. Raises U3DError if it is absent (build with __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise U3DError(f"libu3d.so not found at {LIB_PATH}: build it (python -c 'import __graft_entry__ as g; "
+                           "g.build()'); the HIP path has no fallback")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            f = getattr(h, name)
+            f.argtypes = args
+            f.restype = _RESTYPE.get(name, I)
+        h.u3d_last_error.argtypes = []
+        h.u3d_last_error.restype = ctypes.c_char_p
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS) + ["u3d_last_error"]
+
+
+def call(name, *args):
+    f = getattr(lib(), name)
+    rc = f(*args)
+    if rc != 0:
+        msg = lib().u3d_last_error().decode(errors="replace")
+        raise U3DError(f"{name} failed (rc={rc}): {msg}")
+    return rc
+
+
+def query(name, *args):
+    return getattr(lib(), name)(*args)

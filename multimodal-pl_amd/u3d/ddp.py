@@ -1,0 +1,121 @@
+"""Data parallelism for the native trunk: bucketed gradient all-reduce over RCCL (torch.distributed backend
+"nccl" = RCCL on ROCm, xGMI between the GPUs of a node), launched from INSIDE the native backward as soon as
+a bucket's last gradient is written, so the all-reduce of the decoder/bottleneck buckets overlaps the
+remaining encoder backward. This is the data-parallel wrapper the reference reached through
+engine.data_parallel (engine.py:30-32; original run: torch.distributed.launch + DDP, run_amos_atlas_final.sh:2).
+
+Per step every rank writes its parameter gradients straight into fresh flat bucket buffers (no copy); the
+bucket is averaged in place; the trunk's autograd Function returns the bucket views as parameter grads.
+"""
+import contextlib
+import threading
+
+import torch
+import torch.distributed as dist
+
+_local = threading.local()
+
+
+def current_sink():
+    return getattr(_local, "sink", None)
+
+
+@contextlib.contextmanager
+def use_sink(sink):
+    prev = current_sink()
+    _local.sink = sink
+    try:
+        yield
+    finally:
+        _local.sink = prev
+
+
+class GradBucketer:
+    def __init__(self, named_params, bucket_mb=25.0, group=None):
+        params = [(n, p) for n, p in named_params if p.requires_grad]
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.avg_native = dist.get_backend(group) == "nccl"
+        cap = int(bucket_mb * 1024 * 1024 / 4)
+        self.buckets = []       # list of [names, numel]
+        self.where = {}         # name -> (bucket index, offset, shape)
+        cur, cur_n = [], 0
+        for n, p in reversed(params):  # reverse registration order ~= order the native backward produces grads
+            if cur and cur_n + p.numel() > cap:
+                self.buckets.append((cur, cur_n))
+                cur, cur_n = [], 0
+            self.where[n] = (len(self.buckets), cur_n, tuple(p.shape))
+            cur.append(n)
+            cur_n += p.numel()
+        if cur:
+            self.buckets.append((cur, cur_n))
+        self.device = params[0][1].device if params else None
+        self.active = False
+
+    def begin(self):
+        self.bufs = [torch.empty(nel, dtype=torch.float32, device=self.device) for _, nel in self.buckets]
+        self.left = [len(names) for names, _ in self.buckets]
+        self.done_names = set()
+        self.works = [None] * len(self.buckets)
+        self.active = True
+
+    def out(self, name):
+        if not self.active or name not in self.where:
+            return None
+        return self.view(name)
+
+    def view(self, name):
+        b, off, shape = self.where[name]
+        nel = 1
+        for s in shape:
+            nel *= s
+        return self.bufs[b][off:off + nel].view(shape)
+
+    def _launch(self, b):
+        op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
+        self.works[b] = dist.all_reduce(self.bufs[b], op=op, group=self.group, async_op=True)
+
+    def done(self, name):
+        if not self.active or name not in self.where or name in self.done_names:
+            return
+        self.done_names.add(name)
+        b = self.where[name][0]
+        self.left[b] -= 1
+        if self.left[b] == 0:
+            self._launch(b)
+
+    def finish(self):
+        """Zero never-produced grads, launch the rest, wait (stream-level) for every bucket."""
+        if not self.active:
+            return
+        for b, (names, _) in enumerate(self.buckets):
+            if self.works[b] is None:
+                for n in names:
+                    if n not in self.done_names:
+                        self.out(n).zero_()
+                self._launch(b)
+        for b, w in enumerate(self.works):
+            w.wait()
+            if not self.avg_native:
+                self.bufs[b].div_(self.world)
+        self.active = False
+
+
+class U3DDataParallel(torch.nn.Module):
+    """DDP-style wrapper: ``.module`` is the wrapped model (train_amos_atlas_final.py:391 uses it)."""
+
+    def __init__(self, module, group=None, bucket_mb=25.0):
+        super().__init__()
+        self.module = module
+        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.bucketer = GradBucketer(module.named_parameters(), bucket_mb, group) if self.distributed else None
+        if self.distributed:
+            with torch.no_grad():  # start from identical weights on every rank (DDP's init broadcast)
+                for p in module.parameters():
+                    dist.broadcast(p.data, 0, group=group)
+
+    def forward(self, *args, **kwargs):
+        if self.bucketer is None or not torch.is_grad_enabled():
+            return self.module(*args, **kwargs)
+        with use_sink(self.bucketer):
+            return self.module(*args, **kwargs)

@@ -1,0 +1,240 @@
+"""Tensor-level wrappers over the libu3d C ABI. Torch is only the allocator / stream provider here: every
+value is computed by a HIP kernel. All activations are NDHWC tensors of shape [n, d, h, w, c]."""
+import torch
+
+from . import _lib
+from ._lib import BF16, F32, call, query
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dt_code(dtype):
+    if dtype == torch.float32:
+        return F32
+    if dtype == torch.bfloat16:
+        return BF16
+    raise _lib.U3DError(f"u3d: unsupported dtype {dtype}")
+
+
+def require_device(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.U3DError("u3d: the HIP path needs ROCm device tensors (no CPU fallback; the CPU "
+                                "restatement lives in oracle/ and is test-only)")
+
+
+def round32(c):
+    return (c + 31) // 32 * 32
+
+
+def out_dim(d, k, s):
+    return (d + 2 * (k // 2) - k) // s + 1
+
+
+class _WS:
+    """Grow-only per-device scratch buffer (device memory owned by torch's caching allocator)."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, nbytes, device, slot=0):
+        key = (device, slot)
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+
+WS = _WS()
+
+
+# ------------------------------------------------------------------------------------------ weights
+def wstd_fwd(w, dtype, standardize=True, need_dgrad=True):
+    """Standardise (unet3D.py:21-26) and pack a [cout, cin, k, k, k] fp32 weight."""
+    require_device(w)
+    cout, cin, k = w.shape[0], w.shape[1], w.shape[2]
+    k3 = k * k * k
+    pf = torch.empty((k3, round32(cout), round32(cin)), dtype=dtype, device=w.device)
+    pd = torch.empty((k3, round32(cin), round32(cout)), dtype=dtype, device=w.device) if need_dgrad else None
+    st = torch.empty((cout, 2), dtype=torch.float32, device=w.device) if standardize else None
+    call("u3d_wstd_fwd", dt_code(dtype), w.data_ptr(), cout, cin, k, int(standardize), pf.data_ptr(), _ptr(pd),
+         _ptr(st), _stream())
+    return pf, pd, st
+
+
+def wstd_bwd(partials, nsplit, w, wstats, standardize, dw=None, accumulate=False):
+    cout, cin, k = w.shape[0], w.shape[1], w.shape[2]
+    if dw is None:
+        dw = torch.empty_like(w)
+        accumulate = False
+    call("u3d_wstd_bwd", partials.data_ptr(), nsplit, w.data_ptr(), _ptr(wstats), cout, cin, k, int(standardize),
+         dw.data_ptr(), int(accumulate), _stream())
+    return dw
+
+
+# ------------------------------------------------------------------------------------------ convs
+def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32=False):
+    """x: [n,d,h,w,cin] -> [n,od,oh,ow,cout]. gn = (stats, gamma, beta, groups) fuses GroupNorm+ReLU."""
+    require_device(x)
+    n, d, h, w_, cin = x.shape
+    od, oh, ow = out_dim(d, k, stride), out_dim(h, k, stride), out_dim(w_, k, stride)
+    y = torch.empty((n, od, oh, ow, cout), dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
+    st, ga, be, G = gn if gn is not None else (None, None, None, 0)
+    call("u3d_conv_fwd", dt_code(x.dtype), x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, k, stride, _ptr(st),
+         _ptr(ga), _ptr(be), G, _ptr(residual), _ptr(bias), y.data_ptr(), int(out_f32), _stream())
+    return y
+
+
+def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
+    n, d, h, w_ = in_shape
+    cout = dy.shape[-1]
+    dx = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
+    call("u3d_conv_dgrad", dt_code(dy.dtype), dy.data_ptr(), n, cout, wpk_dgrad.data_ptr(), cin, d, h, w_, k, stride,
+         dx.data_ptr(), _stream())
+    return dx
+
+
+def conv_wgrad(dy, x, k, stride, gn=None):
+    """Returns (partials fp32 [nsplit, k^3, cout_p, cin_p], nsplit)."""
+    n, d, h, w_, cin = x.shape
+    cout = dy.shape[-1]
+    ns = query("u3d_conv_wgrad_splits", n, cin, d, h, w_, cout, k, stride)
+    part = torch.empty((ns, k ** 3, round32(cout), round32(cin)), dtype=torch.float32, device=x.device)
+    st, ga, be, G = gn if gn is not None else (None, None, None, 0)
+    call("u3d_conv_wgrad", dt_code(x.dtype), dy.data_ptr(), x.data_ptr(), n, cin, d, h, w_, cout, k, stride, _ptr(st),
+         _ptr(ga), _ptr(be), G, part.data_ptr(), ns, _stream())
+    return part, ns
+
+
+def stem_fwd(x_ncdhw, wpk, cout, stride, dtype):
+    require_device(x_ncdhw)
+    n, cin, d, h, w_ = x_ncdhw.shape
+    od, oh, ow = out_dim(d, 3, stride), out_dim(h, 3, stride), out_dim(w_, 3, stride)
+    y = torch.empty((n, od, oh, ow, cout), dtype=dtype, device=x_ncdhw.device)
+    call("u3d_stem_fwd", dt_code(dtype), x_ncdhw.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, stride,
+         y.data_ptr(), _stream())
+    return y
+
+
+def stem_wgrad(dy, x_ncdhw, stride):
+    n, cin, d, h, w_ = x_ncdhw.shape
+    cout = dy.shape[-1]
+    ns = query("u3d_stem_wgrad_splits", n, d, h, w_, stride)
+    part = torch.empty((ns, 27, round32(cout), round32(cin)), dtype=torch.float32, device=dy.device)
+    call("u3d_stem_wgrad", dt_code(dy.dtype), dy.data_ptr(), x_ncdhw.data_ptr(), n, cin, d, h, w_, cout, stride,
+         part.data_ptr(), ns, _stream())
+    return part, ns
+
+
+# ------------------------------------------------------------------------------------------ GroupNorm
+def _gn_ws(n, c, v, device):
+    return WS.get(query("u3d_gn_workspace_bytes", n, c, v), device, slot=1)
+
+
+def gn_stats(x, groups):
+    n, c = x.shape[0], x.shape[-1]
+    v = x.numel() // (n * c)
+    st = torch.empty((n, groups, 2), dtype=torch.float32, device=x.device)
+    call("u3d_gn_stats", dt_code(x.dtype), x.data_ptr(), n, c, v, groups, st.data_ptr(),
+         _gn_ws(n, c, v, x.device).data_ptr(), _stream())
+    return st
+
+
+def gn_bwd(da, x, stats, gamma, beta, groups, dx=None, accumulate=False, dgamma=None, dbeta=None, acc_params=False):
+    n, c = x.shape[0], x.shape[-1]
+    v = x.numel() // (n * c)
+    if dx is None:
+        dx = torch.empty_like(x)
+        accumulate = False
+    call("u3d_gn_bwd", dt_code(x.dtype), da.data_ptr(), x.data_ptr(), n, c, v, groups, stats.data_ptr(),
+         gamma.data_ptr(), beta.data_ptr(), dx.data_ptr(), int(accumulate), _ptr(dgamma), _ptr(dbeta), int(acc_params),
+         _gn_ws(n, c, v, x.device).data_ptr(), _stream())
+    return dx
+
+
+# ------------------------------------------------------------------------------------------ upsample
+def upsample2x_add(x, skip=None):
+    n, d, h, w_, c = x.shape
+    y = torch.empty((n, 2 * d, 2 * h, 2 * w_, c), dtype=x.dtype, device=x.device)
+    call("u3d_upsample2x_add", dt_code(x.dtype), x.data_ptr(), n, c, d, h, w_, _ptr(skip), y.data_ptr(), _stream())
+    return y
+
+
+def upsample2x_bwd(dy, in_shape, dx=None, accumulate=False):
+    n, d, h, w_, c = in_shape
+    if dx is None:
+        dx = torch.empty(in_shape, dtype=dy.dtype, device=dy.device)
+        accumulate = False
+    call("u3d_upsample2x_bwd", dt_code(dy.dtype), dy.data_ptr(), n, c, d, h, w_, dx.data_ptr(), int(accumulate),
+         _stream())
+    return dx
+
+
+# ------------------------------------------------------------------------------------------ misc
+def add_(y, x):
+    call("u3d_add_inplace", dt_code(y.dtype), y.data_ptr(), x.data_ptr(), y.numel(), _stream())
+    return y
+
+
+def cast(x, dtype, pad_to=1):
+    """Convert dtype and zero-pad the channel (last) dim to a multiple of ``pad_to``."""
+    c = x.shape[-1]
+    cp = (c + pad_to - 1) // pad_to * pad_to
+    if x.dtype == dtype and cp == c:
+        return x
+    y = torch.empty(tuple(x.shape[:-1]) + (cp,), dtype=dtype, device=x.device)
+    call("u3d_cast", dt_code(x.dtype), x.data_ptr(), dt_code(dtype), y.data_ptr(), x.numel() // c, c, cp, _stream())
+    return y
+
+
+def channel_sum(x, out=None, accumulate=False):
+    c = x.shape[-1]
+    rows = x.numel() // c
+    if out is None:
+        out = torch.empty((c,), dtype=torch.float32, device=x.device)
+        accumulate = False
+    ws = WS.get(query("u3d_channel_sum_workspace_bytes", rows, c), x.device, slot=2)
+    call("u3d_channel_sum", dt_code(x.dtype), x.data_ptr(), rows, c, out.data_ptr(), int(accumulate), ws.data_ptr(),
+         _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------ loss / metric
+def partial_loss_fwd(logits, labels, weights, softmax=True, uce=True):
+    """logits fp32 [S, ..., C] NDHWC-contiguous, labels fp32 [S, ...] -> (loss fp32[1], sums fp64[C,4])."""
+    S, C = logits.shape[0], logits.shape[-1]
+    V = logits.numel() // (S * C)
+    sums = torch.empty((C, 4), dtype=torch.float64, device=logits.device)
+    loss = torch.empty((1,), dtype=torch.float32, device=logits.device)
+    ws = WS.get(query("u3d_loss_workspace_bytes", S, V, C), logits.device, slot=3)
+    call("u3d_partial_loss_fwd", logits.data_ptr(), labels.data_ptr(), S, V, C, int(softmax), weights.data_ptr(),
+         int(uce), sums.data_ptr(), loss.data_ptr(), ws.data_ptr(), _stream())
+    return loss, sums
+
+
+def partial_loss_bwd(logits, labels, weights, sums, grad_out, softmax=True, uce=True, out_dtype=torch.float32):
+    S, C = logits.shape[0], logits.shape[-1]
+    V = logits.numel() // (S * C)
+    dl = torch.empty(logits.shape, dtype=out_dtype, device=logits.device)
+    call("u3d_partial_loss_bwd", dt_code(out_dtype), logits.data_ptr(), labels.data_ptr(), S, V, C, int(softmax),
+         weights.data_ptr(), int(uce), sums.data_ptr(), grad_out.data_ptr(), dl.data_ptr(), _stream())
+    return dl
+
+
+def dice_metric(logits, labels, num_class, want_argmax=False):
+    """logits fp32 NDHWC [S, ..., C]; returns (metrics [num_class, 3] = dice/sens/prec, counts, argmax|None)."""
+    S, C = logits.shape[0], logits.shape[-1]
+    V = logits.numel() // (S * C)
+    counts = torch.empty((S, num_class, 3), dtype=torch.int64, device=logits.device)
+    metrics = torch.empty((num_class, 3), dtype=torch.float32, device=logits.device)
+    am = torch.empty(logits.shape[:-1], dtype=torch.int64, device=logits.device) if want_argmax else None
+    call("u3d_dice_metric", logits.data_ptr(), labels.data_ptr(), S, V, C, num_class, counts.data_ptr(),
+         metrics.data_ptr(), _ptr(am), _stream())
+    return metrics, counts, am

@@ -1,0 +1,245 @@
+"""Native executor for the reference U-Net trunks (unet3D.py): forward records a tape of backward closures,
+backward replays it in reverse. Every value is produced by a libu3d kernel; torch provides memory and the
+stream. Activations live NDHWC in the compute dtype (fp32 parity mode or bf16 fast mode) with fp32 master
+weights; weight standardisation is re-applied from the fp32 master each step (unet3D.py:21-26).
+
+Graph (reference unet3D.forward :1734-1806 / unet3D_baseline.forward :663-718 / unet3D_g.forward :1568-1623):
+  stem conv1 (or conv0 s2 -> conv1) -> layer0..4 (NoBottleneck :40-73) -> fusionConv (GN,ReLU,1^3)
+  -> 4 x [trilinear x2 + skip -> x{8,4,2,1}_resb] -> precls_conv (GN,ReLU,1^3+bias) [-> x2 upsample (unet3D_g)]
+"""
+from dataclasses import dataclass
+
+import torch
+
+from . import ops
+
+
+@dataclass(frozen=True)
+class TrunkCfg:
+    layers: tuple = (1, 2, 2, 2, 2)
+    groups: int = 16          # GroupNorm groups inside NoBottleneck / downsample
+    fusion_groups: int = 16
+    head_groups: int = 16
+    conv0: bool = False       # unet3D_g: stride-2 stem conv0 then a plain conv1
+    final_up: bool = False    # unet3D_g: x2 trilinear upsample of the logits
+    weight_std: bool = True
+
+
+class Act:
+    """An NDHWC activation, its cached GroupNorm statistics and its accumulated gradient."""
+    __slots__ = ("t", "stats", "grad")
+
+    def __init__(self, t):
+        self.t = t
+        self.stats = {}
+        self.grad = None
+
+
+class Tape:
+    def __init__(self, params, dtype, record):
+        self.P = params
+        self.dtype = dtype
+        self.record = record
+        self.packs = {}
+        self.pgrad = {}
+        self.ops = []
+        self.sink = None
+        self.std = True
+
+    # ------------------------------------------------------------------ helpers
+    def packed(self, key, standardize, need_dgrad=True):
+        if key not in self.packs:
+            self.packs[key] = ops.wstd_fwd(self.P[key + ".weight"], self.dtype, standardize,
+                                           need_dgrad and self.record)
+        return self.packs[key]
+
+    def stats(self, act, G):
+        if G not in act.stats:
+            act.stats[G] = ops.gn_stats(act.t, G)
+        return act.stats[G]
+
+    @staticmethod
+    def acc_grad(act, g):
+        if act.grad is None:
+            act.grad = g
+        else:
+            ops.add_(act.grad, g)
+
+    def grad_out(self, name, like):
+        """Destination of a parameter gradient: a DDP bucket view when data-parallel, else a fresh tensor."""
+        t = self.sink.out(name) if self.sink is not None else None
+        if t is None:
+            t = torch.empty_like(like)
+        self.pgrad[name] = t
+        return t
+
+    def grad_done(self, name):
+        if self.sink is not None:
+            self.sink.done(name)
+
+    # ------------------------------------------------------------------ ops
+    def stem(self, x, key, stride):
+        """conv with cin <= 4 from the fp32 NCDHW input volume (unet3D.py:1632 / :1514)."""
+        W = self.P[key + ".weight"]
+        pf, _, st = self.packed(key, self.std, need_dgrad=False)
+        out = Act(ops.stem_fwd(x, pf, W.shape[0], stride, self.dtype))
+        if self.record:
+            def bwd():
+                if out.grad is None:
+                    return
+                part, ns = ops.stem_wgrad(out.grad, x, stride)
+                ops.wstd_bwd(part, ns, W, st, self.std, dw=self.grad_out(key + ".weight", W))
+                self.grad_done(key + ".weight")
+            self.ops.append(bwd)
+        return out
+
+    def gn_conv(self, x, key, k, stride, gn_key=None, G=0, residual=None, bias=False, out_f32=False,
+                standardize=None):
+        """conv(relu(gn(x))) [+ residual] [+ bias] — Conv3d/conv3x3x3 :16-35 behind GN+ReLU :44-53."""
+        std = self.std if standardize is None else standardize
+        W = self.P[key + ".weight"]
+        cout, cin = W.shape[0], W.shape[1]
+        pf, pd, st = self.packed(key, std)
+        gn = None
+        if gn_key is not None:
+            gn = (self.stats(x, G), self.P[gn_key + ".weight"], self.P[gn_key + ".bias"], G)
+        b = self.P[key + ".bias"] if bias else None
+        y = ops.conv_fwd(x.t, pf, cout, k, stride, gn, residual.t if residual is not None else None, b, out_f32)
+        out = Act(y)
+        if self.record:
+            def bwd():
+                dy = out.grad
+                if dy is None:
+                    return
+                if bias:
+                    ops.channel_sum(dy, out=self.grad_out(key + ".bias", b))
+                    self.grad_done(key + ".bias")
+                if residual is not None:
+                    self.acc_grad(residual, dy)
+                dyT = ops.cast(dy, self.dtype, pad_to=8)  # GEMM operand: channels padded to 8 (2-class head)
+                part, ns = ops.conv_wgrad(dyT, x.t, k, stride, gn)
+                ops.wstd_bwd(part, ns, W, st, std, dw=self.grad_out(key + ".weight", W))
+                self.grad_done(key + ".weight")
+                dA = ops.conv_dgrad(dyT, pd, cin, x.t.shape[:4], k, stride)
+                if gn is not None:
+                    dg = self.grad_out(gn_key + ".weight", gn[1])
+                    db = self.grad_out(gn_key + ".bias", gn[2])
+                    x.grad = ops.gn_bwd(dA, x.t, gn[0], gn[1], gn[2], G, dx=x.grad,
+                                        accumulate=x.grad is not None, dgamma=dg, dbeta=db)
+                    self.grad_done(gn_key + ".weight")
+                    self.grad_done(gn_key + ".bias")
+                else:
+                    self.acc_grad(x, dA)
+            self.ops.append(bwd)
+        return out
+
+    def up_add(self, x, skip):
+        """upsamplex2 (trilinear, align_corners=False) + skip, unet3D.py:1646 / :1764-1783."""
+        out = Act(ops.upsample2x_add(x.t, skip.t if skip is not None else None))
+        if self.record:
+            def bwd():
+                dy = out.grad
+                if dy is None:
+                    return
+                if skip is not None:
+                    self.acc_grad(skip, dy)
+                x.grad = ops.upsample2x_bwd(dy, tuple(x.t.shape), dx=x.grad, accumulate=x.grad is not None)
+            self.ops.append(bwd)
+        return out
+
+    def block(self, x, pre, stride, G):
+        """NoBottleneck.forward, unet3D.py:56-73."""
+        h = self.gn_conv(x, pre + "conv1", 3, stride, gn_key=pre + "gn1", G=G)
+        if pre + "downsample.2.weight" in self.P:
+            r = self.gn_conv(x, pre + "downsample.2", 1, stride, gn_key=pre + "downsample.0", G=G)
+        else:
+            r = x
+        return self.gn_conv(h, pre + "conv2", 3, 1, gn_key=pre + "gn2", G=G, residual=r)
+
+    # ------------------------------------------------------------------ graph
+    def trunk(self, x, cfg):
+        self.std = cfg.weight_std
+        if cfg.conv0:
+            t = self.stem(x, "conv0", 2)
+            t = self.gn_conv(t, "conv1", 3, 1)
+        else:
+            t = self.stem(x, "conv1", 1)
+        skips = []
+        for i in range(5):
+            for b in range(cfg.layers[i]):
+                stride = 2 if (i > 0 and b == 0) else 1
+                t = self.block(t, f"layer{i}.{b}.", stride, cfg.groups)
+            skips.append(t)
+        f = self.gn_conv(t, "fusionConv.2", 1, 1, gn_key="fusionConv.0", G=cfg.fusion_groups)
+        bott = f
+        for name, s in zip(["x8_resb", "x4_resb", "x2_resb", "x1_resb"], [skips[3], skips[2], skips[1], skips[0]]):
+            u = self.up_add(f, s)
+            f = self.block(u, name + ".0.", 1, cfg.groups)
+        return f, bott
+
+    def head(self, f, cfg):
+        lg = self.gn_conv(f, "precls_conv.2", 1, 1, gn_key="precls_conv.0", G=cfg.head_groups, bias=True,
+                          out_f32=True, standardize=False)
+        if cfg.final_up:
+            lg = self.up_add(lg, None)
+        return lg
+
+    def backward(self, out_act, grad):
+        out_act.grad = grad
+        for fn in reversed(self.ops):
+            fn()
+        self.ops = []
+
+
+def compute_dtype(explicit=None):
+    """bf16 under torch.autocast('cuda') (the reference's --FP16 amp path), fp32 otherwise."""
+    if explicit is not None:
+        return explicit
+    if torch.is_autocast_enabled("cuda"):
+        return torch.bfloat16
+    return torch.float32
+
+
+class _TrunkFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg, dtype, names, x, *tensors):
+        from .ddp import current_sink
+        P = dict(zip(names, tensors))
+        tape = Tape(P, dtype, record=True)
+        tape.sink = current_sink()
+        if tape.sink is not None:
+            tape.sink.begin()
+        f, _ = tape.trunk(x, cfg)
+        lg = tape.head(f, cfg)
+        ctx.tape, ctx.out, ctx.names = tape, lg, names
+        return lg.t.permute(0, 4, 1, 2, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.permute(0, 2, 3, 4, 1)
+        if not g.is_contiguous():
+            g = g.contiguous()
+        tape = ctx.tape
+        tape.backward(ctx.out, g.float())
+        if tape.sink is not None:
+            tape.sink.finish()
+        grads = [tape.pgrad.get(n) for n in ctx.names]
+        ctx.tape = ctx.out = None
+        return (None, None, None, None, *grads)
+
+
+def run_trunk(cfg, x, named_params, dtype=None):
+    """Forward the trunk + classification head. Returns NCDHW-shaped fp32 logits (NDHWC storage)."""
+    dtype = compute_dtype(dtype)
+    ops.require_device(x)
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        x = x.float().contiguous()
+    names = [n for n, _ in named_params]
+    tensors = [p for _, p in named_params]
+    if torch.is_grad_enabled() and any(p.requires_grad for p in tensors):
+        return _TrunkFn.apply(cfg, dtype, names, x, *tensors)
+    with torch.no_grad():
+        tape = Tape(dict(zip(names, tensors)), dtype, record=False)
+        f, _ = tape.trunk(x, cfg)
+        lg = tape.head(f, cfg)
+        return lg.t.permute(0, 4, 1, 2, 3)

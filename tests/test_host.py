@@ -1,0 +1,183 @@
+"""CPU-side checks: the C-ABI library loads and exports every symbol include/u3d.h declares, the drop-in
+modules keep the reference's names / signatures / state_dict keys, the host logic (class weights, engine
+flags, DDP bucketing over gloo with world_size 2) behaves like the reference. No compute calls here."""
+import os
+import re
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO, golden
+
+
+def _header_symbols():
+    src = open(os.path.join(REPO, "include", "u3d.h")).read()
+    return sorted(set(re.findall(r"\b(u3d_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from u3d import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libu3d.so not built")
+    h = _lib.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(h, s), s
+        assert s in _lib.exported_symbols(), f"{s} missing from the ctypes signature table"
+    assert h.u3d_abi_version() == 1
+
+
+def test_header_compiles_as_c():
+    import subprocess
+    r = subprocess.run(["gcc", "-fsyntax-only", "-x", "c", os.path.join(REPO, "include", "u3d.h")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_state_dict_keys_match_reference():
+    import unet3D
+    for name, ctor in [("g3_baseline16_16.npz", lambda: unet3D.unet3D_baseline([1, 2, 2, 2, 2], 16, True)),
+                       ("g1_unet3d_dyn_32.npz", lambda: unet3D.UNet3D(2, True)),
+                       ("g2_unet3d_g_32.npz",
+                        lambda: unet3D.unet3D_g([1] * 5, num_classes=2, weight_std=True, init_filter=24, in_channel=2))]:
+        m = ctor()
+        assert [k for k, _ in m.named_parameters()] == list(golden(name)["gnames"])
+    m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], 16, True)
+    assert m.layer1[0].conv1.weight.shape == (64, 32, 3, 3, 3)
+    assert sum(p.numel() for p in m.parameters()) == 17286512  # 16-class trunk
+
+
+def test_unet3d_param_count():
+    import unet3D
+    assert sum(p.numel() for p in unet3D.UNet3D(2, True).parameters()) == 17329528  # SURVEY A8 probe
+
+
+def test_reference_names_exported():
+    import evaluate_amos
+    import unet3D
+    from loss_functions import loss_partial, losses
+    for n in ["unet3D_with_feam3", "get_style_discriminator_output", "norm_style_discriminator_output",
+              "deep_style_discriminator_output", "unet3D_with_deepsup", "unet3D_g", "UNet3D", "unet3D_with_eam",
+              "unet3D_with_eam_baseline", "unet3D_with_feam2", "unet3D_baseline", "Conv3d", "conv3x3x3",
+              "NoBottleneck"]:
+        assert hasattr(unet3D, n), n
+    for n in ["DiceLoss", "EDiceLoss_partial", "EDiceLoss_full", "EDiceLoss_full2"]:
+        assert hasattr(loss_partial, n)
+    assert hasattr(losses, "get_loss")
+    for n in ["dice_score", "spec_score", "senc_score", "get_dice", "predict_sliding"]:
+        assert hasattr(evaluate_amos, n)
+
+
+def test_cpu_forward_raises_not_falls_back():
+    import unet3D
+    from u3d import U3DError
+    m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], 16, True)
+    with pytest.raises(U3DError):
+        m(torch.zeros(1, 1, 16, 16, 16))
+
+
+def test_class_weights_quirks():
+    from u3d.loss import class_weights
+    w = class_weights([torch.tensor([0, 1, 1, 0, 1]), torch.tensor([1, 1, 1, 1, 1])], 4, "cpu")
+    assert w.tolist() == [0.0, 1.0, 1.0, 0.0]  # mask[0] only, truncated to C
+    assert class_weights(None, 3, "cpu").tolist() == [1.0, 1.0, 1.0]
+    with pytest.raises(IndexError):
+        class_weights([torch.ones(15)], 16, "cpu")
+
+
+def test_dice_score_helpers_match_oracle():
+    from evaluate_amos import dice_score, senc_score, spec_score
+    rng = np.random.default_rng(0)
+    p = torch.from_numpy(rng.random((2, 1000)) > 0.5)
+    t = torch.from_numpy(rng.random((2, 1000)) > 0.7)
+    num = (p & t).sum(1).double()
+    np.testing.assert_allclose(float(dice_score(p, t)), (2 * num / (p.sum(1) + t.sum(1) + 1)).mean().item(), rtol=1e-6)
+    np.testing.assert_allclose(float(senc_score(p, t)), (num / (t.sum(1) + 1)).mean().item(), rtol=1e-6)
+    np.testing.assert_allclose(float(spec_score(p, t)), (num / (p.sum(1) + 1)).mean().item(), rtol=1e-6)
+
+
+def test_engine_flags_and_single_process():
+    import argparse
+    import engine
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch_size", type=int, default=2)
+    import sys
+    old = sys.argv
+    sys.argv = ["x", "-d", "0"]
+    try:
+        with engine.Engine(custom_parser=p) as e:
+            assert e.args.devices == "0" and e.world_size == 1 and not e.distributed
+            assert float(e.all_reduce_tensor(torch.tensor([1.0, 3.0]))) == 2.0
+            m = torch.nn.Linear(2, 2)
+            w = e.data_parallel(m)
+            assert w.module is m
+    finally:
+        sys.argv = old
+
+
+def test_lr_poly():
+    import utils
+    opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=1.0)
+    lr = utils.adjust_learning_rate(opt, 10, 0.01, 100, 0.9)
+    assert abs(lr - 0.01 * (0.9 ** 0.9)) < 1e-12 and opt.param_groups[0]["lr"] == lr
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _ddp_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from u3d.ddp import GradBucketer, U3DDataParallel
+    torch.manual_seed(rank)
+    params = [(f"p{i}", torch.nn.Parameter(torch.randn(n))) for i, n in enumerate([5, 300, 7, 1000, 3])]
+    b = GradBucketer(params, bucket_mb=0.002)  # ~524 floats per bucket -> several buckets
+    assert len(b.buckets) >= 3
+    b.begin()
+    for n, p in reversed(params):
+        if n == "p2":
+            continue  # never produced -> zero-filled, still reduced
+        b.out(n).fill_(float(rank + 1) * (1 + int(n[1:])))
+        b.done(n)
+    b.finish()
+    vals = {n: b.view(n).clone() for n, _ in params}
+    m = torch.nn.Linear(3, 3)
+    torch.manual_seed(100 + rank)
+    m.reset_parameters()
+    U3DDataParallel(m)
+    q.put((rank, {k: v.tolist() for k, v in vals.items()}, m.weight.detach().clone().tolist(), True))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_bucketer_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=60) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort()
+    for rank, vals, w, _ in out:
+        for n, v in vals.items():
+            i = int(n[1:])
+            expect = 0.0 if n == "p2" else (1 + 2) / 2 * (1 + i)  # mean over ranks of (rank+1)*(1+i)
+            assert np.allclose(v, expect), (n, v[:3], expect)
+    assert np.allclose(out[0][2], out[1][2])  # init broadcast: identical weights on both ranks
