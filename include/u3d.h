@@ -71,6 +71,13 @@ int u3d_conv_wgrad(int dtype, const void* dy, const void* x, int n, int cin, int
                    int ksize, int stride, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
                    int gn_groups, float* partials, int nsplit, u3d_stream_t stream);
 
+/* bf16 3^3 weight gradient in halo-brick form (ds_read_b64_tr_b16 operands, all 27 taps per workgroup);
+ * same partial-slab output as u3d_conv_wgrad (nsplit from u3d_conv_wgrad_brick_splits). */
+int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, int cout, int stride);
+int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout, int stride,
+                         const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                         float* partials, int nsplit, u3d_stream_t stream);
+
 /* Stem conv with cin <= 4 (conv1 1->32, unet3D.py:1632; conv0 2->f stride 2, :1514): fp32 NCDHW input,
  * direct VALU conv (K = 27*cin is too short for MFMA), NDHWC output. */
 int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,

@@ -21,6 +21,8 @@ _SIGS = {
     "u3d_conv_dgrad": [I, P, I, I, P, I, I, I, I, I, I, P, P],
     "u3d_conv_wgrad_splits": [I, I, I, I, I, I, I, I],
     "u3d_conv_wgrad": [I, P, P, I, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
+    "u3d_conv_wgrad_brick_splits": [I, I, I, I, I, I, I],
+    "u3d_conv_wgrad_brick": [P, P, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_stem_fwd": [I, P, I, I, I, I, I, P, I, I, P, P],
     "u3d_stem_wgrad_splits": [I, I, I, I, I],
     "u3d_stem_wgrad": [I, P, P, I, I, I, I, I, I, I, P, I, P],

@@ -101,13 +101,24 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     return dx
 
 
-def conv_wgrad(dy, x, k, stride, gn=None):
-    """Returns (partials fp32 [nsplit, k^3, cout_p, cin_p], nsplit)."""
+USE_BRICK_WGRAD = True
+
+
+def conv_wgrad(dy, x, k, stride, gn=None, brick=None):
+    """Returns (partials fp32 [nsplit, k^3, cout_p, cin_p], nsplit). bf16 3^3 convs use the halo-brick kernel."""
     n, d, h, w_, cin = x.shape
     cout = dy.shape[-1]
+    st, ga, be, G = gn if gn is not None else (None, None, None, 0)
+    if brick is None:
+        brick = USE_BRICK_WGRAD and x.dtype == torch.bfloat16 and k == 3
+    if brick:
+        ns = query("u3d_conv_wgrad_brick_splits", n, cin, d, h, w_, cout, stride)
+        part = torch.empty((ns, 27, round32(cout), round32(cin)), dtype=torch.float32, device=x.device)
+        call("u3d_conv_wgrad_brick", dy.data_ptr(), x.data_ptr(), n, cin, d, h, w_, cout, stride, _ptr(st), _ptr(ga),
+             _ptr(be), G, part.data_ptr(), ns, _stream())
+        return part, ns
     ns = query("u3d_conv_wgrad_splits", n, cin, d, h, w_, cout, k, stride)
     part = torch.empty((ns, k ** 3, round32(cout), round32(cin)), dtype=torch.float32, device=x.device)
-    st, ga, be, G = gn if gn is not None else (None, None, None, 0)
     call("u3d_conv_wgrad", dt_code(x.dtype), dy.data_ptr(), x.data_ptr(), n, cin, d, h, w_, cout, k, stride, _ptr(st),
          _ptr(ga), _ptr(be), G, part.data_ptr(), ns, _stream())
     return part, ns
