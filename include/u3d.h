@@ -55,21 +55,30 @@ int u3d_wstd_bwd(float* dwpk_partials, int nsplit, const float* w, const float* 
  * apply + ReLU runs in the operand prologue (zero padding stays zero). residual (same layout as y) is
  * added in the epilogue (NoBottleneck `out + residual`, unet3D.py:71); bias (fp32 [cout]) too.
  * y_f32 != 0 writes fp32 output (logit head) whatever dtype is. ksize in {1,3}; stride in {1,2};
- * cin % 8 == 0 (use u3d_stem_fwd for cin <= 4). */
+ * cin % 8 == 0 (use u3d_stem_fwd for cin <= 4). ws (nullable, ws_bytes) holds fp32 split-K slabs for
+ * deep small-volume layers whose output tiles cannot fill the chip; results are identical either way up
+ * to fp32 summation order. */
 int u3d_conv_fwd(int dtype, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                  int ksize, int stride, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
-                 int gn_groups, const void* residual, const float* bias, void* y, int y_f32,
-                 u3d_stream_t stream);
+                 int gn_groups, const void* residual, const float* bias, void* y, int y_f32, float* ws,
+                 long long ws_bytes, u3d_stream_t stream);
 /* Data gradient: dA = conv_transpose(dy, W_hat) into dA [n][d][h][w][cin] (overwritten), where (d,h,w)
  * is the forward INPUT grid. Stride-2 layers run as 8 parity-class dense sub-convolutions. */
 int u3d_conv_dgrad(int dtype, const void* dy, int n, int cout, const void* wpk_dgrad, int cin, int d, int h,
-                   int w, int ksize, int stride, void* dx, u3d_stream_t stream);
+                   int w, int ksize, int stride, void* dx, float* ws, long long ws_bytes, u3d_stream_t stream);
 /* Weight gradient partial slabs: partials[s][t][co][ci] = sum over voxel split s of dy * A, with
  * A = relu(gn(x)) recomputed in the prologue (same gn_* as the forward call). */
 int u3d_conv_wgrad_splits(int n, int cin, int d, int h, int w, int cout, int ksize, int stride);
 int u3d_conv_wgrad(int dtype, const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout,
                    int ksize, int stride, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
                    int gn_groups, float* partials, int nsplit, u3d_stream_t stream);
+
+/* bf16 32->32 3^3 stride-1 conv (cin = cout = 32; the full-resolution layers) in halo-brick form with the
+ * weights held in registers: flip=0 forward (wpk = forward pack, optional GN+ReLU prologue and residual),
+ * flip=1 data gradient (wpk = data-grad pack, no prologue). Same results as u3d_conv_fwd/_dgrad; n <= 16. */
+int u3d_conv32_brick(int flip, const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
+                     const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
+                     u3d_stream_t stream);
 
 /* bf16 3^3 weight gradient in halo-brick form (ds_read_b64_tr_b16 operands, all 27 taps per workgroup);
  * same partial-slab output as u3d_conv_wgrad (nsplit from u3d_conv_wgrad_brick_splits). */

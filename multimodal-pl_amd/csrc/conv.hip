@@ -30,6 +30,8 @@ struct Geom {
   int si;
   int ntaps;
   int gn_groups;
+  int nsamp, nsplit, kps;  // samples; split-K count and K-steps per split
+  float* slab;             // split-K partials [nsplit][nsamp][Mq][cout] (nsplit > 1)
   int tap_w[27];
   signed char tap_d[27], tap_h[27], tap_x[27];
 };
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(NTHR) void igemm_kernel(const T* __restrict__ x, co
   auto Bs = [&](int b) -> char* { return smem + 2 * BM * ROWB + b * (BN * ROWB); };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n = blockIdx.z;
+  const int n = blockIdx.z / g.nsplit, split = blockIdx.z % g.nsplit;
   const int bm0 = blockIdx.x * BM, bn0 = blockIdx.y * BN;
   const int Mq = g.qd * g.qh * g.qw;
   const bool has_gn = gstat != nullptr;
@@ -240,15 +242,19 @@ __global__ __launch_bounds__(NTHR) void igemm_kernel(const T* __restrict__ x, co
   const int wr = wave / WN, wc = wave % WN;
   const int arow0 = wr * (BM / WM), brow0 = wc * (BN / WN);
 
+  // split-K: this block covers K-steps [kk0, kk1)
+  const int kk0 = split * g.kps, kk1 = min(nk, kk0 + g.kps);
   __syncthreads();  // gn table
-  gload(0);
-  swrite(0, 0);
+  if (kk0 < kk1) {
+    gload(kk0);
+    swrite(kk0, 0);
+  }
   __syncthreads();
-  for (int kk = 0; kk < nk; ++kk) {
-    const int cur = kk & 1;
-    if (kk + 1 < nk) gload(kk + 1);
+  for (int kk = kk0; kk < kk1; ++kk) {
+    const int cur = (kk - kk0) & 1;
+    if (kk + 1 < kk1) gload(kk + 1);
     mfma_step<T, TM, TN>(As(cur), Bs(cur), arow0, brow0, lane, acc);
-    if (kk + 1 < nk) swrite(kk + 1, cur ^ 1);
+    if (kk + 1 < kk1) swrite(kk + 1, cur ^ 1);
     __syncthreads();
   }
 
@@ -266,6 +272,10 @@ __global__ __launch_bounds__(NTHR) void igemm_kernel(const T* __restrict__ x, co
       for (int i = 0; i < 16; ++i) {
         const int q = bm0 + arow0 + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
         if (q >= Mq) continue;
+        if (g.nsplit > 1) {  // fp32 partial slab [split][n][q][cout]; reduce kernel applies the epilogue
+          g.slab[(((long long)split * g.nsamp + n) * Mq + q) * g.cout + co] = acc[tm][tn][i];
+          continue;
+        }
         long long ov;
         if (g.so == 1) {
           ov = q;
@@ -481,21 +491,67 @@ static void fill_taps(Geom& g, int ksize, bool transpose) {
   g.ntaps = t;
 }
 
+// split-K epilogue: y[map(n, q)][co] = sum_s slab[s][n][q][co] (+ bias) (+ residual)
 template <typename T, typename TO>
-static int launch_igemm(const Geom& g, int n, const T* x, const T* wpk, TO* y, const T* res, const float* bias,
-                        const float* st, const float* ga, const float* be, hipStream_t s) {
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(Geom g, const T* __restrict__ res,
+                                                           const float* __restrict__ bias, TO* __restrict__ y) {
+  const int Mq = g.qd * g.qh * g.qw;
+  const long long per = (long long)g.nsamp * Mq * g.cout;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < per; i += (long long)gridDim.x * 256) {
+    const int co = (int)(i % g.cout);
+    const long long nq = i / g.cout;
+    const int q = (int)(nq % Mq), n = (int)(nq / Mq);
+    float v = bias ? bias[co] : 0.f;
+    for (int s = 0; s < g.nsplit; ++s) v += g.slab[s * per + i];
+    long long ov;
+    if (g.so == 1) {
+      ov = q;
+    } else {
+      int qw_ = q % g.qw, t = q / g.qw;
+      int qh_ = t % g.qh, qd_ = t / g.qh;
+      ov = ((long long)(qd_ * g.so + g.pod) * g.oh + (qh_ * g.so + g.poh)) * g.ow + (qw_ * g.so + g.pow_);
+    }
+    const long long off = ((long long)n * g.od * g.oh * g.ow + ov) * g.cout + co;
+    if (res) v += to_f(res[off]);
+    y[off] = from_f<TO>(v);
+  }
+}
+
+template <typename T, typename TO>
+static int launch_igemm(Geom g, int n, const T* x, const T* wpk, TO* y, const T* res, const float* bias,
+                        const float* st, const float* ga, const float* be, float* ws, long long ws_bytes,
+                        hipStream_t s) {
   const int Mq = g.qd * g.qh * g.qw;
   if (Mq <= 0) return U3D_OK;
-  if (g.cout_p <= 32) {
-    dim3 grid(cdiv(Mq, 128), cdiv(g.cout, 32), n);
+  const int BN = g.cout_p <= 32 ? 32 : 64;
+  const long long tiles = (long long)cdiv(Mq, 128) * cdiv(g.cout, BN) * n;
+  const int nk = g.ntaps * (g.cin_p / BK);
+  // split K when the output tiles cannot fill the 256 CUs (deep, small-volume layers)
+  int ns = 1;
+  if (ws && tiles < 256 && nk >= 8) {
+    ns = (int)std::min<long long>(nk / 4, (512 + tiles - 1) / tiles);
+    const long long slab1 = (long long)n * Mq * g.cout * 4;
+    while (ns > 1 && ns * slab1 > ws_bytes) --ns;
+  }
+  g.nsamp = n;
+  g.nsplit = ns;
+  g.kps = (nk + ns - 1) / ns;
+  g.slab = ns > 1 ? ws : nullptr;
+  if (BN == 32) {
+    dim3 grid(cdiv(Mq, 128), cdiv(g.cout, 32), n * ns);
     hipLaunchKernelGGL((igemm_kernel<T, TO, 128, 32, 4, 1>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st, ga,
                        be, g);
   } else {
-    dim3 grid(cdiv(Mq, 128), cdiv(g.cout, 64), n);
+    dim3 grid(cdiv(Mq, 128), cdiv(g.cout, 64), n * ns);
     hipLaunchKernelGGL((igemm_kernel<T, TO, 128, 64, 2, 2>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st, ga,
                        be, g);
   }
-  return check_launch("igemm_kernel");
+  int rc = check_launch("igemm_kernel");
+  if (rc || ns == 1) return rc;
+  const long long per = (long long)n * Mq * g.cout;
+  const int nb = (int)std::min<long long>(4096, (per + 255) / 256);
+  hipLaunchKernelGGL((splitk_reduce_kernel<T, TO>), dim3(nb), dim3(256), 0, s, g, res, bias, y);
+  return check_launch("splitk_reduce_kernel");
 }
 
 static int out_dim(int d, int k, int s) { return (d + 2 * (k / 2) - k) / s + 1; }
@@ -507,7 +563,7 @@ using namespace u3d;
 extern "C" int u3d_conv_fwd(int dtype, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                             int ksize, int stride, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
                             int gn_groups, const void* residual, const float* bias, void* y, int y_f32,
-                            u3d_stream_t stream) {
+                            float* ws, long long ws_bytes, u3d_stream_t stream) {
   U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "conv_fwd: bad dtype %d", dtype);
   U3D_REQUIRE(ksize == 1 || ksize == 3, "conv_fwd: ksize %d unsupported", ksize);
   U3D_REQUIRE(stride == 1 || stride == 2, "conv_fwd: stride %d unsupported", stride);
@@ -533,16 +589,17 @@ extern "C" int u3d_conv_fwd(int dtype, const void* x, int n, int cin, int d, int
   if (dtype == U3D_BF16) {
     if (y_f32)
       return launch_igemm<bf16, float>(g, n, (const bf16*)x, (const bf16*)wpk, (float*)y, nullptr, bias, gn_stats,
-                                       gn_gamma, gn_beta, s);
+                                       gn_gamma, gn_beta, ws, ws_bytes, s);
     return launch_igemm<bf16, bf16>(g, n, (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, bias,
-                                    gn_stats, gn_gamma, gn_beta, s);
+                                    gn_stats, gn_gamma, gn_beta, ws, ws_bytes, s);
   }
   return launch_igemm<float, float>(g, n, (const float*)x, (const float*)wpk, (float*)y, (const float*)residual, bias,
-                                    gn_stats, gn_gamma, gn_beta, s);
+                                    gn_stats, gn_gamma, gn_beta, ws, ws_bytes, s);
 }
 
 extern "C" int u3d_conv_dgrad(int dtype, const void* dy, int n, int cout, const void* wpk_dgrad, int cin, int d,
-                              int h, int w, int ksize, int stride, void* dx, u3d_stream_t stream) {
+                              int h, int w, int ksize, int stride, void* dx, float* ws, long long ws_bytes,
+                              u3d_stream_t stream) {
   U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "conv_dgrad: bad dtype %d", dtype);
   U3D_REQUIRE(ksize == 1 || ksize == 3, "conv_dgrad: ksize %d unsupported", ksize);
   U3D_REQUIRE(stride == 1 || stride == 2, "conv_dgrad: stride %d unsupported", stride);
@@ -563,9 +620,9 @@ extern "C" int u3d_conv_dgrad(int dtype, const void* dy, int n, int cout, const 
   auto run = [&](const Geom& gg) -> int {
     if (dtype == U3D_BF16)
       return launch_igemm<bf16, bf16>(gg, n, (const bf16*)dy, (const bf16*)wpk_dgrad, (bf16*)dx, nullptr, nullptr,
-                                      nullptr, nullptr, nullptr, s);
+                                      nullptr, nullptr, nullptr, ws, ws_bytes, s);
     return launch_igemm<float, float>(gg, n, (const float*)dy, (const float*)wpk_dgrad, (float*)dx, nullptr, nullptr,
-                                      nullptr, nullptr, nullptr, s);
+                                      nullptr, nullptr, nullptr, ws, ws_bytes, s);
   };
   if (stride == 1) {
     g.qd = d; g.qh = h; g.qw = w;

@@ -1,0 +1,216 @@
+// 32 -> 32 channel 3^3 stride-1 convolution (forward and data gradient), bf16, halo-brick form (gfx950).
+//
+// These convolutions (layer0, x1_resb at the full 96^3 resolution) carry ~51% of the U-Net's FLOPs
+// (SURVEY §2.1). As a GEMM they are M = voxels (1.77M) x N = 32 x K = 27*32, so each A fragment is used by
+// exactly one 32-wide MFMA column block; the design keeps the MFMA pipe fed from LDS:
+//   * a persistent workgroup of 8 waves (two per SIMD) walks output bricks of 2 x 8 x 32 voxels;
+//   * per brick the input halo (4 x 10 x 34 voxels x 32 ch) is staged once into LDS with the GroupNorm +
+//     ReLU prologue applied once per element (not once per tap) and zero padding after it; the next brick's
+//     halo is prefetched into registers while the MFMAs run;
+//   * the weights of all 27 taps (55 KB) stay in LDS for the workgroup's lifetime;
+//   * LDS images are "chunk-planar": plane c holds 16 B (8 channels) of every row, so the 32 consecutive
+//     rows of an MFMA A fragment are 512 contiguous bytes (conflict-free ds_read_b128) and every tap's
+//     window is the same per-lane address plus a compile-time offset;
+//   * each wave computes two 32-voxel w-rows x 32 co; the B fragment is shared by both.
+// Data gradient = the same kernel with the flipped tap offsets and the [t][ci][co] weight pack.
+// Reference: F.conv3d in Conv3d.forward (unet3D.py:27) via NoBottleneck (:56-73) and its autograd.
+#include "common.h"
+
+namespace u3d {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+constexpr int CB_BD = 2, CB_BH = 8, CB_BW = 32;
+constexpr int CB_HD = CB_BD + 2, CB_HH = CB_BH + 2, CB_HW = CB_BW + 2;
+constexpr int CB_NH = CB_HD * CB_HH * CB_HW;            // 1360 halo rows
+constexpr int CB_NWR = 27 * 32;                          // weight rows (t, co)
+constexpr int CB_CHUNKS = CB_NH * 4;                     // 16-B chunks per halo
+constexpr int CB_NT = 512;
+constexpr int CB_LD = (CB_CHUNKS + CB_NT - 1) / CB_NT;   // 11 prefetch loads per thread
+constexpr int CB_MAXN = 16;
+
+struct CBGeom {
+  int n, d, h, w;
+  int nbd, nbh, nbw;
+  int nbricks;
+  int gn_groups;
+};
+
+template <bool FLIP>
+__global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
+                                                               bf16* __restrict__ y, const bf16* __restrict__ res,
+                                                               const float* __restrict__ gstat,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, CBGeom g) {
+  __shared__ __attribute__((aligned(16))) char hal[4 * CB_NH * 16];
+  __shared__ __attribute__((aligned(16))) char wts[4 * CB_NWR * 16];
+  __shared__ float gsc[CB_MAXN][32], gsh[CB_MAXN][32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const bool has_gn = gstat != nullptr;
+  if (has_gn) {
+    const int cpg = 32 / g.gn_groups;
+    for (int i = tid; i < g.n * 32; i += CB_NT) {
+      const int nn = i >> 5, c = i & 31, gg = c / cpg;
+      const float mean = gstat[(nn * g.gn_groups + gg) * 2], rstd = gstat[(nn * g.gn_groups + gg) * 2 + 1];
+      const float s = rstd * gamma[c];
+      gsc[nn][c] = s;
+      gsh[nn][c] = beta[c] - mean * s;
+    }
+  }
+  // weights: plane ch, row t*32 + co
+  for (int i = tid; i < CB_NWR * 4; i += CB_NT) {
+    const int ch = i / CB_NWR, row = i % CB_NWR;
+    *reinterpret_cast<u32x4*>(wts + (ch * CB_NWR + row) * 16) =
+        *reinterpret_cast<const u32x4*>(wpk + row * 32 + ch * 8);
+  }
+
+  u32x4 pre[CB_LD];
+  auto brick_origin = [&](int b, int& nn, int& d0, int& h0, int& w0) {
+    int t = b;
+    const int bw_ = t % g.nbw; t /= g.nbw;
+    const int bh_ = t % g.nbh; t /= g.nbh;
+    const int bd_ = t % g.nbd;
+    nn = t / g.nbd;
+    d0 = bd_ * CB_BD; h0 = bh_ * CB_BH; w0 = bw_ * CB_BW;
+  };
+  // chunk ci -> (plane ch = ci / NH, halo row = ci % NH): consecutive threads fill consecutive rows of a plane
+  auto prefetch = [&](int b) {
+    int nn, d0, h0, w0;
+    brick_origin(b, nn, d0, h0, w0);
+#pragma unroll
+    for (int i = 0; i < CB_LD; ++i) {
+      const int ci = tid + i * CB_NT;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (ci < CB_CHUNKS) {
+        const int ch = ci / CB_NH, row = ci % CB_NH;
+        const int hw = row % CB_HW, hh = (row / CB_HW) % CB_HH, hd = row / (CB_HW * CB_HH);
+        const int zd = d0 - 1 + hd, zh = h0 - 1 + hh, zw = w0 - 1 + hw;
+        if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w)
+          v = *reinterpret_cast<const u32x4*>(x + ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * 32 + ch * 8);
+      }
+      pre[i] = v;
+    }
+  };
+  auto commit = [&](int b) {
+    int nn, d0, h0, w0;
+    brick_origin(b, nn, d0, h0, w0);
+#pragma unroll
+    for (int i = 0; i < CB_LD; ++i) {
+      const int ci = tid + i * CB_NT;
+      if (ci < CB_CHUNKS) {
+        const int ch = ci / CB_NH, row = ci % CB_NH;
+        u32x4 v = pre[i];
+        if (has_gn) {
+          const int hw = row % CB_HW, hh = (row / CB_HW) % CB_HH, hd = row / (CB_HW * CB_HH);
+          const int zd = d0 - 1 + hd, zh = h0 - 1 + hh, zw = w0 - 1 + hw;
+          if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w) {
+            float f[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              f[2 * e] = __uint_as_float(v[e] << 16);
+              f[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = fmaxf(0.f, fmaf(f[e], gsc[nn][ch * 8 + e], gsh[nn][ch * 8 + e]));
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              v[e] = (uint32_t)from_f<bf16>(f[2 * e]) | ((uint32_t)from_f<bf16>(f[2 * e + 1]) << 16);
+          }
+        }
+        *reinterpret_cast<u32x4*>(hal + (ch * CB_NH + row) * 16) = v;
+      }
+    }
+  };
+
+  int b = blockIdx.x;
+  if (b >= g.nbricks) return;
+  __syncthreads();  // gn tables
+  prefetch(b);
+  commit(b);
+  __syncthreads();
+  // per-lane fragment bases: A row of tap (0,0,0) for w-row tm: ((tm)*HH + wave)*HW + r ; plane (2s + h)
+  const char* abase = hal + (h * CB_NH + wave * CB_HW + r) * 16;
+  const char* bbase = wts + (h * CB_NWR + r) * 16;
+  for (; b < g.nbricks; b += gridDim.x) {
+    const int bn = b + gridDim.x;
+    const bool more = bn < g.nbricks;
+    prefetch(more ? bn : b);  // unconditional: keeps the prefetch registers phi-free (no copies, no early wait)
+    int nn, d0, h0, w0;
+    brick_origin(b, nn, d0, h0, w0);
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc0[e] = acc1[e] = 0.f;
+    // 54 steps (tap t, k16 half s); fragments of step i+1 are read while step i's MFMAs run
+    auto aoff = [](int st) {
+      const int t = st >> 1, s = st & 1;
+      const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
+      const int od = FLIP ? 2 - td : td, oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
+      return ((od * CB_HH + oh) * CB_HW + ow) * 16 + 2 * s * CB_NH * 16;
+    };
+    auto boff = [](int st) { return (2 * (st & 1) * CB_NWR + (st >> 1) * 32) * 16; };
+    bf16x8 ca0 = *reinterpret_cast<const bf16x8*>(abase + aoff(0));
+    bf16x8 ca1 = *reinterpret_cast<const bf16x8*>(abase + aoff(0) + CB_HH * CB_HW * 16);
+    bf16x8 cb = *reinterpret_cast<const bf16x8*>(bbase + boff(0));
+#pragma unroll
+    for (int st = 0; st < 54; ++st) {
+      bf16x8 na0 = ca0, na1 = ca1, nb = cb;
+      if (st + 1 < 54) {
+        na0 = *reinterpret_cast<const bf16x8*>(abase + aoff(st + 1));
+        na1 = *reinterpret_cast<const bf16x8*>(abase + aoff(st + 1) + CB_HH * CB_HW * 16);
+        nb = *reinterpret_cast<const bf16x8*>(bbase + boff(st + 1));
+      }
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ca0, cb, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ca1, cb, acc1, 0, 0, 0);
+      ca0 = na0;
+      ca1 = na1;
+      cb = nb;
+    }
+    __syncthreads();  // all waves done reading the halo before it is overwritten
+    if (more) commit(bn);
+    // epilogue: lane column co = r; rows w = (i&3) + 8(i>>2) + 4h of w-row (d0+tm, h0+wave)
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+      const int zd = d0 + tm, zh = h0 + wave;
+      if (zd < g.d && zh < g.h) {
+        const long long rowbase = (((long long)nn * g.d + zd) * g.h + zh) * g.w;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int zw = w0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (zw < g.w) {
+            const long long off = (rowbase + zw) * 32 + r;
+            float v = tm ? acc1[i] : acc0[i];
+            if (res) v += to_f(res[off]);
+            y[off] = from_f<bf16>(v);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace u3d
+
+using namespace u3d;
+
+extern "C" int u3d_conv32_brick(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
+                                const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                                const void* residual, void* y, u3d_stream_t stream) {
+  U3D_REQUIRE(x && wpk && y && n >= 1 && n <= CB_MAXN, "conv32_brick: bad args (n <= %d)", CB_MAXN);
+  U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0), "conv32_brick: bad GN");
+  CBGeom g{};
+  g.n = n; g.d = d; g.h = h; g.w = w;
+  g.nbd = cdiv(d, CB_BD); g.nbh = cdiv(h, CB_BH); g.nbw = cdiv(w, CB_BW);
+  g.nbricks = n * g.nbd * g.nbh * g.nbw;
+  g.gn_groups = gn_groups;
+  const int grid = std::min(g.nbricks, 256);
+  hipStream_t s = (hipStream_t)stream;
+  if (flip)
+    hipLaunchKernelGGL(conv32_brick_kernel<true>, dim3(grid), dim3(CB_NT), 0, s, (const bf16*)x, (const bf16*)wpk,
+                       (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
+  else
+    hipLaunchKernelGGL(conv32_brick_kernel<false>, dim3(grid), dim3(CB_NT), 0, s, (const bf16*)x, (const bf16*)wpk,
+                       (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
+  return check_launch("conv32_brick_kernel");
+}

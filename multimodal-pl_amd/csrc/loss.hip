@@ -5,6 +5,7 @@
 // the whole batch (the reference sums every sample together, :24-36), combined in fp64; the scalar loss
 // is formed on the device (no host sync: the reference's per-class .item() at :55 is dropped).
 // Backward is one elementwise pass: dL/dp from the sums, then the softmax (or sigmoid) Jacobian.
+// Class counts the models use (2, 8, 14, 16) are compile-time so every per-voxel array stays in registers.
 #include "common.h"
 
 namespace u3d {
@@ -12,30 +13,38 @@ namespace u3d {
 constexpr int LT = 256;
 constexpr int CMAX = 32;
 
-__device__ __forceinline__ void probs(const float* __restrict__ lg, int C, int softmax, float (&p)[CMAX]) {
-  if (softmax) {
+// softmax == 1: softmax, 0: sigmoid, 2: identity (inputs are probabilities)
+template <int NC>
+__device__ __forceinline__ void probs(const float* __restrict__ lg, int C, int softmax, float (&p)[NC]) {
+  if constexpr (NC % 4 == 0 && NC <= 16) {
+#pragma unroll
+    for (int c = 0; c < NC; c += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(lg + c);
+      p[c] = v[0]; p[c + 1] = v[1]; p[c + 2] = v[2]; p[c + 3] = v[3];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) p[c] = c < C ? lg[c] : 0.f;
+  }
+  if (softmax == 1) {
     float m = -INFINITY;
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
-      if (c < C) m = fmaxf(m, lg[c]);
+    for (int c = 0; c < NC; ++c)
+      if (c < C) m = fmaxf(m, p[c]);
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) {
-        p[c] = expf(lg[c] - m);
+        p[c] = expf(p[c] - m);
         s += p[c];
       }
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) p[c] = p[c] / s;
   } else if (softmax == 0) {
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
-      if (c < C) p[c] = 1.f / (1.f + expf(-lg[c]));
-  } else {  // 2: inputs are already probabilities (DiceLoss called directly, loss_partial.py:38)
-#pragma unroll
-    for (int c = 0; c < CMAX; ++c)
-      if (c < C) p[c] = lg[c];
+    for (int c = 0; c < NC; ++c)
+      if (c < C) p[c] = 1.f / (1.f + expf(-p[c]));
   }
 }
 
@@ -44,21 +53,22 @@ __device__ __forceinline__ float bce_elem(float p, float t) {
   return (t - 1.f) * fmaxf(log1pf(-p), -100.f) - t * fmaxf(logf(p), -100.f);
 }
 
+template <int NC>
 __global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
                                                          long long nvox, int C, int softmax, int uce,
                                                          float* __restrict__ ws) {
-  __shared__ float red[LT / 64][4 * CMAX];
-  float acc[4][CMAX];
+  __shared__ float red[LT / 64][4 * NC];
+  float acc[4][NC];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c) acc[k][c] = 0.f;
+    for (int c = 0; c < NC; ++c) acc[k][c] = 0.f;
   for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < nvox; v += (long long)gridDim.x * LT) {
-    float p[CMAX];
-    probs(lg + v * C, C, softmax, p);
+    float p[NC];
+    probs<NC>(lg + v * C, C, softmax, p);
     const float t = lab[v];
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) {
         const float tc = (t == (float)c) ? 1.f : 0.f;
         acc[0][c] = fmaf(p[c], tc, acc[0][c]);
@@ -71,38 +81,42 @@ __global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restric
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c)
       if (c < C) {
         float s = wave_sum(acc[k][c]);
-        if (lane == 0) red[wave][k * CMAX + c] = s;
+        if (lane == 0) red[wave][k * NC + c] = s;
       }
   __syncthreads();
   for (int i = threadIdx.x; i < 4 * C; i += LT) {
     const int k = i / C, c = i % C;
     float s = 0.f;
-    for (int w = 0; w < LT / 64; ++w) s += red[w][k * CMAX + c];
+    for (int w = 0; w < LT / 64; ++w) s += red[w][k * NC + c];
     ws[(long long)blockIdx.x * 4 * C + k * C + c] = s;
   }
 }
 
-__global__ __launch_bounds__(LT) void loss_final_kernel(const float* __restrict__ ws, int nblk, int C,
-                                                       const float* __restrict__ wt, int uce, double count,
-                                                       double* __restrict__ sums, float* __restrict__ loss) {
-  __shared__ double s[4 * CMAX];
-  for (int i = threadIdx.x; i < 4 * C; i += LT) {
-    double a = 0;
-    for (int b = 0; b < nblk; ++b) a += ws[(long long)b * 4 * C + i];
-    s[i] = a;
-  }
+// one block per (k, c): s = sum over the per-block partials, fixed order (fp64)
+__global__ __launch_bounds__(LT) void loss_combine_kernel(const float* __restrict__ ws, int nblk, int C,
+                                                         double* __restrict__ sums) {
+  __shared__ double red[LT / 64];
+  const int i = blockIdx.x;  // = k*C + c
+  double a = 0;
+  for (int b = threadIdx.x; b < nblk; b += LT) a += ws[(long long)b * 4 * C + i];
+  a = wave_sum(a);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
   __syncthreads();
+  if (threadIdx.x == 0) {
+    const int k = i / C, c = i % C;
+    sums[c * 4 + k] = red[0] + red[1] + red[2] + red[3];
+  }
+}
+
+__global__ void loss_final_kernel(int C, const float* __restrict__ wt, int uce, double count,
+                                  const double* __restrict__ sums, float* __restrict__ loss) {
   if (threadIdx.x == 0) {
     double dice = 0, ce = 0;
     for (int c = 0; c < C; ++c) {
-      const double I = s[c], Z = s[C + c], Y = s[2 * C + c], B = s[3 * C + c];
-      sums[c * 4 + 0] = I;
-      sums[c * 4 + 1] = Z;
-      sums[c * 4 + 2] = Y;
-      sums[c * 4 + 3] = B;
+      const double I = sums[c * 4 + 0], Z = sums[c * 4 + 1], Y = sums[c * 4 + 2], B = sums[c * 4 + 3];
       const float d = 1.f - (float)((2.0 * I + 1e-5) / (Z + Y + 1e-5));
       dice += (double)d * wt[c];
       ce += (double)(float)(B / count) * wt[c];
@@ -113,30 +127,37 @@ __global__ __launch_bounds__(LT) void loss_final_kernel(const float* __restrict_
   }
 }
 
-template <typename TO>
+template <int NC, typename TO>
 __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
                                                      long long nvox, int C, int softmax, int uce,
                                                      const float* __restrict__ wt, const double* __restrict__ sums,
                                                      const float* __restrict__ gout, double count, TO* __restrict__ dl) {
-  __shared__ float kd_a[CMAX], kd_b[CMAX], kb[CMAX];
-  if (threadIdx.x < C) {
+  __shared__ float kd_a[NC], kd_b[NC], kb[NC];
+  if (threadIdx.x < NC) {
     const int c = threadIdx.x;
-    const double I = sums[c * 4], Z = sums[c * 4 + 1], Y = sums[c * 4 + 2];
-    const double num = 2.0 * I + 1e-5, den = Z + Y + 1e-5;
-    const double scale = (double)wt[c] / C * gout[0];
-    // d(1 - num/den)/dp = -(2 t den - num * 2 p) / den^2  =  t * a + p * b
-    kd_a[c] = (float)(-2.0 / den * scale);
-    kd_b[c] = (float)(2.0 * num / (den * den) * scale);
-    kb[c] = uce ? (float)((double)wt[c] / count * gout[0]) : 0.f;
+    float a = 0.f, b = 0.f, e = 0.f;
+    if (c < C) {
+      const double I = sums[c * 4], Z = sums[c * 4 + 1], Y = sums[c * 4 + 2];
+      const double num = 2.0 * I + 1e-5, den = Z + Y + 1e-5;
+      const double scale = (double)wt[c] / C * gout[0];
+      // d(1 - num/den)/dp = -(2 t den - num * 2 p) / den^2  =  t * a + p * b
+      a = (float)(-2.0 / den * scale);
+      b = (float)(2.0 * num / (den * den) * scale);
+      e = uce ? (float)((double)wt[c] / count * gout[0]) : 0.f;
+    }
+    kd_a[c] = a;
+    kd_b[c] = b;
+    kb[c] = e;
   }
   __syncthreads();
   for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < nvox; v += (long long)gridDim.x * LT) {
-    float p[CMAX], g[CMAX];
-    probs(lg + v * C, C, softmax, p);
+    float p[NC], g[NC];
+    probs<NC>(lg + v * C, C, softmax, p);
     const float t = lab[v];
     float dot = 0.f;
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
+    for (int c = 0; c < NC; ++c) {
+      g[c] = 0.f;
       if (c < C) {
         const float tc = (t == (float)c) ? 1.f : 0.f;
         float gc = fmaf(tc, kd_a[c], p[c] * kd_b[c]);
@@ -144,16 +165,25 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
         g[c] = gc;
         dot = fmaf(gc, p[c], dot);
       }
+    }
+    float r[NC];
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c)
-      if (c < C) {
-        const float r = softmax == 1 ? p[c] * (g[c] - dot) : softmax == 0 ? g[c] * (1.f - p[c]) * p[c] : g[c];
-        dl[v * C + c] = from_f<TO>(r);
-      }
+    for (int c = 0; c < NC; ++c)
+      r[c] = softmax == 1 ? p[c] * (g[c] - dot) : softmax == 0 ? g[c] * (1.f - p[c]) * p[c] : g[c];
+    if constexpr (NC == 16 && sizeof(TO) == 4) {
+#pragma unroll
+      for (int c = 0; c < 16; c += 4)
+        *reinterpret_cast<f32x4*>(dl + v * 16 + c) = f32x4{r[c], r[c + 1], r[c + 2], r[c + 3]};
+    } else {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c < C) dl[v * C + c] = from_f<TO>(r[c]);
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------- Dice metric
+template <int NC>
 __global__ __launch_bounds__(LT) void dice_count_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
                                                        long long V, int C, int ncls,
                                                        unsigned long long* __restrict__ cnt,
@@ -164,12 +194,12 @@ __global__ __launch_bounds__(LT) void dice_count_kernel(const float* __restrict_
   const int s = blockIdx.y;
   const float* base = lg + (long long)s * V * C;
   for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < V; v += (long long)gridDim.x * LT) {
-    float p[CMAX];
-    probs(base + v * C, C, 1, p);
+    float p[NC];
+    probs<NC>(base + v * C, C, 1, p);
     int am = 0;
     float best = p[0];
 #pragma unroll
-    for (int c = 1; c < CMAX; ++c)
+    for (int c = 1; c < NC; ++c)
       if (c < C && p[c] > best) {
         best = p[c];
         am = c;
@@ -192,12 +222,10 @@ __global__ void dice_final_kernel(const unsigned long long* __restrict__ cnt, in
   float sd = 0.f, ss = 0.f, sp = 0.f;
   for (int s = 0; s < S; ++s) {
     const unsigned long long* c = cnt + ((long long)s * ncls + l) * 3;
-    const float num = (float)c[0], P = (float)c[1], T = (float)c[2];
+    const float num = (float)c[0];
     sd += (float)(2 * c[0]) / (float)(c[1] + c[2] + 1);
     ss += num / (float)(c[2] + 1);
     sp += num / (float)(c[1] + 1);
-    (void)P;
-    (void)T;
   }
   m[l * 3 + 0] = sd / (float)S;
   m[l * 3 + 1] = ss / (float)S;
@@ -205,6 +233,16 @@ __global__ void dice_final_kernel(const unsigned long long* __restrict__ cnt, in
 }
 
 static int loss_blocks(long long nvox) { return (int)std::min<long long>(1024, std::max<long long>(1, (nvox + LT - 1) / LT)); }
+
+// dispatch on the class count: exact instantiations for the model heads, a guarded 32-wide fallback
+#define U3D_NC_DISPATCH(C, F)        \
+  switch (C) {                       \
+    case 2: F(2); break;             \
+    case 8: F(8); break;             \
+    case 14: F(14); break;           \
+    case 16: F(16); break;           \
+    default: F(32); break;           \
+  }
 
 }  // namespace u3d
 
@@ -222,8 +260,12 @@ extern "C" int u3d_partial_loss_fwd(const float* logits, const float* labels, in
   hipStream_t s = (hipStream_t)stream;
   const long long nvox = (long long)S * V;
   const int nb = loss_blocks(nvox);
-  hipLaunchKernelGGL(loss_partial_kernel, dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, ws);
-  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(LT), 0, s, ws, nb, C, weights, uce, (double)nvox, sums, loss);
+#define LAUNCH(NCV) \
+  hipLaunchKernelGGL(loss_partial_kernel<NCV>, dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, ws)
+  U3D_NC_DISPATCH(C, LAUNCH)
+#undef LAUNCH
+  hipLaunchKernelGGL(loss_combine_kernel, dim3(4 * C), dim3(LT), 0, s, ws, nb, C, sums);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, s, C, weights, uce, (double)nvox, sums, loss);
   return check_launch("partial_loss_fwd");
 }
 
@@ -235,12 +277,19 @@ extern "C" int u3d_partial_loss_bwd(int dtype_out, const float* logits, const fl
   hipStream_t s = (hipStream_t)stream;
   const long long nvox = (long long)S * V;
   const int nb = (int)std::min<long long>(8192, (nvox + LT - 1) / LT);
-  if (dtype_out == U3D_BF16)
-    hipLaunchKernelGGL(loss_bwd_kernel<bf16>, dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, weights,
-                       sums, grad_out, (double)nvox, (bf16*)dlogits);
-  else
-    hipLaunchKernelGGL(loss_bwd_kernel<float>, dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, weights,
-                       sums, grad_out, (double)nvox, (float*)dlogits);
+  if (dtype_out == U3D_BF16) {
+#define LAUNCH(NCV)                                                                                                   \
+  hipLaunchKernelGGL((loss_bwd_kernel<NCV, bf16>), dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, \
+                     weights, sums, grad_out, (double)nvox, (bf16*)dlogits)
+    U3D_NC_DISPATCH(C, LAUNCH)
+#undef LAUNCH
+  } else {
+#define LAUNCH(NCV)                                                                                                    \
+  hipLaunchKernelGGL((loss_bwd_kernel<NCV, float>), dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, \
+                     weights, sums, grad_out, (double)nvox, (float*)dlogits)
+    U3D_NC_DISPATCH(C, LAUNCH)
+#undef LAUNCH
+  }
   return check_launch("partial_loss_bwd");
 }
 
@@ -251,8 +300,11 @@ extern "C" int u3d_dice_metric(const float* logits, const float* labels, int S, 
   hipStream_t s = (hipStream_t)stream;
   U3D_HIP(hipMemsetAsync(counts, 0, (size_t)S * num_class * 3 * 8, s));
   const int nb = (int)std::min<long long>(1024, (V + LT - 1) / LT);
-  hipLaunchKernelGGL(dice_count_kernel, dim3(nb, S), dim3(LT), 0, s, logits, labels, V, C, num_class,
-                     (unsigned long long*)counts, argmax);
+#define LAUNCH(NCV)                                                                                         \
+  hipLaunchKernelGGL(dice_count_kernel<NCV>, dim3(nb, S), dim3(LT), 0, s, logits, labels, V, C, num_class, \
+                     (unsigned long long*)counts, argmax)
+  U3D_NC_DISPATCH(C, LAUNCH)
+#undef LAUNCH
   hipLaunchKernelGGL(dice_final_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)counts, S, num_class,
                      metrics);
   return check_launch("dice_metric");

@@ -47,12 +47,17 @@ __global__ __launch_bounds__(256) void chsum_partial(const T* __restrict__ x, lo
   }
 }
 
-__global__ void chsum_final(const float* __restrict__ ws, int nblk, int c, float* __restrict__ out, int accum) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
+// one block per channel, fixed-order fp64 combine of the block partials
+__global__ __launch_bounds__(256) void chsum_final(const float* __restrict__ ws, int nblk, int c, float* __restrict__ out,
+                                                  int accum) {
+  __shared__ double red[4];
+  const int ch = blockIdx.x;
   double s = 0;
-  for (int b = 0; b < nblk; ++b) s += ws[(long long)b * c + ch];
-  out[ch] = (accum ? out[ch] : 0.f) + (float)s;
+  for (int b = threadIdx.x; b < nblk; b += 256) s += ws[(long long)b * c + ch];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[ch] = (accum ? out[ch] : 0.f) + (float)(red[0] + red[1] + red[2] + red[3]);
 }
 
 static int chsum_blocks(long long rows, int c, int* rpb) {
@@ -99,7 +104,7 @@ extern "C" int u3d_channel_sum(int dtype, const void* x, long long rows, int c, 
   const int nb = chsum_blocks(rows, c, &rpb);
   if (dtype == U3D_BF16) hipLaunchKernelGGL(chsum_partial<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)x, rows, c, rpb, ws);
   else hipLaunchKernelGGL(chsum_partial<float>, dim3(nb), dim3(256), 0, s, (const float*)x, rows, c, rpb, ws);
-  hipLaunchKernelGGL(chsum_final, dim3((c + 63) / 64), dim3(64), 0, s, ws, nb, c, out, accumulate);
+  hipLaunchKernelGGL(chsum_final, dim3(c), dim3(256), 0, s, ws, nb, c, out, accumulate);
   return check_launch("channel_sum");
 }
 

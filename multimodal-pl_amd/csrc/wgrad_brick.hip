@@ -192,7 +192,7 @@ extern "C" int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, 
   const int od = (d - 1) / stride + 1, oh = (h - 1) / stride + 1, ow = (w - 1) / stride + 1;
   const long long nb = (long long)n * cdiv(od, bd) * cdiv(oh, bh) * cdiv(ow, bw);
   const long long tiles = (long long)cdiv(cin, 32) * cdiv(cout, 32);
-  long long want = std::max(1LL, 1024 / tiles);
+  long long want = std::max(1LL, 256 / tiles);
   return (int)std::max(1LL, std::min(want, nb));
 }
 

@@ -1,0 +1,24 @@
+"""Summarise a rocprofv3 --kernel-trace csv: per-kernel totals per step and the top (kernel, grid) groups."""
+import collections
+import csv
+import sys
+
+d = sys.argv[1]
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+tot = collections.defaultdict(float)
+grp = collections.defaultdict(lambda: [0, 0.0])
+for r in rows:
+    n = r["Kernel_Name"].split("(")[0]
+    dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    tot[n] += dt
+    k = (n[-70:], int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]), r["Grid_Size_Y"], r["Grid_Size_Z"])
+    grp[k][0] += 1
+    grp[k][1] += dt
+s = sum(tot.values())
+print(f"GPU busy per step: {s / steps / 1e3:.3f} ms")
+for n, v in sorted(tot.items(), key=lambda kv: -kv[1])[:18]:
+    print(f"{v / steps / 1e3:8.3f} ms/step {100 * v / s:5.1f}%  {n[-90:]}")
+print("--- top (kernel, grid) groups")
+for k, v in sorted(grp.items(), key=lambda kv: -kv[1][1])[:int(sys.argv[3]) if len(sys.argv) > 3 else 20]:
+    print(f"{v[1] / steps / 1e3:7.3f} ms/step n/step={v[0] // steps:3d} avg={v[1] / v[0]:8.1f}us {k}")
