@@ -80,6 +80,13 @@ int u3d_conv32_brick(int flip, const void* x, int n, int d, int h, int w, const 
                      const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
                      u3d_stream_t stream);
 
+/* bf16 3^3 stride-1 conv for any cin/cout (multiples of 8) in halo-brick form: 4x8x16-voxel bricks x 64-channel
+ * co tiles, 32-channel input chunks staged once per brick (GN+ReLU prologue), weights streamed per tap plane.
+ * flip/wpk as u3d_conv32_brick (for flip=1, cin/cout are the data-gradient's input/output channels). */
+int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                    const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                    const void* residual, void* y, u3d_stream_t stream);
+
 /* bf16 3^3 weight gradient in halo-brick form (ds_read_b64_tr_b16 operands, all 27 taps per workgroup);
  * same partial-slab output as u3d_conv_wgrad (nsplit from u3d_conv_wgrad_brick_splits). */
 int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, int cout, int stride);

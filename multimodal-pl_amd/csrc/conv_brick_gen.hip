@@ -1,0 +1,289 @@
+// Generic 3^3 stride-1 convolution (forward / data gradient), bf16, halo-brick form, for the layers with
+// cin >= 64 or spatial extents that are not multiples of 32 (48^3, 24^3, 12^3, 6^3 levels of the U-Net).
+//
+//   * one workgroup (8 waves) = one output brick of 4 x 8 x 16 voxels x one 64- (or 32-) channel co tile;
+//   * K loop = 32-channel input chunks x 3 tap planes (td): per chunk the input halo (6 x 10 x 18 voxels) is
+//     staged once into LDS with the GroupNorm + ReLU prologue applied once per element; per tap plane the
+//     9 taps' weights (9 x 64 x 32 bf16 = 36 KB) are streamed into a double-buffered LDS slot;
+//   * each wave owns 2 row tiles (32 voxels = 2 h-rows x 16 w) x the co tile (TN = CO/32 MFMA columns):
+//     per k16 step 2 A reads + TN B reads feed 2*TN MFMAs (1 KB of LDS per MFMA at CO = 64);
+//   * LDS images are chunk-planar (plane = 8 channels), and the 32 rows of an MFMA tile are ordered so that
+//     each 16-lane ds_read_b128 group reads 16 consecutive halo rows (conflict-free for any halo pitch);
+//   * the next chunk's halo and the next tap plane's weights are prefetched into registers while the MFMAs
+//     of the current plane run.
+// Reference: F.conv3d in Conv3d.forward (unet3D.py:27) through NoBottleneck (:56-73), fusion/decoder blocks.
+#include "common.h"
+
+namespace u3d {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+constexpr int GB_BD = 4, GB_BH = 8, GB_BW = 16;
+constexpr int GB_HD = GB_BD + 2, GB_HH = GB_BH + 2, GB_HW = GB_BW + 2;
+constexpr int GB_NH = GB_HD * GB_HH * GB_HW;  // 1080 halo rows
+constexpr int GB_NT = 512;
+constexpr int GB_HLD = (GB_NH * 4 + GB_NT - 1) / GB_NT;  // 9 halo loads per thread
+constexpr int GB_MAXN = 16;
+
+struct GBGeom {
+  int n, d, h, w;
+  int cin, cout, cin_p, cout_p;
+  int nbd, nbh, nbw;
+  int gn_groups;
+};
+
+// MFMA row r (0..31) -> (segment = which of the 2 h-rows, position = w): the 16 lanes of each ds_read_b128
+// group ({0-3,12-15,20-27} and {4-11,16-19,28-31}) get 16 consecutive w of one h-row.
+__device__ __forceinline__ int gb_seg(int r) {
+  return (r < 4 || (r >= 12 && r < 16) || (r >= 20 && r < 28)) ? 0 : 1;
+}
+__device__ __forceinline__ int gb_pos(int r) {
+  if (r < 4) return r;
+  if (r < 12) return r - 4;
+  if (r < 16) return r - 8;
+  if (r < 20) return r - 8;
+  if (r < 28) return r - 12;
+  return r - 16;
+}
+
+template <int CO, bool FLIP>
+__global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
+                                                              bf16* __restrict__ y, const bf16* __restrict__ res,
+                                                              const float* __restrict__ gstat,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, GBGeom g) {
+  constexpr int TN = CO / 32;
+  constexpr int WROWS = 9 * CO;                            // weight rows per tap plane
+  constexpr int WLD = (WROWS * 4 + GB_NT - 1) / GB_NT;     // weight loads per thread (5 at CO=64)
+  __shared__ __attribute__((aligned(16))) char hal[4 * GB_NH * 16];
+  __shared__ __attribute__((aligned(16))) char wbuf[2][4 * WROWS * 16];
+  __shared__ float gsc[GB_MAXN][32], gsh[GB_MAXN][32];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  int b = blockIdx.x;
+  const int bw_ = b % g.nbw; b /= g.nbw;
+  const int bh_ = b % g.nbh; b /= g.nbh;
+  const int bd_ = b % g.nbd;
+  const int nn = b / g.nbd;
+  const int d0 = bd_ * GB_BD, h0 = bh_ * GB_BH, w0 = bw_ * GB_BW;
+  const int co0 = blockIdx.y * CO;
+  const bool has_gn = gstat != nullptr;
+  const int nchunk = g.cin_p / 32;
+  const int nsteps = nchunk * 3;
+
+  u32x4 hpre[GB_HLD];
+  u32x4 wpre[WLD];
+
+  auto halo_load = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < GB_HLD; ++i) {
+      const int ci = tid + i * GB_NT;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (ci < GB_NH * 4) {
+        const int ch = ci / GB_NH, row = ci % GB_NH;
+        const int hw = row % GB_HW, hr = (row / GB_HW) % GB_HH, hd = row / (GB_HW * GB_HH);
+        const int zd = d0 - 1 + hd, zh = h0 - 1 + hr, zw = w0 - 1 + hw;
+        const int cc = c * 32 + ch * 8;
+        if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w && cc < g.cin)
+          v = *reinterpret_cast<const u32x4*>(x + ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc);
+      }
+      hpre[i] = v;
+    }
+  };
+  auto gn_table = [&](int c) {  // scale/shift of chunk c for this brick's sample
+    if (has_gn && tid < 32) {
+      const int cc = c * 32 + tid;
+      float s = 0.f, sh = 0.f;
+      if (cc < g.cin) {
+        const int gg = cc / (g.cin / g.gn_groups);
+        const float mean = gstat[(nn * g.gn_groups + gg) * 2], rstd = gstat[(nn * g.gn_groups + gg) * 2 + 1];
+        s = rstd * gamma[cc];
+        sh = beta[cc] - mean * s;
+      }
+      gsc[0][tid] = s;
+      gsh[0][tid] = sh;
+    }
+  };
+  auto halo_commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < GB_HLD; ++i) {
+      const int ci = tid + i * GB_NT;
+      if (ci < GB_NH * 4) {
+        const int ch = ci / GB_NH, row = ci % GB_NH;
+        u32x4 v = hpre[i];
+        if (has_gn) {
+          const int hw = row % GB_HW, hr = (row / GB_HW) % GB_HH, hd = row / (GB_HW * GB_HH);
+          const int zd = d0 - 1 + hd, zh = h0 - 1 + hr, zw = w0 - 1 + hw;
+          if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w) {
+            float f[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              f[2 * e] = __uint_as_float(v[e] << 16);
+              f[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = fmaxf(0.f, fmaf(f[e], gsc[0][ch * 8 + e], gsh[0][ch * 8 + e]));
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              v[e] = (uint32_t)from_f<bf16>(f[2 * e]) | ((uint32_t)from_f<bf16>(f[2 * e + 1]) << 16);
+          }
+        }
+        *reinterpret_cast<u32x4*>(hal + (ch * GB_NH + row) * 16) = v;
+      }
+    }
+  };
+  // weights of step s = (chunk c, tap plane td): rows (j, co) for t = td*9 + j
+  auto w_load = [&](int s) {
+    const int c = s / 3, td = s % 3;
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) {
+      const int ci = tid + i * GB_NT;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (ci < WROWS * 4) {
+        const int ch = ci / WROWS, row = ci % WROWS;
+        const int j = row / CO, co = co0 + row % CO;
+        const int t = td * 9 + j;
+        if (co < g.cout_p)
+          v = *reinterpret_cast<const u32x4*>(wpk + ((long long)t * g.cout_p + co) * g.cin_p + c * 32 + ch * 8);
+      }
+      wpre[i] = v;
+    }
+  };
+  auto w_commit = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) {
+      const int ci = tid + i * GB_NT;
+      if (ci < WROWS * 4) {
+        const int ch = ci / WROWS, row = ci % WROWS;
+        *reinterpret_cast<u32x4*>(wbuf[buf] + (ch * WROWS + row) * 16) = wpre[i];
+      }
+    }
+  };
+
+  // prologue: chunk 0 halo + plane 0 weights
+  gn_table(0);
+  halo_load(0);
+  w_load(0);
+  __syncthreads();
+  halo_commit();
+  w_commit(0);
+  __syncthreads();
+
+  f32x16 acc[2][TN];
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.f;
+
+  // per-lane A row of tap (0,0,0) for row tile tm: rt = 2*wave + tm -> (d = rt >> 2, h-pair = rt & 3)
+  int arow[2];
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+    const int rt = 2 * wave + tm, vd = rt >> 2, vh = 2 * (rt & 3) + gb_seg(r);
+    arow[tm] = (vd * GB_HH + vh) * GB_HW + gb_pos(r);
+  }
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int td = s % 3;
+    const bool last_plane = td == 2;
+    if (s + 1 < nsteps) w_load(s + 1);
+    if (last_plane && s + 1 < nsteps) halo_load(s / 3 + 1);
+    const char* wb = wbuf[s & 1];
+    const int od = FLIP ? 2 - td : td;
+#pragma unroll 3
+    for (int j = 0; j < 9; ++j) {
+      const int th = j / 3, tw = j % 3;
+      const int oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
+      const int toff = (od * GB_HH + oh) * GB_HW + ow;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int plane = 2 * k + hh;
+        bf16x8 a[2], bb[TN];
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+          a[tm] = *reinterpret_cast<const bf16x8*>(hal + (plane * GB_NH + arow[tm] + toff) * 16);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          bb[tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tm], bb[tn], acc[tm][tn], 0, 0, 0);
+      }
+    }
+    if (s + 1 < nsteps) {
+      w_commit((s + 1) & 1);  // the other buffer: its readers finished before the previous barrier
+      if (last_plane) {
+        __syncthreads();  // everyone done with this chunk's halo
+        gn_table(s / 3 + 1);
+        __syncthreads();
+        halo_commit();
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane column co = co0 + tn*32 + r; row i -> (h-row seg, w pos) of row tile tm
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+    const int rt = 2 * wave + tm, zd = d0 + (rt >> 2);
+    if (zd >= g.d) continue;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int co = co0 + tn * 32 + r;
+      if (co >= g.cout) continue;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ri = (i & 3) + 8 * (i >> 2) + 4 * hh;
+        const int zh = h0 + 2 * (rt & 3) + gb_seg(ri), zw = w0 + gb_pos(ri);
+        if (zh < g.h && zw < g.w) {
+          const long long off = ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cout + co;
+          float v = acc[tm][tn][i];
+          if (res) v += to_f(res[off]);
+          y[off] = from_f<bf16>(v);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace u3d
+
+using namespace u3d;
+
+extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                               const void* residual, void* y, u3d_stream_t stream) {
+  U3D_REQUIRE(x && wpk && y && n >= 1 && n <= GB_MAXN, "convg_brick: bad args");
+  U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "convg_brick: channels must be multiples of 8");
+  U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "convg_brick: bad GN");
+  GBGeom g{};
+  g.n = n; g.d = d; g.h = h; g.w = w;
+  g.cin = cin; g.cout = cout; g.cin_p = round_up(cin, 32); g.cout_p = round_up(cout, 32);
+  g.nbd = cdiv(d, GB_BD); g.nbh = cdiv(h, GB_BH); g.nbw = cdiv(w, GB_BW);
+  g.gn_groups = gn_groups;
+  const int nb = n * g.nbd * g.nbh * g.nbw;
+  hipStream_t s = (hipStream_t)stream;
+  const bool co64 = g.cout_p >= 64;
+  dim3 grid(nb, co64 ? cdiv(cout, 64) : 1);
+  if (co64) {
+    if (flip)
+      hipLaunchKernelGGL((convg_brick_kernel<64, true>), grid, dim3(GB_NT), 0, s, (const bf16*)x, (const bf16*)wpk,
+                         (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
+    else
+      hipLaunchKernelGGL((convg_brick_kernel<64, false>), grid, dim3(GB_NT), 0, s, (const bf16*)x, (const bf16*)wpk,
+                         (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
+  } else {
+    if (flip)
+      hipLaunchKernelGGL((convg_brick_kernel<32, true>), grid, dim3(GB_NT), 0, s, (const bf16*)x, (const bf16*)wpk,
+                         (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
+    else
+      hipLaunchKernelGGL((convg_brick_kernel<32, false>), grid, dim3(GB_NT), 0, s, (const bf16*)x, (const bf16*)wpk,
+                         (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
+  }
+  return check_launch("convg_brick_kernel");
+}

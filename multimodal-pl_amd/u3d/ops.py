@@ -87,9 +87,13 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
     od, oh, ow = out_dim(d, k, stride), out_dim(h, k, stride), out_dim(w_, k, stride)
     y = torch.empty((n, od, oh, ow, cout), dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
     st, ga, be, G = gn if gn is not None else (None, None, None, 0)
-    if _use_conv32(x.dtype, cin, cout, k, stride, n) and not out_f32 and bias is None:
+    if _use_conv32(x.dtype, cin, cout, k, stride, n, w_) and not out_f32 and bias is None:
         call("u3d_conv32_brick", 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
              _ptr(residual), y.data_ptr(), _stream())
+        return y
+    if _use_gen_brick(x.dtype, cin, cout, k, stride, (n, d, h, w_)) and not out_f32 and bias is None:
+        call("u3d_convg_brick", 0, x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be),
+             G, _ptr(residual), y.data_ptr(), _stream())
         return y
     ws = WS.get(SPLITK_WS_BYTES, x.device, slot=4)
     call("u3d_conv_fwd", dt_code(x.dtype), x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, k, stride, _ptr(st),
@@ -102,18 +106,36 @@ SPLITK_WS_BYTES = 64 << 20
 USE_CONV32_BRICK = True
 
 
-def _use_conv32(dtype, cin, cout, k, stride, n):
+def _use_conv32(dtype, cin, cout, k, stride, n, w=32):
     return USE_CONV32_BRICK and dtype == torch.bfloat16 and cin == 32 and cout == 32 and k == 3 and stride == 1 \
-        and n <= 16
+        and n <= 16 and w % 32 == 0
+
+
+USE_GEN_BRICK = True
+BRICK_MIN_WG = 128  # below this many workgroups the split-K implicit GEMM fills the chip better
+
+
+def _use_gen_brick(dtype, cin, cout, k, stride, shape):
+    if not (USE_GEN_BRICK and dtype == torch.bfloat16 and k == 3 and stride == 1 and cin % 8 == 0 and cout % 8 == 0):
+        return False
+    n, d, h, w_ = shape
+    if n > 16:
+        return False
+    nb = n * -(-d // 4) * -(-h // 8) * -(-w_ // 16)
+    return nb * max(1, -(-cout // 64)) >= BRICK_MIN_WG
 
 
 def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     n, d, h, w_ = in_shape
     cout = dy.shape[-1]
     dx = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
-    if _use_conv32(dy.dtype, cin, cout, k, stride, n):
+    if _use_conv32(dy.dtype, cin, cout, k, stride, n, w_):
         call("u3d_conv32_brick", 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
              dx.data_ptr(), _stream())
+        return dx
+    if _use_gen_brick(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
+        call("u3d_convg_brick", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None, 0,
+             None, dx.data_ptr(), _stream())
         return dx
     ws = WS.get(SPLITK_WS_BYTES, dy.device, slot=4)
     call("u3d_conv_dgrad", dt_code(dy.dtype), dy.data_ptr(), n, cout, wpk_dgrad.data_ptr(), cin, d, h, w_, k, stride,

@@ -44,8 +44,21 @@ SHAPES = [(2, 32, 32, (12, 10, 16), 1), (1, 32, 32, (5, 9, 70), 1), (1, 32, 64, 
           (1, 64, 32, (10, 6, 8), 1), (2, 128, 128, (4, 4, 4), 1), (1, 24, 24, (7, 9, 11), 1)]
 
 
+@pytest.fixture(params=["auto", "gen_brick", "igemm"])
+def conv_path(request):
+    """auto = production routing; gen_brick = force the generic halo-brick kernel; igemm = force implicit GEMM."""
+    from u3d import ops
+    saved = (ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK)
+    if request.param == "gen_brick":
+        ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK = 0, False
+    elif request.param == "igemm":
+        ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK = False, False
+    yield request.param
+    ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK = saved
+
+
 @pytest.mark.parametrize("n,cin,cout,dims,s", SHAPES)
-def test_bf16_conv_fwd(gpu, n, cin, cout, dims, s):
+def test_bf16_conv_fwd(gpu, conv_path, n, cin, cout, dims, s):
     from u3d import ops
     x, w, st, ga, be, G = _case(gpu, n, cin, cout, dims, True, 1)
     pf, pd, wst = ops.wstd_fwd(w, torch.bfloat16, True)
@@ -58,7 +71,7 @@ def test_bf16_conv_fwd(gpu, n, cin, cout, dims, s):
 
 
 @pytest.mark.parametrize("n,cin,cout,dims,s", SHAPES)
-def test_bf16_conv_dgrad(gpu, n, cin, cout, dims, s):
+def test_bf16_conv_dgrad(gpu, conv_path, n, cin, cout, dims, s):
     from u3d import ops
     if s == 2 and any(d % 2 for d in dims):
         pytest.skip("stride-2 dgrad needs even dims (as the trunk has)")
