@@ -96,6 +96,37 @@ __device__ __forceinline__ void storev(T* p, const float (&v)[N]) {
   }
 }
 
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+// GroupNorm apply + ReLU on 8 packed bf16 channels: relu(x * sc + sh), two-wide packed fp32 math
+__device__ __forceinline__ u32x4 gn_relu8(u32x4 v, const f32x2 (&sc)[4], const f32x2 (&sh)[4]) {
+  u32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f32x2 f = {__uint_as_float(v[e] << 16), __uint_as_float(v[e] & 0xffff0000u)};
+    f = f * sc[e] + sh[e];
+    f[0] = fmaxf(f[0], 0.f);
+    f[1] = fmaxf(f[1], 0.f);
+    o[e] = (uint32_t)from_f<bf16>(f[0]) | ((uint32_t)from_f<bf16>(f[1]) << 16);
+  }
+  return o;
+}
+
+// per-thread scale/shift of channels c0 .. c0+7 (clamped) of sample n for gn_relu8
+__device__ __forceinline__ void gn_coef8(const float* __restrict__ st, const float* __restrict__ gamma,
+                                         const float* __restrict__ beta, int groups, int cin, int n, int c0,
+                                         f32x2 (&sc)[4], f32x2 (&sh)[4]) {
+  const int cpg = cin / groups;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = min(c0 + e, cin - 1), gg = c / cpg;
+    const float mean = st[(n * groups + gg) * 2], rstd = st[(n * groups + gg) * 2 + 1];
+    const float s = rstd * gamma[c];
+    sc[e >> 1][e & 1] = s;
+    sh[e >> 1][e & 1] = beta[c] - mean * s;
+  }
+}
+
 // -------------------------------------------------------------------------------- wave reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

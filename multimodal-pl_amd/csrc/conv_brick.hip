@@ -24,9 +24,9 @@ constexpr int CB_BD = 2, CB_BH = 8, CB_BW = 32;
 constexpr int CB_HD = CB_BD + 2, CB_HH = CB_BH + 2, CB_HW = CB_BW + 2;
 constexpr int CB_NH = CB_HD * CB_HH * CB_HW;            // 1360 halo rows
 constexpr int CB_NWR = 27 * 32;                          // weight rows (t, co)
-constexpr int CB_CHUNKS = CB_NH * 4;                     // 16-B chunks per halo
 constexpr int CB_NT = 512;
-constexpr int CB_LD = (CB_CHUNKS + CB_NT - 1) / CB_NT;   // 11 prefetch loads per thread
+constexpr int CB_LD = (CB_NH + CB_NT / 4 - 1) / (CB_NT / 4);  // 11 prefetch loads per thread
+constexpr int CB_PS = CB_NH * 16 + 64;                   // LDS plane stride (+64 B: conflict-free staging writes)
 constexpr int CB_MAXN = 16;
 
 struct CBGeom {
@@ -42,30 +42,22 @@ __global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __re
                                                                const float* __restrict__ gstat,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta, CBGeom g) {
-  __shared__ __attribute__((aligned(16))) char hal[4 * CB_NH * 16];
+  __shared__ __attribute__((aligned(16))) char hal[4 * CB_PS];
   __shared__ __attribute__((aligned(16))) char wts[4 * CB_NWR * 16];
-  __shared__ float gsc[CB_MAXN][32], gsh[CB_MAXN][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
+  const int ch = tid & 3, row0 = tid >> 2;  // staging: fixed 8-channel chunk per thread, rows row0 + 128 i
   const bool has_gn = gstat != nullptr;
-  if (has_gn) {
-    const int cpg = 32 / g.gn_groups;
-    for (int i = tid; i < g.n * 32; i += CB_NT) {
-      const int nn = i >> 5, c = i & 31, gg = c / cpg;
-      const float mean = gstat[(nn * g.gn_groups + gg) * 2], rstd = gstat[(nn * g.gn_groups + gg) * 2 + 1];
-      const float s = rstd * gamma[c];
-      gsc[nn][c] = s;
-      gsh[nn][c] = beta[c] - mean * s;
-    }
-  }
   // weights: plane ch, row t*32 + co
   for (int i = tid; i < CB_NWR * 4; i += CB_NT) {
-    const int ch = i / CB_NWR, row = i % CB_NWR;
-    *reinterpret_cast<u32x4*>(wts + (ch * CB_NWR + row) * 16) =
-        *reinterpret_cast<const u32x4*>(wpk + row * 32 + ch * 8);
+    const int c = i / CB_NWR, row = i % CB_NWR;
+    *reinterpret_cast<u32x4*>(wts + (c * CB_NWR + row) * 16) =
+        *reinterpret_cast<const u32x4*>(wpk + row * 32 + c * 8);
   }
 
   u32x4 pre[CB_LD];
+  f32x2 sc[4], sh[4];
+  int gn_n = -1;
   auto brick_origin = [&](int b, int& nn, int& d0, int& h0, int& w0) {
     int t = b;
     const int bw_ = t % g.nbw; t /= g.nbw;
@@ -74,16 +66,15 @@ __global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __re
     nn = t / g.nbd;
     d0 = bd_ * CB_BD; h0 = bh_ * CB_BH; w0 = bw_ * CB_BW;
   };
-  // chunk ci -> (plane ch = ci / NH, halo row = ci % NH): consecutive threads fill consecutive rows of a plane
+  // 4 consecutive threads read the 64 B (32 channels) of one voxel: fully coalesced loads
   auto prefetch = [&](int b) {
     int nn, d0, h0, w0;
     brick_origin(b, nn, d0, h0, w0);
 #pragma unroll
     for (int i = 0; i < CB_LD; ++i) {
-      const int ci = tid + i * CB_NT;
+      const int row = row0 + i * (CB_NT / 4);
       u32x4 v = {0u, 0u, 0u, 0u};
-      if (ci < CB_CHUNKS) {
-        const int ch = ci / CB_NH, row = ci % CB_NH;
+      if (row < CB_NH) {
         const int hw = row % CB_HW, hh = (row / CB_HW) % CB_HH, hd = row / (CB_HW * CB_HH);
         const int zd = d0 - 1 + hd, zh = h0 - 1 + hh, zw = w0 - 1 + hw;
         if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w)
@@ -95,42 +86,33 @@ __global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __re
   auto commit = [&](int b) {
     int nn, d0, h0, w0;
     brick_origin(b, nn, d0, h0, w0);
+    if (has_gn && nn != gn_n) {
+      gn_n = nn;
+      gn_coef8(gstat, gamma, beta, g.gn_groups, 32, nn, ch * 8, sc, sh);
+    }
 #pragma unroll
     for (int i = 0; i < CB_LD; ++i) {
-      const int ci = tid + i * CB_NT;
-      if (ci < CB_CHUNKS) {
-        const int ch = ci / CB_NH, row = ci % CB_NH;
+      const int row = row0 + i * (CB_NT / 4);
+      if (row < CB_NH) {
         u32x4 v = pre[i];
         if (has_gn) {
           const int hw = row % CB_HW, hh = (row / CB_HW) % CB_HH, hd = row / (CB_HW * CB_HH);
           const int zd = d0 - 1 + hd, zh = h0 - 1 + hh, zw = w0 - 1 + hw;
-          if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w) {
-            float f[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              f[2 * e] = __uint_as_float(v[e] << 16);
-              f[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = fmaxf(0.f, fmaf(f[e], gsc[nn][ch * 8 + e], gsh[nn][ch * 8 + e]));
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              v[e] = (uint32_t)from_f<bf16>(f[2 * e]) | ((uint32_t)from_f<bf16>(f[2 * e + 1]) << 16);
-          }
+          if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w)
+            v = gn_relu8(v, sc, sh);
         }
-        *reinterpret_cast<u32x4*>(hal + (ch * CB_NH + row) * 16) = v;
+        *reinterpret_cast<u32x4*>(hal + ch * CB_PS + row * 16) = v;
       }
     }
   };
 
   int b = blockIdx.x;
   if (b >= g.nbricks) return;
-  __syncthreads();  // gn tables
   prefetch(b);
   commit(b);
   __syncthreads();
   // per-lane fragment bases: A row of tap (0,0,0) for w-row tm: ((tm)*HH + wave)*HW + r ; plane (2s + h)
-  const char* abase = hal + (h * CB_NH + wave * CB_HW + r) * 16;
+  const char* abase = hal + h * CB_PS + (wave * CB_HW + r) * 16;
   const char* bbase = wts + (h * CB_NWR + r) * 16;
   for (; b < g.nbricks; b += gridDim.x) {
     const int bn = b + gridDim.x;
@@ -146,7 +128,7 @@ __global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __re
       const int t = st >> 1, s = st & 1;
       const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
       const int od = FLIP ? 2 - td : td, oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
-      return ((od * CB_HH + oh) * CB_HW + ow) * 16 + 2 * s * CB_NH * 16;
+      return ((od * CB_HH + oh) * CB_HW + ow) * 16 + 2 * s * CB_PS;
     };
     auto boff = [](int st) { return (2 * (st & 1) * CB_NWR + (st >> 1) * 32) * 16; };
     bf16x8 ca0 = *reinterpret_cast<const bf16x8*>(abase + aoff(0));

@@ -22,7 +22,8 @@ constexpr int GB_BD = 4, GB_BH = 8, GB_BW = 16;
 constexpr int GB_HD = GB_BD + 2, GB_HH = GB_BH + 2, GB_HW = GB_BW + 2;
 constexpr int GB_NH = GB_HD * GB_HH * GB_HW;  // 1080 halo rows
 constexpr int GB_NT = 512;
-constexpr int GB_HLD = (GB_NH * 4 + GB_NT - 1) / GB_NT;  // 9 halo loads per thread
+constexpr int GB_HLD = (GB_NH + GB_NT / 4 - 1) / (GB_NT / 4);  // 9 halo loads per thread
+constexpr int GB_PS = GB_NH * 16 + 64;  // LDS plane stride (+64 B: conflict-free staging writes)
 constexpr int GB_MAXN = 16;
 
 struct GBGeom {
@@ -55,9 +56,8 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
   constexpr int TN = CO / 32;
   constexpr int WROWS = 9 * CO;                            // weight rows per tap plane
   constexpr int WLD = (WROWS * 4 + GB_NT - 1) / GB_NT;     // weight loads per thread (5 at CO=64)
-  __shared__ __attribute__((aligned(16))) char hal[4 * GB_NH * 16];
+  __shared__ __attribute__((aligned(16))) char hal[4 * GB_PS];
   __shared__ __attribute__((aligned(16))) char wbuf[2][4 * WROWS * 16];
-  __shared__ float gsc[GB_MAXN][32], gsh[GB_MAXN][32];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -75,61 +75,40 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
   u32x4 hpre[GB_HLD];
   u32x4 wpre[WLD];
 
+  // staging: fixed 8-channel chunk per thread (4 threads = one voxel's 32 channels, coalesced)
+  const int sch = tid & 3, srow0 = tid >> 2;
+  f32x2 sc[4], sh[4];
   auto halo_load = [&](int c) {
 #pragma unroll
     for (int i = 0; i < GB_HLD; ++i) {
-      const int ci = tid + i * GB_NT;
+      const int row = srow0 + i * (GB_NT / 4);
       u32x4 v = {0u, 0u, 0u, 0u};
-      if (ci < GB_NH * 4) {
-        const int ch = ci / GB_NH, row = ci % GB_NH;
+      if (row < GB_NH) {
         const int hw = row % GB_HW, hr = (row / GB_HW) % GB_HH, hd = row / (GB_HW * GB_HH);
         const int zd = d0 - 1 + hd, zh = h0 - 1 + hr, zw = w0 - 1 + hw;
-        const int cc = c * 32 + ch * 8;
+        const int cc = c * 32 + sch * 8;
         if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w && cc < g.cin)
           v = *reinterpret_cast<const u32x4*>(x + ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc);
       }
       hpre[i] = v;
     }
   };
-  auto gn_table = [&](int c) {  // scale/shift of chunk c for this brick's sample
-    if (has_gn && tid < 32) {
-      const int cc = c * 32 + tid;
-      float s = 0.f, sh = 0.f;
-      if (cc < g.cin) {
-        const int gg = cc / (g.cin / g.gn_groups);
-        const float mean = gstat[(nn * g.gn_groups + gg) * 2], rstd = gstat[(nn * g.gn_groups + gg) * 2 + 1];
-        s = rstd * gamma[cc];
-        sh = beta[cc] - mean * s;
-      }
-      gsc[0][tid] = s;
-      gsh[0][tid] = sh;
-    }
+  auto gn_table = [&](int c) {  // scale/shift of this thread's 8 channels of chunk c
+    if (has_gn) gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, nn, c * 32 + sch * 8, sc, sh);
   };
   auto halo_commit = [&]() {
 #pragma unroll
     for (int i = 0; i < GB_HLD; ++i) {
-      const int ci = tid + i * GB_NT;
-      if (ci < GB_NH * 4) {
-        const int ch = ci / GB_NH, row = ci % GB_NH;
+      const int row = srow0 + i * (GB_NT / 4);
+      if (row < GB_NH) {
         u32x4 v = hpre[i];
         if (has_gn) {
           const int hw = row % GB_HW, hr = (row / GB_HW) % GB_HH, hd = row / (GB_HW * GB_HH);
           const int zd = d0 - 1 + hd, zh = h0 - 1 + hr, zw = w0 - 1 + hw;
-          if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w) {
-            float f[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              f[2 * e] = __uint_as_float(v[e] << 16);
-              f[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = fmaxf(0.f, fmaf(f[e], gsc[0][ch * 8 + e], gsh[0][ch * 8 + e]));
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              v[e] = (uint32_t)from_f<bf16>(f[2 * e]) | ((uint32_t)from_f<bf16>(f[2 * e + 1]) << 16);
-          }
+          if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w)
+            v = gn_relu8(v, sc, sh);
         }
-        *reinterpret_cast<u32x4*>(hal + (ch * GB_NH + row) * 16) = v;
+        *reinterpret_cast<u32x4*>(hal + sch * GB_PS + row * 16) = v;
       }
     }
   };
@@ -204,7 +183,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
         bf16x8 a[2], bb[TN];
 #pragma unroll
         for (int tm = 0; tm < 2; ++tm)
-          a[tm] = *reinterpret_cast<const bf16x8*>(hal + (plane * GB_NH + arow[tm] + toff) * 16);
+          a[tm] = *reinterpret_cast<const bf16x8*>(hal + plane * GB_PS + (arow[tm] + toff) * 16);
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
           bb[tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
@@ -218,9 +197,8 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
     if (s + 1 < nsteps) {
       w_commit((s + 1) & 1);  // the other buffer: its readers finished before the previous barrier
       if (last_plane) {
-        __syncthreads();  // everyone done with this chunk's halo
         gn_table(s / 3 + 1);
-        __syncthreads();
+        __syncthreads();  // everyone done with this chunk's halo
         halo_commit();
       }
     }

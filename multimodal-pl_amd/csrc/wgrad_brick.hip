@@ -3,13 +3,13 @@
 //   dW[t][co][ci] = sum_{n, q}  dy[n, q, co] * A[n, q*s + t - 1, ci],   A = relu(gn(x)) (prologue)
 //
 // One workgroup (8 waves) owns a (32 co) x (32 ci) tile for ALL 27 taps and a range of output bricks
-// (BD x BH x 8 voxels). Per brick it stages the dy brick and the input halo brick ((BD-1)s+3 x (BH-1)s+3 x
-// 7s+3 voxels, GroupNorm+ReLU applied once per element) into LDS in their natural channel-contiguous layout,
-// then every wave runs the MFMA K loop (K = brick voxels) for its taps. Both operands need the voxel index
-// as the MFMA k dimension, i.e. a transposed read of channel-contiguous rows: ds_read_b64_tr_b16 gives it,
-// and because every lane supplies its own row address the 27 shifted tap windows of the halo are read with
-// no data movement (row address = brick voxel row + tap offset). The dy fragment is shared by all taps of a
-// wave. Reference: autograd of F.conv3d in Conv3d.forward (unet3D.py:27).
+// (BD x BH x BW voxels). Per brick the dy brick and the input halo brick ((BD-1)s+3 x (BH-1)s+3 x (BW-1)s+3
+// voxels, GroupNorm+ReLU applied once per element) sit in LDS in their natural channel-contiguous layout;
+// the next brick's dy + halo are prefetched into registers while the MFMAs run. Both MFMA operands need
+// the voxel index as the k dimension, i.e. a transposed read of channel-contiguous rows:
+// ds_read_b64_tr_b16 gives it, and because every lane supplies its own row address the 27 shifted tap
+// windows of the halo are read with no data movement (row address = brick voxel row + tap offset). The dy
+// fragment is shared by all taps of a wave. Reference: autograd of F.conv3d in Conv3d.forward (unet3D.py:27).
 #include "common.h"
 
 namespace u3d {
@@ -17,7 +17,6 @@ namespace u3d {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-
 struct WBGeom {
   int cin, cout, cin_p, cout_p;
   int id, ih, iw;
@@ -39,30 +38,32 @@ __device__ __forceinline__ bf16x8 frag_from(v4i16 lo, v4i16 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int BD, int BH, int S>
-__global__ __launch_bounds__(512) void wgrad_brick_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                                         const float* __restrict__ gstat,
-                                                         const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float* __restrict__ part,
-                                                         WBGeom g) {
-  constexpr int BW = 8, NV = BD * BH * BW, NKS = NV / 16;
+template <int BD, int BH, int BW, int S>
+__global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                            const float* __restrict__ gstat,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float* __restrict__ part,
+                                                            WBGeom g) {
+  constexpr int NV = BD * BH * BW, NKS = NV / 16;
   constexpr int HD = (BD - 1) * S + 3, HH = (BH - 1) * S + 3, HW = (BW - 1) * S + 3, NH = HD * HH * HW;
   constexpr int ROWB = 64;  // 32 bf16 channels per LDS row
   constexpr int NT = 512;
+  constexpr int RPP = NT / 4;                       // rows per pass (thread t: chunk t&3 of row t>>2)
+  constexpr int DYL = (NV + RPP - 1) / RPP;         // dy loads per thread
+  constexpr int HLL = (NH + RPP - 1) / RPP;         // halo loads per thread
+  static_assert(NV % 16 == 0, "brick voxels");
   __shared__ __attribute__((aligned(16))) char lds[(NV + NH) * ROWB];
-  __shared__ float gsc[32], gsh[32];
   char* dyt = lds;
   char* hal = lds + NV * ROWB;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = tid & 3, row0 = tid >> 2;  // fixed channel chunk per thread
   const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * 32;
   const long long b0 = (long long)blockIdx.z * g.per_split;
   const long long b1 = min(g.nbricks, b0 + g.per_split);
   const bool has_gn = gstat != nullptr;
-  const int cpg = has_gn ? g.cin / g.gn_groups : 1;
 
-  // taps owned by this wave: t = wave + 8j
-  constexpr int MAXT = 4;
+  constexpr int MAXT = 4;  // taps per wave: t = wave + 8j
   f32x16 acc[MAXT];
 #pragma unroll
   for (int j = 0; j < MAXT; ++j)
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(512) void wgrad_brick_kernel(const bf16* __restrict
   int tap_off[MAXT];
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
-    const int t = wave + 8 * j;
+    const int t = min(wave + 8 * j, 26);
     const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
     tap_off[j] = ((td * HH + th) * HW + tw) * ROWB;
   }
@@ -81,67 +82,84 @@ __global__ __launch_bounds__(512) void wgrad_brick_kernel(const bf16* __restrict
   const int h = lane >> 5, gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   const int colb = (16 * (gq & 1) + 4 * p) * 2;  // byte offset of this lane's 4 columns
 
-  int cur_n = -1;
-  for (long long b = b0; b < b1; ++b) {
+  u32x4 pdy[DYL], phl[HLL];
+  f32x2 sc[4], sh[4];
+  int gn_n = -1;
+
+  auto decode = [&](long long b, int& n, int& od0, int& oh0, int& ow0) {
     long long t = b;
     const int bw_ = (int)(t % g.nbw); t /= g.nbw;
     const int bh_ = (int)(t % g.nbh); t /= g.nbh;
     const int bd_ = (int)(t % g.nbd);
-    const int n = (int)(t / g.nbd);
-    const int od0 = bd_ * BD, oh0 = bh_ * BH, ow0 = bw_ * BW;
-    __syncthreads();  // previous brick's LDS reads done
-    if (has_gn && n != cur_n) {
-      if (tid < 32) {
-        const int c = ci0 + tid;
-        float s = 0.f, sh = 0.f;
-        if (c < g.cin) {
-          const int gg = c / cpg;
-          const float mean = gstat[(n * g.gn_groups + gg) * 2], rstd = gstat[(n * g.gn_groups + gg) * 2 + 1];
-          s = rstd * gamma[c];
-          sh = beta[c] - mean * s;
-        }
-        gsc[tid] = s;
-        gsh[tid] = sh;
-      }
-      cur_n = n;
-      __syncthreads();
-    }
-    // stage dy brick: NV rows x 4 chunks
-    for (int i = tid; i < NV * 4; i += NT) {
-      const int v = i >> 2, ch = i & 3;
-      const int vw = v % BW, vh = (v / BW) % BH, vd = v / (BW * BH);
-      const int zd = od0 + vd, zh = oh0 + vh, zw = ow0 + vw;
+    n = (int)(t / g.nbd);
+    od0 = bd_ * BD; oh0 = bh_ * BH; ow0 = bw_ * BW;
+  };
+  auto prefetch = [&](long long b) {
+    int n, od0, oh0, ow0;
+    decode(b, n, od0, oh0, ow0);
+#pragma unroll
+    for (int i = 0; i < DYL; ++i) {
+      const int v = row0 + i * RPP;
       u32x4 val = {0u, 0u, 0u, 0u};
-      const int co = co0 + ch * 8;
-      if (zd < g.od && zh < g.oh && zw < g.ow && co < g.cout)
+      const int vw = v % BW, vh = (v / BW) % BH, vd = v / (BW * BH);
+      const int zd = od0 + vd, zh = oh0 + vh, zw = ow0 + vw, co = co0 + ch * 8;
+      if (v < NV && zd < g.od && zh < g.oh && zw < g.ow && co < g.cout)
         val = *reinterpret_cast<const u32x4*>(dy + ((((long long)n * g.od + zd) * g.oh + zh) * g.ow + zw) * g.cout + co);
-      *reinterpret_cast<u32x4*>(dyt + v * ROWB + ch * 16) = val;
+      pdy[i] = val;
     }
-    // stage input halo with the GroupNorm+ReLU prologue; zero padding stays zero
-    const int id0 = od0 * S - 1, ih0 = oh0 * S - 1, iw0 = ow0 * S - 1;
-    for (int i = tid; i < NH * 4; i += NT) {
-      const int v = i >> 2, ch = i & 3;
+    const int id0 = od0 * S - 1, ih0 = oh0 * S - 1, iw0 = ow0 * S - 1, c = ci0 + ch * 8;
+#pragma unroll
+    for (int i = 0; i < HLL; ++i) {
+      const int v = row0 + i * RPP;
+      u32x4 val = {0u, 0u, 0u, 0u};
       const int hw = v % HW, hh = (v / HW) % HH, hd = v / (HW * HH);
       const int zd = id0 + hd, zh = ih0 + hh, zw = iw0 + hw;
-      const int c = ci0 + ch * 8;
-      float f[8];
-      if ((unsigned)zd < (unsigned)g.id && (unsigned)zh < (unsigned)g.ih && (unsigned)zw < (unsigned)g.iw && c < g.cin) {
-        load16<bf16>(x + ((((long long)n * g.id + zd) * g.ih + zh) * g.iw + zw) * g.cin + c, f);
-        if (has_gn) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = fmaxf(0.f, fmaf(f[e], gsc[ch * 8 + e], gsh[ch * 8 + e]));
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = 0.f;
-      }
-      store16<bf16>(reinterpret_cast<bf16*>(hal + v * ROWB + ch * 16), f);
+      if (v < NH && (unsigned)zd < (unsigned)g.id && (unsigned)zh < (unsigned)g.ih && (unsigned)zw < (unsigned)g.iw &&
+          c < g.cin)
+        val = *reinterpret_cast<const u32x4*>(x + ((((long long)n * g.id + zd) * g.ih + zh) * g.iw + zw) * g.cin + c);
+      phl[i] = val;
     }
-    __syncthreads();
+  };
+  auto commit = [&](long long b) {
+    int n, od0, oh0, ow0;
+    decode(b, n, od0, oh0, ow0);
+    if (has_gn && n != gn_n) {
+      gn_n = n;
+      gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, n, ci0 + ch * 8, sc, sh);
+    }
+#pragma unroll
+    for (int i = 0; i < DYL; ++i) {
+      const int v = row0 + i * RPP;
+      if (v < NV) *reinterpret_cast<u32x4*>(dyt + v * ROWB + ch * 16) = pdy[i];
+    }
+    const int id0 = od0 * S - 1, ih0 = oh0 * S - 1, iw0 = ow0 * S - 1;
+#pragma unroll
+    for (int i = 0; i < HLL; ++i) {
+      const int v = row0 + i * RPP;
+      if (v < NH) {
+        u32x4 val = phl[i];
+        if (has_gn) {
+          const int hw = v % HW, hh = (v / HW) % HH, hd = v / (HW * HH);
+          const int zd = id0 + hd, zh = ih0 + hh, zw = iw0 + hw;
+          if ((unsigned)zd < (unsigned)g.id && (unsigned)zh < (unsigned)g.ih && (unsigned)zw < (unsigned)g.iw)
+            val = gn_relu8(val, sc, sh);
+        }
+        *reinterpret_cast<u32x4*>(hal + v * ROWB + ch * 16) = val;
+      }
+    }
+  };
+
+  if (b0 < b1) {
+    prefetch(b0);
+    commit(b0);
+  }
+  __syncthreads();
+  for (long long b = b0; b < b1; ++b) {
+    const bool more = b + 1 < b1;
+    prefetch(more ? b + 1 : b);
     // K loop over the brick's voxels, 16 per MFMA
 #pragma unroll 2
     for (int ks = 0; ks < NKS; ++ks) {
-      // rows of this lane for reads m = 0, 1: brick voxel k = ks*16 + 8h + 4m + q
       int arow[2], hrow[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
@@ -159,6 +177,9 @@ __global__ __launch_bounds__(512) void wgrad_brick_kernel(const bf16* __restrict
         }
       }
     }
+    __syncthreads();  // everyone done with this brick's LDS
+    if (more) commit(b + 1);
+    __syncthreads();
   }
   // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h
   const int r = lane & 31;
@@ -180,15 +201,14 @@ __global__ __launch_bounds__(512) void wgrad_brick_kernel(const bf16* __restrict
 
 using namespace u3d;
 
-static int brick_dims(int stride, int* bd, int* bh) {
-  if (stride == 1) { *bd = 4; *bh = 4; }
-  else { *bd = 2; *bh = 4; }
-  return 8;
+static void brick_dims(int stride, int* bd, int* bh, int* bw) {
+  if (stride == 1) { *bd = 2; *bh = 8; *bw = 16; }
+  else { *bd = 2; *bh = 4; *bw = 8; }
 }
 
 extern "C" int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, int cout, int stride) {
-  int bd, bh;
-  const int bw = brick_dims(stride, &bd, &bh);
+  int bd, bh, bw;
+  brick_dims(stride, &bd, &bh, &bw);
   const int od = (d - 1) / stride + 1, oh = (h - 1) / stride + 1, ow = (w - 1) / stride + 1;
   const long long nb = (long long)n * cdiv(od, bd) * cdiv(oh, bh) * cdiv(ow, bw);
   const long long tiles = (long long)cdiv(cin, 32) * cdiv(cout, 32);
@@ -208,8 +228,8 @@ extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int ci
   g.cin = cin; g.cout = cout; g.cin_p = round_up(cin, 32); g.cout_p = round_up(cout, 32);
   g.id = d; g.ih = h; g.iw = w;
   g.od = (d - 1) / stride + 1; g.oh = (h - 1) / stride + 1; g.ow = (w - 1) / stride + 1;
-  int bd, bh;
-  const int bw = brick_dims(stride, &bd, &bh);
+  int bd, bh, bw;
+  brick_dims(stride, &bd, &bh, &bw);
   g.nbd = cdiv(g.od, bd); g.nbh = cdiv(g.oh, bh); g.nbw = cdiv(g.ow, bw);
   g.nbricks = (long long)n * g.nbd * g.nbh * g.nbw;
   g.per_split = (g.nbricks + nsplit - 1) / nsplit;
@@ -221,10 +241,10 @@ extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int ci
                            (size_t)(nsplit - ns_eff) * 27 * g.cout_p * g.cin_p * 4, s));
   dim3 grid(g.cin_p / 32, g.cout_p / 32, ns_eff);
   if (stride == 1)
-    hipLaunchKernelGGL((wgrad_brick_kernel<4, 4, 1>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats,
-                       gn_gamma, gn_beta, partials, g);
+    hipLaunchKernelGGL((wgrad_brick_kernel<2, 8, 16, 1>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
+                       gn_stats, gn_gamma, gn_beta, partials, g);
   else
-    hipLaunchKernelGGL((wgrad_brick_kernel<2, 4, 2>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats,
-                       gn_gamma, gn_beta, partials, g);
+    hipLaunchKernelGGL((wgrad_brick_kernel<2, 4, 8, 2>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
+                       gn_stats, gn_gamma, gn_beta, partials, g);
   return check_launch("wgrad_brick_kernel");
 }
