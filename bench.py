@@ -72,10 +72,24 @@ def dominant_kernel_roofline(device, batch, patch, reps=20):
     flops = 2.0 * batch * patch ** 3 * 27 * 32 * 32
     achieved = flops / (ms * 1e-3) / 1e12
     del y
-    return {"kernel": "igemm_kernel<bf16,bf16,128,32> (conv 32->32 3^3 s1 @%d^3, GN+ReLU prologue, residual)" % patch,
+    traffic, tsrc = pmc_traffic(batch, patch)
+    return {"kernel": "conv32_brick_kernel<false> (conv 32->32 3^3 s1 @%d^3, GN+ReLU prologue, residual)" % patch,
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None, "avg_launch_ms": round(ms, 4),
-            "flop_per_launch": flops}
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+            "traffic_source": tsrc, "algorithmic_bytes": 3 * batch * patch ** 3 * 32 * 2,
+            "avg_launch_ms": round(ms, 4), "flop_per_launch": flops}
+
+
+def pmc_traffic(batch, patch):
+    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
+    (profiles/rNN_pmc_conv32_fwd.json, made by tools/pmc_traffic.py: 2*FETCH_SIZE + WRITE_SIZE, gfx950
+    FETCH_SIZE correction). Only valid for the configuration it was measured on (2x96^3)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_conv32_fwd.json")))
+    if not files or (batch, patch) != (2, 96):
+        return None, None
+    with open(files[-1]) as f:
+        return int(json.load(f)["traffic_bytes"]), os.path.relpath(files[-1], REPO)
 
 
 def cpu_baseline(patch):
