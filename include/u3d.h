@@ -49,6 +49,24 @@ int u3d_wstd_fwd(int dtype, const float* w, int cout, int cin, int ksize, int st
 int u3d_wstd_bwd(float* dwpk_partials, int nsplit, const float* w, const float* wstats, int cout, int cin,
                  int ksize, int standardize, float* dw, int accumulate, u3d_stream_t stream);
 
+/* Batched forms: every conv of the trunk in one launch (Conv3d.forward of each module, unet3D.py:21-27).
+ * Forward uses w, wpk_fwd, wpk_dgrad (nullable), wstats (required when standardize), cout, cin, ksize,
+ * standardize. Backward uses part/nsplit (summed in place into slab 0), w, wstats, dw, accumulate. */
+typedef struct u3d_wstd_desc {
+  const float* w;
+  void* wpk_fwd;
+  void* wpk_dgrad;
+  float* wstats;
+  float* part;
+  float* dw;
+  int cout, cin, ksize, standardize, nsplit, accumulate;
+} u3d_wstd_desc;
+#define U3D_WSTD_BATCH_MAX 48
+int u3d_wstd_fwd_batch(int dtype, const u3d_wstd_desc* descs, int count, u3d_stream_t stream);
+/* scratch: device fp32 buffer of u3d_wstd_bwd_scratch_bytes(descs, count) bytes (per-row sums) */
+long long u3d_wstd_bwd_scratch_bytes(const u3d_wstd_desc* descs, int count);
+int u3d_wstd_bwd_batch(const u3d_wstd_desc* descs, int count, float* scratch, u3d_stream_t stream);
+
 /* ---------------------------------------------------------------- 3-D convolution (A1-A3, A7)
  * F.conv3d(relu(group_norm(x)), W_hat, bias, stride, pad=k//2) (unet3D.py:27, 44-53, 1640-1657) as one
  * MFMA implicit GEMM: M = output voxels, N = cout, K = k^3 * cin. If gn_stats != NULL the GroupNorm

@@ -139,7 +139,7 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
-inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+__host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 }  // namespace u3d

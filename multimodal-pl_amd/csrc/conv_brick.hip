@@ -42,8 +42,11 @@ __global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __re
                                                                const float* __restrict__ gstat,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta, CBGeom g) {
-  __shared__ __attribute__((aligned(16))) char hal[4 * CB_PS];
-  __shared__ __attribute__((aligned(16))) char wts[4 * CB_NWR * 16];
+  // one LDS object: halo image | weights | per-wave epilogue tile (32 voxels x 64 B)
+  __shared__ __attribute__((aligned(16))) char smem[4 * CB_PS + 4 * CB_NWR * 16 + 8 * 2048];
+  char* const hal = smem;
+  char* const wts = smem + 4 * CB_PS;
+  char* const ept = smem + 4 * CB_PS + 4 * CB_NWR * 16 + (threadIdx.x >> 6) * 2048;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int ch = tid & 3, row0 = tid >> 2;  // staging: fixed 8-channel chunk per thread, rows row0 + 128 i
@@ -66,57 +69,74 @@ __global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __re
     nn = t / g.nbd;
     d0 = bd_ * CB_BD; h0 = bh_ * CB_BH; w0 = bw_ * CB_BW;
   };
-  // 4 consecutive threads read the 64 B (32 channels) of one voxel: fully coalesced loads
+  // 4 consecutive threads read the 64 B (32 channels) of one voxel: fully coalesced loads. vmask bit i =
+  // halo row i of this thread lies inside the volume (GN applies there; padding stays zero).
+  unsigned vmask = 0;
   auto prefetch = [&](int b) {
     int nn, d0, h0, w0;
     brick_origin(b, nn, d0, h0, w0);
+    int rb = row0;
+    asm volatile("" : "+v"(rb));  // keep the row decomposition in the loop (no hoisted, spilled invariants)
+    unsigned m = 0;
 #pragma unroll
     for (int i = 0; i < CB_LD; ++i) {
-      const int row = row0 + i * (CB_NT / 4);
+      const int row = rb + i * (CB_NT / 4);
       u32x4 v = {0u, 0u, 0u, 0u};
       if (row < CB_NH) {
         const int hw = row % CB_HW, hh = (row / CB_HW) % CB_HH, hd = row / (CB_HW * CB_HH);
         const int zd = d0 - 1 + hd, zh = h0 - 1 + hh, zw = w0 - 1 + hw;
-        if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w)
+        if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w) {
           v = *reinterpret_cast<const u32x4*>(x + ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * 32 + ch * 8);
+          m |= 1u << i;
+        }
       }
       pre[i] = v;
     }
+    vmask = m;
   };
   auto commit = [&](int b) {
-    int nn, d0, h0, w0;
-    brick_origin(b, nn, d0, h0, w0);
-    if (has_gn && nn != gn_n) {
-      gn_n = nn;
-      gn_coef8(gstat, gamma, beta, g.gn_groups, 32, nn, ch * 8, sc, sh);
+    if (has_gn) {
+      int t = b / (g.nbw * g.nbh * g.nbd);
+      if (t != gn_n) {
+        gn_n = t;
+        gn_coef8(gstat, gamma, beta, g.gn_groups, 32, t, ch * 8, sc, sh);
+      }
     }
 #pragma unroll
     for (int i = 0; i < CB_LD; ++i) {
       const int row = row0 + i * (CB_NT / 4);
       if (row < CB_NH) {
         u32x4 v = pre[i];
-        if (has_gn) {
-          const int hw = row % CB_HW, hh = (row / CB_HW) % CB_HH, hd = row / (CB_HW * CB_HH);
-          const int zd = d0 - 1 + hd, zh = h0 - 1 + hh, zw = w0 - 1 + hw;
-          if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w)
-            v = gn_relu8(v, sc, sh);
-        }
+        if (has_gn && ((vmask >> i) & 1u)) v = gn_relu8(v, sc, sh);
         *reinterpret_cast<u32x4*>(hal + ch * CB_PS + row * 16) = v;
       }
     }
   };
 
-  int b = blockIdx.x;
-  if (b >= g.nbricks) return;
+  // XCD-aware brick order: with a full 256-WG grid, XCD x (= blockIdx % 8) walks one contiguous eighth of
+  // the bricks, so the 32 bricks it runs at a time are spatial neighbours and their shared halo rows hit
+  // its L2 instead of being fetched once per XCD.
+  int b, bend, bstep;
+  if (gridDim.x == 256) {
+    const int per = (g.nbricks + 7) >> 3, xcd = blockIdx.x & 7;
+    b = xcd * per + (blockIdx.x >> 3);
+    bend = min(g.nbricks, (xcd + 1) * per);
+    bstep = 32;
+  } else {
+    b = blockIdx.x;
+    bend = g.nbricks;
+    bstep = gridDim.x;
+  }
+  if (b >= bend) return;
   prefetch(b);
   commit(b);
   __syncthreads();
   // per-lane fragment bases: A row of tap (0,0,0) for w-row tm: ((tm)*HH + wave)*HW + r ; plane (2s + h)
   const char* abase = hal + h * CB_PS + (wave * CB_HW + r) * 16;
   const char* bbase = wts + (h * CB_NWR + r) * 16;
-  for (; b < g.nbricks; b += gridDim.x) {
-    const int bn = b + gridDim.x;
-    const bool more = bn < g.nbricks;
+  for (; b < bend; b += bstep) {
+    const int bn = b + bstep;
+    const bool more = bn < bend;
     prefetch(more ? bn : b);  // unconditional: keeps the prefetch registers phi-free (no copies, no early wait)
     int nn, d0, h0, w0;
     brick_origin(b, nn, d0, h0, w0);
@@ -148,25 +168,48 @@ __global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __re
       ca1 = na1;
       cb = nb;
     }
+    // residual of this brick's two w-rows: 16-B chunks q = lane + 64 u of each row (in flight during commit)
+    u32x4 rv[2][2];
+    const long long orow[2] = {(((long long)nn * g.d + d0) * g.h + h0 + wave) * g.w + w0,
+                               (((long long)nn * g.d + d0 + 1) * g.h + h0 + wave) * g.w + w0};
+    const bool ok[2] = {d0 < g.d && h0 + wave < g.h, d0 + 1 < g.d && h0 + wave < g.h};
+    if (res) {
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          rv[tm][u] = ok[tm] ? *reinterpret_cast<const u32x4*>(res + orow[tm] * 32 + (lane + 64 * u) * 8)
+                             : u32x4{0u, 0u, 0u, 0u};
+    }
     __syncthreads();  // all waves done reading the halo before it is overwritten
     if (more) commit(bn);
-    // epilogue: lane column co = r; rows w = (i&3) + 8(i>>2) + 4h of w-row (d0+tm, h0+wave)
+    // epilogue through the wave's LDS tile: lane column co = r, rows w = (i&3) + 8(i>>2) + 4h of w-row
+    // (d0+tm, h0+wave) -> [w][co] bf16, read back as 16-B chunks (one fully coalesced 1 KB store per row half)
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
-      const int zd = d0 + tm, zh = h0 + wave;
-      if (zd < g.d && zh < g.h) {
-        const long long rowbase = (((long long)nn * g.d + zd) * g.h + zh) * g.w;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int zw = w0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (zw < g.w) {
-            const long long off = (rowbase + zw) * 32 + r;
-            float v = tm ? acc1[i] : acc0[i];
-            if (res) v += to_f(res[off]);
-            y[off] = from_f<bf16>(v);
-          }
-        }
+      for (int i = 0; i < 16; ++i) {
+        const int w = (i & 3) + 8 * (i >> 2) + 4 * h;
+        *reinterpret_cast<bf16*>(ept + w * 64 + r * 2) = from_f<bf16>(tm ? acc1[i] : acc0[i]);
       }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int q = lane + 64 * u;
+        u32x4 v = *reinterpret_cast<const u32x4*>(ept + q * 16);
+        if (res) {
+          float a[8], c[8];
+          load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
+          load16<bf16>(reinterpret_cast<const bf16*>(&rv[tm][u]), c);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] += c[e];
+          store16<bf16>(reinterpret_cast<bf16*>(&v), a);
+        }
+        if (ok[tm]) *reinterpret_cast<u32x4*>(y + orow[tm] * 32 + q * 8) = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
     }
     __syncthreads();
   }

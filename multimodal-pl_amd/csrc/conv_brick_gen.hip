@@ -31,6 +31,7 @@ struct GBGeom {
   int cin, cout, cin_p, cout_p;
   int nbd, nbh, nbw;
   int gn_groups;
+  int nct;
 };
 
 // MFMA row r (0..31) -> (segment = which of the 2 h-rows, position = w): the 16 lanes of each ds_read_b128
@@ -61,13 +62,21 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  int b = blockIdx.x;
+  // XCD-aware order: linear id i runs on XCD i % 8; remap so each XCD owns a contiguous range of
+  // (brick, co tile) pairs -> concurrently running neighbours share halo rows through that XCD's L2.
+  const int nwg = gridDim.x, nct = g.nct;
+  int bid;
+  {
+    const int q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  int b = bid / nct;
   const int bw_ = b % g.nbw; b /= g.nbw;
   const int bh_ = b % g.nbh; b /= g.nbh;
   const int bd_ = b % g.nbd;
   const int nn = b / g.nbd;
   const int d0 = bd_ * GB_BD, h0 = bh_ * GB_BH, w0 = bw_ * GB_BW;
-  const int co0 = blockIdx.y * CO;
+  const int co0 = (bid - (bid / nct) * nct) * CO;
   const bool has_gn = gstat != nullptr;
   const int nchunk = g.cin_p / 32;
   const int nsteps = nchunk * 3;
@@ -205,28 +214,66 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
     __syncthreads();
   }
 
-  // epilogue: lane column co = co0 + tn*32 + r; row i -> (h-row seg, w pos) of row tile tm
+  // epilogue through LDS (the halo image is free now): the wave's tile [tm][h-row seg][w pos][co] bf16 is
+  // written by MFMA lane layout and read back as 16-B chunks, 8 lanes per voxel: coalesced stores / residual.
+  constexpr int VB = CO * 2;  // bytes per voxel in the tile
+  char* const ept = hal + wave * (2 * 32 * VB);
+  u32x4 rv[2][VB / 32];
+  long long obase[2];
+  bool dok[2];
 #pragma unroll
   for (int tm = 0; tm < 2; ++tm) {
     const int rt = 2 * wave + tm, zd = d0 + (rt >> 2);
-    if (zd >= g.d) continue;
+    dok[tm] = zd < g.d;
+    obase[tm] = (((long long)nn * g.d + zd) * g.h + h0 + 2 * (rt & 3)) * g.w + w0;
+  }
+  auto chunk_ok = [&](int tm, int q, long long& off) {
+    const int v = q / (VB / 16), c = q % (VB / 16);
+    const int seg = v >> 4, pos = v & 15;
+    const int rt = 2 * wave + tm, zh = h0 + 2 * (rt & 3) + seg, zw = w0 + pos, co = co0 + c * 8;
+    off = (obase[tm] + (long long)seg * g.w + pos) * g.cout + co;
+    return dok[tm] && zh < g.h && zw < g.w && co < g.cout;
+  };
+  if (res) {
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-      const int co = co0 + tn * 32 + r;
-      if (co >= g.cout) continue;
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int u = 0; u < VB / 32; ++u) {
+        long long off;
+        rv[tm][u] = chunk_ok(tm, lane + 64 * u, off) ? *reinterpret_cast<const u32x4*>(res + off)
+                                                      : u32x4{0u, 0u, 0u, 0u};
+      }
+  }
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int ri = (i & 3) + 8 * (i >> 2) + 4 * hh;
-        const int zh = h0 + 2 * (rt & 3) + gb_seg(ri), zw = w0 + gb_pos(ri);
-        if (zh < g.h && zw < g.w) {
-          const long long off = ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cout + co;
-          float v = acc[tm][tn][i];
-          if (res) v += to_f(res[off]);
-          y[off] = from_f<bf16>(v);
-        }
+        const int v = gb_seg(ri) * 16 + gb_pos(ri);
+        *reinterpret_cast<bf16*>(ept + (tm * 32 + v) * VB + (tn * 32 + r) * 2) = from_f<bf16>(acc[tm][tn][i]);
       }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int u = 0; u < VB / 32; ++u) {
+      const int q = lane + 64 * u;
+      long long off;
+      if (!chunk_ok(tm, q, off)) continue;
+      u32x4 v = *reinterpret_cast<const u32x4*>(ept + tm * 32 * VB + q * 16);
+      if (res) {
+        float a[8], c[8];
+        load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
+        load16<bf16>(reinterpret_cast<const bf16*>(&rv[tm][u]), c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += c[e];
+        store16<bf16>(reinterpret_cast<bf16*>(&v), a);
+      }
+      *reinterpret_cast<u32x4*>(y + off) = v;
     }
-  }
 }
 
 }  // namespace u3d
@@ -247,7 +294,8 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
   const int nb = n * g.nbd * g.nbh * g.nbw;
   hipStream_t s = (hipStream_t)stream;
   const bool co64 = g.cout_p >= 64;
-  dim3 grid(nb, co64 ? cdiv(cout, 64) : 1);
+  g.nct = co64 ? cdiv(cout, 64) : 1;
+  dim3 grid(nb * g.nct);
   if (co64) {
     if (flip)
       hipLaunchKernelGGL((convg_brick_kernel<64, true>), grid, dim3(GB_NT), 0, s, (const bf16*)x, (const bf16*)wpk,

@@ -17,6 +17,9 @@ _SIGS = {
     "u3d_abi_version": [],
     "u3d_wstd_fwd": [I, P, I, I, I, I, P, P, P, P],
     "u3d_wstd_bwd": [P, I, P, P, I, I, I, I, P, I, P],
+    "u3d_wstd_fwd_batch": [I, P, I, P],
+    "u3d_wstd_bwd_batch": [P, I, P, P],
+    "u3d_wstd_bwd_scratch_bytes": [P, I],
     "u3d_conv_fwd": [I, P, I, I, I, I, I, P, I, I, I, P, P, P, I, P, P, P, I, P, L, P],
     "u3d_conv_dgrad": [I, P, I, I, P, I, I, I, I, I, I, P, P, L, P],
     "u3d_conv_wgrad_splits": [I, I, I, I, I, I, I, I],
@@ -45,9 +48,18 @@ _SIGS = {
     "u3d_dyn_controller": [P, I, I, P, I, P, P, I, P, P],
     "u3d_dynhead_fwd": [P, P, I, L, P, P],
 }
-_RESTYPE = {"u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L}
+_RESTYPE = {"u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L}
 
 _lib = None
+
+
+class WstdDesc(ctypes.Structure):
+    """u3d_wstd_desc (include/u3d.h)."""
+    _fields_ = [("w", P), ("wpk_fwd", P), ("wpk_dgrad", P), ("wstats", P), ("part", P), ("dw", P),
+                ("cout", I), ("cin", I), ("ksize", I), ("standardize", I), ("nsplit", I), ("accumulate", I)]
+
+
+WSTD_BATCH_MAX = 48
 
 
 class U3DError(RuntimeError):

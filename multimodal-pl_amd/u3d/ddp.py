@@ -75,6 +75,17 @@ class GradBucketer:
         op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
         self.works[b] = dist.all_reduce(self.bufs[b], op=op, group=self.group, async_op=True)
 
+    def needs_flush(self, pending):
+        """True if producing the ``pending`` gradients would complete a bucket (so they must be written now)."""
+        if not self.active:
+            return False
+        cnt = {}
+        for n in pending:
+            if n in self.where and n not in self.done_names:
+                b = self.where[n][0]
+                cnt[b] = cnt.get(b, 0) + 1
+        return any(self.left[b] == c for b, c in cnt.items())
+
     def done(self, name):
         if not self.active or name not in self.where or name in self.done_names:
             return

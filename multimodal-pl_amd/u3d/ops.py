@@ -1,5 +1,7 @@
 """Tensor-level wrappers over the libu3d C ABI. Torch is only the allocator / stream provider here: every
 value is computed by a HIP kernel. All activations are NDHWC tensors of shape [n, d, h, w, c]."""
+import ctypes
+
 import torch
 
 from . import _lib
@@ -67,6 +69,61 @@ def wstd_fwd(w, dtype, standardize=True, need_dgrad=True):
     call("u3d_wstd_fwd", dt_code(dtype), w.data_ptr(), cout, cin, k, int(standardize), pf.data_ptr(), _ptr(pd),
          _ptr(st), _stream())
     return pf, pd, st
+
+
+def wstd_fwd_batch(items, dtype):
+    """Batched wstd_fwd over [(w, standardize, need_dgrad)]: one launch per 48 convs; packs and stats are
+    views of three flat buffers. Returns [(pf, pd, st)] in item order."""
+    if not items:
+        return []
+    dev = items[0][0].device
+    shp = []
+    nf = ns = 0
+    for w, std, nd in items:
+        require_device(w)
+        cout, cin, k = w.shape[0], w.shape[1], w.shape[2]
+        n = k ** 3 * round32(cout) * round32(cin)
+        shp.append((cout, cin, k, n))
+        nf += n * (2 if nd else 1)
+        ns += 2 * cout if std else 0
+    buf = torch.empty((nf,), dtype=dtype, device=dev)
+    sbuf = torch.empty((max(ns, 1),), dtype=torch.float32, device=dev)
+    out, descs = [], []
+    of = os_ = 0
+    for (w, std, nd), (cout, cin, k, n) in zip(items, shp):
+        pf = buf[of:of + n].view(k ** 3, round32(cout), round32(cin))
+        of += n
+        pd = None
+        if nd:
+            pd = buf[of:of + n].view(k ** 3, round32(cin), round32(cout))
+            of += n
+        st = None
+        if std:
+            st = sbuf[os_:os_ + 2 * cout].view(cout, 2)
+            os_ += 2 * cout
+        out.append((pf, pd, st))
+        descs.append(_lib.WstdDesc(w.data_ptr(), pf.data_ptr(), _ptr(pd), _ptr(st), None, None, cout, cin, k,
+                                   int(std), 1, 0))
+    for i in range(0, len(descs), _lib.WSTD_BATCH_MAX):
+        chunk = descs[i:i + _lib.WSTD_BATCH_MAX]
+        arr = (_lib.WstdDesc * len(chunk))(*chunk)
+        call("u3d_wstd_fwd_batch", dt_code(dtype), ctypes.addressof(arr), len(chunk), _stream())
+    return out
+
+
+def wstd_bwd_batch(items):
+    """Batched wstd_bwd over [(partials, nsplit, w, wstats, standardize, dw, accumulate)]."""
+    descs = [_lib.WstdDesc(w.data_ptr(), None, None, _ptr(st), part.data_ptr(), dw.data_ptr(), w.shape[0],
+                           w.shape[1], w.shape[2], int(std), ns, int(acc))
+             for part, ns, w, st, std, dw, acc in items]
+    if not descs:
+        return
+    dev = items[0][2].device
+    for i in range(0, len(descs), _lib.WSTD_BATCH_MAX):
+        chunk = descs[i:i + _lib.WSTD_BATCH_MAX]
+        arr = (_lib.WstdDesc * len(chunk))(*chunk)
+        ws = WS.get(query("u3d_wstd_bwd_scratch_bytes", ctypes.addressof(arr), len(chunk)), dev, slot=5)
+        call("u3d_wstd_bwd_batch", ctypes.addressof(arr), len(chunk), ws.data_ptr(), _stream())
 
 
 def wstd_bwd(partials, nsplit, w, wstats, standardize, dw=None, accumulate=False):

@@ -45,6 +45,37 @@ class Tape:
         self.ops = []
         self.sink = None
         self.std = True
+        self.pending = []   # weight grads waiting for the batched standardisation backward
+
+    def prepack(self, plan):
+        """Standardise + pack every conv weight of ``plan`` [(key, standardize, need_dgrad)] in one launch."""
+        todo = [(k, s, d and self.record) for k, s, d in plan if k not in self.packs and k + ".weight" in self.P]
+        res = ops.wstd_fwd_batch([(self.P[k + ".weight"], s, d) for k, s, d in todo], self.dtype)
+        for (k, _, _), r in zip(todo, res):
+            self.packs[k] = r
+
+    def conv_plan(self, cfg):
+        """The convs trunk()/head() run: (key, standardize, need_dgrad). Absent keys are skipped."""
+        std = cfg.weight_std
+        plan = [("conv0", std, False), ("conv1", std, True)] if cfg.conv0 else [("conv1", std, False)]
+        blocks = [f"layer{i}.{b}." for i in range(5) for b in range(cfg.layers[i])]
+        blocks += [n + ".0." for n in ("x8_resb", "x4_resb", "x2_resb", "x1_resb")]
+        for pre in blocks:
+            plan += [(pre + c, std, True) for c in ("conv1", "downsample.2", "conv2")]
+        plan += [("fusionConv.2", std, True), ("precls_conv.2", False, True)]
+        return plan
+
+    def pend_wgrad(self, part, ns, W, st, std, name):
+        self.pending.append((part, ns, W, st, std, self.grad_out(name, W), False, name))
+
+    def flush_wgrads(self):
+        if not self.pending:
+            return
+        ops.wstd_bwd_batch([p[:7] for p in self.pending])
+        names = [p[7] for p in self.pending]
+        self.pending = []
+        for n in names:
+            self.grad_done(n)
 
     # ------------------------------------------------------------------ helpers
     def packed(self, key, standardize, need_dgrad=True):
@@ -88,8 +119,7 @@ class Tape:
                 if out.grad is None:
                     return
                 part, ns = ops.stem_wgrad(out.grad, x, stride)
-                ops.wstd_bwd(part, ns, W, st, self.std, dw=self.grad_out(key + ".weight", W))
-                self.grad_done(key + ".weight")
+                self.pend_wgrad(part, ns, W, st, self.std, key + ".weight")
             self.ops.append(bwd)
         return out
 
@@ -118,8 +148,7 @@ class Tape:
                     self.acc_grad(residual, dy)
                 dyT = ops.cast(dy, self.dtype, pad_to=8)  # GEMM operand: channels padded to 8 (2-class head)
                 part, ns = ops.conv_wgrad(dyT, x.t, k, stride, gn)
-                ops.wstd_bwd(part, ns, W, st, std, dw=self.grad_out(key + ".weight", W))
-                self.grad_done(key + ".weight")
+                self.pend_wgrad(part, ns, W, st, std, key + ".weight")
                 dA = ops.conv_dgrad(dyT, pd, cin, x.t.shape[:4], k, stride)
                 if gn is not None:
                     dg = self.grad_out(gn_key + ".weight", gn[1])
@@ -159,6 +188,7 @@ class Tape:
     # ------------------------------------------------------------------ graph
     def trunk(self, x, cfg):
         self.std = cfg.weight_std
+        self.prepack(self.conv_plan(cfg))
         if cfg.conv0:
             t = self.stem(x, "conv0", 2)
             t = self.gn_conv(t, "conv1", 3, 1)
@@ -188,6 +218,9 @@ class Tape:
         out_act.grad = grad
         for fn in reversed(self.ops):
             fn()
+            if self.pending and self.sink is not None and self.sink.needs_flush([p[7] for p in self.pending]):
+                self.flush_wgrads()
+        self.flush_wgrads()
         self.ops = []
 
 

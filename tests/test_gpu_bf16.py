@@ -41,7 +41,8 @@ def _act_ref(x, st, ga, be, G):
 
 
 SHAPES = [(2, 32, 32, (12, 10, 16), 1), (1, 32, 32, (5, 9, 70), 1), (1, 32, 64, (8, 12, 18), 2), (2, 64, 64, (6, 8, 9), 1),
-          (1, 64, 32, (10, 6, 8), 1), (2, 128, 128, (4, 4, 4), 1), (1, 24, 24, (7, 9, 11), 1)]
+          (1, 64, 32, (10, 6, 8), 1), (2, 128, 128, (4, 4, 4), 1), (1, 24, 24, (7, 9, 11), 1),
+          (2, 32, 32, (4, 10, 64), 1), (1, 32, 32, (3, 8, 32), 1), (1, 64, 128, (6, 9, 20), 1)]
 
 
 @pytest.fixture(params=["auto", "gen_brick", "igemm"])
@@ -62,10 +63,12 @@ def test_bf16_conv_fwd(gpu, conv_path, n, cin, cout, dims, s):
     from u3d import ops
     x, w, st, ga, be, G = _case(gpu, n, cin, cout, dims, True, 1)
     pf, pd, wst = ops.wstd_fwd(w, torch.bfloat16, True)
-    y = ops.conv_fwd(x, pf, cout, 3, s, (st, ga, be, G))
+    od = tuple(ops.out_dim(d, 3, s) for d in dims)
+    res = torch.randn((n,) + od + (cout,), device=gpu).to(torch.bfloat16)
+    y = ops.conv_fwd(x, pf, cout, 3, s, (st, ga, be, G), residual=res)
     a = _act_ref(x, st, ga, be, G).permute(0, 4, 1, 2, 3)
     wq = pf.float().cpu()[:, :cout, :cin].permute(1, 2, 0).reshape(cout, cin, 3, 3, 3).double()
-    ref = F.conv3d(a, wq, stride=s, padding=1).permute(0, 2, 3, 4, 1)
+    ref = F.conv3d(a, wq, stride=s, padding=1).permute(0, 2, 3, 4, 1) + res.double().cpu()
     err = (y.double().cpu() - ref).abs().max().item()
     assert err < 1e-2 * ref.abs().max().item(), err
 
@@ -116,3 +119,34 @@ def test_bf16_gn_bwd_and_upsample(gpu):
     y = ops.upsample2x_add(x)
     ref = F.interpolate(x.float().cpu().permute(0, 4, 1, 2, 3), scale_factor=2, mode="trilinear")
     assert (y.float().cpu().permute(0, 4, 1, 2, 3) - ref).abs().max() < 1e-2 * ref.abs().max()
+
+
+def test_wstd_batch_matches_single(gpu):
+    """Batched weight standardisation (one launch for every conv) == the per-conv kernels."""
+    from u3d import ops
+    torch.manual_seed(5)
+    shapes = [(32, 1, 3, True), (32, 32, 3, True), (64, 32, 3, True), (64, 32, 1, True), (320, 256, 3, True),
+              (8, 32, 1, False), (24, 40, 3, True)]
+    ws = [torch.randn(co, ci, k, k, k, device=gpu) * 0.1 + 0.01 for co, ci, k, _ in shapes]
+    for dt in (torch.float32, torch.bfloat16):
+        outs = ops.wstd_fwd_batch([(w, std, ci > 4) for w, (co, ci, k, std) in zip(ws, shapes)], dt)
+        for w, (co, ci, k, std), (pf, pd, st) in zip(ws, shapes, outs):
+            pf1, pd1, st1 = ops.wstd_fwd(w, dt, std, need_dgrad=ci > 4)
+            tol = 1e-6 if dt == torch.float32 else 1e-2
+            assert (pf.float() - pf1.float()).abs().max().item() <= tol * pf1.float().abs().max().item()
+            if pd1 is not None:
+                assert torch.equal(pd.float().permute(0, 2, 1), pf.float())
+            if std:
+                assert torch.allclose(st, st1, rtol=1e-6, atol=1e-7)
+    # backward: random split slabs, nsplit 1 / 3 / 37
+    items, refs = [], []
+    for (w, (co, ci, k, std)), ns in zip(zip(ws, shapes), [1, 3, 37, 2, 5, 1, 4]):
+        _, _, st = ops.wstd_fwd(w, torch.float32, std, need_dgrad=False)
+        part = torch.randn((ns, k ** 3, ops.round32(co), ops.round32(ci)), device=gpu)
+        ref = ops.wstd_bwd(part.clone(), ns, w, st, std)
+        dw = torch.empty_like(w)
+        items.append((part, ns, w, st, std, dw, False))
+        refs.append(ref)
+    ops.wstd_bwd_batch(items)
+    for (part, ns, w, st, std, dw, _), ref in zip(items, refs):
+        assert (dw - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()

@@ -5,7 +5,26 @@ import sys
 
 d = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
-rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+import glob
+import os
+import sqlite3
+
+
+def load(d):
+    """Kernel dispatch rows from a rocprofv3 output dir: csv (run_kernel_trace.csv) or the rocpd SQLite db."""
+    if os.path.exists(f"{d}/run_kernel_trace.csv"):
+        return list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+    out = []
+    for db in glob.glob(f"{d}/**/*.db", recursive=True):
+        c = sqlite3.connect(db)
+        for name, st, en, gx, gy, gz, wx in c.execute(
+                "select name, start, end, grid_x, grid_y, grid_z, workgroup_x from kernels"):
+            out.append({"Kernel_Name": name, "Start_Timestamp": st, "End_Timestamp": en, "Grid_Size_X": gx,
+                        "Grid_Size_Y": gy, "Grid_Size_Z": gz, "Workgroup_Size_X": wx})
+    return out
+
+
+rows = load(d)
 tot = collections.defaultdict(float)
 grp = collections.defaultdict(lambda: [0, 0.0])
 for r in rows:
