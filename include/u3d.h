@@ -112,10 +112,19 @@ int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int cin, int d, i
                          const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                          float* partials, int nsplit, u3d_stream_t stream);
 
+/* bf16 1^3 weight gradient (downsample convs, fusion / classifier heads; stride 1 or 2), same slab layout
+ * [nsplit][1][cout_p][cin_p]; streams 512-voxel chunks, memory-bound (nsplit from u3d_conv_wgrad1_splits). */
+int u3d_conv_wgrad1_splits(int n, int cin, int d, int h, int w, int cout, int stride);
+int u3d_conv_wgrad1(const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout, int stride,
+                    const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                    float* partials, int nsplit, u3d_stream_t stream);
+
 /* Stem conv with cin <= 4 (conv1 1->32, unet3D.py:1632; conv0 2->f stride 2, :1514): fp32 NCDHW input,
  * direct VALU conv (K = 27*cin is too short for MFMA), NDHWC output. */
 int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                  int stride, void* y, u3d_stream_t stream);
+/* split count for u3d_stem_wgrad given its dtype/channels (the bf16 1->32 stride-1 stem runs on MFMA) */
+int u3d_stem_wgrad_splits2(int dtype, int n, int cin, int d, int h, int w, int cout, int stride);
 int u3d_stem_wgrad_splits(int n, int d, int h, int w, int stride);
 int u3d_stem_wgrad(int dtype, const void* dy, const float* x, int n, int cin, int d, int h, int w, int cout,
                    int stride, float* partials, int nsplit, u3d_stream_t stream);

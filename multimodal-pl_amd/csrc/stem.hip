@@ -117,6 +117,136 @@ __global__ __launch_bounds__(ST) void stem_wgrad_kernel(const T* __restrict__ dy
   }
 }
 
+
+// MFMA weight gradient of the 1-channel stride-1 stem (conv1 1->32 of unet3D_baseline / unet3D at 96^3):
+//   dW[co][t] = sum_v dy[v][co] * x[v + off(t)]   (M = co, N = 27 taps padded to 32, K = voxels)
+// A workgroup walks 2 x 8 x 32-voxel bricks of its split; per brick the dy brick (32 KB, read transposed
+// with ds_read_b64_tr_b16) and the fp32 input halo (4 x 10 x 34) sit in LDS. A k-step = 16 consecutive w
+// voxels of one row, so the B fragment of tap t is 8 consecutive halo values of the shifted row. The 8
+// per-wave tiles are summed in fixed order at the end; the slab rows ci > 0 are written as zeros.
+constexpr int SM_BD = 2, SM_BH = 8, SM_BW = 32, SM_NV = SM_BD * SM_BH * SM_BW;
+constexpr int SM_HD = SM_BD + 2, SM_HH = SM_BH + 2, SM_HW = SM_BW + 2, SM_NH = SM_HD * SM_HH * SM_HW;
+
+typedef short sm_v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) sm_v4i16 sm_lds_v4i16;
+typedef __attribute__((ext_vector_type(8))) __bf16 sm_bf16x8;
+
+__device__ __forceinline__ sm_v4i16 sm_tr_read(const char* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (sm_lds_v4i16*)((__attribute__((address_space(3))) char*)base + off));
+}
+
+__global__ __launch_bounds__(512, 1) void stem_wgrad_mfma_kernel(const bf16* __restrict__ dy,
+                                                                const float* __restrict__ x,
+                                                                float* __restrict__ part, int n, int d, int h, int w,
+                                                                int nbh, int nbw, int nbricks, int per_split) {
+  constexpr int ROWB = 64, NT = 512, RPP = NT / 4, DYL = SM_NV / RPP, HLL = (SM_NH + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) char lds[SM_NV * ROWB + SM_NH * 4];
+  char* dyt = lds;
+  float* hal = reinterpret_cast<float*>(lds + SM_NV * ROWB);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = tid & 3, row0 = tid >> 2;
+  const int b0 = blockIdx.x * per_split, b1 = min(nbricks, b0 + per_split);
+  const int hq = lane >> 5, gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int colb = (16 * (gq & 1) + 4 * p) * 2;
+  const int tap = lane & 31;  // B column
+  const int ttap = min(tap, 26);
+  const int toff = ((ttap / 9) * SM_HH + (ttap / 3) % 3) * SM_HW + ttap % 3;
+  u32x4 pdy[DYL];
+  float phl[HLL];
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  auto origin = [&](int b, int& nn, int& d0, int& h0, int& w0) {
+    int t = b;
+    const int bw_ = t % nbw; t /= nbw;
+    const int bh_ = t % nbh; t /= nbh;
+    const int nbd = (d + SM_BD - 1) / SM_BD;
+    const int bd_ = t % nbd;
+    nn = t / nbd;
+    d0 = bd_ * SM_BD; h0 = bh_ * SM_BH; w0 = bw_ * SM_BW;
+  };
+  auto prefetch = [&](int b) {
+    int nn, d0, h0, w0;
+    origin(b, nn, d0, h0, w0);
+#pragma unroll
+    for (int i = 0; i < DYL; ++i) {
+      const int v = row0 + i * RPP;
+      const int vw = v % SM_BW, vh = (v / SM_BW) % SM_BH, vd = v / (SM_BW * SM_BH);
+      const int zd = d0 + vd, zh = h0 + vh;
+      u32x4 val = {0u, 0u, 0u, 0u};
+      if (zd < d && zh < h)
+        val = *reinterpret_cast<const u32x4*>(dy + ((((long long)nn * d + zd) * h + zh) * w + w0 + vw) * 32 + ch * 8);
+      pdy[i] = val;
+    }
+#pragma unroll
+    for (int i = 0; i < HLL; ++i) {
+      const int v = tid + i * NT;
+      float val = 0.f;
+      if (v < SM_NH) {
+        const int hw = v % SM_HW, hh = (v / SM_HW) % SM_HH, hd = v / (SM_HW * SM_HH);
+        const int zd = d0 - 1 + hd, zh = h0 - 1 + hh, zw = w0 - 1 + hw;
+        if ((unsigned)zd < (unsigned)d && (unsigned)zh < (unsigned)h && (unsigned)zw < (unsigned)w)
+          val = x[(((long long)nn * d + zd) * h + zh) * w + zw];
+      }
+      phl[i] = val;
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < DYL; ++i)
+      *reinterpret_cast<u32x4*>(dyt + (row0 + i * RPP) * ROWB + ch * 16) = pdy[i];
+#pragma unroll
+    for (int i = 0; i < HLL; ++i) {
+      const int v = tid + i * NT;
+      if (v < SM_NH) hal[v] = phl[i];
+    }
+  };
+  if (b0 < b1) {
+    prefetch(b0);
+    commit();
+  }
+  __syncthreads();
+  for (int b = b0; b < b1; ++b) {
+    const bool more = b + 1 < b1;
+    prefetch(more ? b + 1 : b);
+#pragma unroll
+    for (int j = 0; j < SM_NV / 16 / 8; ++j) {
+      const int ks = wave + 8 * j;                 // 16 voxels: row (vd, vh), w = 16 * (ks & 1) ...
+      const int k0 = (ks * 16 + 8 * hq + q) * ROWB + colb;
+      const sm_bf16x8 a = __builtin_bit_cast(sm_bf16x8, __builtin_shufflevector(sm_tr_read(dyt, k0),
+                                                                                 sm_tr_read(dyt, k0 + 4 * ROWB),
+                                                                                 0, 1, 2, 3, 4, 5, 6, 7));
+      const int v0 = ks * 16 + 8 * hq;             // first of this lane's 8 voxels
+      const int vw = v0 % SM_BW, vh = (v0 / SM_BW) % SM_BH, vd = v0 / (SM_BW * SM_BH);
+      const float* src = hal + (vd * SM_HH + vh) * SM_HW + vw + toff;
+      typedef short v8i16 __attribute__((ext_vector_type(8)));
+      v8i16 bv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[e] = tap < 27 ? (short)from_f<bf16>(src[e]) : (short)0;
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, __builtin_bit_cast(sm_bf16x8, bv), acc, 0, 0, 0);
+    }
+    __syncthreads();
+    if (more) commit();
+    __syncthreads();
+  }
+  float* red = reinterpret_cast<float*>(lds);
+  const int r = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[(wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * hq) * 32 + r] = acc[i];
+  __syncthreads();
+  // slab [27][32 co][32 ci]: ci = 0 carries dW[co][t], the rest is zero
+  float* pp = part + (long long)blockIdx.x * 27 * 32 * 32;
+  for (int e = tid; e < 27 * 32 * 32; e += NT) {
+    const int ci = e & 31, co = (e >> 5) & 31, t = e >> 10;
+    float s = 0.f;
+    if (ci == 0) {
+#pragma unroll
+      for (int wv = 0; wv < 8; ++wv) s += red[(wv * 32 + co) * 32 + t];
+    }
+    pp[e] = s;
+  }
+}
 }  // namespace u3d
 
 using namespace u3d;
@@ -142,6 +272,19 @@ extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, in
   return check_launch("stem_fwd_kernel");
 }
 
+static bool stem_mfma_ok(int dtype, int cin, int cout, int w, int stride) {
+  return dtype == U3D_BF16 && cin == 1 && cout == 32 && stride == 1 && w % SM_BW == 0;
+}
+static int stem_bricks(int n, int d, int h, int w) {
+  return n * cdiv(d, SM_BD) * cdiv(h, SM_BH) * (w / SM_BW);
+}
+
+extern "C" int u3d_stem_wgrad_splits2(int dtype, int n, int cin, int d, int h, int w, int cout, int stride) {
+  if (stem_mfma_ok(dtype, cin, cout, w, stride)) return std::min(256, stem_bricks(n, d, h, w));
+  const long long total = (long long)n * sdim(d, stride) * sdim(h, stride) * sdim(w, stride);
+  return (int)std::max<long long>(1, std::min<long long>(1024, total / 2048));
+}
+
 extern "C" int u3d_stem_wgrad_splits(int n, int d, int h, int w, int stride) {
   const long long total = (long long)n * sdim(d, stride) * sdim(h, stride) * sdim(w, stride);
   return (int)std::max<long long>(1, std::min<long long>(1024, total / 2048));
@@ -158,6 +301,15 @@ extern "C" int u3d_stem_wgrad(int dtype, const void* dy, const float* x, int n, 
   const long long total = (long long)n * od * oh * ow;
   const long long vps = (total + nsplit - 1) / nsplit;
   const int cout_p = round_up(cout, 32), cin_p = round_up(cin, 32);
+  if (stem_mfma_ok(dtype, cin, cout, w, stride)) {
+    const int nb = stem_bricks(n, d, h, w), per = cdiv(nb, nsplit), ns_eff = cdiv(nb, per);
+    if (ns_eff < nsplit)
+      U3D_HIP(hipMemsetAsync(partials + (long long)ns_eff * 27 * 32 * 32, 0, (size_t)(nsplit - ns_eff) * 27 * 32 * 32 * 4,
+                             s));
+    hipLaunchKernelGGL(stem_wgrad_mfma_kernel, dim3(ns_eff), dim3(512), 0, s, (const bf16*)dy, x, partials, n, d, h, w,
+                       cdiv(h, SM_BH), w / SM_BW, nb, per);
+    return check_launch("stem_wgrad_mfma_kernel");
+  }
   U3D_HIP(hipMemsetAsync(partials, 0, (size_t)nsplit * 27 * cout_p * cin_p * 4, s));
   if (dtype == U3D_BF16)
     hipLaunchKernelGGL(stem_wgrad_kernel<bf16>, dim3(nsplit), dim3(ST), 0, s, (const bf16*)dy, x, partials, n, cin, d, h,

@@ -197,6 +197,133 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------------
+// 1^3 weight gradient (downsample convs, fusion / classifier heads): dW[co][ci] = sum_q dy[q][co] A[q*s][ci].
+// No halo: a workgroup streams chunks of 512 output voxels (linear order) of its split; the dy chunk and
+// the (strided) A chunk are staged channel-contiguous in LDS, read transposed (ds_read_b64_tr_b16), and the
+// 32 k16 steps of a chunk are spread over the 8 waves; the 8 per-wave partial tiles are summed in LDS in
+// fixed order at the end (deterministic). Memory-bound by design (16-32 flop/B): the next chunk is
+// prefetched into registers while the current one is consumed.
+constexpr int W1_NV = 512;
+
+struct W1Geom {
+  int cin, cout, cin_p, cout_p;
+  int id, ih, iw;
+  int od, oh, ow;
+  long long nvox;  // n * od * oh * ow
+  long long per_split;
+  int gn_groups;
+};
+
+template <int S>
+__global__ __launch_bounds__(512, 1) void wgrad1_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                       const float* __restrict__ gstat,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float* __restrict__ part,
+                                                       W1Geom g) {
+  constexpr int ROWB = 64, NT = 512, RPP = NT / 4, LD = W1_NV / RPP;  // 4 loads per operand per thread
+  __shared__ __attribute__((aligned(16))) char lds[2 * W1_NV * ROWB];
+  char* dyt = lds;
+  char* at = lds + W1_NV * ROWB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = tid & 3, row0 = tid >> 2;
+  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * 32;
+  const long long v0 = (long long)blockIdx.z * g.per_split;
+  const long long v1 = min(g.nvox, v0 + g.per_split);
+  const bool has_gn = gstat != nullptr;
+  const int h = lane >> 5, gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int colb = (16 * (gq & 1) + 4 * p) * 2;
+
+  u32x4 pdy[LD], pa[LD];
+  int pn[LD];
+  f32x2 sc[4], sh[4];
+  int gn_n = -1;
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+
+  auto prefetch = [&](long long c0) {
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const long long v = c0 + row0 + i * RPP;
+      u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
+      int n = -1;
+      if (v < v1) {
+        const int co = co0 + ch * 8, ci = ci0 + ch * 8;
+        if (co < g.cout) b = *reinterpret_cast<const u32x4*>(dy + v * g.cout + co);
+        long long src;
+        if (S == 1) {
+          src = v;
+          n = (int)(v / ((long long)g.od * g.oh * g.ow));
+        } else {
+          long long t = v;
+          const int qw = (int)(t % g.ow); t /= g.ow;
+          const int qh = (int)(t % g.oh); t /= g.oh;
+          const int qd = (int)(t % g.od);
+          n = (int)(t / g.od);
+          src = (((long long)n * g.id + 2 * qd) * g.ih + 2 * qh) * g.iw + 2 * qw;
+        }
+        if (ci < g.cin) a = *reinterpret_cast<const u32x4*>(x + src * g.cin + ci);
+      }
+      pdy[i] = b;
+      pa[i] = a;
+      pn[i] = n;
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const int v = row0 + i * RPP;
+      u32x4 a = pa[i];
+      if (has_gn && pn[i] >= 0) {
+        if (pn[i] != gn_n) {
+          gn_n = pn[i];
+          gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, gn_n, ci0 + ch * 8, sc, sh);
+        }
+        a = gn_relu8(a, sc, sh);
+      }
+      *reinterpret_cast<u32x4*>(dyt + v * ROWB + ch * 16) = pdy[i];
+      *reinterpret_cast<u32x4*>(at + v * ROWB + ch * 16) = a;
+    }
+  };
+
+  if (v0 < v1) {
+    prefetch(v0);
+    commit();
+  }
+  __syncthreads();
+  for (long long c0 = v0; c0 < v1; c0 += W1_NV) {
+    const bool more = c0 + W1_NV < v1;
+    prefetch(more ? c0 + W1_NV : c0);
+#pragma unroll
+    for (int j = 0; j < W1_NV / 16 / 8; ++j) {
+      const int ks = wave + 8 * j;
+      const int k0 = (ks * 16 + 8 * h + q) * ROWB + colb, k1 = k0 + 4 * ROWB;
+      const bf16x8 a = frag_from(tr_read(dyt, k0), tr_read(dyt, k1));
+      const bf16x8 b = frag_from(tr_read(at, k0), tr_read(at, k1));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+    if (more) commit();
+    __syncthreads();
+  }
+  // fixed-order sum of the 8 per-wave tiles: D[row = co][col = ci], lane col = lane&31, rows (i&3)+8(i>>2)+4h
+  float* red = reinterpret_cast<float*>(lds);
+  const int r = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[(wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[i];
+  __syncthreads();
+  float* pp = part + (long long)blockIdx.z * g.cout_p * g.cin_p;
+  for (int e = tid; e < 1024; e += NT) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) s += red[w * 1024 + e];
+    const int co = e >> 5, ci = e & 31;
+    pp[(long long)(co0 + co) * g.cin_p + ci0 + ci] = s;
+  }
+}
+
 }  // namespace u3d
 
 using namespace u3d;
@@ -247,4 +374,42 @@ extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int ci
     hipLaunchKernelGGL((wgrad_brick_kernel<2, 4, 8, 2>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
                        gn_stats, gn_gamma, gn_beta, partials, g);
   return check_launch("wgrad_brick_kernel");
+}
+
+extern "C" int u3d_conv_wgrad1_splits(int n, int cin, int d, int h, int w, int cout, int stride) {
+  const int od = (d - 1) / stride + 1, oh = (h - 1) / stride + 1, ow = (w - 1) / stride + 1;
+  const long long chunks = ((long long)n * od * oh * ow + W1_NV - 1) / W1_NV;
+  const long long tiles = (long long)cdiv(cin, 32) * cdiv(cout, 32);
+  long long want = std::max(1LL, 256 / tiles);
+  return (int)std::max(1LL, std::min(want, chunks));
+}
+
+extern "C" int u3d_conv_wgrad1(const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout, int stride,
+                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                               float* partials, int nsplit, u3d_stream_t stream) {
+  U3D_REQUIRE(dy && x && partials && nsplit >= 1, "wgrad1: null pointer");
+  U3D_REQUIRE(stride == 1 || stride == 2, "wgrad1: stride %d", stride);
+  U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "wgrad1: channels must be multiples of 8");
+  U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "wgrad1: bad GN");
+  W1Geom g{};
+  g.cin = cin; g.cout = cout; g.cin_p = round_up(cin, 32); g.cout_p = round_up(cout, 32);
+  g.id = d; g.ih = h; g.iw = w;
+  g.od = (d - 1) / stride + 1; g.oh = (h - 1) / stride + 1; g.ow = (w - 1) / stride + 1;
+  g.nvox = (long long)n * g.od * g.oh * g.ow;
+  const long long chunks = (g.nvox + W1_NV - 1) / W1_NV;
+  g.per_split = (chunks + nsplit - 1) / nsplit * W1_NV;
+  g.gn_groups = gn_groups;
+  const int ns_eff = (int)((g.nvox + g.per_split - 1) / g.per_split);
+  hipStream_t s = (hipStream_t)stream;
+  if (ns_eff < nsplit)
+    U3D_HIP(hipMemsetAsync(partials + (long long)ns_eff * g.cout_p * g.cin_p, 0,
+                           (size_t)(nsplit - ns_eff) * g.cout_p * g.cin_p * 4, s));
+  dim3 grid(g.cin_p / 32, g.cout_p / 32, ns_eff);
+  if (stride == 1)
+    hipLaunchKernelGGL(wgrad1_kernel<1>, grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats, gn_gamma,
+                       gn_beta, partials, g);
+  else
+    hipLaunchKernelGGL(wgrad1_kernel<2>, grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats, gn_gamma,
+                       gn_beta, partials, g);
+  return check_launch("wgrad1_kernel");
 }

@@ -28,8 +28,11 @@ _SIGS = {
     "u3d_convg_brick": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P],
     "u3d_conv_wgrad_brick_splits": [I, I, I, I, I, I, I],
     "u3d_conv_wgrad_brick": [P, P, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
+    "u3d_conv_wgrad1_splits": [I, I, I, I, I, I, I],
+    "u3d_conv_wgrad1": [P, P, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_stem_fwd": [I, P, I, I, I, I, I, P, I, I, P, P],
     "u3d_stem_wgrad_splits": [I, I, I, I, I],
+    "u3d_stem_wgrad_splits2": [I, I, I, I, I, I, I, I],
     "u3d_stem_wgrad": [I, P, P, I, I, I, I, I, I, I, P, I, P],
     "u3d_gn_workspace_bytes": [I, I, L],
     "u3d_gn_stats": [I, P, I, I, L, I, P, P, P],

@@ -209,7 +209,13 @@ def conv_wgrad(dy, x, k, stride, gn=None, brick=None):
     cout = dy.shape[-1]
     st, ga, be, G = gn if gn is not None else (None, None, None, 0)
     if brick is None:
-        brick = USE_BRICK_WGRAD and x.dtype == torch.bfloat16 and k == 3
+        brick = USE_BRICK_WGRAD and x.dtype == torch.bfloat16
+    if brick and k == 1:
+        ns = query("u3d_conv_wgrad1_splits", n, cin, d, h, w_, cout, stride)
+        part = torch.empty((ns, 1, round32(cout), round32(cin)), dtype=torch.float32, device=x.device)
+        call("u3d_conv_wgrad1", dy.data_ptr(), x.data_ptr(), n, cin, d, h, w_, cout, stride, _ptr(st), _ptr(ga),
+             _ptr(be), G, part.data_ptr(), ns, _stream())
+        return part, ns
     if brick:
         ns = query("u3d_conv_wgrad_brick_splits", n, cin, d, h, w_, cout, stride)
         part = torch.empty((ns, 27, round32(cout), round32(cin)), dtype=torch.float32, device=x.device)
@@ -236,7 +242,7 @@ def stem_fwd(x_ncdhw, wpk, cout, stride, dtype):
 def stem_wgrad(dy, x_ncdhw, stride):
     n, cin, d, h, w_ = x_ncdhw.shape
     cout = dy.shape[-1]
-    ns = query("u3d_stem_wgrad_splits", n, d, h, w_, stride)
+    ns = query("u3d_stem_wgrad_splits2", dt_code(dy.dtype), n, cin, d, h, w_, cout, stride)
     part = torch.empty((ns, 27, round32(cout), round32(cin)), dtype=torch.float32, device=dy.device)
     call("u3d_stem_wgrad", dt_code(dy.dtype), dy.data_ptr(), x_ncdhw.data_ptr(), n, cin, d, h, w_, cout, stride,
          part.data_ptr(), ns, _stream())

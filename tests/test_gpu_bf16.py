@@ -150,3 +150,39 @@ def test_wstd_batch_matches_single(gpu):
     ops.wstd_bwd_batch(items)
     for (part, ns, w, st, std, dw, _), ref in zip(items, refs):
         assert (dw - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("n,cin,cout,dims,s", [(2, 32, 16, (8, 10, 12), 1), (2, 32, 64, (8, 10, 12), 2),
+                                               (1, 64, 128, (6, 6, 7), 2), (2, 320, 320, (3, 3, 3), 1),
+                                               (1, 32, 8, (5, 7, 9), 1), (2, 32, 32, (40, 40, 40), 2)])
+def test_bf16_conv_wgrad_1x1(gpu, n, cin, cout, dims, s):
+    """1^3 weight gradient kernel (downsample / heads), GN prologue, strides 1 and 2."""
+    from u3d import ops
+    x, w, st, ga, be, G = _case(gpu, n, cin, cout, dims, True, 6)
+    od = tuple(ops.out_dim(d, 1, s) for d in dims)
+    dy = torch.randn((n,) + od + (cout,), device=gpu).to(torch.bfloat16)
+    part, ns = ops.conv_wgrad(dy, x, 1, s, (st, ga, be, G))
+    dw = part.sum(0).cpu().double()[0, :cout, :cin]
+    a = _act_ref(x, st, ga, be, G).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.grad.conv3d_weight(a, (cout, cin, 1, 1, 1), _bf(dy.cpu().float()).permute(0, 4, 1, 2, 3),
+                                      stride=s, padding=0)[:, :, 0, 0, 0]
+    err = (dw - ref).abs().max().item()
+    assert err < 2e-3 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("dims", [(6, 10, 64), (3, 9, 32), (5, 7, 20)])
+def test_bf16_stem_wgrad(gpu, dims):
+    """conv1 (1 -> 32, 3^3, stride 1) weight gradient: MFMA kernel (w % 32 == 0) and the VALU kernel."""
+    from u3d import ops
+    torch.manual_seed(7)
+    n = 2
+    x = torch.randn((n, 1) + dims, device=gpu)
+    dy = torch.randn((n,) + dims + (32,), device=gpu).to(torch.bfloat16)
+    part, ns = ops.stem_wgrad(dy, x, 1)
+    dw = part.sum(0).cpu().double()[:, :32, 0]                            # [27, 32]
+    xq = x.cpu().to(torch.bfloat16).double() if dims[2] % 32 == 0 else x.cpu().double()
+    ref = torch.nn.grad.conv3d_weight(xq, (32, 1, 3, 3, 3), _bf(dy.cpu().float()).permute(0, 4, 1, 2, 3), padding=1)
+    ref = ref.reshape(32, 27).t()
+    err = (dw - ref).abs().max().item()
+    assert err < 2e-3 * ref.abs().max().item(), err
+    assert part[:, :, :, 1:].abs().max().item() == 0.0   # padded ci columns stay zero
