@@ -135,6 +135,10 @@ int u3d_stem_wgrad(int dtype, const void* dy, const float* x, int n, int cin, in
 long long u3d_gn_workspace_bytes(int n, int c, long long v);
 int u3d_gn_stats(int dtype, const void* x, int n, int c, long long v, int groups, float* stats, float* ws,
                  u3d_stream_t stream);
+/* y = relu(x * scale + shift) with the GroupNorm affine of `stats`/gamma/beta (unet3D.py:44-53), NDHWC,
+ * c % 8 == 0: materialised ahead of the implicit GEMM for small deep-layer activations. */
+int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v, int groups, const float* stats,
+                 const float* gamma, const float* beta, void* y, u3d_stream_t stream);
 /* Backward of relu(group_norm(x)) given dA (grad wrt the ReLU output): dx (+)= ..., dgamma/dbeta (+)= ... */
 int u3d_gn_bwd(int dtype, const void* da, const void* x, int n, int c, long long v, int groups,
                const float* stats, const float* gamma, const float* beta, void* dx, int accumulate,

@@ -13,6 +13,7 @@
 // (unet3D.py:44-53); out-of-range taps read 0 *after* the prologue, as zero padding of the normalised
 // tensor does in the reference.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -31,6 +32,7 @@ struct Geom {
   int ntaps;
   int gn_groups;
   int nsamp, nsplit, kps;  // samples; split-K count and K-steps per split
+  int mtiles, ntiles;      // igemm_bf16_kernel's 1-D grid decomposition
   float* slab;             // split-K partials [nsplit][nsamp][Mq][cout] (nsplit > 1)
   int tap_w[27];
   signed char tap_d[27], tap_h[27], tap_x[27];
@@ -294,6 +296,248 @@ __global__ __launch_bounds__(NTHR) void igemm_kernel(const T* __restrict__ x, co
 }
 
 // ------------------------------------------------------------------------------------------------
+// bf16 implicit GEMM with a D-deep register pipeline: the raw 16-B global loads of K-step kk+D are
+// issued while step kk runs on the MFMAs, so a step costs its MFMA/LDS time instead of one global-load
+// latency (the deep 12^3 / 6^3 layers have only 4 MFMAs per wave per K-step). Same tap-list geometry,
+// split-K slabs and epilogue as igemm_kernel; GroupNorm+ReLU is applied when a stage is written to LDS.
+template <int KC>
+__device__ __forceinline__ int kswz(int r, int c) {  // conflict-free ds_read_b128 for 64-B / 128-B rows
+  if constexpr (KC == 4) return c ^ ((r >> 2) & 3);
+  else return c ^ ((r >> 1) & 7);
+}
+
+template <typename TO, int BM, int BN, int WM, int WN, int KC>
+__global__ __launch_bounds__(NTHR) void igemm_bf16_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
+                                                          TO* __restrict__ y, const bf16* __restrict__ res,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ gstat,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, Geom g) {
+  constexpr int NCH = KC, ROWB = KC * 16, BKC = KC * 8, D = KC == 4 ? 3 : 2;
+  constexpr int A_LOADS = BM * NCH / NTHR;
+  constexpr int B_CH = BN * NCH;
+  constexpr int B_LOADS = (B_CH + NTHR - 1) / NTHR;
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  static_assert(A_LOADS >= 1 && WM * WN == 4, "tile");
+
+  __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * ROWB + 2 * 256 * 4 + 27 * 24];
+  float* gsc = reinterpret_cast<float*>(smem + 2 * (BM + BN) * ROWB);
+  float* gsh = gsc + 256;
+  // tap table in LDS (the kernarg copy is only reachable through dependent vector loads):
+  // [t*2] voxel delta, [t*2+1] packed-weight tap; tdhw[t*4 + 0..2] = (d, h, w) offsets
+  int* taps = reinterpret_cast<int*>(gsh + 256);
+  int* tdhw = taps + 27 * 2;
+  if (threadIdx.x < g.ntaps) {
+    const int td = g.tap_d[threadIdx.x], th = g.tap_h[threadIdx.x], tx = g.tap_x[threadIdx.x];
+    taps[threadIdx.x * 2] = (td * g.ih + th) * g.iw + tx;
+    taps[threadIdx.x * 2 + 1] = g.tap_w[threadIdx.x];
+    tdhw[threadIdx.x * 4] = td;
+    tdhw[threadIdx.x * 4 + 1] = th;
+    tdhw[threadIdx.x * 4 + 2] = tx;
+  }
+  __syncthreads();
+  auto As = [&](int b) -> char* { return smem + b * (BM * ROWB); };
+  auto Bs = [&](int b) -> char* { return smem + 2 * BM * ROWB + b * (BN * ROWB); };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // 1-D grid, XCD-aware: launch id L runs on XCD L % 8; remap so each XCD owns a contiguous range of
+  // work items ordered split-major -> the WGs of one XCD share one K slice (weights + activation taps
+  // stay in that XCD's L2 instead of every XCD streaming the whole weight tensor).
+  int wi;
+  {
+    const int nwg = gridDim.x, q8 = nwg >> 3, r8 = nwg & 7, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  }
+  const int tiles = g.mtiles * g.ntiles * g.nsamp;
+  const int split = wi / tiles, trem = wi - split * tiles;
+  const int n = trem / (g.mtiles * g.ntiles), mn = trem - n * (g.mtiles * g.ntiles);
+  const int bm0 = (mn % g.mtiles) * BM, bn0 = (mn / g.mtiles) * BN;
+  const int Mq = g.qd * g.qh * g.qw;
+  const bool has_gn = gstat != nullptr;
+  if (has_gn) build_gn_table(gsc, gsh, g.cin, g.gn_groups, gstat, gamma, beta, n);
+  const bf16* xn = x + (long long)n * g.id * g.ih * g.iw * g.cin;
+
+  // per A row: voxel index of the tap-origin and a bit mask of the taps that land inside the volume, so a
+  // K-step costs one LDS broadcast + a shift/test + one multiply-add per load (the step was VALU-bound)
+  int a_row[A_LOADS], a_ch[A_LOADS], a_base[A_LOADS];
+  unsigned a_mask[A_LOADS];
+#pragma unroll
+  for (int i = 0; i < A_LOADS; ++i) {
+    const int id = tid + i * NTHR;
+    a_row[i] = id / NCH;
+    a_ch[i] = id % NCH;
+    const int q = bm0 + a_row[i];
+    unsigned m = 0;
+    int base = 0;
+    if (q < Mq) {
+      const int qw_ = q % g.qw, t = q / g.qw;
+      const int bd = (t / g.qh) * g.si, bh = (t % g.qh) * g.si, bw = qw_ * g.si;
+      base = (bd * g.ih + bh) * g.iw + bw;
+      for (int tt = 0; tt < g.ntaps; ++tt) {
+        const int zd = bd + tdhw[tt * 4], zh = bh + tdhw[tt * 4 + 1], zw = bw + tdhw[tt * 4 + 2];
+        if ((unsigned)zd < (unsigned)g.id && (unsigned)zh < (unsigned)g.ih && (unsigned)zw < (unsigned)g.iw)
+          m |= 1u << tt;
+      }
+    }
+    a_base[i] = base;
+    a_mask[i] = m;
+  }
+  const int nchunks = g.cin_p / BKC;
+  const int nk = g.ntaps * nchunks;
+
+  u32x4 ra[D][A_LOADS], rb[D][B_LOADS];
+  unsigned am[D];
+  // every load is issued unconditionally (out-of-range lanes read a valid dummy address and are zeroed
+  // afterwards): the loads in flight are then static, so the compiler's vmcnt waits stay counted.
+  auto gload = [&](int kk, int slot) {
+    const int t = kk / nchunks, c0 = (kk - t * nchunks) * BKC;
+    const int delta = taps[t * 2];
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      const int c = c0 + a_ch[i] * 8;
+      const bool ok = ((a_mask[i] >> t) & 1u) && c < g.cin;
+      const int off = ok ? (a_base[i] + delta) * g.cin + c : 0;
+      ra[slot][i] = *reinterpret_cast<const u32x4*>(xn + off);
+      m |= ok ? 1u << i : 0u;
+    }
+    am[slot] = m;
+    const bf16* wt = wpk + (long long)taps[t * 2 + 1] * g.cout_p * g.cin_p;
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      const int id = min(tid + i * NTHR, B_CH - 1);
+      const int row = id / NCH, ch = id % NCH, co = min(bn0 + row, g.cout_p - 1);
+      rb[slot][i] = *reinterpret_cast<const u32x4*>(wt + co * g.cin_p + c0 + ch * 8);
+    }
+  };
+  auto swrite = [&](int kk, int slot, int buf) {
+    const int t = kk / nchunks, c0 = (kk - t * nchunks) * BKC;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      u32x4 v = ra[slot][i];
+      const bool ok = (am[slot] >> i) & 1u;
+      if (!ok) v = u32x4{0u, 0u, 0u, 0u};
+      if (has_gn && ok) {
+        const int c = c0 + a_ch[i] * 8;
+        f32x2 sc[4], sh[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sc[e] = f32x2{gsc[c + 2 * e], gsc[c + 2 * e + 1]};
+          sh[e] = f32x2{gsh[c + 2 * e], gsh[c + 2 * e + 1]};
+        }
+        v = gn_relu8(v, sc, sh);
+      }
+      *reinterpret_cast<u32x4*>(As(buf) + a_row[i] * ROWB + kswz<KC>(a_row[i], a_ch[i]) * 16) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      const int id = tid + i * NTHR;
+      if (B_CH % NTHR == 0 || id < B_CH) {
+        const int row = id / NCH, ch = id % NCH;
+        u32x4 v = rb[slot][i];
+        if (bn0 + row >= g.cout_p) v = u32x4{0u, 0u, 0u, 0u};
+        *reinterpret_cast<u32x4*>(Bs(buf) + row * ROWB + kswz<KC>(row, ch) * 16) = v;
+      }
+    }
+  };
+
+  const int wr = wave / WN, wc = wave % WN;
+  const int arow0 = wr * (BM / WM), brow0 = wc * (BN / WN);
+  f32x16 acc[TM][TN];
+  auto stage_mfma = [&](const char* Ab, const char* Bb) {
+    const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int s = 0; s < KC / 2; ++s) {
+      bf16x8 av[TM], bv[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = arow0 + tm * 32 + r;
+        av[tm] = *reinterpret_cast<const bf16x8*>(Ab + row * ROWB + kswz<KC>(row, 2 * s + h) * 16);
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = brow0 + tn * 32 + r;
+        bv[tn] = *reinterpret_cast<const bf16x8*>(Bb + row * ROWB + kswz<KC>(row, 2 * s + h) * 16);
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.f;
+
+  const int kk0 = split * g.kps, kk1 = min(nk, kk0 + g.kps);
+  __syncthreads();  // GN + tap tables
+  if (kk0 < kk1) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) gload(min(kk0 + j, kk1 - 1), j);
+    swrite(kk0, 0, 0);
+  }
+  __syncthreads();
+  // stage kk lives in register slot (kk - kk0) % D and LDS buffer (kk - kk0) & 1
+  int kk = kk0;
+  for (; kk + D < kk1; kk += D) {  // full groups: no conditional memory operations inside
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      gload(min(kk + j + D, kk1 - 1), j);  // slot j held stage kk+j, already in LDS
+      const int buf = (kk + j - kk0) & 1;
+      stage_mfma(As(buf), Bs(buf));
+      swrite(kk + j + 1, (j + 1) % D, buf ^ 1);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < D; ++j) {  // tail: the last 1..D stages
+    if (kk + j < kk1) {
+      const int buf = (kk + j - kk0) & 1;
+      stage_mfma(As(buf), Bs(buf));
+      if (kk + j + 1 < kk1) swrite(kk + j + 1, (j + 1) % D, buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  const int r = lane & 31, h = lane >> 5;
+  const long long out_n = (long long)n * g.od * g.oh * g.ow;
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int co = bn0 + brow0 + tn * 32 + r;
+    if (co >= g.cout) continue;
+    const float bv = bias ? bias[co] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int q = bm0 + arow0 + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (q >= Mq) continue;
+        if (g.nsplit > 1) {
+          g.slab[(((long long)split * g.nsamp + n) * Mq + q) * g.cout + co] = acc[tm][tn][i];
+          continue;
+        }
+        long long ov;
+        if (g.so == 1) {
+          ov = q;
+        } else {
+          const int qw_ = q % g.qw, t = q / g.qw;
+          const int qh_ = t % g.qh, qd_ = t / g.qh;
+          ov = ((long long)(qd_ * g.so + g.pod) * g.oh + (qh_ * g.so + g.poh)) * g.ow + (qw_ * g.so + g.pow_);
+        }
+        const long long off = (out_n + ov) * g.cout + co;
+        float v = acc[tm][tn][i] + bv;
+        if (res) v += to_f(res[off]);
+        y[off] = from_f<TO>(v);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // weight gradient: partial[s][t][co][ci] = sum_{vox in split s} dy[vox][co] * A[vox*si + off_t][ci]
 // One workgroup = (co tile 32, ci tile 32, up to 4 taps) over one voxel split: the dy tile is staged
 // once per K-step and shared by the 4 waves, each wave owning one tap's 32x32 accumulator.
@@ -523,13 +767,14 @@ static int launch_igemm(Geom g, int n, const T* x, const T* wpk, TO* y, const T*
                         hipStream_t s) {
   const int Mq = g.qd * g.qh * g.qw;
   if (Mq <= 0) return U3D_OK;
-  const int BN = g.cout_p <= 32 ? 32 : 64;
+  const int BN = g.cout_p <= 32 ? 32 : (sizeof(T) == 2 && g.cout_p >= 128) ? 128 : 64;
   const long long tiles = (long long)cdiv(Mq, 128) * cdiv(g.cout, BN) * n;
   const int nk = g.ntaps * (g.cin_p / BK);
   // split K when the output tiles cannot fill the 256 CUs (deep, small-volume layers)
   int ns = 1;
   if (ws && tiles < 256 && nk >= 8) {
     ns = (int)std::min<long long>(nk / 4, (512 + tiles - 1) / tiles);
+    if (sizeof(T) == 2 && ns > 8) ns = ns / 8 * 8;  // split-major XCD mapping: one K slice per XCD
     const long long slab1 = (long long)n * Mq * g.cout * 4;
     while (ns > 1 && ns * slab1 > ws_bytes) --ns;
   }
@@ -537,7 +782,38 @@ static int launch_igemm(Geom g, int n, const T* x, const T* wpk, TO* y, const T*
   g.nsplit = ns;
   g.kps = (nk + ns - 1) / ns;
   g.slab = ns > 1 ? ws : nullptr;
-  if (BN == 32) {
+  if constexpr (sizeof(T) == 2) {
+    g.mtiles = cdiv(Mq, 128);
+    g.ntiles = cdiv(g.cout, BN);
+    if (g.cin_p % 64 == 0) {  // 64-channel stages: twice the MFMAs per barrier
+      g.kps = (g.ntaps * (g.cin_p / 64) + ns - 1) / ns;
+      g.nsplit = ns = std::min(ns, g.ntaps * (g.cin_p / 64));
+    }
+    dim3 grid(g.mtiles * g.ntiles * n * ns);
+    const bool k64 = g.cin_p % 64 == 0;
+    if (BN == 32) {
+      if (k64)
+        hipLaunchKernelGGL((igemm_bf16_kernel<TO, 128, 32, 4, 1, 8>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st,
+                           ga, be, g);
+      else
+        hipLaunchKernelGGL((igemm_bf16_kernel<TO, 128, 32, 4, 1, 4>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st,
+                           ga, be, g);
+    } else if (BN == 64) {
+      if (k64)
+        hipLaunchKernelGGL((igemm_bf16_kernel<TO, 128, 64, 2, 2, 8>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st,
+                           ga, be, g);
+      else
+        hipLaunchKernelGGL((igemm_bf16_kernel<TO, 128, 64, 2, 2, 4>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st,
+                           ga, be, g);
+    } else {
+      if (k64)
+        hipLaunchKernelGGL((igemm_bf16_kernel<TO, 128, 128, 2, 2, 8>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias,
+                           st, ga, be, g);
+      else
+        hipLaunchKernelGGL((igemm_bf16_kernel<TO, 128, 128, 2, 2, 4>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias,
+                           st, ga, be, g);
+    }
+  } else if (BN == 32) {
     dim3 grid(cdiv(Mq, 128), cdiv(g.cout, 32), n * ns);
     hipLaunchKernelGGL((igemm_kernel<T, TO, 128, 32, 4, 1>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st, ga,
                        be, g);

@@ -253,6 +253,28 @@ __global__ __launch_bounds__(GT) void gn_bwd_apply(const T* __restrict__ da, con
   }
 }
 
+
+// y = relu(x * scale[n,c] + shift[n,c]) materialised (8 channels per thread): used ahead of the implicit
+// GEMM on the small deep-layer activations so its K loop carries no GroupNorm arithmetic.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, T* __restrict__ y, int n, int c,
+                                                       long long v, int groups, const float* __restrict__ st,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta) {
+  constexpr int VEC = 8;
+  const int c8 = c / VEC;
+  const long long per = v * c8, total = per * n;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int nn = (int)(i / per), cc = (int)(i % c8) * VEC;
+    f32x2 sc[4], sh[4];
+    gn_coef8(st, gamma, beta, groups, c, nn, cc, sc, sh);
+    float a[VEC];
+    loadv<T, VEC>(x + i * VEC, a);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) a[e] = fmaxf(0.f, fmaf(a[e], sc[e >> 1][e & 1], sh[e >> 1][e & 1]));
+    storev<T, VEC>(y + i * VEC, a);
+  }
+}
 }  // namespace u3d
 
 using namespace u3d;
@@ -310,4 +332,21 @@ extern "C" int u3d_gn_bwd(int dtype, const void* da, const void* x, int n, int c
                        gamma, beta, csum, (float*)dx, accumulate);
   }
   return check_launch("gn_bwd");
+}
+
+extern "C" int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v, int groups, const float* stats,
+                            const float* gamma, const float* beta, void* y, u3d_stream_t stream) {
+  U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "gn_apply: bad dtype");
+  U3D_REQUIRE(x && y && stats && gamma && beta && n >= 1 && c % 8 == 0 && groups > 0 && c % groups == 0,
+              "gn_apply: bad args (c %% 8 == 0)");
+  const long long total = (long long)n * v * (c / 8);
+  const int grid = (int)std::min<long long>(4096, (total + 255) / 256);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == U3D_BF16)
+    hipLaunchKernelGGL(gn_apply_kernel<bf16>, dim3(grid), dim3(256), 0, s, (const bf16*)x, (bf16*)y, n, c, v, groups,
+                       stats, gamma, beta);
+  else
+    hipLaunchKernelGGL(gn_apply_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)x, (float*)y, n, c, v,
+                       groups, stats, gamma, beta);
+  return check_launch("gn_apply_kernel");
 }

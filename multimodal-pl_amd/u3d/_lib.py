@@ -36,6 +36,7 @@ _SIGS = {
     "u3d_stem_wgrad": [I, P, P, I, I, I, I, I, I, I, P, I, P],
     "u3d_gn_workspace_bytes": [I, I, L],
     "u3d_gn_stats": [I, P, I, I, L, I, P, P, P],
+    "u3d_gn_apply": [I, P, I, I, L, I, P, P, P, P, P],
     "u3d_gn_bwd": [I, P, P, I, I, L, I, P, P, P, P, I, P, P, I, P, P],
     "u3d_upsample2x_add": [I, P, I, I, I, I, I, P, P, P],
     "u3d_upsample2x_bwd": [I, P, I, I, I, I, I, P, I, P],

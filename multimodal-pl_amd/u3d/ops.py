@@ -152,6 +152,11 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
         call("u3d_convg_brick", 0, x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be),
              G, _ptr(residual), y.data_ptr(), _stream())
         return y
+    if st is not None and x.dtype == torch.bfloat16 and cin >= 64 and x.numel() * 2 <= GN_MATERIALIZE_BYTES:
+        # small deep-layer activation: materialise relu(gn(x)) once so the GEMM K loop has no GN arithmetic
+        x = gn_apply(x, st, ga, be, G)
+        st = ga = be = None
+        G = 0
     ws = WS.get(SPLITK_WS_BYTES, x.device, slot=4)
     call("u3d_conv_fwd", dt_code(x.dtype), x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, k, stride, _ptr(st),
          _ptr(ga), _ptr(be), G, _ptr(residual), _ptr(bias), y.data_ptr(), int(out_f32), ws.data_ptr(), ws.numel(),
@@ -261,6 +266,19 @@ def gn_stats(x, groups):
     call("u3d_gn_stats", dt_code(x.dtype), x.data_ptr(), n, c, v, groups, st.data_ptr(),
          _gn_ws(n, c, v, x.device).data_ptr(), _stream())
     return st
+
+
+GN_MATERIALIZE_BYTES = 32 << 20
+
+
+def gn_apply(x, stats, gamma, beta, groups):
+    """relu(group_norm(x)) materialised (NDHWC, same dtype)."""
+    n, c = x.shape[0], x.shape[-1]
+    v = x.numel() // (n * c)
+    y = torch.empty_like(x)
+    call("u3d_gn_apply", dt_code(x.dtype), x.data_ptr(), n, c, v, groups, stats.data_ptr(), gamma.data_ptr(),
+         beta.data_ptr(), y.data_ptr(), _stream())
+    return y
 
 
 def gn_bwd(da, x, stats, gamma, beta, groups, dx=None, accumulate=False, dgamma=None, dbeta=None, acc_params=False):

@@ -1,0 +1,81 @@
+"""Kernel micro-benchmarks on cuda:0 (HIP events, per-launch average). Usage: python tools/kbench.py [case ...]
+Cases reproduce the trunk's launches at 2 x 96^3 (bf16) so rocprofv3 PMC passes can target one kernel."""
+import os
+import sys
+
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "multimodal-pl_amd")]
+import torch  # noqa: E402
+from u3d import ops  # noqa: E402
+
+dev = torch.device("cuda:0")
+bf = torch.bfloat16
+
+
+def t_(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def conv_case(n, cin, cout, s, k, stride, gn=True, res=False):
+    x = torch.randn((n, s, s, s, cin), device=dev).to(bf)
+    w = torch.randn(cout, cin, k, k, k, device=dev)
+    pf, pd, _ = ops.wstd_fwd(w, bf, True)
+    G = 16
+    g = (ops.gn_stats(x, G), torch.ones(cin, device=dev), torch.zeros(cin, device=dev), G) if gn else None
+    os_ = ops.out_dim(s, k, stride)
+    r = torch.randn((n, os_, os_, os_, cout), device=dev).to(bf) if res else None
+    dy = torch.randn((n, os_, os_, os_, cout), device=dev).to(bf)
+    flop = 2.0 * n * os_ ** 3 * k ** 3 * cin * cout
+    return x, pf, pd, g, r, dy, flop
+
+
+CASES = {}
+
+
+def case(name):
+    def deco(f):
+        CASES[name] = f
+        return f
+    return deco
+
+
+def _fwd(n, cin, cout, s, k, stride, gn=True, res=False):
+    x, pf, pd, g, r, dy, flop = conv_case(n, cin, cout, s, k, stride, gn, res)
+    us = t_(lambda: ops.conv_fwd(x, pf, cout, k, stride, g, r))
+    return us, flop
+
+
+def _dgrad(n, cin, cout, s, k, stride):
+    x, pf, pd, g, r, dy, flop = conv_case(n, cin, cout, s, k, stride, False)
+    us = t_(lambda: ops.conv_dgrad(dy, pd, cin, x.shape[:4], k, stride))
+    return us, flop
+
+
+def _wgrad(n, cin, cout, s, k, stride):
+    x, pf, pd, g, r, dy, flop = conv_case(n, cin, cout, s, k, stride, True)
+    us = t_(lambda: ops.conv_wgrad(dy, x, k, stride, g))
+    return us, flop
+
+
+for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 256), ("6", 6, 320)]:
+    CASES[f"fwd{lvl}"] = (lambda s=s, c=c: _fwd(2, c, c, s, 3, 1, True, True))
+    CASES[f"dgrad{lvl}"] = (lambda s=s, c=c: _dgrad(2, c, c, s, 3, 1))
+    CASES[f"wgrad{lvl}"] = (lambda s=s, c=c: _wgrad(2, c, c, s, 3, 1))
+CASES["fwd12nogn"] = lambda: _fwd(2, 256, 256, 12, 3, 1, False, False)
+CASES["fwd_s2_24"] = lambda: _fwd(2, 128, 256, 24, 3, 2, True, False)
+CASES["dgrad_s2_24"] = lambda: _dgrad(2, 128, 256, 24, 3, 2)
+CASES["head96"] = lambda: _fwd(2, 32, 16, 96, 1, 1, True, False)
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(CASES)
+    for nm in names:
+        us, flop = CASES[nm]()
+        print(f"{nm:14s} {us:9.1f} us  {flop / us / 1e6:8.1f} TFLOP/s", flush=True)
