@@ -36,6 +36,8 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--eager", action="store_true", help="launch kernel by kernel instead of replaying the "
+                   "captured hipGraph of the step")
     return p.parse_args()
 
 
@@ -136,8 +138,12 @@ def main():
     net = U3DDataParallel(model) if world > 1 else model
     opt = torch.optim.SGD(model.parameters(), lr=5e-4, momentum=0.9, weight_decay=1e-4)
     crit = EDiceLoss_partial(16)
-    x, lab, mask = synthetic(a.batch, a.patch, device, 1000 + rank)
-    target = lab.squeeze(1)
+    # two resident synthetic batches; each step consumes the other one (copied into the step's input buffers)
+    batches = []
+    for j in range(2):
+        xb, lb, mb = synthetic(a.batch, a.patch, device, 1000 + 17 * j + rank)
+        batches.append((xb, lb.squeeze(1), mb.to(device)))
+    x, target, mask = (t.clone() for t in batches[0])
     amp = a.dtype == "bf16"
 
     def step():
@@ -149,15 +155,34 @@ def main():
         opt.step()
         return loss
 
-    for _ in range(a.warmup):
-        step()
+    graphed = None
+    if not a.eager:
+        from u3d.graph import GraphedStep
+        try:
+            graphed = GraphedStep(step, (x, target, mask), warmup=3, optimizer=opt)
+        except Exception as e:  # capture refused (e.g. a collective backend without graph support): run eager
+            print(f"[bench] hipGraph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
+            torch.cuda.synchronize()
+            a.eager = True
+    if a.eager:
+        def run(i):
+            x.copy_(batches[i % 2][0], non_blocking=True)
+            target.copy_(batches[i % 2][1], non_blocking=True)
+            mask.copy_(batches[i % 2][2], non_blocking=True)
+            return step()
+    else:
+        def run(i):
+            return graphed(*batches[i % 2])
+
+    for i in range(a.warmup):
+        run(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        loss = step()
+    for i in range(a.steps):
+        loss = run(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -167,6 +192,7 @@ def main():
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
+    loss_v = float(loss)
     ms = dt / a.steps * 1e3
     vox = world * a.batch * a.patch ** 3 * a.steps / dt
 
@@ -187,7 +213,7 @@ def main():
             "config": {"workload": "unet3D_baseline([1,2,2,2,2],16,weight_std) fwd+EDiceLoss_partial+bwd+SGD",
                        "model": "unet3D_baseline-16", "global_batch": world * a.batch, "seq_len": a.patch ** 3,
                        "patch": [a.patch] * 3, "parallelism": f"dp{world}"},
-            "loss": round(float(loss), 6),
+            "loss": round(loss_v, 6), "launch": "eager" if a.eager else "hipgraph",
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -91,6 +91,12 @@ int u3d_conv_wgrad(int dtype, const void* dy, const void* x, int n, int cin, int
                    int ksize, int stride, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
                    int gn_groups, float* partials, int nsplit, u3d_stream_t stream);
 
+/* bf16 stride-2 3^3 data gradient in ONE launch (replaces the 8 parity-class launches of u3d_conv_dgrad):
+ * dy [n][od][oh][ow][cout] (od = (d-1)/2+1) -> dx [n][d][h][w][cin] (overwritten), wpk = data-grad pack
+ * [27][cin_p][cout_p]. Autograd of F.conv3d(stride=2, padding=1) in Conv3d.forward (reference unet3D.py:27). */
+int u3d_conv_dgrad_s2(const void* dy, int n, int cout, const void* wpk_dgrad, int cin, int d, int h, int w, void* dx,
+                      u3d_stream_t stream);
+
 /* bf16 32->32 3^3 stride-1 conv (cin = cout = 32; the full-resolution layers) in halo-brick form with the
  * weights held in registers: flip=0 forward (wpk = forward pack, optional GN+ReLU prologue and residual),
  * flip=1 data gradient (wpk = data-grad pack, no prologue). Same results as u3d_conv_fwd/_dgrad; n <= 16. */

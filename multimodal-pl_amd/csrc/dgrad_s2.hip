@@ -1,0 +1,233 @@
+// Stride-2 3^3 data gradient (the transposed convolution of a stride-2 forward conv), bf16, one launch.
+//
+// Reference: autograd of F.conv3d(stride=2, padding=1) in Conv3d.forward (unet3D.py:27) for the first conv of
+// every down-sampling NoBottleneck (layer1..4 .0.conv1, _make_layer unet3D.py:1666-1686).
+//
+// dx[2q + p] = sum over the taps of parity class p of dy[q + delta] . W[tap]: per dim, p = 0 takes tap 1 at
+// delta 0, p = 1 takes tap 0 at delta 1 and tap 2 at delta 0 — the 27 taps split into 8 parity classes, and
+// the dy window a tap reads is one of 8 shifts delta in {0,1}^3 of a q-brick.
+//   * one workgroup (8 waves) = one q-brick of up to 256 dy voxels x one 32-channel dx tile; each wave owns
+//     32 q rows and ALL 8 parity accumulators (8 x 32x32 fp32), so one workgroup writes the whole 2x-sized
+//     dx region of its brick: every dx voxel is produced once, with no zero-fill and no per-class launches;
+//   * K loop = 32-channel dy chunks: the dy halo ((bd+1)(bh+1)(bw+1) voxels) and the 27 taps' weights of
+//     the chunk are staged once in LDS (chunk-planar, padded planes: conflict-free staging writes); each of
+//     the 8 shifted A fragments is read once per k16 step and feeds the 1..8 taps that use that shift;
+//   * the next chunk is prefetched into registers while the MFMAs of the current one run;
+//   * epilogue through LDS: (pw = 0, 1) of consecutive q are adjacent dx voxels -> 128-B contiguous rows.
+#include "common.h"
+
+namespace u3d {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+constexpr int S2_NT = 512;
+constexpr int S2_HMAX = 512;                     // halo rows (max)
+constexpr int S2_PS = S2_HMAX * 16 + 64;         // halo plane stride
+constexpr int S2_NWR = 27 * 32;                  // weight rows (tap, co)
+constexpr int S2_WPS = S2_NWR * 16 + 64;         // weight plane stride
+constexpr int S2_HLD = S2_HMAX * 4 / S2_NT;      // 4 halo loads per thread
+constexpr int S2_WLD = (S2_NWR * 4 + S2_NT - 1) / S2_NT;  // 7 weight loads per thread
+constexpr int S2_LDS = 4 * S2_PS + 4 * S2_WPS;
+
+struct S2Geom {
+  int n, qd, qh, qw;       // dy spatial dims (the forward's output)
+  int D, H, W;             // dx spatial dims (the forward's input)
+  int cy, cy_p, cx, cx_p;  // dy channels (contraction), dx channels (output)
+  int bd, bh, bw;          // q-brick
+  int hh, hw, nh;          // halo pitch (bh+1, bw+1) and rows
+  int nbd, nbh, nbw, nct;  // bricks per dim, 32-wide dx channel tiles
+  int nvq;                 // q voxels per brick (<= 256)
+};
+
+__global__ __launch_bounds__(S2_NT, 1) void dgrad_s2_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wpk,
+                                                           bf16* __restrict__ dx, S2Geom g) {
+  __shared__ __attribute__((aligned(16))) char smem[S2_LDS];
+  char* const hal = smem;
+  char* const wts = smem + 4 * S2_PS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+
+  int bid;  // XCD-aware: each XCD owns a contiguous range of (brick, co tile) -> shared halo rows in its L2
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  int b = bid / g.nct;
+  const int co0 = (bid - b * g.nct) * 32;
+  const int bw_ = b % g.nbw; b /= g.nbw;
+  const int bh_ = b % g.nbh; b /= g.nbh;
+  const int bd_ = b % g.nbd;
+  const int nn = b / g.nbd;
+  const int q0d = bd_ * g.bd, q0h = bh_ * g.bh, q0w = bw_ * g.bw;
+
+  // this lane's q row (clamped into the brick for the idle rows of the last tile)
+  const int v = min(wave * 32 + r, g.nvq - 1);
+  const int vw = v % g.bw, vh = (v / g.bw) % g.bh, vd = v / (g.bw * g.bh);
+  const int arow = (vd * g.hh + vh) * g.hw + vw;
+  const bool active = wave * 32 < g.nvq;
+
+  const int sch = tid & 3, srow0 = tid >> 2;
+  u32x4 hpre[S2_HLD], wpre[S2_WLD];
+  auto halo_load = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < S2_HLD; ++i) {
+      const int row = srow0 + i * (S2_NT / 4);
+      u32x4 val = {0u, 0u, 0u, 0u};
+      if (row < g.nh) {
+        const int xw = row % g.hw, xh = (row / g.hw) % g.hh, xd = row / (g.hw * g.hh);
+        const int zd = q0d + xd, zh = q0h + xh, zw = q0w + xw, cc = c * 32 + sch * 8;
+        if (zd < g.qd && zh < g.qh && zw < g.qw && cc < g.cy)
+          val = *reinterpret_cast<const u32x4*>(dy + ((((long long)nn * g.qd + zd) * g.qh + zh) * g.qw + zw) * g.cy + cc);
+      }
+      hpre[i] = val;
+    }
+  };
+  auto w_load = [&](int c) {  // rows (tap t, co): 4 consecutive threads read one row's 64 B
+#pragma unroll
+    for (int i = 0; i < S2_WLD; ++i) {
+      const int id = tid + i * S2_NT;
+      u32x4 val = {0u, 0u, 0u, 0u};
+      if (id < S2_NWR * 4) {
+        const int row = id >> 2, t = row >> 5, co = co0 + (row & 31);
+        if (co < g.cx_p)
+          val = *reinterpret_cast<const u32x4*>(wpk + ((long long)t * g.cx_p + co) * g.cy_p + c * 32 + (id & 3) * 8);
+      }
+      wpre[i] = val;
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < S2_HLD; ++i) {
+      const int row = srow0 + i * (S2_NT / 4);
+      if (row < g.nh) *reinterpret_cast<u32x4*>(hal + sch * S2_PS + row * 16) = hpre[i];
+    }
+#pragma unroll
+    for (int i = 0; i < S2_WLD; ++i) {
+      const int id = tid + i * S2_NT;
+      if (id < S2_NWR * 4) *reinterpret_cast<u32x4*>(wts + (id & 3) * S2_WPS + (id >> 2) * 16) = wpre[i];
+    }
+  };
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[p][e] = 0.f;
+
+  const int nchunk = g.cy_p / 32;
+  halo_load(0);
+  w_load(0);
+  commit();
+  __syncthreads();
+  for (int c = 0; c < nchunk; ++c) {
+    const bool more = c + 1 < nchunk;
+    if (more) {
+      halo_load(c + 1);
+      w_load(c + 1);
+    }
+    if (active) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int plane = 2 * s + hh;
+        const char* ab = hal + plane * S2_PS + arow * 16;
+        const char* bb = wts + plane * S2_WPS + r * 16;
+        // shift (dd, dh, dw) in {0,1}^3; per dim: shift 1 -> (tap 0, p 1); shift 0 -> (tap 1, p 0), (tap 2, p 1)
+#pragma unroll
+        for (int sh = 0; sh < 8; ++sh) {
+          const int dd = sh >> 2, dh = (sh >> 1) & 1, dw = sh & 1;
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(ab + ((dd * g.hh + dh) * g.hw + dw) * 16);
+#pragma unroll
+          for (int kd = 0; kd < (dd ? 1 : 2); ++kd)
+#pragma unroll
+            for (int kh = 0; kh < (dh ? 1 : 2); ++kh)
+#pragma unroll
+              for (int kw = 0; kw < (dw ? 1 : 2); ++kw) {
+                const int td = dd ? 0 : 1 + kd, th = dh ? 0 : 1 + kh, tw = dw ? 0 : 1 + kw;
+                const int p = ((td != 1) << 2) | ((th != 1) << 1) | (tw != 1);
+                const int t = (td * 3 + th) * 3 + tw;
+                const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bb + t * 32 * 16);
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[p], 0, 0, 0);
+              }
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      commit();
+      __syncthreads();
+    }
+  }
+
+  // epilogue, one half (pd) at a time: wave tile [ph][pw][32 q rows][32 co] bf16 = 8 KB, read back as 16-B
+  // chunks ordered (row, pw, part) so 8 lanes write one q row's two adjacent dx voxels (128 B contiguous)
+  char* const ept = smem + wave * 8192;
+#pragma unroll
+  for (int pd = 0; pd < 2; ++pd) {
+    if (pd) __syncthreads();  // all waves done reading the pd = 0 tiles
+    if (active) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
+          *reinterpret_cast<bf16*>(ept + ((j >> 1) * 2048 + (row * 2 + (j & 1)) * 32 + r) * 2) =
+              from_f<bf16>(acc[pd * 4 + j][i]);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (active) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int qi = lane + 64 * u;               // (ph, row, pw, part)
+        const int part = qi & 3, pw = (qi >> 2) & 1, row = (qi >> 3) & 31, ph = qi >> 8;
+        const int vv = wave * 32 + row;
+        const int uw = vv % g.bw, uh = (vv / g.bw) % g.bh, ud = vv / (g.bw * g.bh);
+        const int xd = 2 * (q0d + ud) + pd, xh = 2 * (q0h + uh) + ph, xw = 2 * (q0w + uw) + pw;
+        const int co = co0 + part * 8;
+        if (vv < g.nvq && q0d + ud < g.qd && q0h + uh < g.qh && q0w + uw < g.qw && xd < g.D && xh < g.H &&
+            xw < g.W && co < g.cx) {
+          const u32x4 val = *reinterpret_cast<const u32x4*>(ept + qi * 16);
+          *reinterpret_cast<u32x4*>(dx + ((((long long)nn * g.D + xd) * g.H + xh) * g.W + xw) * g.cx + co) = val;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+}  // namespace u3d
+
+using namespace u3d;
+
+// dy [n, od, oh, ow, cout] (od = (d-1)/2+1 ...) -> dx [n, d, h, w, cin]; W packed [27][cin_p][cout_p] (dgrad pack)
+extern "C" int u3d_conv_dgrad_s2(const void* dy, int n, int cout, const void* wpk_dgrad, int cin, int d, int h, int w,
+                                 void* dx, u3d_stream_t stream) {
+  U3D_REQUIRE(dy && wpk_dgrad && dx && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv_dgrad_s2: bad args");
+  U3D_REQUIRE(cout % 8 == 0 && cin % 8 == 0, "conv_dgrad_s2: channels must be multiples of 8");
+  S2Geom g{};
+  g.n = n;
+  g.D = d; g.H = h; g.W = w;
+  g.qd = (d - 1) / 2 + 1; g.qh = (h - 1) / 2 + 1; g.qw = (w - 1) / 2 + 1;
+  g.cy = cout; g.cy_p = round_up(cout, 32); g.cx = cin; g.cx_p = round_up(cin, 32);
+  // q-brick: up to 256 voxels, w extent first (contiguous dy rows), extents that tile the volume evenly,
+  // halo <= S2_HMAX rows
+  auto even = [](int q, int mx) { return cdiv(q, cdiv(q, std::max(1, mx))); };
+  g.bw = even(g.qw, 16);
+  g.bh = even(g.qh, 256 / (g.bw * 2));
+  g.bd = even(g.qd, std::min(g.qd, 256 / (g.bw * g.bh)));
+  while ((g.bd + 1) * (g.bh + 1) * (g.bw + 1) > S2_HMAX && g.bd > 1) --g.bd;
+  while ((g.bd + 1) * (g.bh + 1) * (g.bw + 1) > S2_HMAX && g.bh > 1) --g.bh;
+  U3D_REQUIRE((g.bd + 1) * (g.bh + 1) * (g.bw + 1) <= S2_HMAX, "conv_dgrad_s2: halo too large");
+  g.nvq = g.bd * g.bh * g.bw;
+  g.hh = g.bh + 1; g.hw = g.bw + 1;
+  g.nh = (g.bd + 1) * g.hh * g.hw;
+  g.nbd = cdiv(g.qd, g.bd); g.nbh = cdiv(g.qh, g.bh); g.nbw = cdiv(g.qw, g.bw);
+  g.nct = g.cx_p / 32;
+  const long long nwg = (long long)n * g.nbd * g.nbh * g.nbw * g.nct;
+  U3D_REQUIRE(nwg < (1LL << 31), "conv_dgrad_s2: grid too large");
+  hipLaunchKernelGGL(dgrad_s2_kernel, dim3((unsigned)nwg), dim3(S2_NT), 0, (hipStream_t)stream, (const bf16*)dy,
+                     (const bf16*)wpk_dgrad, (bf16*)dx, g);
+  return check_launch("dgrad_s2_kernel");
+}

@@ -53,6 +53,39 @@ __device__ __forceinline__ float bce_elem(float p, float t) {
   return (t - 1.f) * fmaxf(log1pf(-p), -100.f) - t * fmaxf(logf(p), -100.f);
 }
 
+constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+
+// Softmax path on the hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp): e_c = 2^((x_c-m)
+// log2 e), p_c = e_c / s, and the two logs BCE needs are exact identities of the softmax instead of log(p):
+//   log p_c = (x_c - m) - ln s,   log(1 - p_c) = ln(s - e_c) - ln s.
+// The loss was transcendental-bound with libm expf/logf/log1pf (48 calls per voxel at C = 16).
+template <int NC>
+__device__ __forceinline__ void softmax_fast(const float* __restrict__ lg, int C, float (&x)[NC], float (&e)[NC],
+                                             float& s, float& inv) {
+  if constexpr (NC % 4 == 0 && NC <= 16) {
+#pragma unroll
+    for (int c = 0; c < NC; c += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(lg + c);
+      x[c] = v[0]; x[c + 1] = v[1]; x[c + 2] = v[2]; x[c + 3] = v[3];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) x[c] = c < C ? lg[c] : 0.f;
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (c < C) m = fmaxf(m, x[c]);
+  s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    x[c] -= m;
+    e[c] = c < C ? __builtin_amdgcn_exp2f(x[c] * LOG2E) : 0.f;
+    s += e[c];
+  }
+  inv = __builtin_amdgcn_rcpf(s);
+}
+
 template <int NC>
 __global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
                                                          long long nvox, int C, int softmax, int uce,
@@ -64,18 +97,37 @@ __global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restric
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[k][c] = 0.f;
   for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < nvox; v += (long long)gridDim.x * LT) {
-    float p[NC];
-    probs<NC>(lg + v * C, C, softmax, p);
     const float t = lab[v];
+    if (softmax == 1) {
+      float x[NC], e[NC], s, inv;
+      softmax_fast<NC>(lg + v * C, C, x, e, s, inv);
+      const float ls = __builtin_amdgcn_logf(s) * LN2;
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (c < C) {
-        const float tc = (t == (float)c) ? 1.f : 0.f;
-        acc[0][c] = fmaf(p[c], tc, acc[0][c]);
-        acc[1][c] = fmaf(p[c], p[c], acc[1][c]);
-        acc[2][c] += tc;
-        if (uce) acc[3][c] += bce_elem(p[c], tc);
-      }
+      for (int c = 0; c < NC; ++c)
+        if (c < C) {
+          const bool hit = t == (float)c;
+          const float tc = hit ? 1.f : 0.f, p = e[c] * inv;
+          acc[0][c] = fmaf(p, tc, acc[0][c]);
+          acc[1][c] = fmaf(p, p, acc[1][c]);
+          acc[2][c] += tc;
+          if (uce) {
+            const float lq = hit ? x[c] - ls : __builtin_amdgcn_logf(s - e[c]) * LN2 - ls;
+            acc[3][c] -= fmaxf(lq, -100.f);
+          }
+        }
+    } else {
+      float p[NC];
+      probs<NC>(lg + v * C, C, softmax, p);
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c < C) {
+          const float tc = (t == (float)c) ? 1.f : 0.f;
+          acc[0][c] = fmaf(p[c], tc, acc[0][c]);
+          acc[1][c] = fmaf(p[c], p[c], acc[1][c]);
+          acc[2][c] += tc;
+          if (uce) acc[3][c] += bce_elem(p[c], tc);
+        }
+    }
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -152,7 +204,14 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
   __syncthreads();
   for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < nvox; v += (long long)gridDim.x * LT) {
     float p[NC], g[NC];
-    probs<NC>(lg + v * C, C, softmax, p);
+    if (softmax == 1) {
+      float x[NC], s, inv;
+      softmax_fast<NC>(lg + v * C, C, x, p, s, inv);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) p[c] *= inv;
+    } else {
+      probs<NC>(lg + v * C, C, softmax, p);
+    }
     const float t = lab[v];
     float dot = 0.f;
 #pragma unroll
@@ -161,7 +220,7 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
       if (c < C) {
         const float tc = (t == (float)c) ? 1.f : 0.f;
         float gc = fmaf(tc, kd_a[c], p[c] * kd_b[c]);
-        if (uce) gc += kb[c] * (p[c] - tc) / fmaxf((1.f - p[c]) * p[c], 1e-12f);
+        if (uce) gc += kb[c] * (p[c] - tc) * __builtin_amdgcn_rcpf(fmaxf((1.f - p[c]) * p[c], 1e-12f));
         g[c] = gc;
         dot = fmaf(gc, p[c], dot);
       }

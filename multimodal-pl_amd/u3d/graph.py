@@ -1,0 +1,52 @@
+"""Whole-step hipGraph capture for the native training step.
+
+A training step of the 96^3 trunk issues ~440 libu3d launches (plus the loss, the bucketed all-reduce and
+the SGD foreach kernels). Launched one by one from Python that is a host-bound stream; captured once into a
+hipGraph (torch.cuda.CUDAGraph is hipGraph on ROCm) the whole step replays with one launch. Every kernel of
+the step runs on every replay — nothing is cached — so replay does exactly the work of an eager step.
+
+Requirements the native path meets: no host syncs (no .item()), every libu3d call is asynchronous on torch's
+current stream (the capture stream during capture), scratch buffers are grow-only and reach their steady
+size in the warm-up steps, parameter gradients are written into fresh tensors (set_to_none=True) that the
+capture pool keeps at fixed addresses.
+
+The reference has no train-step function (train_amos_atlas_final.py:209-399 runs it inline); this is the
+additive helper Engine.graphed_train_step / bench.py use.
+"""
+import torch
+
+
+class GraphedStep:
+    """Capture ``step_fn() -> tensor`` once; ``__call__`` replays it and returns the captured output.
+
+    ``static_inputs`` are the tensors the step reads; ``__call__(*new)`` copies ``new`` into them first
+    (on the stream, inside the caller's timing) so each replay sees the new batch.
+    """
+
+    def __init__(self, step_fn, static_inputs=(), warmup=3, optimizer=None):
+        self.static_inputs = tuple(static_inputs)
+        self.optimizer = optimizer
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._zero()
+                step_fn()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        self._zero()
+        with torch.cuda.graph(self.graph):
+            self.out = step_fn()
+        torch.cuda.synchronize()
+
+    def _zero(self):
+        if self.optimizer is not None:
+            self.optimizer.zero_grad(set_to_none=True)
+
+    def __call__(self, *new_inputs):
+        for dst, src in zip(self.static_inputs, new_inputs):
+            if src is not None and src.data_ptr() != dst.data_ptr():
+                dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        return self.out

@@ -195,6 +195,10 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
         call("u3d_conv32_brick", 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
              dx.data_ptr(), _stream())
         return dx
+    if USE_S2_BRICK and dy.dtype == torch.bfloat16 and k == 3 and stride == 2:
+        call("u3d_conv_dgrad_s2", dy.data_ptr(), n, cout, wpk_dgrad.data_ptr(), cin, d, h, w_, dx.data_ptr(),
+             _stream())
+        return dx
     if _use_gen_brick(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
         call("u3d_convg_brick", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None, 0,
              None, dx.data_ptr(), _stream())
@@ -206,6 +210,7 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
 
 
 USE_BRICK_WGRAD = True
+USE_S2_BRICK = True  # stride-2 3^3 bf16 data gradient: one-launch parity-merged kernel (dgrad_s2.hip)
 
 
 def conv_wgrad(dy, x, k, stride, gn=None, brick=None):

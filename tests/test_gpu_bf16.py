@@ -42,20 +42,22 @@ def _act_ref(x, st, ga, be, G):
 
 SHAPES = [(2, 32, 32, (12, 10, 16), 1), (1, 32, 32, (5, 9, 70), 1), (1, 32, 64, (8, 12, 18), 2), (2, 64, 64, (6, 8, 9), 1),
           (1, 64, 32, (10, 6, 8), 1), (2, 128, 128, (4, 4, 4), 1), (1, 24, 24, (7, 9, 11), 1),
-          (2, 32, 32, (4, 10, 64), 1), (1, 32, 32, (3, 8, 32), 1), (1, 64, 128, (6, 9, 20), 1)]
+          (2, 32, 32, (4, 10, 64), 1), (1, 32, 32, (3, 8, 32), 1), (1, 64, 128, (6, 9, 20), 1),
+          (2, 32, 64, (12, 16, 34), 2), (1, 64, 128, (8, 8, 8), 2), (2, 128, 256, (12, 12, 12), 2),
+          (1, 256, 256, (6, 6, 6), 2), (1, 40, 48, (6, 10, 14), 2)]
 
 
 @pytest.fixture(params=["auto", "gen_brick", "igemm"])
 def conv_path(request):
     """auto = production routing; gen_brick = force the generic halo-brick kernel; igemm = force implicit GEMM."""
     from u3d import ops
-    saved = (ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK)
+    saved = (ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK)
     if request.param == "gen_brick":
         ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK = 0, False
     elif request.param == "igemm":
-        ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK = False, False
+        ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK = False, False, False
     yield request.param
-    ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK = saved
+    ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK = saved
 
 
 @pytest.mark.parametrize("n,cin,cout,dims,s", SHAPES)
@@ -76,8 +78,8 @@ def test_bf16_conv_fwd(gpu, conv_path, n, cin, cout, dims, s):
 @pytest.mark.parametrize("n,cin,cout,dims,s", SHAPES)
 def test_bf16_conv_dgrad(gpu, conv_path, n, cin, cout, dims, s):
     from u3d import ops
-    if s == 2 and any(d % 2 for d in dims):
-        pytest.skip("stride-2 dgrad needs even dims (as the trunk has)")
+    if s == 2 and any(d % 2 for d in dims) and conv_path == "igemm":
+        pytest.skip("the parity-class implicit-GEMM stride-2 dgrad needs even dims (as the trunk has)")
     x, w, *_ = _case(gpu, n, cin, cout, dims, False, 2)
     pf, pd, wst = ops.wstd_fwd(w, torch.bfloat16, True)
     od = tuple(ops.out_dim(d, 3, s) for d in dims)

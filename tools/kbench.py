@@ -65,13 +65,17 @@ def _wgrad(n, cin, cout, s, k, stride):
     return us, flop
 
 
-for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 256), ("6", 6, 320)]:
+for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 256), ("6", 6, 256)]:
     CASES[f"fwd{lvl}"] = (lambda s=s, c=c: _fwd(2, c, c, s, 3, 1, True, True))
     CASES[f"dgrad{lvl}"] = (lambda s=s, c=c: _dgrad(2, c, c, s, 3, 1))
     CASES[f"wgrad{lvl}"] = (lambda s=s, c=c: _wgrad(2, c, c, s, 3, 1))
 CASES["fwd12nogn"] = lambda: _fwd(2, 256, 256, 12, 3, 1, False, False)
 CASES["fwd_s2_24"] = lambda: _fwd(2, 128, 256, 24, 3, 2, True, False)
 CASES["dgrad_s2_24"] = lambda: _dgrad(2, 128, 256, 24, 3, 2)
+CASES["dgrad_s2_96"] = lambda: _dgrad(2, 32, 64, 96, 3, 2)
+CASES["dgrad_s2_48"] = lambda: _dgrad(2, 64, 128, 48, 3, 2)
+CASES["dgrad_s2_12"] = lambda: _dgrad(2, 256, 256, 12, 3, 2)
+CASES["fwd6nogn"] = lambda: _fwd(2, 256, 256, 6, 3, 1, False, False)
 CASES["head96"] = lambda: _fwd(2, 32, 16, 96, 1, 1, True, False)
 
 if __name__ == "__main__":
