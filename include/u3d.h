@@ -61,6 +61,20 @@ typedef struct u3d_wstd_desc {
   float* dw;
   int cout, cin, ksize, standardize, nsplit, accumulate;
 } u3d_wstd_desc;
+/* Fused SGD step over up to U3D_SGD_BATCH_MAX fp32 tensors (torch.optim.SGD semantics: d = g (+ wd*p),
+ * buf = momentum*buf + (1-dampening)*d (buf = d when init), d = nesterov ? d + momentum*buf : buf, p -= lr*d;
+ * maximize negates g). lr is read from device memory (graph-capturable LR changes). Reference: the SGD of
+ * train_amos_atlas_final.py:132-135,378. */
+typedef struct {
+  float* p;
+  const float* g;
+  float* buf; /* momentum buffer (nullptr when momentum == 0) */
+  long long n;
+} u3d_sgd_desc;
+#define U3D_SGD_BATCH_MAX 48
+int u3d_sgd_step(const u3d_sgd_desc* descs, int count, const float* lr, float momentum, float dampening,
+                 float weight_decay, int nesterov, int maximize, int init, u3d_stream_t stream);
+
 #define U3D_WSTD_BATCH_MAX 48
 int u3d_wstd_fwd_batch(int dtype, const u3d_wstd_desc* descs, int count, u3d_stream_t stream);
 /* scratch: device fp32 buffer of u3d_wstd_bwd_scratch_bytes(descs, count) bytes (per-row sums) */
@@ -96,6 +110,15 @@ int u3d_conv_wgrad(int dtype, const void* dy, const void* x, int n, int cin, int
  * [27][cin_p][cout_p]. Autograd of F.conv3d(stride=2, padding=1) in Conv3d.forward (reference unet3D.py:27). */
 int u3d_conv_dgrad_s2(const void* dy, int n, int cout, const void* wpk_dgrad, int cin, int d, int h, int w, void* dx,
                       u3d_stream_t stream);
+
+/* bf16 3^3 stride-1 conv for the small deep-level volumes (24^3 and below): one workgroup = a brick of <= 256
+ * output voxels x 32 output channels with the whole contraction (no split-K slabs), GN+ReLU prologue applied
+ * once per staged element, residual epilogue. flip/wpk/cin/cout as u3d_convg_brick. When there are too few
+ * (brick, co tile) pairs to occupy the GPU the contraction is split over workgroups into fp32 partials in ws
+ * (ws_bytes; nullptr/0 = no split) summed in fixed order by a second kernel. */
+int u3d_conv_small(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                   const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                   const void* residual, void* y, float* ws, long long ws_bytes, u3d_stream_t stream);
 
 /* bf16 32->32 3^3 stride-1 conv (cin = cout = 32; the full-resolution layers) in halo-brick form with the
  * weights held in registers: flip=0 forward (wpk = forward pack, optional GN+ReLU prologue and residual),
@@ -137,7 +160,9 @@ int u3d_stem_wgrad(int dtype, const void* dy, const float* x, int n, int cin, in
 
 /* ---------------------------------------------------------------- GroupNorm (A4) statistics / backward
  * nn.GroupNorm(G, C) statistics (biased variance, eps 1e-5): stats[n][g] = (mean, 1/sqrt(var+eps)).
- * Deterministic: per-block shifted partial sums in fp32, combined in fp64 in fixed order. */
+ * Deterministic: per-block shifted partial sums in fp32, combined in fp64 in fixed order by the last block to
+ * finish (one launch). ws (u3d_gn_workspace_bytes) must be ZERO-FILLED when first allocated: its first 256 B
+ * hold completion counters that every launch leaves at zero (calls sharing one ws must be stream-ordered). */
 long long u3d_gn_workspace_bytes(int n, int c, long long v);
 int u3d_gn_stats(int dtype, const void* x, int n, int c, long long v, int groups, float* stats, float* ws,
                  u3d_stream_t stream);
@@ -145,7 +170,9 @@ int u3d_gn_stats(int dtype, const void* x, int n, int c, long long v, int groups
  * c % 8 == 0: materialised ahead of the implicit GEMM for small deep-layer activations. */
 int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v, int groups, const float* stats,
                  const float* gamma, const float* beta, void* y, u3d_stream_t stream);
-/* Backward of relu(group_norm(x)) given dA (grad wrt the ReLU output): dx (+)= ..., dgamma/dbeta (+)= ... */
+/* Backward of relu(group_norm(x)) given dA (grad wrt the ReLU output): dx (+)= ..., dgamma/dbeta (+)= ...
+ * Two launches (partial sums + last-block combine into per-(n,c) coefficients; elementwise apply); same ws
+ * rules as u3d_gn_stats; n * c <= 2048, <= 64 channels per group. */
 int u3d_gn_bwd(int dtype, const void* da, const void* x, int n, int c, long long v, int groups,
                const float* stats, const float* gamma, const float* beta, void* dx, int accumulate,
                float* dgamma, float* dbeta, int accumulate_params, float* ws, u3d_stream_t stream);

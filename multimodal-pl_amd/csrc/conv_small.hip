@@ -1,0 +1,306 @@
+// 3^3 stride-1 convolution (forward / data gradient) for the small deep-level volumes (24^3, 12^3, 6^3 of the
+// 96^3 U-Net: 128 / 256 channels), bf16, halo-brick form sized for PARALLELISM rather than reuse.
+//
+// Reference: F.conv3d in Conv3d.forward (unet3D.py:27) through NoBottleneck (:56-73) at layer2..4, fusion and
+// x8/x4 decoder blocks, and its autograd data gradient.
+//
+// At 12^3 x 2 samples a layer is 3456 output voxels x 256 channels = 864 output tiles of 32x32 with a
+// 6912-deep contraction: the implicit GEMM's 128x128 tiles leave most CUs idle or need split-K slabs, and
+// re-read every tap's operands through L2. Here:
+//   * one workgroup (8 waves) = one brick of up to 256 output voxels x one 32-channel output tile; each wave
+//     owns one 32-voxel row tile and the full contraction (27 taps x cin) -> no split-K, no slab traffic;
+//   * the brick's extents divide the volume evenly (3x6x12 at 12^3, 6^3 whole at 6^3) so few rows idle;
+//   * K loop = 32-channel input chunks: the input halo ((bd+2)(bh+2)(bw+2) voxels) is staged once per chunk
+//     into LDS with GroupNorm + ReLU applied once per element, the 27 taps' weights of the chunk beside it;
+//     the 27 taps are 27 shifted windows of the halo (per-lane row + tap offset); the next chunk is prefetched
+//     into registers while the MFMAs run;
+//   * epilogue through LDS: coalesced 64-B voxel rows, residual added on the way out.
+// FLIP = data gradient: flipped tap offsets with the [t][ci][co] pack, no prologue.
+#include "common.h"
+
+namespace u3d {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+constexpr int SC_NT = 512;
+constexpr int SC_HMAX = 640;                     // halo rows (max)
+constexpr int SC_PS = SC_HMAX * 16 + 64;         // halo plane stride (+64 B: conflict-free staging writes)
+constexpr int SC_NWR = 27 * 32;                  // weight rows (tap, co)
+constexpr int SC_WPS = SC_NWR * 16 + 64;         // weight plane stride
+constexpr int SC_HLD = SC_HMAX * 4 / SC_NT;      // 5 halo loads per thread
+constexpr int SC_WLD = (SC_NWR * 4 + SC_NT - 1) / SC_NT;  // 7 weight loads per thread
+constexpr int SC_LDS = 4 * SC_PS + 4 * SC_WPS;
+
+struct SCGeom {
+  int n, d, h, w;
+  int cin, cin_p, cout, cout_p;
+  int bd, bh, bw;          // output brick
+  int hh, hw, nh;          // halo pitch (bh+2, bw+2) and rows
+  int nbd, nbh, nbw, nct;  // bricks per dim, 32-wide output channel tiles
+  int nv;                  // voxels per brick (<= 256)
+  int gn_groups;
+  int nks, cpk;            // K split: workgroups per output tile, 32-channel chunks per split
+  float* slab;             // fp32 partials [nks][n][d][h][w][cout] when nks > 1
+};
+
+template <bool FLIP>
+__global__ __launch_bounds__(SC_NT, 1) void conv_small_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
+                                                             bf16* __restrict__ y, const bf16* __restrict__ res,
+                                                             const float* __restrict__ gstat,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, SCGeom g) {
+  __shared__ __attribute__((aligned(16))) char smem[SC_LDS];
+  char* const hal = smem;
+  char* const wts = smem + 4 * SC_PS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+
+  int bid;  // XCD-aware: each XCD owns a contiguous range of (brick, co tile)
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int ks = bid % g.nks;
+  int b = bid / g.nks;
+  const int co0 = (b % g.nct) * 32;
+  b /= g.nct;
+  const int bw_ = b % g.nbw; b /= g.nbw;
+  const int bh_ = b % g.nbh; b /= g.nbh;
+  const int bd_ = b % g.nbd;
+  const int nn = b / g.nbd;
+  const int o0d = bd_ * g.bd, o0h = bh_ * g.bh, o0w = bw_ * g.bw;
+
+  const int v = min(wave * 32 + r, g.nv - 1);
+  const int vw = v % g.bw, vh = (v / g.bw) % g.bh, vd = v / (g.bw * g.bh);
+  const int arow = (vd * g.hh + vh) * g.hw + vw;  // halo row of tap (0,0,0)
+  const bool active = wave * 32 < g.nv;
+  const bool has_gn = gstat != nullptr;
+
+  const int sch = tid & 3, srow0 = tid >> 2;
+  u32x4 hpre[SC_HLD], wpre[SC_WLD];
+  unsigned hmask = 0;
+  auto halo_load = [&](int c) {
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < SC_HLD; ++i) {
+      const int row = srow0 + i * (SC_NT / 4);
+      u32x4 val = {0u, 0u, 0u, 0u};
+      if (row < g.nh) {
+        const int xw = row % g.hw, xh = (row / g.hw) % g.hh, xd = row / (g.hw * g.hh);
+        const int zd = o0d - 1 + xd, zh = o0h - 1 + xh, zw = o0w - 1 + xw, cc = c * 32 + sch * 8;
+        if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w &&
+            cc < g.cin) {
+          val = *reinterpret_cast<const u32x4*>(x + ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc);
+          m |= 1u << i;
+        }
+      }
+      hpre[i] = val;
+    }
+    hmask = m;
+  };
+  auto w_load = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < SC_WLD; ++i) {
+      const int id = tid + i * SC_NT;
+      u32x4 val = {0u, 0u, 0u, 0u};
+      if (id < SC_NWR * 4) {
+        const int row = id >> 2, t = row >> 5, co = co0 + (row & 31);
+        if (co < g.cout_p)
+          val = *reinterpret_cast<const u32x4*>(wpk + ((long long)t * g.cout_p + co) * g.cin_p + c * 32 + (id & 3) * 8);
+      }
+      wpre[i] = val;
+    }
+  };
+  f32x2 sc[4], sh[4];  // GN scale/shift of the chunk being staged (computed with its prefetch)
+  auto gn_load = [&](int c) {
+    if (has_gn) gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, nn, c * 32 + sch * 8, sc, sh);
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < SC_HLD; ++i) {
+      const int row = srow0 + i * (SC_NT / 4);
+      if (row < g.nh) {
+        u32x4 val = hpre[i];
+        if (has_gn && ((hmask >> i) & 1u)) val = gn_relu8(val, sc, sh);
+        *reinterpret_cast<u32x4*>(hal + sch * SC_PS + row * 16) = val;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < SC_WLD; ++i) {
+      const int id = tid + i * SC_NT;
+      if (id < SC_NWR * 4) *reinterpret_cast<u32x4*>(wts + (id & 3) * SC_WPS + (id >> 2) * 16) = wpre[i];
+    }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+
+  const int c0 = ks * g.cpk, c1 = min(g.cin_p / 32, c0 + g.cpk);
+  halo_load(c0);
+  w_load(c0);
+  gn_load(c0);
+  commit();
+  __syncthreads();
+  for (int c = c0; c < c1; ++c) {
+    const bool more = c + 1 < c1;
+    if (more) {
+      halo_load(c + 1);
+      w_load(c + 1);
+      gn_load(c + 1);
+    }
+    if (active) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int plane = 2 * s + hh;
+        const char* ab = hal + plane * SC_PS + arow * 16;
+        const char* bb = wts + plane * SC_WPS + r * 16;
+#pragma unroll
+        for (int t = 0; t < 27; ++t) {
+          const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
+          const int od = FLIP ? 2 - td : td, oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(ab + ((od * g.hh + oh) * g.hw + ow) * 16);
+          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bb + t * 32 * 16);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc, 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      commit();
+      __syncthreads();
+    }
+  }
+  if (g.nks > 1) {  // fp32 partial through the wave's LDS tile: 128-B rows, coalesced
+    float* const ept = reinterpret_cast<float*>(smem + wave * 4096);
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ept[((i & 3) + 8 * (i >> 2) + 4 * hh) * 32 + r] = acc[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (active) {
+      float* const sl = g.slab + (long long)ks * g.n * g.d * g.h * g.w * g.cout;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int qi = lane + 64 * u, part = qi & 7, row = qi >> 3;
+        const int vv = wave * 32 + row;
+        const int uw = vv % g.bw, uh = (vv / g.bw) % g.bh, ud = vv / (g.bw * g.bh);
+        const int zd = o0d + ud, zh = o0h + uh, zw = o0w + uw, co = co0 + part * 4;
+        if (vv < g.nv && zd < g.d && zh < g.h && zw < g.w && co < g.cout)
+          *reinterpret_cast<f32x4*>(sl + ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cout + co) =
+              *reinterpret_cast<const f32x4*>(ept + qi * 4);
+      }
+    }
+    return;
+  }
+
+  // epilogue: wave tile [32 rows][32 co] bf16 (2 KB) -> 16-B chunks, 4 lanes per output voxel
+  char* const ept = smem + wave * 2048;
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
+      *reinterpret_cast<bf16*>(ept + (row * 32 + r) * 2) = from_f<bf16>(acc[i]);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  if (active) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qi = lane + 64 * u, part = qi & 3, row = qi >> 2;
+      const int vv = wave * 32 + row;
+      const int uw = vv % g.bw, uh = (vv / g.bw) % g.bh, ud = vv / (g.bw * g.bh);
+      const int zd = o0d + ud, zh = o0h + uh, zw = o0w + uw, co = co0 + part * 8;
+      if (vv < g.nv && zd < g.d && zh < g.h && zw < g.w && co < g.cout) {
+        const long long off = ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cout + co;
+        u32x4 val = *reinterpret_cast<const u32x4*>(ept + qi * 16);
+        if (res) {
+          float a[8], q[8];
+          load16<bf16>(reinterpret_cast<const bf16*>(&val), a);
+          load16<bf16>(res + off, q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] += q[e];
+          store16<bf16>(reinterpret_cast<bf16*>(&val), a);
+        }
+        *reinterpret_cast<u32x4*>(y + off) = val;
+      }
+    }
+  }
+}
+
+// y = bf16(sum_s slab[s] (+ residual)), 4 channels per thread, splits summed in fixed order
+__global__ __launch_bounds__(256) void small_reduce_kernel(const float* __restrict__ slab, int nks, long long per4,
+                                                           const bf16* __restrict__ res, bf16* __restrict__ y) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < per4; i += (long long)gridDim.x * 256) {
+    f32x4 v = reinterpret_cast<const f32x4*>(slab)[i];
+    for (int s = 1; s < nks; ++s) v += reinterpret_cast<const f32x4*>(slab)[s * per4 + i];
+    if (res) {
+      const uint2 q = reinterpret_cast<const uint2*>(res)[i];
+      v[0] += __uint_as_float(q.x << 16);
+      v[1] += __uint_as_float(q.x & 0xffff0000u);
+      v[2] += __uint_as_float(q.y << 16);
+      v[3] += __uint_as_float(q.y & 0xffff0000u);
+    }
+    uint2 o;
+    o.x = (uint32_t)from_f<bf16>(v[0]) | ((uint32_t)from_f<bf16>(v[1]) << 16);
+    o.y = (uint32_t)from_f<bf16>(v[2]) | ((uint32_t)from_f<bf16>(v[3]) << 16);
+    reinterpret_cast<uint2*>(y)[i] = o;
+  }
+}
+
+}  // namespace u3d
+
+using namespace u3d;
+
+extern "C" int u3d_conv_small(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                              const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                              const void* residual, void* y, float* ws, long long ws_bytes, u3d_stream_t stream) {
+  U3D_REQUIRE(x && wpk && y && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv_small: bad args");
+  U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "conv_small: channels must be multiples of 8");
+  U3D_REQUIRE(!gn_stats || (!flip && gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0),
+              "conv_small: bad GN prologue");
+  SCGeom g{};
+  g.n = n; g.d = d; g.h = h; g.w = w;
+  g.cin = cin; g.cin_p = round_up(cin, 32); g.cout = cout; g.cout_p = round_up(cout, 32);
+  g.gn_groups = gn_groups;
+  auto even = [](int q, int mx) { return cdiv(q, cdiv(q, std::max(1, mx))); };
+  g.bw = even(w, 16);
+  g.bh = even(h, 256 / (g.bw * 2));
+  g.bd = even(d, std::min(d, 256 / (g.bw * g.bh)));
+  while ((g.bd + 2) * (g.bh + 2) * (g.bw + 2) > SC_HMAX && g.bd > 1) --g.bd;
+  while ((g.bd + 2) * (g.bh + 2) * (g.bw + 2) > SC_HMAX && g.bh > 1) --g.bh;
+  while ((g.bd + 2) * (g.bh + 2) * (g.bw + 2) > SC_HMAX && g.bw > 1) --g.bw;
+  g.nv = g.bd * g.bh * g.bw;
+  g.hh = g.bh + 2; g.hw = g.bw + 2;
+  g.nh = (g.bd + 2) * g.hh * g.hw;
+  g.nbd = cdiv(d, g.bd); g.nbh = cdiv(h, g.bh); g.nbw = cdiv(w, g.bw);
+  g.nct = g.cout_p / 32;
+  const long long tiles = (long long)n * g.nbd * g.nbh * g.nbw * g.nct;
+  // split the contraction over workgroups until ~2 workgroups per CU: the per-CU operand stream (55 KB of
+  // weights + the halo per 32-channel chunk), not the MFMAs, bounds these small layers
+  const int nchunk = g.cin_p / 32;
+  int nks = (int)std::min<long long>(nchunk, std::max<long long>(1, (512 + tiles - 1) / tiles));
+  const long long slab1 = (long long)n * d * h * w * cout * 4;
+  if (cout % 4) nks = 1;
+  while (nks > 1 && (!ws || nks * slab1 > ws_bytes)) --nks;
+  g.cpk = cdiv(nchunk, nks);
+  g.nks = cdiv(nchunk, g.cpk);
+  g.slab = g.nks > 1 ? ws : nullptr;
+  const long long nwg = tiles * g.nks;
+  U3D_REQUIRE(nwg < (1LL << 31), "conv_small: grid too large");
+  hipStream_t s = (hipStream_t)stream;
+  if (flip)
+    hipLaunchKernelGGL(conv_small_kernel<true>, dim3((unsigned)nwg), dim3(SC_NT), 0, s, (const bf16*)x,
+                       (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
+  else
+    hipLaunchKernelGGL(conv_small_kernel<false>, dim3((unsigned)nwg), dim3(SC_NT), 0, s, (const bf16*)x,
+                       (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
+  int rc = check_launch("conv_small_kernel");
+  if (rc || g.nks == 1) return rc;
+  const long long per4 = slab1 / 16;
+  hipLaunchKernelGGL(small_reduce_kernel, dim3((unsigned)std::min<long long>(4096, (per4 + 255) / 256)), dim3(256), 0,
+                     s, ws, g.nks, per4, (const bf16*)residual, (bf16*)y);
+  return check_launch("small_reduce_kernel");
+}

@@ -4,13 +4,19 @@
 // prologue (conv.hip), so only statistics are produced here.
 //
 // Determinism: each block reduces a fixed voxel range into per-channel fp32 partials (of values shifted
-// by a per-group constant, so the sum of squares does not cancel), and a finalize pass combines blocks
-// and channels in fp64 in a fixed order. No float atomics.
+// by a per-group constant, so the sum of squares does not cancel); the LAST block to finish (completion
+// counter, agent-scope release/acquire) combines blocks and channels in fp64 in a fixed order — one launch for
+// the statistics, two for the backward (partial+final, apply). No float atomics.
+//
+// Workspace (u3d_gn_workspace_bytes): [256 B completion counters][partials n x nblk x 2 x c f32][coef n x 5 x c
+// f32]. It must be zero-filled when first allocated; every launch leaves its counter at zero again.
 #include "common.h"
 
 namespace u3d {
 
-constexpr int GT = 256;
+constexpr int GT = 512;
+constexpr int GN_CNT_BYTES = 256;
+constexpr int GN_PAIRS_MAX = 2048;  // n * c of the backward's last-block combine (LDS)
 
 struct RedGeom {
   int n, c, groups, cpg, nblk, vpb, chn, vlanes;  // chn = 16-B chunks per voxel, vlanes = voxels per pass
@@ -26,7 +32,11 @@ static RedGeom make_geom(int n, int c, long long v, int groups, int vec) {
   g.cpg = groups > 0 ? c / groups : 0;
   g.chn = c / vec;
   g.vlanes = std::max(1, GT / g.chn);
-  long long want = std::max<long long>(g.vlanes, (v * n + 2047) / 2048);
+  // blocks in all ~ bytes / 64 KB, 16..256 (512 threads, 32 KB of loads in flight each): every CU streams on
+  // the big tensors, and the partials stay few enough for a one-round last-block combine
+  const long long bytes = v * n * c * (vec == 8 ? 2 : 4);
+  const long long nb = std::min<long long>(256, std::max<long long>(16, bytes >> 16));
+  long long want = std::max<long long>((long long)g.vlanes * 4, (v * n + nb - 1) / nb);
   g.vpb = (int)((want + g.vlanes - 1) / g.vlanes * g.vlanes);
   g.nblk = (int)((v + g.vpb - 1) / g.vpb);
   return g;
@@ -47,13 +57,79 @@ __device__ __forceinline__ void block_channel_reduce(float (&acc)[NV][VEC], floa
       const int j = c / VEC, e = c % VEC;
       float s = 0.f;
       for (int l = 0; l < g.vlanes; ++l) s += lds[(l * g.chn + j) * VEC + e];
-      out[k * g.c + c] = s;
+      __hip_atomic_store(out + k * g.c + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: write-through
     }
   }
 }
 
+// True (in every thread) for the block that finished last. Hand-off without fences (MI355X guide, inter-
+// workgroup visibility): partials are written with sc1 (write-through) stores, every wave drains them
+// (vmcnt(0)) before the barrier, one lane per block adds to the counter (agent scope), and the last block
+// reads the partials with sc1 loads (L2-served, not a stale L1).
+__device__ __forceinline__ bool block_is_last(unsigned* cnt, unsigned total) {
+  __shared__ unsigned s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(cnt, 1u) == total - 1;
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) atomicExch(cnt, 0u);  // ready for the next launch
+  return s_last;
+}
+
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Last-block combine, phase 1: cs[p] = (sum_b P[n][b][0][c], sum_b P[n][b][1][c]) in fp64 for p = n*C + c.
+// Threads run along channels (coalesced partial rows) and over block slices; slices combine in fixed order.
+__device__ __forceinline__ void combine_channels(const float* __restrict__ ws, const RedGeom& g, double (*cs)[2]) {
+  __shared__ double part[GT][2];
+  const int tid = threadIdx.x, npairs = g.n * g.c;
+  const int spl = npairs >= GT ? 1 : GT / npairs;
+  for (int p0 = 0; p0 < npairs; p0 += GT) {
+    const int p = p0 + tid % min(npairs, GT), sl = tid / min(npairs, GT);
+    double s1 = 0, s2 = 0;
+    if (p < npairs && sl < spl) {
+      const int nn = p / g.c, c = p % g.c;
+      const float* q = ws + (long long)nn * g.nblk * 2 * g.c + c;  // partials of other blocks: sc1 loads only
+      int b = sl;
+      for (; b + 31 * spl < g.nblk; b += 32 * spl) {  // 64 loads in flight: the combine is one latency round
+        float a[32], bb[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+          a[u] = ld_sc1(q + (long long)(b + u * spl) * 2 * g.c);
+          bb[u] = ld_sc1(q + (long long)(b + u * spl) * 2 * g.c + g.c);
+        }
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+          s1 += a[u];
+          s2 += bb[u];
+        }
+      }
+      for (; b < g.nblk; b += spl) {
+        s1 += ld_sc1(q + (long long)b * 2 * g.c);
+        s2 += ld_sc1(q + (long long)b * 2 * g.c + g.c);
+      }
+    }
+    part[tid][0] = s1;
+    part[tid][1] = s2;
+    __syncthreads();
+    if (tid < min(npairs - p0, GT)) {
+      double t1 = 0, t2 = 0;
+      for (int k = 0; k < spl; ++k) {
+        t1 += part[k * min(npairs, GT) + tid][0];
+        t2 += part[k * min(npairs, GT) + tid][1];
+      }
+      cs[p0 + tid][0] = t1;
+      cs[p0 + tid][1] = t2;
+    }
+    __syncthreads();
+  }
+}
+
 template <typename T>
-__global__ __launch_bounds__(GT) void gn_stats_partial(const T* __restrict__ x, RedGeom g, float* __restrict__ ws) {
+__global__ __launch_bounds__(GT) void gn_stats_kernel(const T* __restrict__ x, RedGeom g, float* __restrict__ ws,
+                                                     unsigned* __restrict__ cnt, float* __restrict__ stats) {
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float lds[GT * VEC];
   const int n = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
@@ -65,191 +141,178 @@ __global__ __launch_bounds__(GT) void gn_stats_partial(const T* __restrict__ x, 
     float shift[VEC];
     for (int e = 0; e < VEC; ++e) shift[e] = to_f(xn[((j * VEC + e) / g.cpg) * g.cpg]);  // x[n, voxel 0, first ch of group]
     const long long v0 = (long long)blk * g.vpb, v1 = std::min<long long>(g.v, v0 + g.vpb);
-    for (long long v = v0 + vl; v < v1; v += g.vlanes) {
+    long long v = v0 + vl;
+    for (; v + 3 * g.vlanes < v1; v += 4 * g.vlanes) {  // 4 loads in flight per thread
+      float xv[4][VEC];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load16<T>(xn + (v + u * g.vlanes) * g.c + j * VEC, xv[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float d = xv[u][e] - shift[e];
+          acc[0][e] += d;
+          acc[1][e] = fmaf(d, d, acc[1][e]);
+        }
+    }
+    for (; v < v1; v += g.vlanes) {
       float xv[VEC];
       load16<T>(xn + v * g.c + j * VEC, xv);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        float d = xv[e] - shift[e];
+        const float d = xv[e] - shift[e];
         acc[0][e] += d;
         acc[1][e] = fmaf(d, d, acc[1][e]);
       }
     }
   }
   block_channel_reduce<VEC, 2>(acc, lds, g, ws + ((long long)n * g.nblk + blk) * 2 * g.c);
-}
-
-// one block per (n, group)
-template <typename T>
-__global__ __launch_bounds__(GT) void gn_stats_final(const T* __restrict__ x, RedGeom g, const float* __restrict__ ws,
-                                                    float* __restrict__ stats) {
-  __shared__ double red[2][GT / 64];
-  const int n = blockIdx.x / g.groups, gr = blockIdx.x % g.groups;
-  double s1 = 0, s2 = 0;
-  const int items = g.nblk * g.cpg;
-  for (int it = threadIdx.x; it < items; it += GT) {
-    const int b = it / g.cpg, c = gr * g.cpg + it % g.cpg;
-    const float* p = ws + ((long long)n * g.nblk + b) * 2 * g.c;
-    s1 += p[c];
-    s2 += p[g.c + c];
-  }
-  s1 = wave_sum(s1);
-  s2 = wave_sum(s2);
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = s1;
-    red[1][threadIdx.x >> 6] = s2;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double a = 0, b = 0;
-    for (int i = 0; i < GT / 64; ++i) {
-      a += red[0][i];
-      b += red[1][i];
+  if (!block_is_last(cnt, (unsigned)(g.n * g.nblk))) return;
+  // combine: per (n, c) sums over the blocks, then per (n, group) over its channels, fixed order, fp64
+  __shared__ double cs[GN_PAIRS_MAX][2];
+  combine_channels(ws, g, cs);
+  for (int p = tid; p < g.n * g.groups; p += GT) {
+    const int nn = p / g.groups, gr = p % g.groups;
+    double s1 = 0, s2 = 0;
+    for (int k = 0; k < g.cpg; ++k) {
+      s1 += cs[nn * g.c + gr * g.cpg + k][0];
+      s2 += cs[nn * g.c + gr * g.cpg + k][1];
     }
     const double M = (double)g.v * g.cpg;
-    const double shift = to_f(x[(long long)n * g.v * g.c + gr * g.cpg]);
-    const double dm = a / M;
-    double var = b / M - dm * dm;
+    const double shift = to_f(x[(long long)nn * g.v * g.c + gr * g.cpg]);
+    const double dm = s1 / M;
+    double var = s2 / M - dm * dm;
     if (var < 0) var = 0;
-    stats[(n * g.groups + gr) * 2] = (float)(shift + dm);
-    stats[(n * g.groups + gr) * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+    stats[(nn * g.groups + gr) * 2] = (float)(shift + dm);
+    stats[(nn * g.groups + gr) * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
   }
 }
 
-// backward partial: per channel s1 = sum dA*m, s2 = sum dA*m*xhat, m = [gamma*xhat + beta > 0]
+// backward: per channel s1 = sum g, s2 = sum g*xhat (g = m*dA, m = the forward prologue's relu test
+// x*sc + sh > 0), then in the last block the apply coefficients of every (n, c), SoA coef[n][5][C]:
+//   sc, sh, alpha = rs*gamma_c, bx = -rs^2 * b_g, d = -rs*a_g + rs^2*b_g*mu
+// with a_g = sum_{c in g} gamma_c s1_c / M, b_g = sum gamma_c s2_c / M, so that
+//   dx = alpha * m * dA + bx * x + d  ==  rs * (gamma*m*dA - a_g - xhat * b_g)   (autograd of GN, unet3D.py:44-53)
+// and dgamma_c = sum_n s2, dbeta_c = sum_n s1.
 template <typename T>
 __global__ __launch_bounds__(GT) void gn_bwd_partial(const T* __restrict__ da, const T* __restrict__ x, RedGeom g,
                                                     const float* __restrict__ stats, const float* __restrict__ gamma,
-                                                    const float* __restrict__ beta, float* __restrict__ ws) {
+                                                    const float* __restrict__ beta, float* __restrict__ ws,
+                                                    unsigned* __restrict__ cnt, float* __restrict__ coef,
+                                                    float* __restrict__ dgamma, float* __restrict__ dbeta, int accp) {
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float lds[GT * VEC];
+  __shared__ double cs[GN_PAIRS_MAX][2];
   const int n = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
   const long long base = (long long)n * g.v * g.c;
   const int j = tid % g.chn, vl = tid / g.chn;
   float acc[2][VEC];
   for (int e = 0; e < VEC; ++e) acc[0][e] = acc[1][e] = 0.f;
   if (vl < g.vlanes) {
-    float mu[VEC], rs[VEC], ga[VEC], be[VEC];
+    float mu[VEC], rs[VEC], sc[VEC], sh[VEC];
     for (int e = 0; e < VEC; ++e) {
       const int c = j * VEC + e, gr = c / g.cpg;
       mu[e] = stats[(n * g.groups + gr) * 2];
       rs[e] = stats[(n * g.groups + gr) * 2 + 1];
-      ga[e] = gamma[c];
-      be[e] = beta[c];
+      sc[e] = rs[e] * gamma[c];
+      sh[e] = beta[c] - mu[e] * sc[e];
     }
     const long long v0 = (long long)blk * g.vpb, v1 = std::min<long long>(g.v, v0 + g.vpb);
-    for (long long v = v0 + vl; v < v1; v += g.vlanes) {
-      float xv[VEC], dv[VEC];
-      load16<T>(x + base + v * g.c + j * VEC, xv);
-      load16<T>(da + base + v * g.c + j * VEC, dv);
+    auto step = [&](const float (&xv)[VEC], const float (&dv)[VEC]) {
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
         const float xh = (xv[e] - mu[e]) * rs[e];
-        const float gd = fmaf(ga[e], xh, be[e]) > 0.f ? dv[e] : 0.f;
+        const float gd = fmaf(xv[e], sc[e], sh[e]) > 0.f ? dv[e] : 0.f;
         acc[0][e] += gd;
         acc[1][e] = fmaf(gd, xh, acc[1][e]);
       }
+    };
+    long long v = v0 + vl;
+    for (; v + g.vlanes < v1; v += 2 * g.vlanes) {  // 4 loads in flight per thread
+      float xv[2][VEC], dv[2][VEC];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        load16<T>(x + base + (v + u * g.vlanes) * g.c + j * VEC, xv[u]);
+        load16<T>(da + base + (v + u * g.vlanes) * g.c + j * VEC, dv[u]);
+      }
+      step(xv[0], dv[0]);
+      step(xv[1], dv[1]);
+    }
+    for (; v < v1; v += g.vlanes) {
+      float xv[VEC], dv[VEC];
+      load16<T>(x + base + v * g.c + j * VEC, xv);
+      load16<T>(da + base + v * g.c + j * VEC, dv);
+      step(xv, dv);
     }
   }
   block_channel_reduce<VEC, 2>(acc, lds, g, ws + ((long long)n * g.nblk + blk) * 2 * g.c);
-}
-
-// one block per channel: csum[n][c] = (s1, s2) in fp64; dgamma/dbeta
-__global__ __launch_bounds__(GT) void gn_bwd_final(RedGeom g, const float* __restrict__ ws, double* __restrict__ csum,
-                                                  float* __restrict__ dgamma, float* __restrict__ dbeta, int accp) {
-  __shared__ double red[2][GT / 64];
-  const int c = blockIdx.x;
-  double tg = 0, tb = 0;
-  for (int n = 0; n < g.n; ++n) {
-    double s1 = 0, s2 = 0;
-    for (int b = threadIdx.x; b < g.nblk; b += GT) {
-      const float* p = ws + ((long long)n * g.nblk + b) * 2 * g.c;
-      s1 += p[c];
-      s2 += p[g.c + c];
+  if (!block_is_last(cnt, (unsigned)(g.n * g.nblk))) return;
+  // (1) per (n, c): fp64 sums over the blocks, fixed order
+  const int npairs = g.n * g.c;
+  combine_channels(ws, g, cs);
+  // (2) apply coefficients per (n, c); (3) dgamma / dbeta per c
+  const double M = (double)g.v * g.cpg;
+  for (int p = tid; p < npairs; p += GT) {
+    const int nn = p / g.c, c = p % g.c, gr = c / g.cpg;
+    double a = 0, bb = 0;
+    for (int k = 0; k < g.cpg; ++k) {
+      const int cc = gr * g.cpg + k;
+      a += (double)gamma[cc] * cs[nn * g.c + cc][0];
+      bb += (double)gamma[cc] * cs[nn * g.c + cc][1];
     }
-    s1 = wave_sum(s1);
-    s2 = wave_sum(s2);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) {
-      red[0][threadIdx.x >> 6] = s1;
-      red[1][threadIdx.x >> 6] = s2;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double a = 0, b = 0;
-      for (int i = 0; i < GT / 64; ++i) {
-        a += red[0][i];
-        b += red[1][i];
-      }
-      csum[(n * g.c + c) * 2] = a;
-      csum[(n * g.c + c) * 2 + 1] = b;
-      tb += a;
-      tg += b;
-    }
+    const float ca = (float)(a / M), cb = (float)(bb / M);
+    const float mu = stats[(nn * g.groups + gr) * 2], rs = stats[(nn * g.groups + gr) * 2 + 1];
+    const float scv = rs * gamma[c];
+    float* o = coef + (long long)nn * 5 * g.c;
+    o[c] = scv;
+    o[g.c + c] = beta[c] - mu * scv;
+    o[2 * g.c + c] = rs * gamma[c];
+    o[3 * g.c + c] = -rs * rs * cb;
+    o[4 * g.c + c] = -rs * ca + rs * rs * cb * mu;
   }
-  if (threadIdx.x == 0) {
+  for (int c = tid; c < g.c; c += GT) {
+    double tg = 0, tb = 0;
+    for (int nn = 0; nn < g.n; ++nn) {
+      tb += cs[nn * g.c + c][0];
+      tg += cs[nn * g.c + c][1];
+    }
     if (dgamma) dgamma[c] = (accp ? dgamma[c] : 0.f) + (float)tg;
     if (dbeta) dbeta[c] = (accp ? dbeta[c] : 0.f) + (float)tb;
   }
 }
 
-// dx (+)= rstd * (gamma*m*dA - (a_g + xhat*b_g)/M),  a_g = sum_{c in g} gamma_c s1, b_g = sum gamma_c s2
+// dx (+)= alpha*m*dA + bx*x + d per element; grid (blocks, n): a thread's 16-B channel chunk is fixed (the
+// grid stride is a multiple of the chunks per voxel), so its 5 x VEC coefficients load once into registers.
 template <typename T>
 __global__ __launch_bounds__(GT) void gn_bwd_apply(const T* __restrict__ da, const T* __restrict__ x, RedGeom g,
-                                                  const float* __restrict__ stats, const float* __restrict__ gamma,
-                                                  const float* __restrict__ beta, const double* __restrict__ csum,
-                                                  T* __restrict__ dx, int accum) {
+                                                  const float* __restrict__ coef, T* __restrict__ dx, int accum) {
   constexpr int VEC = 16 / sizeof(T);
-  __shared__ float coef[2][2 * 256];  // per (n, group): a/M, b/M  (n <= 2 cached; else recomputed)
-  const int tid = threadIdx.x;
-  const double M = (double)g.v * g.cpg;
-  const int ncache = std::min(g.n, 2);
-  for (int i = tid; i < ncache * g.groups; i += GT) {
-    const int n = i / g.groups, gr = i % g.groups;
-    double a = 0, b = 0;
-    for (int k = 0; k < g.cpg; ++k) {
-      const int c = gr * g.cpg + k;
-      a += gamma[c] * csum[(n * g.c + c) * 2];
-      b += gamma[c] * csum[(n * g.c + c) * 2 + 1];
-    }
-    coef[n][2 * gr] = (float)(a / M);
-    coef[n][2 * gr + 1] = (float)(b / M);
-  }
-  __syncthreads();
-  const long long nvec = (long long)g.n * g.v * g.chn;
-  for (long long i = blockIdx.x * (long long)GT + tid; i < nvec; i += (long long)gridDim.x * GT) {
-    const int j = (int)(i % g.chn);
-    const long long vv = i / g.chn;
-    const int n = (int)(vv / g.v);
-    const long long off = vv * g.c + j * VEC;
+  const int n = blockIdx.y;
+  const int first = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;  // chn | blockDim
+  const int j = first % g.chn;
+  float cf[5][VEC];
+  const float* cb = coef + (long long)n * 5 * g.c + j * VEC;
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) cf[k][e] = cb[k * g.c + e];
+  const T* xn = x + (long long)n * g.v * g.c + j * VEC;
+  const T* dan = da + (long long)n * g.v * g.c + j * VEC;
+  T* dxn = dx + (long long)n * g.v * g.c + j * VEC;
+  const int vstep = stride / g.chn;
+  for (long long vox = first / g.chn; vox < g.v; vox += vstep) {
+    const long long off = vox * g.c;
     float xv[VEC], dv[VEC], o[VEC];
-    load16<T>(x + off, xv);
-    load16<T>(da + off, dv);
-    if (accum) load16<T>(dx + off, o);
+    load16<T>(xn + off, xv);
+    load16<T>(dan + off, dv);
+    if (accum) load16<T>(dxn + off, o);
 #pragma unroll
     for (int e = 0; e < VEC; ++e) {
-      const int c = j * VEC + e, gr = c / g.cpg;
-      const float mu = stats[(n * g.groups + gr) * 2], rs = stats[(n * g.groups + gr) * 2 + 1];
-      float ca, cb;
-      if (n < 2) {
-        ca = coef[n][2 * gr];
-        cb = coef[n][2 * gr + 1];
-      } else {
-        double a = 0, b = 0;
-        for (int k = 0; k < g.cpg; ++k) {
-          const int cc = gr * g.cpg + k;
-          a += gamma[cc] * csum[(n * g.c + cc) * 2];
-          b += gamma[cc] * csum[(n * g.c + cc) * 2 + 1];
-        }
-        ca = (float)(a / M);
-        cb = (float)(b / M);
-      }
-      const float xh = (xv[e] - mu) * rs;
-      const float gd = fmaf(gamma[c], xh, beta[c]) > 0.f ? dv[e] : 0.f;
-      const float r = rs * (gamma[c] * gd - ca - xh * cb);
+      const float gd = fmaf(xv[e], cf[0][e], cf[1][e]) > 0.f ? dv[e] : 0.f;
+      const float r = fmaf(cf[2][e], gd, fmaf(cf[3][e], xv[e], cf[4][e]));
       o[e] = accum ? o[e] + r : r;
     }
-    store16<T>(dx + off, o);
+    store16<T>(dxn + off, o);
   }
 }
 
@@ -280,12 +343,16 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, 
 using namespace u3d;
 
 extern "C" long long u3d_gn_workspace_bytes(int n, int c, long long v) {
-  RedGeom g = make_geom(n, c, v, 1, 4);  // f32 VEC gives the larger block count
-  RedGeom g2 = make_geom(n, c, v, 1, 8);
-  long long nb = std::max(g.nblk, g2.nblk);
-  // partials [n][nblk][2][c] floats + channel sums [n][c][2] doubles
-  return (long long)n * nb * 2 * c * 4 + (long long)n * c * 2 * 8 + 256;
+  long long nb = 0;
+  for (int vec : {4, 8}) nb = std::max<long long>(nb, make_geom(n, c, v, 1, vec).nblk);
+  return GN_CNT_BYTES + (long long)n * nb * 2 * c * 4 + 256 + (long long)n * c * 5 * 4;
 }
+
+static float* gn_coef_ptr(float* ws, const RedGeom& g) {
+  return reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GN_CNT_BYTES +
+                                  (((long long)g.n * g.nblk * 2 * g.c * 4 + 255) / 256) * 256);
+}
+static float* gn_part_ptr(float* ws) { return reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GN_CNT_BYTES); }
 
 extern "C" int u3d_gn_stats(int dtype, const void* x, int n, int c, long long v, int groups, float* stats, float* ws,
                             u3d_stream_t stream) {
@@ -293,15 +360,16 @@ extern "C" int u3d_gn_stats(int dtype, const void* x, int n, int c, long long v,
   U3D_REQUIRE(x && stats && ws && n > 0 && v > 0 && groups > 0 && c % groups == 0, "gn_stats: bad args");
   const int vec = dtype == U3D_BF16 ? 8 : 4;
   U3D_REQUIRE(c % vec == 0 && c / vec <= GT, "gn_stats: channels %d unsupported", c);
+  U3D_REQUIRE(n * c <= GN_PAIRS_MAX, "gn_stats: n * c must be <= %d", GN_PAIRS_MAX);
   RedGeom g = make_geom(n, c, v, groups, vec);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == U3D_BF16) {
-    hipLaunchKernelGGL(gn_stats_partial<bf16>, dim3(g.nblk, n), dim3(GT), 0, s, (const bf16*)x, g, ws);
-    hipLaunchKernelGGL(gn_stats_final<bf16>, dim3(n * groups), dim3(GT), 0, s, (const bf16*)x, g, ws, stats);
-  } else {
-    hipLaunchKernelGGL(gn_stats_partial<float>, dim3(g.nblk, n), dim3(GT), 0, s, (const float*)x, g, ws);
-    hipLaunchKernelGGL(gn_stats_final<float>, dim3(n * groups), dim3(GT), 0, s, (const float*)x, g, ws, stats);
-  }
+  unsigned* cnt = reinterpret_cast<unsigned*>(ws);
+  if (dtype == U3D_BF16)
+    hipLaunchKernelGGL(gn_stats_kernel<bf16>, dim3(g.nblk, n), dim3(GT), 0, s, (const bf16*)x, g, gn_part_ptr(ws), cnt,
+                       stats);
+  else
+    hipLaunchKernelGGL(gn_stats_kernel<float>, dim3(g.nblk, n), dim3(GT), 0, s, (const float*)x, g, gn_part_ptr(ws),
+                       cnt, stats);
   return check_launch("gn_stats");
 }
 
@@ -312,24 +380,24 @@ extern "C" int u3d_gn_bwd(int dtype, const void* da, const void* x, int n, int c
   U3D_REQUIRE(da && x && stats && gamma && beta && dx && ws && groups > 0 && c % groups == 0, "gn_bwd: bad args");
   const int vec = dtype == U3D_BF16 ? 8 : 4;
   U3D_REQUIRE(c % vec == 0 && c <= 256, "gn_bwd: channels %d unsupported", c);
+  U3D_REQUIRE(n * c <= GN_PAIRS_MAX, "gn_bwd: n * c must be <= %d", GN_PAIRS_MAX);
   RedGeom g = make_geom(n, c, v, groups, vec);
   hipStream_t s = (hipStream_t)stream;
-  double* csum = reinterpret_cast<double*>(
-      reinterpret_cast<char*>(ws) + (((long long)n * g.nblk * 2 * c * 4 + 255) / 256) * 256);
-  const long long nvec = (long long)n * v * g.chn;
-  const int ablk = (int)std::min<long long>(4096, (nvec + GT - 1) / GT);
+  unsigned* cnt = reinterpret_cast<unsigned*>(ws) + 1;
+  float* coef = gn_coef_ptr(ws, g);
+  const long long nvec = v * g.chn;  // per sample
+  const int athr = GT / g.chn * g.chn;  // a multiple of the chunks per voxel: each thread keeps one chunk
+  const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + athr - 1) / athr);
   if (dtype == U3D_BF16) {
     hipLaunchKernelGGL(gn_bwd_partial<bf16>, dim3(g.nblk, n), dim3(GT), 0, s, (const bf16*)da, (const bf16*)x, g, stats,
-                       gamma, beta, ws);
-    hipLaunchKernelGGL(gn_bwd_final, dim3(c), dim3(GT), 0, s, g, ws, csum, dgamma, dbeta, accumulate_params);
-    hipLaunchKernelGGL(gn_bwd_apply<bf16>, dim3(ablk), dim3(GT), 0, s, (const bf16*)da, (const bf16*)x, g, stats, gamma,
-                       beta, csum, (bf16*)dx, accumulate);
+                       gamma, beta, gn_part_ptr(ws), cnt, coef, dgamma, dbeta, accumulate_params);
+    hipLaunchKernelGGL(gn_bwd_apply<bf16>, dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da, (const bf16*)x, g, coef,
+                       (bf16*)dx, accumulate);
   } else {
     hipLaunchKernelGGL(gn_bwd_partial<float>, dim3(g.nblk, n), dim3(GT), 0, s, (const float*)da, (const float*)x, g,
-                       stats, gamma, beta, ws);
-    hipLaunchKernelGGL(gn_bwd_final, dim3(c), dim3(GT), 0, s, g, ws, csum, dgamma, dbeta, accumulate_params);
-    hipLaunchKernelGGL(gn_bwd_apply<float>, dim3(ablk), dim3(GT), 0, s, (const float*)da, (const float*)x, g, stats,
-                       gamma, beta, csum, (float*)dx, accumulate);
+                       stats, gamma, beta, gn_part_ptr(ws), cnt, coef, dgamma, dbeta, accumulate_params);
+    hipLaunchKernelGGL(gn_bwd_apply<float>, dim3(ablk, n), dim3(athr), 0, s, (const float*)da, (const float*)x, g, coef,
+                       (float*)dx, accumulate);
   }
   return check_launch("gn_bwd");
 }

@@ -11,6 +11,7 @@ F32, BF16 = 0, 1
 P = ctypes.c_void_p
 I = ctypes.c_int
 L = ctypes.c_longlong
+F = ctypes.c_float
 
 # name -> argtypes (restype int unless noted)
 _SIGS = {
@@ -24,7 +25,9 @@ _SIGS = {
     "u3d_conv_dgrad": [I, P, I, I, P, I, I, I, I, I, I, P, P, L, P],
     "u3d_conv_wgrad_splits": [I, I, I, I, I, I, I, I],
     "u3d_conv_wgrad": [I, P, P, I, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
+    "u3d_sgd_step": [P, I, P, F, F, F, I, I, I, P],
     "u3d_conv_dgrad_s2": [P, I, I, P, I, I, I, I, P, P],
+    "u3d_conv_small": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P],
     "u3d_conv32_brick": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],
     "u3d_convg_brick": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P],
     "u3d_conv_wgrad_brick_splits": [I, I, I, I, I, I, I],
@@ -65,6 +68,14 @@ class WstdDesc(ctypes.Structure):
 
 
 WSTD_BATCH_MAX = 48
+
+
+class SgdDesc(ctypes.Structure):
+    """u3d_sgd_desc (include/u3d.h)."""
+    _fields_ = [("p", P), ("g", P), ("buf", P), ("n", L)]
+
+
+SGD_BATCH_MAX = 48
 
 
 class U3DError(RuntimeError):

@@ -48,5 +48,7 @@ class GraphedStep:
         for dst, src in zip(self.static_inputs, new_inputs):
             if src is not None and src.data_ptr() != dst.data_ptr():
                 dst.copy_(src, non_blocking=True)
+        if hasattr(self.optimizer, "sync_lr"):
+            self.optimizer.sync_lr()  # device-side lr of u3d.optim.SGD: LR schedule changes reach the replay
         self.graph.replay()
         return self.out

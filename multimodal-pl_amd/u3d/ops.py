@@ -40,7 +40,9 @@ def out_dim(d, k, s):
 
 
 class _WS:
-    """Grow-only per-device scratch buffer (device memory owned by torch's caching allocator)."""
+    """Grow-only per-device scratch buffer (device memory owned by torch's caching allocator). Zero-filled when
+    (re)allocated: the GroupNorm kernels keep completion counters at the head of their workspace and leave
+    them at zero after every launch."""
 
     def __init__(self):
         self.buf = {}
@@ -49,7 +51,7 @@ class _WS:
         key = (device, slot)
         b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
-            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            b = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
             self.buf[key] = b
         return b
 
@@ -148,6 +150,11 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
         call("u3d_conv32_brick", 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
              _ptr(residual), y.data_ptr(), _stream())
         return y
+    if _use_small(x.dtype, cin, cout, k, stride, (n, d, h, w_)) and not out_f32 and bias is None:
+        ws = WS.get(SPLITK_WS_BYTES, x.device, slot=4)
+        call("u3d_conv_small", 0, x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be),
+             G, _ptr(residual), y.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        return y
     if _use_gen_brick(x.dtype, cin, cout, k, stride, (n, d, h, w_)) and not out_f32 and bias is None:
         call("u3d_convg_brick", 0, x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be),
              G, _ptr(residual), y.data_ptr(), _stream())
@@ -171,6 +178,16 @@ USE_CONV32_BRICK = True
 def _use_conv32(dtype, cin, cout, k, stride, n, w=32):
     return USE_CONV32_BRICK and dtype == torch.bfloat16 and cin == 32 and cout == 32 and k == 3 and stride == 1 \
         and n <= 16 and w % 32 == 0
+
+
+USE_SMALL_CONV = True
+SMALL_MAX_VOX = 2 * 12 ** 3  # n*d*h*w up to which the small-volume brick kernel (conv_small.hip) runs (24^3: convg)
+
+
+def _use_small(dtype, cin, cout, k, stride, shape):
+    n, d, h, w_ = shape
+    return USE_SMALL_CONV and dtype == torch.bfloat16 and k == 3 and stride == 1 and cin % 8 == 0 \
+        and cout % 8 == 0 and n * d * h * w_ <= SMALL_MAX_VOX
 
 
 USE_GEN_BRICK = True
@@ -198,6 +215,11 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     if USE_S2_BRICK and dy.dtype == torch.bfloat16 and k == 3 and stride == 2:
         call("u3d_conv_dgrad_s2", dy.data_ptr(), n, cout, wpk_dgrad.data_ptr(), cin, d, h, w_, dx.data_ptr(),
              _stream())
+        return dx
+    if _use_small(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
+        ws = WS.get(SPLITK_WS_BYTES, dy.device, slot=4)
+        call("u3d_conv_small", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None, 0,
+             None, dx.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         return dx
     if _use_gen_brick(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
         call("u3d_convg_brick", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None, 0,

@@ -47,17 +47,21 @@ SHAPES = [(2, 32, 32, (12, 10, 16), 1), (1, 32, 32, (5, 9, 70), 1), (1, 32, 64, 
           (1, 256, 256, (6, 6, 6), 2), (1, 40, 48, (6, 10, 14), 2)]
 
 
-@pytest.fixture(params=["auto", "gen_brick", "igemm"])
+@pytest.fixture(params=["auto", "gen_brick", "igemm", "small"])
 def conv_path(request):
     """auto = production routing; gen_brick = force the generic halo-brick kernel; igemm = force implicit GEMM."""
     from u3d import ops
-    saved = (ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK)
+    saved = (ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK, ops.USE_SMALL_CONV,
+             ops.SMALL_MAX_VOX)
     if request.param == "gen_brick":
-        ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK = 0, False
+        ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_SMALL_CONV = 0, False, False
     elif request.param == "igemm":
-        ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK = False, False, False
+        ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK, ops.USE_SMALL_CONV = False, False, False, False
+    elif request.param == "small":
+        ops.USE_CONV32_BRICK, ops.SMALL_MAX_VOX = False, 1 << 40
     yield request.param
-    ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK = saved
+    (ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK, ops.USE_SMALL_CONV,
+     ops.SMALL_MAX_VOX) = saved
 
 
 @pytest.mark.parametrize("n,cin,cout,dims,s", SHAPES)

@@ -8,20 +8,31 @@ import torch  # noqa: E402
 from u3d import ops  # noqa: E402
 
 dev = torch.device("cuda:0")
+for kv in os.environ.get("KB_SET", "").split(","):  # e.g. KB_SET=USE_SMALL_CONV=0,SMALL_MAX_VOX=1e9
+    if kv:
+        k, v = kv.split("=")
+        setattr(ops, k, type(getattr(ops, k))(float(v)))
 bf = torch.bfloat16
 
 
 def t_(fn, reps=20):
+    """GPU time per call: `reps` calls captured in one hipGraph and replayed (no host launch overhead)."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(reps):
-        fn()
+    for _ in range(3):
+        g.replay()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps * 1e3
+    return e0.elapsed_time(e1) / (3 * reps) * 1e3
 
 
 def conv_case(n, cin, cout, s, k, stride, gn=True, res=False):
