@@ -120,6 +120,19 @@ int u3d_conv_small(int flip, const void* x, int n, int cin, int d, int h, int w,
                    const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                    const void* residual, void* y, float* ws, long long ws_bytes, u3d_stream_t stream);
 
+/* Classifier head precls_conv (unet3D.py:1653-1657): GN+ReLU + 1^3 conv cin (16..64, %16) -> cout (<= 32) + bias,
+ * bf16 NDHWC input, fp32 NDHWC logits [n*v][cout]; wpk = forward pack [1][cout_p][cin_p]. Streaming MFMA kernel
+ * (operands straight from global memory in fragment layout). */
+int u3d_head_fwd(const void* x, int n, long long v, int cin, const void* wpk, int cout, const float* bias,
+                 const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups, float* y,
+                 u3d_stream_t stream);
+/* Head data gradient in one pass over the fp32 dlogits dy [rows][cout]: dA = dy W (bf16 [rows][cin], wpk_dgrad =
+ * [1][cin_p][cout_p] pack), dy_bf16 [rows][round8(cout)] (the weight-gradient operand) and per-block bias-gradient
+ * partials dbias_partials [u3d_head_bwd_blocks(rows)][cout] (sum them with u3d_channel_sum). */
+int u3d_head_bwd_blocks(long long rows);
+int u3d_head_bwd(const float* dy, long long rows, int cout, const void* wpk_dgrad, int cin, void* dA, void* dy_bf16,
+                 float* dbias_partials, u3d_stream_t stream);
+
 /* bf16 32->32 3^3 stride-1 conv (cin = cout = 32; the full-resolution layers) in halo-brick form with the
  * weights held in registers: flip=0 forward (wpk = forward pack, optional GN+ReLU prologue and residual),
  * flip=1 data gradient (wpk = data-grad pack, no prologue). Same results as u3d_conv_fwd/_dgrad; n <= 16. */

@@ -1,0 +1,201 @@
+// Classifier head of the trunk: precls_conv = GroupNorm + ReLU + 1^3 conv (cin -> cout <= 32, + bias) at full
+// resolution (reference unet3D.py:1653-1657 / :647-650), forward and data gradient, bf16 activations.
+//
+// At 96^3 x 2 the head is pure streaming (32 -> 16 channels: 64 B in, 64 B fp32 out per voxel, 1 kFLOP per
+// voxel): one wave handles 32 voxels per step with the operands loaded straight from global memory in MFMA
+// fragment layout (no LDS), GN+ReLU applied in registers, the weights (B fragments) held in registers for
+// the whole grid-stride loop.
+//   forward : logits[v][co] = sum_ci relu(gn(x))[v][ci] W[co][ci] + b[co]   (fp32 out, as the reference returns)
+//   backward: dA[v][ci] = sum_co dy[v][co] W[co][ci] (bf16), plus dy in bf16 for the weight gradient and the
+//             per-block column sums of dy (bias gradient partials) — the fp32 dy is read once.
+#include "common.h"
+
+namespace u3d {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+constexpr int HD_T = 256;  // 4 waves
+
+__device__ __forceinline__ bf16x8 as_frag(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// KS = cin / 16 k-steps (cin in {16, 32, 48, 64})
+template <int KS>
+__global__ __launch_bounds__(HD_T) void head_fwd_kernel(const bf16* __restrict__ x, long long v, int cin,
+                                                       const bf16* __restrict__ wpk, int cout, int cin_p,
+                                                       const float* __restrict__ bias, const float* __restrict__ st,
+                                                       const float* __restrict__ ga, const float* __restrict__ be,
+                                                       int groups, int n, float* __restrict__ y) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  // B fragments: lane (col co = r, half h) holds W[co][16 s + 8 h .. +7]
+  bf16x8 bw[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    bw[s] = as_frag(*reinterpret_cast<const u32x4*>(wpk + (long long)r * cin_p + 16 * s + 8 * h));
+  const float bv = r < cout && bias ? bias[r] : 0.f;
+  const long long tiles = (n * v + 31) / 32;
+  const long long wid = (long long)blockIdx.x * (HD_T / 64) + (threadIdx.x >> 6);
+  const long long nw = (long long)gridDim.x * (HD_T / 64);
+  int gn_n = -1;
+  f32x2 sc[KS][4], sh[KS][4];
+  for (long long tile = wid; tile < tiles; tile += nw) {
+    const long long row = tile * 32 + r;  // this lane's A row (voxel over all samples)
+    const bool ok = row < n * v;
+    const int nn = ok ? (int)(row / v) : 0;
+    if (st && nn != gn_n) {
+      gn_n = nn;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) gn_coef8(st, ga, be, groups, cin, nn, 16 * s + 8 * h, sc[s], sh[s]);
+    }
+    u32x4 a[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      a[s] = ok ? *reinterpret_cast<const u32x4*>(x + row * cin + 16 * s + 8 * h) : u32x4{0u, 0u, 0u, 0u};
+      if (st && ok) a[s] = gn_relu8(a[s], sc[s], sh[s]);
+    }
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(a[s]), bw[s], acc, 0, 0, 0);
+    // acc[i]: row (i&3) + 8(i>>2) + 4h, column co = r
+    if (r < cout) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const long long orow = tile * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (orow < n * v) y[orow * cout + r] = acc[i] + bv;
+      }
+    }
+  }
+}
+
+// dA = dy W: A operand = dy tile (32 voxels x cout, fp32 -> bf16 in registers), B = W^T from the data-grad
+// pack [ci_p][co_p]; 2 k-steps cover cout <= 32. Also writes dy as bf16 [v][cout_p8] and per-block dy column sums.
+__global__ __launch_bounds__(HD_T) void head_bwd_kernel(const float* __restrict__ dy, long long rows, int cout,
+                                                       const bf16* __restrict__ wpd, int cout_p, int cin,
+                                                       bf16* __restrict__ dA, bf16* __restrict__ dyb, int cout8,
+                                                       float* __restrict__ dbp) {
+  __shared__ float red[HD_T / 64][32];
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  bf16x8 bw[2][2];  // [k-step][n-tile of 32 ci]
+  const int ntn = (cin + 31) / 32;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      const int ci = tn * 32 + r, co = 16 * s + 8 * h;
+      bw[s][tn] = (tn < ntn && co < cout_p)
+                      ? as_frag(*reinterpret_cast<const u32x4*>(wpd + (long long)ci * cout_p + co))
+                      : as_frag(u32x4{0u, 0u, 0u, 0u});
+    }
+  float colsum[2][8];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) colsum[s][e] = 0.f;
+  const long long tiles = (rows + 31) / 32;
+  const long long wid = (long long)blockIdx.x * (HD_T / 64) + wave;
+  const long long nw = (long long)gridDim.x * (HD_T / 64);
+  for (long long tile = wid; tile < tiles; tile += nw) {
+    const long long row = tile * 32 + r;
+    const bool ok = row < rows;
+    u32x4 a[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float f[8];
+      const int cb = 16 * s + 8 * h;
+      if (ok && cb + 8 <= cout && (cout & 3) == 0) {  // two 16-B loads
+        const f32x4 u0 = *reinterpret_cast<const f32x4*>(dy + row * cout + cb);
+        const f32x4 u1 = *reinterpret_cast<const f32x4*>(dy + row * cout + cb + 4);
+        f[0] = u0[0]; f[1] = u0[1]; f[2] = u0[2]; f[3] = u0[3];
+        f[4] = u1[0]; f[5] = u1[1]; f[6] = u1[2]; f[7] = u1[3];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = ok && cb + e < cout ? dy[row * cout + cb + e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) colsum[s][e] += f[e];
+      store16<bf16>(reinterpret_cast<bf16*>(&a[s]), f);
+      if (ok && 16 * s + 8 * h < cout8) *reinterpret_cast<u32x4*>(dyb + row * cout8 + 16 * s + 8 * h) = a[s];
+    }
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      if (tn >= ntn) break;
+      f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(a[0]), bw[0][tn], acc, 0, 0, 0);
+      if (cout_p > 16) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(a[1]), bw[1][tn], acc, 0, 0, 0);
+      const int ci = tn * 32 + r;
+      if (ci < cin) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const long long orow = tile * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (orow < rows) dA[orow * cin + ci] = from_f<bf16>(acc[i]);
+        }
+      }
+    }
+  }
+  // bias-gradient partials: lanes (r, h) hold columns 16 s + 8 h + e summed over their rows; reduce the 32
+  // rows of the wave (lanes with equal h), then the waves in fixed order
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = colsum[s][e];
+      for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o, 32);
+      colsum[s][e] = t;
+    }
+  if (r == 0) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wave][16 * s + 8 * h + e] = colsum[s][e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float t = 0.f;
+    for (int w = 0; w < HD_T / 64; ++w) t += red[w][threadIdx.x];
+    if (threadIdx.x < cout) dbp[(long long)blockIdx.x * cout + threadIdx.x] = t;
+  }
+}
+
+static int head_blocks(long long rows) { return (int)std::min<long long>(2048, std::max<long long>(1, (rows + 127) / 128)); }
+
+}  // namespace u3d
+
+using namespace u3d;
+
+extern "C" int u3d_head_fwd(const void* x, int n, long long v, int cin, const void* wpk, int cout, const float* bias,
+                            const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                            float* y, u3d_stream_t stream) {
+  U3D_REQUIRE(x && wpk && y && n >= 1 && v >= 1, "head_fwd: bad args");
+  U3D_REQUIRE(cin % 16 == 0 && cin >= 16 && cin <= 64 && cout >= 1 && cout <= 32, "head_fwd: cin %d / cout %d", cin,
+              cout);
+  U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "head_fwd: bad GN");
+  const int cin_p = round_up(cin, 32);
+  const int nb = head_blocks(n * v);
+  hipStream_t s = (hipStream_t)stream;
+#define HF(KS)                                                                                                       \
+  hipLaunchKernelGGL(head_fwd_kernel<KS>, dim3(nb), dim3(HD_T), 0, s, (const bf16*)x, v, cin, (const bf16*)wpk, cout, \
+                     cin_p, bias, gn_stats, gn_gamma, gn_beta, gn_groups, n, y)
+  switch (cin / 16) {
+    case 1: HF(1); break;
+    case 2: HF(2); break;
+    case 3: HF(3); break;
+    default: HF(4); break;
+  }
+#undef HF
+  return check_launch("head_fwd_kernel");
+}
+
+extern "C" int u3d_head_bwd_blocks(long long rows) { return head_blocks(rows); }
+
+extern "C" int u3d_head_bwd(const float* dy, long long rows, int cout, const void* wpk_dgrad, int cin, void* dA,
+                            void* dy_bf16, float* dbias_partials, u3d_stream_t stream) {
+  U3D_REQUIRE(dy && wpk_dgrad && dA && dy_bf16 && dbias_partials && rows >= 1, "head_bwd: bad args");
+  U3D_REQUIRE(cout >= 1 && cout <= 32 && cin % 8 == 0 && cin <= 64, "head_bwd: cout %d / cin %d", cout, cin);
+  const int cout_p = round_up(cout, 32), cout8 = round_up(cout, 8);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(head_blocks(rows)), dim3(HD_T), 0, (hipStream_t)stream, dy, rows, cout,
+                     (const bf16*)wpk_dgrad, cout_p, cin, (bf16*)dA, (bf16*)dy_bf16, cout8, dbias_partials);
+  return check_launch("head_bwd_kernel");
+}

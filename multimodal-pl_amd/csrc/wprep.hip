@@ -189,77 +189,122 @@ __global__ __launch_bounds__(WB_T) void wstd_sum_slabs_kernel(WBatch<WSum> bt) {
   }
 }
 
-// (4) per-row mean(g) and sum(g * W_hat)/(K-1), one block per row; g read along ci (contiguous)
-__global__ __launch_bounds__(WB_T) void wstd_rowgrad_kernel(WBatch<WRow> bt) {
-  __shared__ double red[WB_T / 64];
-  const WRow& D = bt.d[find_desc(bt, blockIdx.x)];
-  const int co = blockIdx.x - D.b0;
-  const int K = D.cin * D.k3, cout_p = round_up(D.cout, 32), cin_p = round_up(D.cin, 32);
-  const float mean = D.st[co * 2], rsd = 1.f / D.st[co * 2 + 1];
-  const float* wr = D.w + (long long)co * K;
-  double m1 = 0.0, m2 = 0.0;
-  const int n = D.k3 * D.cin;
-  for (int j = threadIdx.x; j < n; j += WB_T) {  // j = t * cin + ci
-    const int t = j / D.cin, ci = j - t * D.cin;
-    const float gv = D.g[((long long)t * cout_p + co) * cin_p + ci];
-    const float wh = (wr[ci * D.k3 + t] - mean) * rsd;
-    m1 += gv;
-    m2 += (double)gv * wh;
+// (4+5) dW of 8 output channels: pass 1 accumulates the row sums of g and g*W_hat over 32-channel chunks
+// staged through LDS (w rows [co][ci][t] contiguous, g [t][co][ci] rows contiguous), pass 2 re-stages the
+// chunks and writes dW = (g - mean(g) - W_hat * sum(g W_hat)/(K-1)) / std in parameter order (contiguous rows).
+// 32 threads per row, fixed-order reductions (deterministic).
+constexpr int WG_R = 8, WG_T = 256;
+
+template <int K3>
+__device__ __forceinline__ void wgrad_stage(const WPack& D, float* ws, float* gs, int co0, int ci0) {
+  // 16-B loads, all issued before the LDS stores (the stage is latency-bound otherwise)
+  constexpr int SEG = WB_CI * K3, WQ = WG_R * SEG / 4, GQ = K3 * WG_R * WB_CI / 4;
+  constexpr int WL = (WQ + WG_T - 1) / WG_T, GL = (GQ + WG_T - 1) / WG_T;
+  const int cout_p = round_up(D.cout, 32), cin_p = round_up(D.cin, 32);
+  const int K = D.cin * K3, valid = min(WB_CI, D.cin - ci0) * K3;
+  f32x4 wv[WL], gv[GL];
+#pragma unroll
+  for (int i = 0; i < WL; ++i) {  // w rows [co][ci0*K3 ..): valid is a multiple of 4 (cin % 8 == 0 or K3 == 27 ... )
+    const int q = threadIdx.x + i * WG_T, r = q / (SEG / 4), c = (q - r * (SEG / 4)) * 4, co = co0 + r;
+    wv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (q < WQ && D.st && co < D.cout) {
+      const float* src = D.w + (long long)co * K + ci0 * K3 + c;
+      if (c + 4 <= valid && (((uintptr_t)src) & 15) == 0) {
+        wv[i] = *reinterpret_cast<const f32x4*>(src);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wv[i][e] = c + e < valid ? src[e] : 0.f;
+      }
+    }
   }
-  const double s1 = block_sum(m1, red), s2 = block_sum(m2, red);
-  if (threadIdx.x == 0) {
-    D.rowbuf[co * 2] = (float)(s1 / K);
-    D.rowbuf[co * 2 + 1] = (float)(s2 / (K > 1 ? K - 1 : 1));
+#pragma unroll
+  for (int i = 0; i < GL; ++i) {  // g rows [t][co][ci0 .. ci0+32): 8 x 16 B each
+    const int q = threadIdx.x + i * WG_T, c = (q % (WB_CI / 4)) * 4, r = (q / (WB_CI / 4)) % WG_R,
+              t = q / (WB_CI / 4 * WG_R);
+    gv[i] = (q < GQ && co0 + r < D.cout)
+                ? *reinterpret_cast<const f32x4*>(D.g + ((long long)t * cout_p + co0 + r) * cin_p + ci0 + c)
+                : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < WL; ++i) {
+    const int q = threadIdx.x + i * WG_T, r = q / (SEG / 4), c = (q - r * (SEG / 4)) * 4;
+    if (q < WQ)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ws[r * (SEG + 1) + c + e] = wv[i][e];
+  }
+#pragma unroll
+  for (int i = 0; i < GL; ++i) {
+    const int q = threadIdx.x + i * WG_T, c = (q % (WB_CI / 4)) * 4, r = (q / (WB_CI / 4)) % WG_R,
+              t = q / (WB_CI / 4 * WG_R);
+    if (q < GQ)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gs[(t * WG_R + r) * (WB_CI + 1) + c + e] = gv[i][e];
   }
 }
 
 template <int K3>
-__device__ __forceinline__ void apply_tile(const WPack& D, float* ws, float* gs, const float* mu, const float* rsg,
-                                           const float* f1, const float* f2, int co0, int ci0) {
-  constexpr int SEG = WB_CI * K3, RS = SEG + 1, GSZ = WB_CO * WB_CI + 1;
-  const int cout_p = round_up(D.cout, 32), cin_p = round_up(D.cin, 32);
-  const bool std_ = D.st != nullptr;
-  if (std_) stage_rows<K3>(ws, D.w, D.cout, D.cin, co0, ci0);
-  for (int e = threadIdx.x; e < K3 * WB_CO * WB_CI; e += WB_TT) {  // g[t][co][ci] rows: coalesced along ci
-    const int c = e % WB_CI, r = (e / WB_CI) % WB_CO, t = e / (WB_CI * WB_CO);
-    gs[t * GSZ + r * WB_CI + c] = D.g[((long long)t * cout_p + co0 + r) * cin_p + ci0 + c];
+__device__ __forceinline__ void wgrad_rows(const WPack& D, int co0) {
+  constexpr int SEG = WB_CI * K3;
+  __shared__ float ws[WG_R * (SEG + 1)];
+  __shared__ float gs[K3 * WG_R * (WB_CI + 1)];
+  __shared__ float f1s[WG_R], f2s[WG_R];
+  const int tid = threadIdx.x, r = tid >> 5, l = tid & 31, co = co0 + r;
+  const bool std_ = D.st != nullptr, rok = co < D.cout;
+  const float mu = std_ && rok ? D.st[co * 2] : 0.f;
+  const float rsg = std_ && rok ? 1.f / D.st[co * 2 + 1] : 1.f;
+  const int K = D.cin * K3;
+  if (std_) {
+    float m1 = 0.f, m2 = 0.f;
+    for (int ci0 = 0; ci0 < D.cin; ci0 += WB_CI) {
+      __syncthreads();
+      wgrad_stage<K3>(D, ws, gs, co0, ci0);
+      __syncthreads();
+      const int valid = min(WB_CI, D.cin - ci0) * K3;
+      for (int e = l; e < valid; e += 32) {
+        const int c = e / K3, t = e - c * K3;
+        const float gv = gs[(t * WG_R + r) * (WB_CI + 1) + c];
+        m1 += gv;
+        m2 = fmaf(gv, (ws[r * (SEG + 1) + e] - mu) * rsg, m2);
+      }
+    }
+    double d1 = m1, d2 = m2;
+    for (int o = 16; o > 0; o >>= 1) {
+      d1 += __shfl_xor(d1, o, 32);
+      d2 += __shfl_xor(d2, o, 32);
+    }
+    if (l == 0) {
+      f1s[r] = (float)(d1 / K);
+      f2s[r] = (float)(d2 / (K > 1 ? K - 1 : 1));
+    }
   }
   __syncthreads();
-  const int K = D.cin * K3, valid = min(WB_CI, D.cin - ci0) * K3;
-  for (int e = threadIdx.x; e < WB_CO * SEG; e += WB_TT) {  // (r, c, t), t fastest = parameter order
-    const int r = e / SEG, ct = e - r * SEG, c = ct / K3, t = ct - c * K3, co = co0 + r;
-    if (co >= D.cout || ct >= valid) continue;
-    const float gv = gs[t * GSZ + r * WB_CI + c];
-    float v = gv;
-    if (std_) {
-      const float wh = (ws[r * RS + ct] - mu[r]) * rsg[r];
-      v = (gv - f1[r] - wh * f2[r]) * rsg[r];
+  const float f1 = std_ ? f1s[r] : 0.f, f2 = std_ ? f2s[r] : 0.f;
+  const bool staged = std_ && D.cin <= WB_CI;  // one chunk: pass 1 left it in LDS
+  for (int ci0 = 0; ci0 < D.cin; ci0 += WB_CI) {
+    if (!staged) {
+      __syncthreads();
+      wgrad_stage<K3>(D, ws, gs, co0, ci0);
+      __syncthreads();
     }
-    float* o = D.dw + (long long)co * K + ci0 * K3 + ct;
-    *o = (D.acc ? *o : 0.f) + v;
+    if (!rok) continue;
+    const int valid = min(WB_CI, D.cin - ci0) * K3;
+    float* o = D.dw + (long long)co * K + ci0 * K3;
+    for (int e = l; e < valid; e += 32) {
+      const int c = e / K3, t = e - c * K3;
+      const float gv = gs[(t * WG_R + r) * (WB_CI + 1) + c];
+      const float v = std_ ? (gv - f1 - (ws[r * (SEG + 1) + e] - mu) * rsg * f2) * rsg : gv;
+      o[e] = (D.acc ? o[e] : 0.f) + v;
+    }
   }
 }
 
-// (5) dW of one 16 x 32 tile in parameter order
-__global__ __launch_bounds__(WB_TT) void wstd_apply_kernel(WBatch<WPack> bt) {
-  __shared__ float ws[WB_CO * (WB_CI * 27 + 1)];
-  __shared__ float gs[27 * (WB_CO * WB_CI + 1)];
-  __shared__ float mu[WB_CO], rsg[WB_CO], f1[WB_CO], f2[WB_CO];
+__global__ __launch_bounds__(WG_T) void wstd_grad_kernel(WBatch<WPack> bt) {
   const WPack& D = bt.d[find_desc(bt, blockIdx.x)];
-  const int nci = round_up(D.cin, 32) / WB_CI;
-  const int tile = blockIdx.x - D.b0, co0 = (tile / nci) * WB_CO, ci0 = (tile % nci) * WB_CI;
-  if (threadIdx.x < WB_CO) {
-    const int co = co0 + threadIdx.x;
-    const bool s = D.st && co < D.cout;
-    mu[threadIdx.x] = s ? D.st[co * 2] : 0.f;
-    rsg[threadIdx.x] = s ? 1.f / D.st[co * 2 + 1] : 1.f;
-    f1[threadIdx.x] = s ? D.rowbuf[co * 2] : 0.f;
-    f2[threadIdx.x] = s ? D.rowbuf[co * 2 + 1] : 0.f;
-  }
+  const int co0 = (blockIdx.x - D.b0) * WG_R;
   if (D.k3 == 27)
-    apply_tile<27>(D, ws, gs, mu, rsg, f1, f2, co0, ci0);
+    wgrad_rows<27>(D, co0);
   else
-    apply_tile<1>(D, ws, gs, mu, rsg, f1, f2, co0, ci0);
+    wgrad_rows<1>(D, co0);
 }
 
 }  // namespace u3d
@@ -302,22 +347,20 @@ extern "C" int u3d_wstd_fwd_batch(int dtype, const u3d_wstd_desc* descs, int cou
 }
 
 extern "C" long long u3d_wstd_bwd_scratch_bytes(const u3d_wstd_desc* descs, int count) {
-  long long rows = 0;
-  for (int i = 0; i < count; ++i) rows += descs[i].cout;
-  return rows * 2 * (long long)sizeof(float);
+  (void)descs;
+  (void)count;
+  return 256;  // no scratch needed any more (row sums stay in LDS); kept for the ABI
 }
 
 extern "C" int u3d_wstd_bwd_batch(const u3d_wstd_desc* descs, int count, float* scratch, u3d_stream_t stream) {
+  (void)scratch;
   U3D_REQUIRE(descs && count >= 0 && count <= U3D_WSTD_BATCH_MAX, "wstd_bwd_batch: count must be <= %d",
               U3D_WSTD_BATCH_MAX);
   if (count == 0) return U3D_OK;
-  U3D_REQUIRE(scratch, "wstd_bwd_batch: scratch required (u3d_wstd_bwd_scratch_bytes)");
   hipStream_t st = (hipStream_t)stream;
   WBatch<WSum> sb{};
-  WBatch<WRow> rb{};
   WBatch<WPack> ab{};
-  int sblocks = 0, rblocks = 0, ablocks = 0;
-  long long roff = 0;
+  int sblocks = 0, ablocks = 0;
   for (int i = 0; i < count; ++i) {
     const u3d_wstd_desc& s = descs[i];
     U3D_REQUIRE(s.part && s.w && s.dw && s.nsplit >= 1 && s.cout > 0 && s.cin > 0 && (s.ksize == 1 || s.ksize == 3),
@@ -331,26 +374,15 @@ extern "C" int u3d_wstd_bwd_batch(const u3d_wstd_desc* descs, int count, float* 
       sb.d[sb.count++] = WSum{s.part, s.nsplit, (int)per4, sg, sblocks};
       sblocks += cdiv(per4, WB_T / sg);
     }
-    float* rowbuf = scratch + roff;
-    roff += 2LL * s.cout;
-    if (s.standardize) {
-      rb.d[rb.count++] = WRow{s.w, s.part, s.wstats, rowbuf, s.cout, s.cin, k3, rblocks};
-      rblocks += s.cout;
-    }
-    ab.d[ab.count++] = WPack{s.w, s.standardize ? s.wstats : nullptr, nullptr, nullptr, s.part, rowbuf, s.dw,
+    ab.d[ab.count++] = WPack{s.w, s.standardize ? s.wstats : nullptr, nullptr, nullptr, s.part, nullptr, s.dw,
                              s.cout, s.cin, k3, s.accumulate, ablocks};
-    ablocks += (round_up(s.cout, 32) / WB_CO) * (round_up(s.cin, 32) / WB_CI);
+    ablocks += cdiv(s.cout, WG_R);
   }
   if (sb.count) {
     hipLaunchKernelGGL(wstd_sum_slabs_kernel, dim3(sblocks), dim3(WB_T), 0, st, sb);
     int rc = check_launch("wstd_sum_slabs_kernel");
     if (rc) return rc;
   }
-  if (rb.count) {
-    hipLaunchKernelGGL(wstd_rowgrad_kernel, dim3(rblocks), dim3(WB_T), 0, st, rb);
-    int rc = check_launch("wstd_rowgrad_kernel");
-    if (rc) return rc;
-  }
-  hipLaunchKernelGGL(wstd_apply_kernel, dim3(ablocks), dim3(WB_TT), 0, st, ab);
-  return check_launch("wstd_apply_kernel");
+  hipLaunchKernelGGL(wstd_grad_kernel, dim3(ablocks), dim3(WG_T), 0, st, ab);
+  return check_launch("wstd_grad_kernel");
 }

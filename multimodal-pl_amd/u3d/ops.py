@@ -261,6 +261,44 @@ def conv_wgrad(dy, x, k, stride, gn=None, brick=None):
     return part, ns
 
 
+def use_head(dtype, cin, cout, k, stride):
+    """The streaming MFMA head kernel (head.hip) serves GN+ReLU + 1^3 conv with cout <= 32 (precls_conv)."""
+    return USE_HEAD and dtype == torch.bfloat16 and k == 1 and stride == 1 and cout <= 32 and cin % 16 == 0 \
+        and 16 <= cin <= 64
+
+
+USE_HEAD = True
+
+
+def head_fwd(x, wpk, cout, bias, gn):
+    """x bf16 [n,d,h,w,cin] -> fp32 logits [n,d,h,w,cout] = conv1(relu(gn(x))) + bias."""
+    n, cin = x.shape[0], x.shape[-1]
+    v = x.numel() // (n * cin)
+    y = torch.empty(tuple(x.shape[:-1]) + (cout,), dtype=torch.float32, device=x.device)
+    st, ga, be, G = gn if gn is not None else (None, None, None, 0)
+    call("u3d_head_fwd", x.data_ptr(), n, v, cin, wpk.data_ptr(), cout, _ptr(bias), _ptr(st), _ptr(ga), _ptr(be), G,
+         y.data_ptr(), _stream())
+    return y
+
+
+def head_bwd(dy, wpk_dgrad, cin, dbias=None):
+    """dy fp32 [..., cout] -> (dA bf16 [..., cin], dy bf16 [..., round8(cout)]); the bias gradient is written
+    into ``dbias`` (sum over all voxels) when given."""
+    cout = dy.shape[-1]
+    rows = dy.numel() // cout
+    if dy.dtype != torch.float32 or not dy.is_contiguous():
+        dy = dy.float().contiguous()
+    dA = torch.empty(tuple(dy.shape[:-1]) + (cin,), dtype=torch.bfloat16, device=dy.device)
+    dyb = torch.empty(tuple(dy.shape[:-1]) + ((cout + 7) // 8 * 8,), dtype=torch.bfloat16, device=dy.device)
+    nb = query("u3d_head_bwd_blocks", rows)
+    dbp = torch.empty((nb, cout), dtype=torch.float32, device=dy.device)
+    call("u3d_head_bwd", dy.data_ptr(), rows, cout, wpk_dgrad.data_ptr(), cin, dA.data_ptr(), dyb.data_ptr(),
+         dbp.data_ptr(), _stream())
+    if dbias is not None:
+        channel_sum(dbp, out=dbias)
+    return dA, dyb
+
+
 def stem_fwd(x_ncdhw, wpk, cout, stride, dtype):
     require_device(x_ncdhw)
     n, cin, d, h, w_ = x_ncdhw.shape

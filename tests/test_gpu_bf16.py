@@ -192,3 +192,29 @@ def test_bf16_stem_wgrad(gpu, dims):
     err = (dw - ref).abs().max().item()
     assert err < 2e-3 * ref.abs().max().item(), err
     assert part[:, :, :, 1:].abs().max().item() == 0.0   # padded ci columns stay zero
+
+
+@pytest.mark.parametrize("cin,cout,dims", [(32, 16, (6, 10, 12)), (32, 2, (4, 4, 7)), (64, 8, (3, 5, 6)),
+                                           (16, 32, (2, 3, 4))])
+def test_head_fwd_bwd(gpu, cin, cout, dims):
+    """Streaming precls head (head.hip): logits = conv1(relu(gn(x))) + b; dA = dy W, bf16 dy, bias grad."""
+    from u3d import ops
+    n = 2
+    x, _, st, ga, be, G = _case(gpu, n, cin, cout, dims, True, 7)
+    w = torch.randn(cout, cin, 1, 1, 1, device=gpu)
+    pf, pd, _ = ops.wstd_fwd(w, torch.bfloat16, False)
+    b = torch.randn(cout, device=gpu)
+    y = ops.head_fwd(x, pf, cout, b, (st, ga, be, G))
+    a = _act_ref(x, st, ga, be, G)                                       # [n, ..., cin] fp64 of bf16 values
+    wq = pf.float().cpu()[0, :cout, :cin].double()
+    ref = a @ wq.t() + b.double().cpu()
+    assert y.dtype == torch.float32
+    assert (y.double().cpu() - ref).abs().max().item() < 1e-4 * ref.abs().max().item() + 1e-5
+    dy = torch.randn(y.shape, device=gpu)
+    db = torch.empty(cout, device=gpu)
+    dA, dyb = ops.head_bwd(dy, pd, cin, dbias=db)
+    dyq = _bf(dy.cpu())
+    refA = dyq @ wq
+    assert (dA.double().cpu() - refA).abs().max().item() < 1e-2 * refA.abs().max().item()
+    assert torch.equal(dyb[..., :cout].cpu(), dy.to(torch.bfloat16).cpu())
+    torch.testing.assert_close(db.cpu().double(), dy.cpu().double().reshape(-1, cout).sum(0), rtol=1e-4, atol=1e-3)
