@@ -36,8 +36,9 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-roofline", action="store_true")
-    p.add_argument("--eager", action="store_true", help="launch kernel by kernel instead of replaying the "
-                   "captured hipGraph of the step")
+    p.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph (~1%% faster at "
+                   "N=1; the roofline kernel then falls back to a standalone timing: graph event nodes are not "
+                   "timeable)")
     return p.parse_args()
 
 
@@ -51,9 +52,10 @@ def synthetic(batch, patch, device, seed):
     return x, lab, mask
 
 
-def dominant_kernel_roofline(device, batch, patch, reps=20):
-    """Time the 32->32 3^3 stride-1 conv (GN+ReLU prologue, residual epilogue) at patch^3, bf16, as launched
-    in the trunk, with HIP events on torch's current stream (the stream libu3d launches on)."""
+def dominant_kernel_roofline(device, batch, patch, live=None, reps=20):
+    """The 32->32 3^3 stride-1 conv (GN+ReLU prologue, residual epilogue) at patch^3, bf16. `live` = (avg ms,
+    launches, voxels) from HIP events recorded around its launches inside the timed steps (on the stream it runs
+    on); a standalone timing of the same launch is reported beside it (and used when `live` is None)."""
     from u3d import ops
     x = torch.randn((batch, patch, patch, patch, 32), device=device).to(torch.bfloat16)
     w = torch.randn(32, 32, 3, 3, 3, device=device)
@@ -70,8 +72,11 @@ def dominant_kernel_roofline(device, batch, patch, reps=20):
         y = ops.conv_fwd(x, pf, 32, 3, 1, (st, ga, be, 16), residual=x)
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    ms_alone = e0.elapsed_time(e1) / reps
     flops = 2.0 * batch * patch ** 3 * 27 * 32 * 32
+    ms, src = ms_alone, "standalone"
+    if live is not None and live[2] == batch * patch ** 3:
+        ms, src = live[0], f"HIP events, {live[1]} launches, {live[3]}"
     achieved = flops / (ms * 1e-3) / 1e12
     del y
     traffic, tsrc = pmc_traffic(batch, patch)
@@ -79,7 +84,8 @@ def dominant_kernel_roofline(device, batch, patch, reps=20):
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_source": tsrc, "algorithmic_bytes": 3 * batch * patch ** 3 * 32 * 2,
-            "avg_launch_ms": round(ms, 4), "flop_per_launch": flops}
+            "avg_launch_ms": round(ms, 4), "timing": src, "standalone_launch_ms": round(ms_alone, 4),
+            "flop_per_launch": flops}
 
 
 def pmc_traffic(batch, patch):
@@ -157,10 +163,15 @@ def main():
         return loss
 
     graphed = None
+    a.eager = not a.graph  # default: kernel-by-kernel launches (live HIP-event timing of the roofline kernel)
+    from u3d import ops as _ops
     if not a.eager:
         from u3d.graph import GraphedStep
         try:
+            _ops.PROBE = []  # the capture records event nodes around the dominant kernel; replays re-time them
             graphed = GraphedStep(step, (x, target, mask), warmup=3, optimizer=opt)
+            probes = _ops.PROBE[-4:]
+            _ops.PROBE = None
         except Exception as e:  # capture refused (e.g. a collective backend without graph support): run eager
             print(f"[bench] hipGraph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
             torch.cuda.synchronize()
@@ -177,6 +188,8 @@ def main():
 
     for i in range(a.warmup):
         run(i)
+    if a.eager:
+        _ops.PROBE = probes = []  # events around every dominant-kernel launch of the timed steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -194,13 +207,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     loss_v = float(loss)
+    _ops.PROBE = None
+    live = None
+    try:  # dominant kernel timed live over the timed region (eager: every launch; graph: the last replay)
+        durs = [e0.elapsed_time(e1) for e0, e1, _ in probes]
+        if durs:
+            live = (sum(durs) / len(durs), len(durs), probes[0][2],
+                    "every launch of the timed steps" if a.eager else "the last timed hipGraph replay")
+    except Exception as e:  # noqa: BLE001 - event nodes not timeable on this runtime: fall back below
+        print(f"[bench] live kernel timing unavailable ({e}); using the standalone measurement", file=sys.stderr)
     ms = dt / a.steps * 1e3
     vox = world * a.batch * a.patch ** 3 * a.steps / dt
 
     roof = None
     cpu = None
     if rank == 0 and not a.no_roofline:
-        roof = dominant_kernel_roofline(device, a.batch, a.patch)
+        roof = dominant_kernel_roofline(device, a.batch, a.patch, live)
         step_gflop = STEP_GFLOP_PER_SAMPLE * a.batch * (a.patch / 96) ** 3
         roof["step_mfma_frac"] = round(step_gflop / (ms * 1e-3) / 1e3 / PEAK_BF16_TFLOPS, 4)
     if rank == 0 and world == 1 and not a.no_cpu:

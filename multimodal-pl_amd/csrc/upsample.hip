@@ -32,95 +32,100 @@ __device__ __forceinline__ float wt_of(int o, int i, int n) {
   return w;
 }
 
+// grid: x = (ow, chunk) pairs of one output row, y = oh, z = n * D + od: no 64-bit index arithmetic per element
 template <typename T, int VEC>
 __global__ __launch_bounds__(256) void up_fwd_kernel(const T* __restrict__ x, const T* __restrict__ skip,
                                                     T* __restrict__ y, int n, int c, int d, int h, int w) {
   const int chn = c / VEC, D = 2 * d, H = 2 * h, W = 2 * w;
-  const long long total = (long long)n * D * H * W * chn;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(i % chn);
-    long long t = i / chn;
-    const int ow = (int)(t % W); t /= W;
-    const int oh = (int)(t % H); t /= H;
-    const int od = (int)(t % D);
-    const int nn = (int)(t / D);
-    const Lerp Ld = lerp_of(od, d), Lh = lerp_of(oh, h), Lw = lerp_of(ow, w);
-    const T* xb = x + (long long)nn * d * h * w * c + j * VEC;
-    auto at = [&](int a, int b, int e, float (&v)[VEC]) { loadv<T, VEC>(xb + (((long long)a * h + b) * w + e) * c, v); };
-    float v000[VEC], v001[VEC], v010[VEC], v011[VEC], v100[VEC], v101[VEC], v110[VEC], v111[VEC];
-    at(Ld.i0, Lh.i0, Lw.i0, v000); at(Ld.i0, Lh.i0, Lw.i1, v001);
-    at(Ld.i0, Lh.i1, Lw.i0, v010); at(Ld.i0, Lh.i1, Lw.i1, v011);
-    at(Ld.i1, Lh.i0, Lw.i0, v100); at(Ld.i1, Lh.i0, Lw.i1, v101);
-    at(Ld.i1, Lh.i1, Lw.i0, v110); at(Ld.i1, Lh.i1, Lw.i1, v111);
-    float o[VEC];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W * chn) return;
+  const int j = i % chn, ow = i / chn, oh = blockIdx.y, od = blockIdx.z % D, nn = blockIdx.z / D;
+  const Lerp Ld = lerp_of(od, d), Lh = lerp_of(oh, h), Lw = lerp_of(ow, w);
+  const T* xb = x + (long long)nn * d * h * w * c + j * VEC;
+  auto at = [&](int a, int b, int e, float (&v)[VEC]) { loadv<T, VEC>(xb + ((long long)(a * h + b) * w + e) * c, v); };
+  float v000[VEC], v001[VEC], v010[VEC], v011[VEC], v100[VEC], v101[VEC], v110[VEC], v111[VEC];
+  at(Ld.i0, Lh.i0, Lw.i0, v000); at(Ld.i0, Lh.i0, Lw.i1, v001);
+  at(Ld.i0, Lh.i1, Lw.i0, v010); at(Ld.i0, Lh.i1, Lw.i1, v011);
+  at(Ld.i1, Lh.i0, Lw.i0, v100); at(Ld.i1, Lh.i0, Lw.i1, v101);
+  at(Ld.i1, Lh.i1, Lw.i0, v110); at(Ld.i1, Lh.i1, Lw.i1, v111);
+  const long long off = ((((long long)nn * D + od) * H + oh) * W + ow) * c + j * VEC;
+  float sv[VEC];
+  if (skip) loadv<T, VEC>(skip + off, sv);
+  float o[VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e)  // PyTorch CPU nesting order: t0*(h0*(w0*a + w1*b) + h1*(...)) + t1*(...)
-      o[e] = Ld.l0 * (Lh.l0 * (Lw.l0 * v000[e] + Lw.l1 * v001[e]) + Lh.l1 * (Lw.l0 * v010[e] + Lw.l1 * v011[e])) +
-             Ld.l1 * (Lh.l0 * (Lw.l0 * v100[e] + Lw.l1 * v101[e]) + Lh.l1 * (Lw.l0 * v110[e] + Lw.l1 * v111[e]));
-    const long long off = i * VEC;
-    if (skip) {
-      float sv[VEC];
-      loadv<T, VEC>(skip + off, sv);
+  for (int e = 0; e < VEC; ++e)  // PyTorch CPU nesting order: t0*(h0*(w0*a + w1*b) + h1*(...)) + t1*(...)
+    o[e] = Ld.l0 * (Lh.l0 * (Lw.l0 * v000[e] + Lw.l1 * v001[e]) + Lh.l1 * (Lw.l0 * v010[e] + Lw.l1 * v011[e])) +
+           Ld.l1 * (Lh.l0 * (Lw.l0 * v100[e] + Lw.l1 * v101[e]) + Lh.l1 * (Lw.l0 * v110[e] + Lw.l1 * v111[e]));
+  if (skip)
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) o[e] += sv[e];
-    }
-    storev<T, VEC>(y + off, o);
-  }
+    for (int e = 0; e < VEC; ++e) o[e] += sv[e];
+  storev<T, VEC>(y + off, o);
 }
 
-// gather form of the adjoint: input i collects outputs {2i-1, 2i, 2i+1, 2i+2} per dim
+// outputs o (and weights) that read input i along one dim of size n (output 2n): o in {2i-1, 2i, 2i+1, 2i+2}
+__device__ __forceinline__ int taps_of(int i, int n, int (&o)[4], float (&wt)[4]) {
+  int k = 0;
+#pragma unroll
+  for (int q = -1; q <= 2; ++q) {
+    const int oo = 2 * i + q;
+    if (oo < 0 || oo >= 2 * n) continue;
+    const float ww = wt_of(oo, i, n);
+    if (ww != 0.f) {
+      o[k] = oo;
+      wt[k++] = ww;
+    }
+  }
+  return k;
+}
+
+// gather form of the adjoint; grid: x = (iw, chunk) pairs of one input row, y = ih, z = n * d + id
 template <typename T, int VEC>
 __global__ __launch_bounds__(256) void up_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, int c, int d,
                                                     int h, int w, int accum) {
   const int chn = c / VEC, D = 2 * d, H = 2 * h, W = 2 * w;
-  const long long total = (long long)n * d * h * w * chn;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int j = (int)(i % chn);
-    long long t = i / chn;
-    const int iw = (int)(t % w); t /= w;
-    const int ih = (int)(t % h); t /= h;
-    const int id = (int)(t % d);
-    const int nn = (int)(t / d);
-    int od_[4], oh_[4], ow_[4];
-    float wd[4], wh[4], ww[4];
-    int cd = 0, ch = 0, cw = 0;
-    for (int k = -1; k <= 2; ++k) {
-      int o = 2 * id + k;
-      if (o >= 0 && o < D) { float q = wt_of(o, id, d); if (q != 0.f) { od_[cd] = o; wd[cd++] = q; } }
-      o = 2 * ih + k;
-      if (o >= 0 && o < H) { float q = wt_of(o, ih, h); if (q != 0.f) { oh_[ch] = o; wh[ch++] = q; } }
-      o = 2 * iw + k;
-      if (o >= 0 && o < W) { float q = wt_of(o, iw, w); if (q != 0.f) { ow_[cw] = o; ww[cw++] = q; } }
-    }
-    float acc[VEC];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w * chn) return;
+  const int j = i % chn, iw = i / chn, ih = blockIdx.y, id = blockIdx.z % d, nn = blockIdx.z / d;
+  int od_[4], oh_[4], ow_[4];
+  float wd[4], wh[4], ww[4];
+  const int cd = taps_of(id, d, od_, wd), ch = taps_of(ih, h, oh_, wh), cw = taps_of(iw, w, ow_, ww);
+  float acc[VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
-    const T* yb = dy + (long long)nn * D * H * W * c + j * VEC;
-    for (int a = 0; a < cd; ++a)
-      for (int b = 0; b < ch; ++b)
-        for (int q = 0; q < cw; ++q) {
+  for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+  const T* yb = dy + (long long)nn * D * H * W * c + j * VEC;
+  for (int a = 0; a < cd; ++a)
+    for (int b = 0; b < ch; ++b) {
+      const T* yr = yb + ((long long)od_[a] * H + oh_[b]) * W * c;
+      float part[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) part[e] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q < cw) {
           float v[VEC];
-          loadv<T, VEC>(yb + (((long long)od_[a] * H + oh_[b]) * W + ow_[q]) * c, v);
-          const float wgt = wd[a] * wh[b] * ww[q];
+          loadv<T, VEC>(yr + ow_[q] * c, v);
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) acc[e] = fmaf(wgt, v[e], acc[e]);
+          for (int e = 0; e < VEC; ++e) part[e] = fmaf(ww[q], v[e], part[e]);
         }
-    const long long off = i * VEC;
-    if (accum) {
-      float o[VEC];
-      loadv<T, VEC>(dx + off, o);
+      }
+      const float wdh = wd[a] * wh[b];
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) acc[e] += o[e];
+      for (int e = 0; e < VEC; ++e) acc[e] = fmaf(wdh, part[e], acc[e]);
     }
-    storev<T, VEC>(dx + off, acc);
+  const long long off = ((((long long)nn * d + id) * h + ih) * w + iw) * c + j * VEC;
+  if (accum) {
+    float o[VEC];
+    loadv<T, VEC>(dx + off, o);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] += o[e];
   }
+  storev<T, VEC>(dx + off, acc);
 }
 
 }  // namespace u3d
 
 using namespace u3d;
 
-static int grid_for(long long total) { return (int)std::min<long long>(8192, std::max<long long>(1, (total + 255) / 256)); }
 
 extern "C" int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
                                   u3d_stream_t stream) {
@@ -129,8 +134,9 @@ extern "C" int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d,
   hipStream_t s = (hipStream_t)stream;
   const int vec = dtype == U3D_BF16 ? 8 : 4;
   const bool vect = c % vec == 0;
-  const long long total = (long long)n * 8 * d * h * w * (vect ? c / vec : c);
-  const dim3 gr(grid_for(total)), bl(256);
+  const int row = 2 * w * (vect ? c / vec : c);
+  U3D_REQUIRE((long long)n * 2 * d < 65536 && 2 * h < 65536, "upsample: volume too large for the row grid");
+  const dim3 gr(cdiv(row, 256), 2 * h, n * 2 * d), bl(256);
   if (dtype == U3D_BF16) {
     if (vect) hipLaunchKernelGGL((up_fwd_kernel<bf16, 8>), gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w);
     else hipLaunchKernelGGL((up_fwd_kernel<bf16, 1>), gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w);
@@ -148,8 +154,9 @@ extern "C" int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d
   hipStream_t s = (hipStream_t)stream;
   const int vec = dtype == U3D_BF16 ? 8 : 4;
   const bool vect = c % vec == 0;
-  const long long total = (long long)n * d * h * w * (vect ? c / vec : c);
-  const dim3 gr(grid_for(total)), bl(256);
+  const int row = w * (vect ? c / vec : c);
+  U3D_REQUIRE((long long)n * d < 65536 && h < 65536, "upsample_bwd: volume too large for the row grid");
+  const dim3 gr(cdiv(row, 256), h, n * d), bl(256);
   if (dtype == U3D_BF16) {
     if (vect) hipLaunchKernelGGL((up_bwd_kernel<bf16, 8>), gr, bl, 0, s, (const bf16*)dy, (bf16*)dx, n, c, d, h, w, accumulate);
     else hipLaunchKernelGGL((up_bwd_kernel<bf16, 1>), gr, bl, 0, s, (const bf16*)dy, (bf16*)dx, n, c, d, h, w, accumulate);

@@ -147,8 +147,15 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
     y = torch.empty((n, od, oh, ow, cout), dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
     st, ga, be, G = gn if gn is not None else (None, None, None, 0)
     if _use_conv32(x.dtype, cin, cout, k, stride, n, w_) and not out_f32 and bias is None:
+        probe = PROBE is not None
+        if probe:  # bench.py: HIP events around the dominant kernel, on the stream it runs on
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         call("u3d_conv32_brick", 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
              _ptr(residual), y.data_ptr(), _stream())
+        if probe:
+            e1.record()
+            PROBE.append((e0, e1, n * d * h * w_))
         return y
     if _use_small(x.dtype, cin, cout, k, stride, (n, d, h, w_)) and not out_f32 and bias is None:
         ws = WS.get(SPLITK_WS_BYTES, x.device, slot=4)
@@ -172,6 +179,7 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
 
 
 SPLITK_WS_BYTES = 64 << 20
+PROBE = None  # list -> conv32_brick forward launches record (start, end, voxels) HIP events (bench.py roofline)
 USE_CONV32_BRICK = True
 
 

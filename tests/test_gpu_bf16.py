@@ -218,3 +218,19 @@ def test_head_fwd_bwd(gpu, cin, cout, dims):
     assert (dA.double().cpu() - refA).abs().max().item() < 1e-2 * refA.abs().max().item()
     assert torch.equal(dyb[..., :cout].cpu(), dy.to(torch.bfloat16).cpu())
     torch.testing.assert_close(db.cpu().double(), dy.cpu().double().reshape(-1, cout).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("cin,cout,dims,s", [(1, 32, (8, 10, 12), 1), (2, 24, (8, 6, 10), 2), (1, 8, (5, 7, 9), 1),
+                                             (2, 32, (4, 4, 6), 1)])
+def test_bf16_stem_fwd(gpu, cin, cout, dims, s):
+    """Stem conv (fp32 input, bf16 packed weights, fp32 math, bf16 output) against fp64."""
+    from u3d import ops
+    torch.manual_seed(3)
+    x = torch.randn((2, cin) + dims, device=gpu)
+    w = torch.randn(cout, cin, 3, 3, 3, device=gpu)
+    pf, _, _ = ops.wstd_fwd(w, torch.bfloat16, True, need_dgrad=False)
+    y = ops.stem_fwd(x, pf, cout, s, torch.bfloat16)
+    wq = pf.float().cpu()[:, :cout, :cin].permute(1, 2, 0).reshape(cout, cin, 3, 3, 3).double()
+    ref = F.conv3d(x.cpu().double(), wq, stride=s, padding=1).permute(0, 2, 3, 4, 1)
+    err = (y.double().cpu() - ref).abs().max().item()
+    assert err < 1e-2 * ref.abs().max().item(), err
