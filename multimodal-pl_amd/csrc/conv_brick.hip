@@ -140,6 +140,20 @@ __global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __re
     prefetch(more ? bn : b);  // unconditional: keeps the prefetch registers phi-free (no copies, no early wait)
     int nn, d0, h0, w0;
     brick_origin(b, nn, d0, h0, w0);
+    // residual of this brick's two w-rows (16-B chunks q = lane + 64 u of each row): loaded before the MFMAs
+    // so their latency hides under them
+    u32x4 rv[2][2];
+    const long long orow[2] = {(((long long)nn * g.d + d0) * g.h + h0 + wave) * g.w + w0,
+                               (((long long)nn * g.d + d0 + 1) * g.h + h0 + wave) * g.w + w0};
+    const bool ok[2] = {d0 < g.d && h0 + wave < g.h, d0 + 1 < g.d && h0 + wave < g.h};
+    if (res) {
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          rv[tm][u] = ok[tm] ? *reinterpret_cast<const u32x4*>(res + orow[tm] * 32 + (lane + 64 * u) * 8)
+                             : u32x4{0u, 0u, 0u, 0u};
+    }
     f32x16 acc0, acc1;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc0[e] = acc1[e] = 0.f;
@@ -167,19 +181,6 @@ __global__ __launch_bounds__(CB_NT, 1) void conv32_brick_kernel(const bf16* __re
       ca0 = na0;
       ca1 = na1;
       cb = nb;
-    }
-    // residual of this brick's two w-rows: 16-B chunks q = lane + 64 u of each row (in flight during commit)
-    u32x4 rv[2][2];
-    const long long orow[2] = {(((long long)nn * g.d + d0) * g.h + h0 + wave) * g.w + w0,
-                               (((long long)nn * g.d + d0 + 1) * g.h + h0 + wave) * g.w + w0};
-    const bool ok[2] = {d0 < g.d && h0 + wave < g.h, d0 + 1 < g.d && h0 + wave < g.h};
-    if (res) {
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          rv[tm][u] = ok[tm] ? *reinterpret_cast<const u32x4*>(res + orow[tm] * 32 + (lane + 64 * u) * 8)
-                             : u32x4{0u, 0u, 0u, 0u};
     }
     __syncthreads();  // all waves done reading the halo before it is overwritten
     if (more) commit(bn);

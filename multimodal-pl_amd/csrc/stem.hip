@@ -280,7 +280,10 @@ static int stem_bricks(int n, int d, int h, int w) {
 }
 
 extern "C" int u3d_stem_wgrad_splits2(int dtype, int n, int cin, int d, int h, int w, int cout, int stride) {
-  if (stem_mfma_ok(dtype, cin, cout, w, stride)) return std::min(256, stem_bricks(n, d, h, w));
+  if (stem_mfma_ok(dtype, cin, cout, w, stride)) {
+    const int nb = stem_bricks(n, d, h, w), per = cdiv(nb, std::min(256, nb));
+    return cdiv(nb, per);  // splits that all receive bricks: no zero-filled slabs
+  }
   const long long total = (long long)n * sdim(d, stride) * sdim(h, stride) * sdim(w, stride);
   return (int)std::max<long long>(1, std::min<long long>(1024, total / 2048));
 }

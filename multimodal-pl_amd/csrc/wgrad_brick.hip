@@ -340,7 +340,9 @@ extern "C" int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, 
   const long long nb = (long long)n * cdiv(od, bd) * cdiv(oh, bh) * cdiv(ow, bw);
   const long long tiles = (long long)cdiv(cin, 32) * cdiv(cout, 32);
   long long want = std::max(1LL, 256 / tiles);
-  return (int)std::max(1LL, std::min(want, nb));
+  const long long ns = std::max(1LL, std::min(want, nb));
+  const long long per = (nb + ns - 1) / ns;
+  return (int)((nb + per - 1) / per);  // splits that all receive bricks: no zero-filled slabs
 }
 
 extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout,
@@ -381,7 +383,9 @@ extern "C" int u3d_conv_wgrad1_splits(int n, int cin, int d, int h, int w, int c
   const long long chunks = ((long long)n * od * oh * ow + W1_NV - 1) / W1_NV;
   const long long tiles = (long long)cdiv(cin, 32) * cdiv(cout, 32);
   long long want = std::max(1LL, 256 / tiles);
-  return (int)std::max(1LL, std::min(want, chunks));
+  const long long ns = std::max(1LL, std::min(want, chunks));
+  const long long per = (chunks + ns - 1) / ns;
+  return (int)((chunks + per - 1) / per);  // splits that all receive voxels: no zero-filled slabs
 }
 
 extern "C" int u3d_conv_wgrad1(const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout, int stride,

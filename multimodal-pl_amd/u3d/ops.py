@@ -151,7 +151,7 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
         if probe:  # bench.py: HIP events around the dominant kernel, on the stream it runs on
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        call("u3d_conv32_brick", 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
+        call(CONV32_FN, 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
              _ptr(residual), y.data_ptr(), _stream())
         if probe:
             e1.record()
@@ -181,6 +181,7 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
 SPLITK_WS_BYTES = 64 << 20
 PROBE = None  # list -> conv32_brick forward launches record (start, end, voxels) HIP events (bench.py roofline)
 USE_CONV32_BRICK = True
+CONV32_FN = "u3d_conv32_brick"
 
 
 def _use_conv32(dtype, cin, cout, k, stride, n, w=32):
@@ -217,7 +218,7 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     cout = dy.shape[-1]
     dx = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
     if _use_conv32(dy.dtype, cin, cout, k, stride, n, w_):
-        call("u3d_conv32_brick", 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
+        call(CONV32_FN, 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
              dx.data_ptr(), _stream())
         return dx
     if USE_S2_BRICK and dy.dtype == torch.bfloat16 and k == 3 and stride == 2:

@@ -43,6 +43,7 @@ def _act_ref(x, st, ga, be, G):
 SHAPES = [(2, 32, 32, (12, 10, 16), 1), (1, 32, 32, (5, 9, 70), 1), (1, 32, 64, (8, 12, 18), 2), (2, 64, 64, (6, 8, 9), 1),
           (1, 64, 32, (10, 6, 8), 1), (2, 128, 128, (4, 4, 4), 1), (1, 24, 24, (7, 9, 11), 1),
           (2, 32, 32, (4, 10, 64), 1), (1, 32, 32, (3, 8, 32), 1), (1, 64, 128, (6, 9, 20), 1),
+          (2, 32, 32, (6, 7, 96), 1), (3, 32, 32, (9, 5, 32), 1),
           (2, 32, 64, (12, 16, 34), 2), (1, 64, 128, (8, 8, 8), 2), (2, 128, 256, (12, 12, 12), 2),
           (1, 256, 256, (6, 6, 6), 2), (1, 40, 48, (6, 10, 14), 2)]
 
@@ -52,7 +53,7 @@ def conv_path(request):
     """auto = production routing; gen_brick = force the generic halo-brick kernel; igemm = force implicit GEMM."""
     from u3d import ops
     saved = (ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK, ops.USE_SMALL_CONV,
-             ops.SMALL_MAX_VOX)
+             ops.SMALL_MAX_VOX, ops.CONV32_FN)
     if request.param == "gen_brick":
         ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_SMALL_CONV = 0, False, False
     elif request.param == "igemm":
@@ -61,7 +62,7 @@ def conv_path(request):
         ops.USE_CONV32_BRICK, ops.SMALL_MAX_VOX = False, 1 << 40
     yield request.param
     (ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK, ops.USE_SMALL_CONV,
-     ops.SMALL_MAX_VOX) = saved
+     ops.SMALL_MAX_VOX, ops.CONV32_FN) = saved
 
 
 @pytest.mark.parametrize("n,cin,cout,dims,s", SHAPES)
@@ -234,3 +235,25 @@ def test_bf16_stem_fwd(gpu, cin, cout, dims, s):
     ref = F.conv3d(x.cpu().double(), wq, stride=s, padding=1).permute(0, 2, 3, 4, 1)
     err = (y.double().cpu() - ref).abs().max().item()
     assert err < 1e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n,cin,cout,dims", [(2, 32, 64, (8, 6, 10)), (1, 64, 128, (4, 4, 4)), (2, 256, 256, (4, 6, 2))])
+def test_conv1_s2_dgrad_writes_every_voxel(gpu, dt, n, cin, cout, dims):
+    """1^3 stride-2 data gradient (downsample convs): the odd-parity voxels get exact zeros from the GEMM kernel
+    itself (no memset) — dx is pre-filled with NaN to prove every voxel is written."""
+    from u3d import ops
+    torch.manual_seed(4)
+    w = torch.randn(cout, cin, 1, 1, 1, device=gpu)
+    pf, pd, _ = ops.wstd_fwd(w, dt, True)
+    od = tuple(ops.out_dim(d, 1, 2) for d in dims)
+    dy = torch.randn((n,) + od + (cout,), device=gpu).to(dt)
+    torch.cuda.synchronize()
+    dx = ops.conv_dgrad(dy, pd, cin, (n,) + dims, 1, 2)
+    wq = pf.float().cpu()[:, :cout, :cin].permute(1, 2, 0).reshape(cout, cin, 1, 1, 1).double()
+    ref = torch.nn.grad.conv3d_input((n, cin) + dims, wq, dy.cpu().double().permute(0, 4, 1, 2, 3),
+                                     stride=2).permute(0, 2, 3, 4, 1)
+    got = dx.double().cpu()
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+    assert torch.count_nonzero(got[:, 1::2]) == 0 and torch.count_nonzero(got[:, :, 1::2]) == 0

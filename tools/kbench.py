@@ -11,7 +11,8 @@ dev = torch.device("cuda:0")
 for kv in os.environ.get("KB_SET", "").split(","):  # e.g. KB_SET=USE_SMALL_CONV=0,SMALL_MAX_VOX=1e9
     if kv:
         k, v = kv.split("=")
-        setattr(ops, k, type(getattr(ops, k))(float(v)))
+        cur = getattr(ops, k)
+        setattr(ops, k, v if isinstance(cur, str) else type(cur)(float(v)))
 bf = torch.bfloat16
 
 
@@ -87,6 +88,9 @@ CASES["dgrad_s2_96"] = lambda: _dgrad(2, 32, 64, 96, 3, 2)
 CASES["dgrad_s2_48"] = lambda: _dgrad(2, 64, 128, 48, 3, 2)
 CASES["dgrad_s2_12"] = lambda: _dgrad(2, 256, 256, 12, 3, 2)
 CASES["fwd6nogn"] = lambda: _fwd(2, 256, 256, 6, 3, 1, False, False)
+CASES["dgrad1_s2_96"] = lambda: _dgrad(2, 32, 64, 96, 1, 2)
+CASES["dgrad1_s2_48"] = lambda: _dgrad(2, 64, 128, 48, 1, 2)
+CASES["fwd1_s2_96"] = lambda: _fwd(2, 32, 64, 96, 1, 2, True, False)
 CASES["head96"] = lambda: _fwd(2, 32, 16, 96, 1, 1, True, False)
 
 if __name__ == "__main__":
