@@ -238,6 +238,18 @@ int u3d_dyn_controller(const float* feat, int n, int kf, const long long* task, 
                        const float* b, int m, float* params, u3d_stream_t stream);
 /* heads_forward (unet3D.py:1720-1732, 1788-1804): h fp32 [n][v][8] -> out fp32 [n][v][2] */
 int u3d_dynhead_fwd(const float* h, const float* params, int n, long long v, float* out, u3d_stream_t stream);
+/* DynConv head backward (autograd of heads_forward, unet3D.py:1720-1732): from dlogits [n][v][2] and the head
+ * input h [n][v][8] (recomputed MLP): dh [n][v][8] and dparams [n][162] (layout of params; per-block partials
+ * part [n][u3d_dynhead_bwd_blocks(v)][162] summed in fixed order). */
+int u3d_dynhead_bwd_blocks(long long v);
+int u3d_dynhead_bwd(const float* h, const float* params, const float* dlogits, int n, long long v, float* dh,
+                    float* part, float* dparams, u3d_stream_t stream);
+/* Controller (1^3 conv kf+kt -> m, bias) backward: dw [m][kf+kt], db [m] (+= when accumulate), and the GAP's
+ * AdaptiveAvgPool3d backward: dA [n][v][kf] (dtype) = (W^T dparams)[n][k] / v (the GN+ReLU input gradient of the
+ * GAP, unet3D.py:1659-1663), ready for u3d_gn_bwd. */
+int u3d_dyn_controller_bwd(int dtype, const float* feat, int n, int kf, const long long* task, int kt, const float* w,
+                           const float* dparams, int m, float* dw, float* db, int accumulate, long long v, void* dA,
+                           u3d_stream_t stream);
 
 #ifdef __cplusplus
 }

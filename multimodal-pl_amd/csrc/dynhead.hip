@@ -80,6 +80,148 @@ __global__ __launch_bounds__(256) void dynhead_fwd_kernel(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------------------- backward
+// Per voxel: recompute the 8-8-2 MLP (h -> a1 -> r1 -> a2 -> r2 -> out), back-propagate dlogits, write dh and
+// accumulate the 162 parameter gradients (same layout as params) per thread; block partials are reduced by
+// wave shuffles + LDS in fixed order into part[n][block][162].
+__global__ __launch_bounds__(256) void dynhead_bwd_kernel(const float* __restrict__ h, const float* __restrict__ prm,
+                                                         const float* __restrict__ dout, long long v,
+                                                         float* __restrict__ dh, float* __restrict__ part) {
+  __shared__ float p[162];
+  __shared__ float red[4][162];
+  const int n = blockIdx.y;
+  for (int i = threadIdx.x; i < 162; i += 256) p[i] = prm[n * 162 + i];
+  __syncthreads();
+  float g[162];
+#pragma unroll
+  for (int k = 0; k < 162; ++k) g[k] = 0.f;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < v; i += (long long)gridDim.x * 256) {
+    const float* hv = h + ((long long)n * v + i) * 8;
+    float x0[8], a1[8], r1[8], a2[8], r2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x0[k] = hv[k];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      float s = p[144 + o];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s = fmaf(p[o * 8 + k], x0[k], s);
+      a1[o] = s;
+      r1[o] = fmaxf(s, 0.f);
+    }
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      float s = p[152 + o];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s = fmaf(p[64 + o * 8 + k], r1[k], s);
+      a2[o] = s;
+      r2[o] = fmaxf(s, 0.f);
+    }
+    const float* dv = dout + ((long long)n * v + i) * 2;
+    const float d0 = dv[0], d1 = dv[1];
+    // layer 3: out = W3 r2 + b3
+    float dr2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      g[128 + k] = fmaf(d0, r2[k], g[128 + k]);
+      g[136 + k] = fmaf(d1, r2[k], g[136 + k]);
+      dr2[k] = fmaf(p[128 + k], d0, p[136 + k] * d1);
+    }
+    g[160] += d0;
+    g[161] += d1;
+    // layer 2: a2 = W2 r1 + b2, r2 = relu(a2)
+    float da2[8], dr1[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) da2[o] = a2[o] > 0.f ? dr2[o] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dr1[k] = 0.f;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      g[152 + o] += da2[o];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g[64 + o * 8 + k] = fmaf(da2[o], r1[k], g[64 + o * 8 + k]);
+        dr1[k] = fmaf(p[64 + o * 8 + k], da2[o], dr1[k]);
+      }
+    }
+    // layer 1: a1 = W1 x0 + b1, r1 = relu(a1)
+    float da1[8], dx0[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) da1[o] = a1[o] > 0.f ? dr1[o] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dx0[k] = 0.f;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      g[144 + o] += da1[o];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g[o * 8 + k] = fmaf(da1[o], x0[k], g[o * 8 + k]);
+        dx0[k] = fmaf(p[o * 8 + k], da1[o], dx0[k]);
+      }
+    }
+    float* dhv = dh + ((long long)n * v + i) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dhv[k] = dx0[k];
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 162; ++k) {
+    const float t = wave_sum(g[k]);
+    if (lane == 0) red[wave][k] = t;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 162; k += 256)
+    part[((long long)n * gridDim.x + blockIdx.x) * 162 + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+}
+
+// dparams[n][k] = sum_b part[n][b][k] (fp64, fixed order)
+__global__ void dyn_param_reduce_kernel(const float* __restrict__ part, int nblk, float* __restrict__ dparams) {
+  const int n = blockIdx.x;
+  for (int k = threadIdx.x; k < 162; k += blockDim.x) {
+    double s = 0;
+    for (int b = 0; b < nblk; ++b) s += part[((long long)n * nblk + b) * 162 + k];
+    dparams[n * 162 + k] = (float)s;
+  }
+}
+
+// Controller backward (1^3 conv 263 -> m with bias on x = cat(feat, onehot(task))):
+//   blocks 0..m-1: dW[o][k] (+)= sum_n dy[n][o] x[n][k], db[o] (+)= sum_n dy[n][o]
+//   blocks m..m+n-1: dfeat[n][k] = sum_o W[o][k] dy[n][o] (k < kf), written as the GAP's dA broadcast over the
+//   v bottleneck voxels: dA[n][v][k] = dfeat[n][k] / v   (AdaptiveAvgPool3d backward; NDHWC, dtype T)
+template <typename T>
+__global__ void controller_bwd_kernel(const float* __restrict__ feat, int n, int kf, const long long* __restrict__ task,
+                                      int kt, const float* __restrict__ w, const float* __restrict__ dy, int m,
+                                      float* __restrict__ dw, float* __restrict__ db, int accp, long long v,
+                                      T* __restrict__ dA) {
+  const int kx = kf + kt;
+  if ((int)blockIdx.x < m) {
+    const int o = blockIdx.x;
+    for (int k = threadIdx.x; k < kx; k += blockDim.x) {
+      float s = 0.f;
+      for (int i = 0; i < n; ++i) {
+        const long long t = task[i];
+        const float xv = k < kf ? feat[i * kf + k] : (t == k - kf ? 1.f : 0.f);
+        s = fmaf(dy[i * m + o], xv, s);
+      }
+      dw[(long long)o * kx + k] = (accp ? dw[(long long)o * kx + k] : 0.f) + s;
+    }
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+      for (int i = 0; i < n; ++i) s += dy[i * m + o];
+      db[o] = (accp ? db[o] : 0.f) + s;
+    }
+    return;
+  }
+  extern __shared__ float df[];
+  const int i = blockIdx.x - m;
+  for (int k = threadIdx.x; k < kf; k += blockDim.x) {
+    float s = 0.f;
+    for (int o = 0; o < m; ++o) s = fmaf(w[(long long)o * kx + k], dy[i * m + o], s);
+    df[k] = s / (float)v;
+  }
+  __syncthreads();
+  for (long long e = threadIdx.x; e < v * kf; e += blockDim.x) dA[(long long)i * v * kf + e] = from_f<T>(df[e % kf]);
+}
+
 }  // namespace u3d
 
 using namespace u3d;
@@ -112,4 +254,32 @@ extern "C" int u3d_dynhead_fwd(const float* h, const float* params, int n, long 
   const int nb = (int)std::min<long long>(2048, (v + 255) / 256);
   hipLaunchKernelGGL(dynhead_fwd_kernel, dim3(nb, n), dim3(256), 0, (hipStream_t)stream, h, params, v, out);
   return check_launch("dynhead_fwd_kernel");
+}
+
+extern "C" int u3d_dynhead_bwd_blocks(long long v) { return (int)std::min<long long>(512, (v + 255) / 256); }
+
+extern "C" int u3d_dynhead_bwd(const float* h, const float* params, const float* dlogits, int n, long long v, float* dh,
+                               float* part, float* dparams, u3d_stream_t stream) {
+  U3D_REQUIRE(h && params && dlogits && dh && part && dparams && n > 0 && v > 0, "dynhead_bwd: bad args");
+  const int nb = u3d_dynhead_bwd_blocks(v);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(dynhead_bwd_kernel, dim3(nb, n), dim3(256), 0, s, h, params, dlogits, v, dh, part);
+  hipLaunchKernelGGL(dyn_param_reduce_kernel, dim3(n), dim3(192), 0, s, part, nb, dparams);
+  return check_launch("dynhead_bwd");
+}
+
+extern "C" int u3d_dyn_controller_bwd(int dtype, const float* feat, int n, int kf, const long long* task, int kt,
+                                      const float* w, const float* dparams, int m, float* dw, float* db, int accumulate,
+                                      long long v, void* dA, u3d_stream_t stream) {
+  U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "dyn_controller_bwd: bad dtype");
+  U3D_REQUIRE(feat && task && w && dparams && dw && db && dA && n > 0 && v > 0 && kf <= 1024,
+              "dyn_controller_bwd: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == U3D_BF16)
+    hipLaunchKernelGGL(controller_bwd_kernel<bf16>, dim3(m + n), dim3(256), kf * 4, s, feat, n, kf, task, kt, w,
+                       dparams, m, dw, db, accumulate, v, (bf16*)dA);
+  else
+    hipLaunchKernelGGL(controller_bwd_kernel<float>, dim3(m + n), dim3(256), kf * 4, s, feat, n, kf, task, kt, w,
+                       dparams, m, dw, db, accumulate, v, (float*)dA);
+  return check_launch("controller_bwd_kernel");
 }

@@ -58,6 +58,9 @@ _SIGS = {
     "u3d_gn_relu_mean": [I, P, I, I, L, I, P, P, P, P, P],
     "u3d_dyn_controller": [P, I, I, P, I, P, P, I, P, P],
     "u3d_dynhead_fwd": [P, P, I, L, P, P],
+    "u3d_dynhead_bwd_blocks": [L],
+    "u3d_dynhead_bwd": [P, P, P, I, L, P, P, P, P],
+    "u3d_dyn_controller_bwd": [I, P, I, I, P, I, P, P, I, P, P, I, L, P, P],
 }
 _RESTYPE = {"u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L}
 

@@ -216,6 +216,22 @@ def test_g1_unet3d_dynconv_forward_dice(gpu):
     np.testing.assert_allclose([float(v) for v in d], g["dice"], atol=DICE_TOL)
 
 
+def test_g1_unet3d_dynconv_backward(gpu):
+    """UNet3D DynConv 8,8,2 trained natively: every parameter gradient (trunk, precls, GAP GroupNorm, controller)
+    against the reference's autograd on the same weights / input / upstream gradient (golden G1)."""
+    g = golden("g1_unet3d_dyn_32.npz")
+    m = _model("dyn").to(gpu).train()
+    y = m(torch.from_numpy(g["x2"]).to(gpu), torch.from_numpy(g["task_id2"]))
+    assert np.abs(y.detach().cpu().numpy() - g["logits2"]).max() < LOGIT_TOL
+    (y * torch.from_numpy(g["up2"]).to(gpu)).sum().backward()
+    P = dict(m.named_parameters())
+    for i, k in enumerate(g["gnames"]):
+        gr = P[k].grad.reshape(-1).double().cpu()
+        np.testing.assert_allclose(gr.norm().item(), g["gnorm"][i], rtol=2e-3, atol=1e-9, err_msg=k)
+    names = set(str(k) for k in g["gnames"])
+    assert {"controller.weight", "controller.bias", "GAP.0.weight", "GAP.0.bias"} <= names
+
+
 def test_bf16_mode_close_to_fp32(gpu):
     """bf16 activations/weights with fp32 accumulation: logits track the fp32 path (stated tolerance 0.25
     max-abs on O(1..10) logits after 36 bf16 layers), loss within 1e-2 relative."""
