@@ -34,6 +34,9 @@ def parse():
     p.add_argument("--batch", type=int, default=2, help="patches per GPU")
     p.add_argument("--patch", type=int, default=96)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--modality", default="ct", choices=["ct", "mixed"],
+                   help="mixed = BASELINE configs[3]: per GPU one CT-normalised and one z-scored MRI-like patch "
+                        "(MOTSDataset.py:171-185), the batch's mask[0] applied to both (loss_partial.py:87)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph (~1%% faster at "
@@ -42,10 +45,15 @@ def parse():
     return p.parse_args()
 
 
-def synthetic(batch, patch, device, seed):
+def synthetic(batch, patch, device, seed, modality="ct"):
     g = torch.Generator(device="cpu").manual_seed(seed)
     hu = torch.rand((batch, 1, patch, patch, patch), generator=g) * 2000 - 1000
-    x = (hu.clamp(-325, 325) / 325).to(device)            # CT normalisation, MOTSDataset.py:171-182
+    x = hu.clamp(-325, 325) / 325                          # CT normalisation, MOTSDataset.py:171-182
+    if modality == "mixed":                                # odd samples: MRI z-scored (MOTSDataset.py:183-185)
+        mri = torch.rand((batch, 1, patch, patch, patch), generator=g) * 900
+        mri = (mri - mri.mean(dim=(2, 3, 4), keepdim=True)) / mri.std(dim=(2, 3, 4), keepdim=True)
+        x[1::2] = mri[1::2]
+    x = x.to(device)
     lab = torch.randint(0, 16, (batch, 1, patch, patch, patch), generator=g).float().to(device)
     mask = (torch.rand(16, generator=g) < 0.6).long()
     mask[1] = 1
@@ -148,7 +156,7 @@ def main():
     # two resident synthetic batches; each step consumes the other one (copied into the step's input buffers)
     batches = []
     for j in range(2):
-        xb, lb, mb = synthetic(a.batch, a.patch, device, 1000 + 17 * j + rank)
+        xb, lb, mb = synthetic(a.batch, a.patch, device, 1000 + 17 * j + rank, a.modality)
         batches.append((xb, lb.squeeze(1), mb.to(device)))
     x, target, mask = (t.clone() for t in batches[0])
     amp = a.dtype == "bf16"

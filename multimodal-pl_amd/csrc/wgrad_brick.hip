@@ -10,6 +10,9 @@
 // ds_read_b64_tr_b16 gives it, and because every lane supplies its own row address the 27 shifted tap
 // windows of the halo are read with no data movement (row address = brick voxel row + tap offset). The dy
 // fragment is shared by all taps of a wave. Reference: autograd of F.conv3d in Conv3d.forward (unet3D.py:27).
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 
 namespace u3d {
@@ -51,7 +54,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
   constexpr int RPP = NT / 4;                       // rows per pass (thread t: chunk t&3 of row t>>2)
   constexpr int DYL = (NV + RPP - 1) / RPP;         // dy loads per thread
   constexpr int HLL = (NH + RPP - 1) / RPP;         // halo loads per thread
-  static_assert(NV % 16 == 0, "brick voxels");
+  static_assert(NV % 32 == 0, "brick voxels (an even number of 16-voxel k-steps)");
   __shared__ __attribute__((aligned(16))) char lds[(NV + NH) * ROWB];
   char* dyt = lds;
   char* hal = lds + NV * ROWB;
@@ -157,26 +160,44 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
   for (long long b = b0; b < b1; ++b) {
     const bool more = b + 1 < b1;
     prefetch(more ? b + 1 : b);
-    // K loop over the brick's voxels, 16 per MFMA
-#pragma unroll 2
-    for (int ks = 0; ks < NKS; ++ks) {
-      int arow[2], hrow[2];
+    // K loop over the brick's voxels, 16 per MFMA; software-pipelined: the fragments of step ks+1 are read
+    // while step ks's MFMAs run, and the tap count is a compile-time constant per wave (4 or 3) so the loop
+    // has no divergent branches between the LDS reads and the MFMAs
+    auto kloop = [&](auto ntc) {
+      constexpr int NT = decltype(ntc)::value;
+      auto rows = [&](int ks, int (&ar)[2], int (&hr)[2]) {
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const int k = ks * 16 + 8 * h + 4 * m + q;
-        const int vw = k % BW, vh = (k / BW) % BH, vd = k / (BW * BH);
-        arow[m] = k * ROWB + colb;
-        hrow[m] = ((vd * S * HH + vh * S) * HW + vw * S) * ROWB + colb;
-      }
-      const bf16x8 a = frag_from(tr_read(dyt, arow[0]), tr_read(dyt, arow[1]));
-#pragma unroll
-      for (int j = 0; j < MAXT; ++j) {
-        if (j < ntap) {
-          const bf16x8 bb = frag_from(tr_read(hal, hrow[0] + tap_off[j]), tr_read(hal, hrow[1] + tap_off[j]));
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc[j], 0, 0, 0);
+        for (int m = 0; m < 2; ++m) {
+          const int k = ks * 16 + 8 * h + 4 * m + q;
+          const int vw = k % BW, vh = (k / BW) % BH, vd = k / (BW * BH);
+          ar[m] = k * ROWB + colb;
+          hr[m] = ((vd * S * HH + vh * S) * HW + vw * S) * ROWB + colb;
         }
+      };
+      auto frags = [&](int ks, bf16x8& a, bf16x8 (&bb)[NT]) {
+        int ar[2], hr[2];
+        rows(ks, ar, hr);
+        a = frag_from(tr_read(dyt, ar[0]), tr_read(dyt, ar[1]));
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          bb[j] = frag_from(tr_read(hal, hr[0] + tap_off[j]), tr_read(hal, hr[1] + tap_off[j]));
+      };
+      bf16x8 a0, a1, b0[NT], b1[NT];
+      frags(0, a0, b0);
+#pragma unroll 1
+      for (int ks = 0; ks < NKS; ks += 2) {
+        frags(ks + 1, a1, b1);  // NKS is even
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0[j], acc[j], 0, 0, 0);
+        if (ks + 2 < NKS) frags(ks + 2, a0, b0);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1[j], acc[j], 0, 0, 0);
       }
-    }
+    };
+    if (ntap == 4)
+      kloop(std::integral_constant<int, 4>{});
+    else
+      kloop(std::integral_constant<int, 3>{});
     __syncthreads();  // everyone done with this brick's LDS
     if (more) commit(b + 1);
     __syncthreads();
@@ -328,8 +349,16 @@ __global__ __launch_bounds__(512, 1) void wgrad1_kernel(const bf16* __restrict__
 
 using namespace u3d;
 
+static int wgrad_bd() {  // brick depth of the stride-1 kernel (3; U3D_WGRAD_BD=2 selects the 2x8x16 brick)
+  static const int bd = [] {
+    const char* e = getenv("U3D_WGRAD_BD");
+    return (e && atoi(e) == 2) ? 2 : 3;
+  }();
+  return bd;
+}
+
 static void brick_dims(int stride, int* bd, int* bh, int* bw) {
-  if (stride == 1) { *bd = 2; *bh = 8; *bw = 16; }
+  if (stride == 1) { *bd = wgrad_bd(); *bh = 8; *bw = 16; }
   else { *bd = 2; *bh = 4; *bw = 8; }
 }
 
@@ -369,8 +398,11 @@ extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int ci
     U3D_HIP(hipMemsetAsync(partials + (long long)ns_eff * 27 * g.cout_p * g.cin_p, 0,
                            (size_t)(nsplit - ns_eff) * 27 * g.cout_p * g.cin_p * 4, s));
   dim3 grid(g.cin_p / 32, g.cout_p / 32, ns_eff);
-  if (stride == 1)
+  if (stride == 1 && bd == 2)
     hipLaunchKernelGGL((wgrad_brick_kernel<2, 8, 16, 1>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
+                       gn_stats, gn_gamma, gn_beta, partials, g);
+  else if (stride == 1)
+    hipLaunchKernelGGL((wgrad_brick_kernel<3, 8, 16, 1>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
                        gn_stats, gn_gamma, gn_beta, partials, g);
   else
     hipLaunchKernelGGL((wgrad_brick_kernel<2, 4, 8, 2>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
