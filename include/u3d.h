@@ -225,6 +225,15 @@ int u3d_partial_loss_bwd(int dtype_out, const float* logits, const float* labels
  * get_dice(preds, labels, t_id, atlas=None, num_class), evaluate_amos.py:128-154 with dice_score :92-102:
  * argmax(softmax(logits)) per voxel; counts[s][l-1] = (sum P*T, sum P, sum T) for l = 1..num_class, and
  * metrics[l-1] = (dice, sensitivity, precision) averaged over samples in fp32 like the reference. */
+/* Sliding-window inference (evaluate_amos.py:198-279): full[n][c][D][H][W] += scale * pred * g and (when
+ * add_count) count[n][D][H][W] += g for one tile at (d1, y1, x1); pred = the tile's NDHWC fp32 logits [n][td][th][tw][C];
+ * g = gd[a] gh[b] gw[e] (each profile max 1), zeros -> gmin; flips bit0/1/2 = the prediction of a d/h/w-flipped
+ * input (read mirrored). u3d_window_normalize divides full by count. */
+int u3d_window_accumulate(const float* pred, int n, int C, int td, int th, int tw, const float* gd, const float* gh,
+                          const float* gw, float gmin, float scale, float* full, float* count, int D, int H, int W,
+                          int d1, int y1, int x1, int flips, int add_count, u3d_stream_t stream);
+int u3d_window_normalize(float* full, const float* count, int n, int C, long long dhw, u3d_stream_t stream);
+
 int u3d_dice_metric(const float* logits, const float* labels, int S, long long V, int C, int num_class,
                     long long* counts, float* metrics, long long* argmax /* nullable, [S][V] */,
                     u3d_stream_t stream);

@@ -4,8 +4,13 @@ get_dice (evaluate_amos.py:128-154, atlas=None branch) runs as one fused HIP pas
 softmax, integer per-class counts, and the fp32 dice / sensitivity / precision averaged over samples exactly
 as the reference's dice_score / senc_score / spec_score (:92-126) compute them from the counts.
 dice_score / spec_score / senc_score themselves are kept as the reference's small tensor helpers.
-Sliding-window inference (predict_sliding, _get_gaussian) is SURVEY.md §8(f) row f1.
+Sliding-window inference (predict_sliding, _get_gaussian, :184-279) keeps the
+reference's tiling, multi-net averaging and flip test-time augmentation, but accumulates on the device
+(libu3d window kernels, fp32) instead of copying every tile's prediction to float64 host arrays.
 """
+import math
+
+import numpy as np
 import torch
 
 from u3d import ops
@@ -51,5 +56,85 @@ def get_dice(preds, labels, t_id, atlas=None, num_class=13):
     return dices, senc, spec, am
 
 
-def predict_sliding(*a, **k):
-    raise NotImplementedError("predict_sliding: sliding-window inference is SURVEY.md §8(f) row f1 — next round")
+def _gaussian_profiles(patch_size, sigma_scale=1.0 / 8):
+    """The 1-D factors of _get_gaussian (evaluate_amos.py:184-197): scipy.ndimage.gaussian_filter (truncate 4.0,
+    mode 'constant') of a centred delta is the product of three normalised 1-D kernels; each factor is scaled
+    to max 1 (so the map's max is 1) and the map's zeros become its minimum non-zero value ``gmin``."""
+    profs, mins = [], []
+    for n in patch_size:
+        sigma = n * sigma_scale
+        radius = int(4.0 * sigma + 0.5)
+        xs = np.arange(-radius, radius + 1, dtype=np.float64)
+        k = np.exp(-0.5 * (xs / sigma) ** 2)
+        k /= k.sum()
+        c = n // 2
+        prof = np.zeros(n, dtype=np.float64)
+        for i in range(n):
+            if -radius <= i - c <= radius:
+                prof[i] = k[i - c + radius]
+        prof /= prof.max()
+        profs.append(prof)
+        mins.append(prof[prof > 0].min())
+    return profs, float(np.float32(np.prod(mins)))
+
+
+def _get_gaussian(patch_size, sigma_scale=1.0 / 8):
+    """The full importance map (float32, as the reference returns it) — for inspection; predict_sliding uses the
+    separable factors on the device."""
+    (pd, ph, pw), gmin = _gaussian_profiles(patch_size, sigma_scale)
+    g = (pd[:, None, None] * ph[None, :, None] * pw[None, None, :]).astype(np.float32)
+    g[g == 0] = gmin
+    return g
+
+
+def _as_ndhwc(pred):
+    pred = pred[0] if isinstance(pred, (tuple, list)) else pred
+    p = pred.float().permute(0, 2, 3, 4, 1)
+    return p if p.is_contiguous() else p.contiguous()
+
+
+def predict_sliding(args, net_list, image, tile_size, classes, task_id, tta=False):
+    """Reference evaluate_amos.py:198-279. Returns full_probs [N, classes, D, H, W] as a device fp32 tensor (the
+    reference returns a float64 CPU tensor)."""
+    from u3d import _lib
+    dev = next(net_list[0].parameters()).device
+    img_all = torch.as_tensor(image).to(device=dev, dtype=torch.float32)
+    ops.require_device(img_all)
+    image_size = img_all.shape
+    overlap = 1 / 4
+    strideHW = math.ceil(tile_size[1] * (1 - overlap))
+    strideD = math.ceil(tile_size[0] * (1 - overlap))
+    tile_deps = int(math.ceil((image_size[2] - tile_size[0]) / strideD) + 1)
+    tile_rows = int(math.ceil((image_size[3] - tile_size[1]) / strideHW) + 1)
+    tile_cols = int(math.ceil((image_size[4] - tile_size[2]) / strideHW) + 1)
+    N, D, H, W = image_size[0], image_size[2], image_size[3], image_size[4]
+    full = torch.zeros((N, classes, D, H, W), dtype=torch.float32, device=dev)
+    count = torch.zeros((N, D, H, W), dtype=torch.float32, device=dev)
+    (pd, ph, pw), gmin = _gaussian_profiles(tile_size)
+    gd, gh, gw = (torch.tensor(p, dtype=torch.float32, device=dev) for p in (pd, ph, pw))
+    flip_sets = [()] + ([(2,), (3,), (4,), (2, 3), (2, 4), (3, 4), (2, 3, 4)] if tta else [])
+    scale = 1.0 / (len(net_list) * len(flip_sets))
+    for dep in range(tile_deps):
+        for row in range(tile_rows):
+            for col in range(tile_cols):
+                d1, x1, y1 = int(dep * strideD), int(col * strideHW), int(row * strideHW)
+                d2 = min(d1 + tile_size[0], D)
+                x2 = min(x1 + tile_size[2], W)
+                y2 = min(y1 + tile_size[1], H)
+                d1, x1, y1 = max(int(d2 - tile_size[0]), 0), max(int(x2 - tile_size[2]), 0), max(int(y2 - tile_size[1]), 0)
+                img = img_all[:, :, d1:d2, y1:y2, x1:x2].contiguous()
+                first = 1
+                for dims in flip_sets:
+                    inp = torch.flip(img, dims) if dims else img
+                    flags = sum({2: 1, 3: 2, 4: 4}[d] for d in dims)
+                    for net in net_list:
+                        p = _as_ndhwc(net(inp, task_id))
+                        if p.shape[-1] != classes or tuple(p.shape[1:4]) != (d2 - d1, y2 - y1, x2 - x1):
+                            raise ValueError(f"predict_sliding: prediction {tuple(p.shape)} does not match the tile "
+                                             f"({d2 - d1}, {y2 - y1}, {x2 - x1}) x {classes} classes")
+                        _lib.call("u3d_window_accumulate", p.data_ptr(), N, classes, d2 - d1, y2 - y1, x2 - x1,
+                                  gd.data_ptr(), gh.data_ptr(), gw.data_ptr(), float(gmin), float(scale),
+                                  full.data_ptr(), count.data_ptr(), D, H, W, d1, y1, x1, flags, first, ops._stream())
+                        first = 0
+    _lib.call("u3d_window_normalize", full.data_ptr(), count.data_ptr(), N, classes, D * H * W, ops._stream())
+    return full

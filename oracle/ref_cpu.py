@@ -190,6 +190,35 @@ def gaussian_map(patch_size, sigma_scale=1.0 / 8):
     return g
 
 
+def predict_sliding(pred_fn, image, tile_size, classes, tta=False):
+    """predict_sliding, evaluate_amos.py:198-279, in float64 numpy. ``pred_fn(tile) -> [N, classes, td, th, tw]``
+    stands for multi_net (:207-217: the mean over the nets, computed by the caller). Tiling, clamping, the flip
+    TTA average, the Gaussian weighting of each tile and full /= count follow the reference line by line."""
+    g = gaussian_map(tile_size)
+    N, _, D, H, W = image.shape
+    overlap = 1 / 4
+    sHW = math.ceil(tile_size[1] * (1 - overlap))
+    sD = math.ceil(tile_size[0] * (1 - overlap))
+    nd = int(math.ceil((D - tile_size[0]) / sD) + 1)
+    nr = int(math.ceil((H - tile_size[1]) / sHW) + 1)
+    nc = int(math.ceil((W - tile_size[2]) / sHW) + 1)
+    full = np.zeros((N, classes, D, H, W))
+    count = np.zeros((N, classes, D, H, W))
+    flips = [()] + ([(2,), (3,), (4,), (2, 3), (2, 4), (3, 4), (2, 3, 4)] if tta else [])
+    for dep in range(nd):
+        for row in range(nr):
+            for col in range(nc):
+                d1, x1, y1 = int(dep * sD), int(col * sHW), int(row * sHW)
+                d2, x2, y2 = min(d1 + tile_size[0], D), min(x1 + tile_size[2], W), min(y1 + tile_size[1], H)
+                d1, x1, y1 = max(d2 - tile_size[0], 0), max(x2 - tile_size[2], 0), max(y2 - tile_size[1], 0)
+                img = image[:, :, d1:d2, y1:y2, x1:x2]
+                pred = sum(np.flip(pred_fn(np.ascontiguousarray(np.flip(img, f))), f) if f else pred_fn(img)
+                           for f in flips) / len(flips)
+                count[:, :, d1:d2, y1:y2, x1:x2] += g
+                full[:, :, d1:d2, y1:y2, x1:x2] += pred * g
+    return full / count
+
+
 def params_from_module_dict(sd):
     return {k: v.detach().float().cpu() for k, v in sd.items()}
 

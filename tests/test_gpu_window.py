@@ -1,0 +1,80 @@
+"""Sliding-window inference: evaluate_amos.predict_sliding (device accumulation through
+u3d_window_accumulate / u3d_window_normalize) against the float64 restatement oracle.ref_cpu.predict_sliding of
+reference evaluate_amos.py:198-279, on the same per-tile network outputs."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu as O
+
+pytestmark = pytest.mark.gpu
+
+WIN_TOL = 2e-5   # fp32 device accumulation vs the reference's float64 host accumulation (relative to max |logit|)
+
+
+class _RampNet(torch.nn.Module):
+    """Position-dependent (so flip bugs show) deterministic stand-in: out[:, c] = x * ramp_c + 0.1 c."""
+
+    def __init__(self, classes, k=1.0):
+        super().__init__()
+        self.k = torch.nn.Parameter(torch.tensor(float(k)))
+        self.classes = classes
+
+    def forward(self, x, task_id=None):
+        d, h, w = x.shape[2:]
+        r = (torch.arange(d, device=x.device).view(d, 1, 1) * 0.37 + torch.arange(h, device=x.device).view(1, h, 1)
+             * 0.11 - torch.arange(w, device=x.device).view(1, 1, w) * 0.05)
+        outs = [x[:, 0] * torch.sin(r * (c + 1) * 0.1) * self.k + 0.1 * c for c in range(self.classes)]
+        return torch.stack(outs, 1)
+
+
+def _ref(nets, image, tile, classes, tta):
+    def pred_fn(t):
+        with torch.no_grad():
+            xs = torch.from_numpy(np.ascontiguousarray(t)).float().cuda()
+            outs = [n(xs, None) for n in nets]
+            outs = [o[0] if isinstance(o, (tuple, list)) else o for o in outs]
+            return (sum(outs) / len(outs)).double().cpu().numpy()
+    return O.predict_sliding(pred_fn, image, tile, classes, tta=tta)
+
+
+@pytest.mark.parametrize("shape,tile,tta,nnets", [
+    ((2, 1, 20, 40, 36), (16, 24, 24), False, 1),
+    ((1, 1, 23, 37, 50), (16, 24, 24), True, 2),
+    ((1, 1, 16, 24, 24), (16, 24, 24), True, 1),      # one tile covering the volume
+    ((1, 1, 64, 40, 40), (16, 24, 32), False, 1),     # anisotropic tile, many depth steps
+])
+def test_predict_sliding_ramp(gpu, shape, tile, tta, nnets):
+    import evaluate_amos as E
+    rng = np.random.default_rng(0)
+    image = rng.standard_normal(shape).astype(np.float32)
+    nets = [_RampNet(3, k=1.0 + 0.5 * i).cuda() for i in range(nnets)]
+    with torch.no_grad():
+        out = E.predict_sliding(None, nets, image, list(tile), 3, None, tta=tta)
+    torch.cuda.synchronize()
+    ref = _ref(nets, image, tile, 3, tta)
+    got = out.double().cpu().numpy()
+    assert got.shape == ref.shape
+    assert np.isfinite(got).all()
+    np.testing.assert_allclose(got, ref, atol=WIN_TOL * np.abs(ref).max(), rtol=0)
+
+
+def test_predict_sliding_baseline_model(gpu):
+    """The native UNet3D baseline as the per-tile network, two nets averaged, flip TTA."""
+    import unet3D
+    import evaluate_amos as E
+    from oracle.weights_recipe import apply_recipe
+    nets = []
+    for seed in (0, 1):
+        m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=4, weight_std=True)
+        apply_recipe(m, seed=seed)
+        nets.append(m.cuda().eval())
+    rng = np.random.default_rng(3)
+    image = rng.standard_normal((1, 1, 24, 48, 40)).astype(np.float32)
+    tile = (16, 32, 32)
+    with torch.no_grad():
+        out = E.predict_sliding(None, nets, image, list(tile), 4, None, tta=True)
+        ref = _ref(nets, image, tile, 4, True)
+    got = out.double().cpu().numpy()
+    np.testing.assert_allclose(got, ref, atol=WIN_TOL * np.abs(ref).max(), rtol=0)
+

@@ -156,3 +156,18 @@ def test_g6_gaussian():
     pts = g["pts"]
     np.testing.assert_allclose(m[pts[:, 0], pts[:, 1], pts[:, 2]], g["vals"], rtol=1e-4, atol=1e-12)
     np.testing.assert_allclose(m.min(), g["gmin"], rtol=1e-4)
+
+
+def test_f1_gaussian_product_vs_scipy_and_oracle():
+    """evaluate_amos._get_gaussian (separable factors) vs the oracle and vs scipy.ndimage.gaussian_filter of a
+    centred delta — the reference's own construction (evaluate_amos.py:184-197) — on small odd/even tiles."""
+    import evaluate_amos as E
+    from scipy.ndimage import gaussian_filter
+    for ts in [(16, 24, 24), (17, 30, 22), (9, 8, 13)]:
+        tmp = np.zeros(ts)
+        tmp[tuple(i // 2 for i in ts)] = 1
+        ref = gaussian_filter(tmp, [i / 8 for i in ts], 0, mode="constant", cval=0)
+        ref = (ref / ref.max()).astype(np.float32)
+        ref[ref == 0] = ref[ref != 0].min()
+        np.testing.assert_allclose(O.gaussian_map(ts), ref, rtol=1e-6, atol=0)
+        np.testing.assert_allclose(E._get_gaussian(ts), ref, rtol=1e-6, atol=0)
