@@ -1,0 +1,67 @@
+"""Inference benchmark for BASELINE.json configs[4]: evaluate_amos.predict_sliding over one 1x256x512x512 volume,
+tile 64x192x192, overlap 1/4 (80 tiles, evaluate_amos.py:211-221), the 16-organ unet3D_baseline trunk, forward
+only, bf16 activations (the config names fp16; the native path computes bf16 with fp32 accumulation), device
+Gaussian accumulation. Prints one JSON line: volume voxels/s, per-tile ms and the conv-stack MFMA fraction
+(1025.7 GFLOP per tile forward)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "multimodal-pl_amd"), REPO]
+
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0
+GFLOP_PER_TILE = 1025.7
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--volume", type=int, nargs=3, default=[256, 512, 512])
+    p.add_argument("--tile", type=int, nargs=3, default=[64, 192, 192])
+    p.add_argument("--classes", type=int, default=16)
+    p.add_argument("--reps", type=int, default=2)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--tta", action="store_true")
+    a = p.parse_args()
+    import unet3D
+    import evaluate_amos as E
+    from oracle.weights_recipe import apply_recipe
+    dev = torch.device("cuda:0")
+    m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=a.classes, weight_std=True)
+    apply_recipe(m, seed=0)
+    m = m.to(dev).eval()
+    m.compute_dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    g = torch.Generator(device="cpu").manual_seed(0)
+    D, H, W = a.volume
+    vol = ((torch.rand((1, 1, D, H, W), generator=g) * 2000 - 1000).clamp(-325, 325) / 325).to(dev)
+    with torch.no_grad():
+        out = E.predict_sliding(None, [m], vol, a.tile, a.classes, None, tta=a.tta)    # warm-up volume
+        torch.cuda.synchronize()
+        del out
+        ts = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            out = E.predict_sliding(None, [m], vol, a.tile, a.classes, None, tta=a.tta)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+            del out
+    import math
+    sHW, sD = math.ceil(a.tile[1] * 0.75), math.ceil(a.tile[0] * 0.75)
+    tiles = ((math.ceil((D - a.tile[0]) / sD) + 1) * (math.ceil((H - a.tile[1]) / sHW) + 1)
+             * (math.ceil((W - a.tile[2]) / sHW) + 1)) * (8 if a.tta else 1)
+    t = min(ts)
+    gflop = GFLOP_PER_TILE * tiles * (a.tile[0] * a.tile[1] * a.tile[2]) / (64 * 192 * 192)
+    print(json.dumps({"metric": "sliding-window inference voxels/sec (configs[4])", "value": D * H * W / t,
+                      "unit": "voxels/s", "s_per_volume": t, "tiles": tiles, "ms_per_tile": 1e3 * t / tiles,
+                      "dtype": a.dtype, "data": "synthetic CT-like volume, random-init weights",
+                      "conv_tflops": gflop / t / 1e3, "mfma_frac": gflop / t / 1e3 / PEAK_BF16_TFLOPS,
+                      "config": {"workload": "unet3D_baseline(16) predict_sliding", "volume": a.volume,
+                                 "tile": a.tile, "tta": a.tta}}))
+
+
+if __name__ == "__main__":
+    main()
