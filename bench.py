@@ -88,7 +88,8 @@ def dominant_kernel_roofline(device, batch, patch, live=None, reps=20):
     achieved = flops / (ms * 1e-3) / 1e12
     del y
     traffic, tsrc = pmc_traffic(batch, patch)
-    return {"kernel": "conv32_brick_kernel<false> (conv 32->32 3^3 s1 @%d^3, GN+ReLU prologue, residual)" % patch,
+    kname = ops.CONV32_FN.replace("u3d_", "") + "_kernel"
+    return {"kernel": "%s (conv 32->32 3^3 s1 @%d^3, GN+ReLU prologue, residual)" % (kname, patch),
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_source": tsrc, "algorithmic_bytes": 3 * batch * patch ** 3 * 32 * 2,

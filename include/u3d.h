@@ -140,6 +140,13 @@ int u3d_conv32_brick(int flip, const void* x, int n, int d, int h, int w, const 
                      const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
                      u3d_stream_t stream);
 
+/* Same operation and arguments as u3d_conv32_brick, depth-streaming schedule (conv_ring.hip): a workgroup walks
+ * a range of output planes down d through a 4-plane LDS ring (each input plane staged once, staging overlapped
+ * with the MFMAs, one barrier per plane). Any n, d, h, w. */
+int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
+                    const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
+                    u3d_stream_t stream);
+
 /* bf16 3^3 stride-1 conv for any cin/cout (multiples of 8) in halo-brick form: 4x8x16-voxel bricks x 64-channel
  * co tiles, 32-channel input chunks staged once per brick (GN+ReLU prologue), weights streamed per tap plane.
  * flip/wpk as u3d_conv32_brick (for flip=1, cin/cout are the data-gradient's input/output channels). */

@@ -44,6 +44,19 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) short s16x2;
+
+// two floats -> packed bf16 pair (lo = a), one v_cvt_pk_bf16_f32 (round to nearest even)
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2_t));
+}
+// max(x, 0) of both bf16 halves (v_pk_max_i16)
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t u) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0}));
+}
+
 // 16-byte vector of T: 8 bf16 or 4 f32.
 template <typename T> struct Vec16 { static constexpr int N = 16 / sizeof(T); };
 
@@ -70,8 +83,7 @@ __device__ __forceinline__ void store16(T* p, const float (&v)[Vec16<T>::N]) {
     for (int i = 0; i < 4; ++i) r[i] = __float_as_uint(v[i]);
   } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      r[i] = (uint32_t)from_f<bf16>(v[2 * i]) | ((uint32_t)from_f<bf16>(v[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) r[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
   }
   *reinterpret_cast<u32x4*>(p) = r;
 }
@@ -96,18 +108,16 @@ __device__ __forceinline__ void storev(T* p, const float (&v)[N]) {
   }
 }
 
-typedef __attribute__((ext_vector_type(2))) float f32x2;
-
-// GroupNorm apply + ReLU on 8 packed bf16 channels: relu(x * sc + sh), two-wide packed fp32 math
+// GroupNorm apply + ReLU on 8 packed bf16 channels: relu(x * sc + sh), two-wide packed fp32 math, one
+// v_cvt_pk_bf16_f32 (RNE) per pair and the ReLU on the packed bf16 pair as a signed 16-bit max (v_pk_max_i16:
+// a negative bf16 has its sign bit set; rounding preserves the sign, so relu(round(x)) == round(relu(x)))
 __device__ __forceinline__ u32x4 gn_relu8(u32x4 v, const f32x2 (&sc)[4], const f32x2 (&sh)[4]) {
   u32x4 o;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     f32x2 f = {__uint_as_float(v[e] << 16), __uint_as_float(v[e] & 0xffff0000u)};
     f = f * sc[e] + sh[e];
-    f[0] = fmaxf(f[0], 0.f);
-    f[1] = fmaxf(f[1], 0.f);
-    o[e] = (uint32_t)from_f<bf16>(f[0]) | ((uint32_t)from_f<bf16>(f[1]) << 16);
+    o[e] = relu_bf16x2(pack_bf16x2(f[0], f[1]));
   }
   return o;
 }

@@ -1,0 +1,342 @@
+// 32 -> 32 channel 3^3 stride-1 convolution (forward and data gradient), bf16, depth-streaming ring form
+// (gfx950). Same contract as conv32_brick (u3d_conv32_brick), different schedule:
+//
+//   * a persistent workgroup (8 waves) owns a contiguous range of OUTPUT PLANES in (column, d) order, a column
+//     being (n, 8-row h tile, 32-voxel w tile); it walks down d, so each input plane (10 x 34 halo rows x 32
+//     ch) is staged once and used by three output planes (the brick form staged 4 input planes per 2 outputs);
+//   * LDS keeps a ring of 4 staged planes: output plane z is computed from the three slots holding z-1, z,
+//     z+1 while the fourth slot receives the next plane, so staging (global loads one step ahead in
+//     registers, GroupNorm + ReLU applied once per element, LDS writes issued between the MFMAs) overlaps the
+//     MFMAs and each output plane costs ONE barrier;
+//   * the weights of all 27 taps stay in LDS (55 KB), the first KR k16 steps' weights also in registers;
+//   * the MFMA is issued transposed (A = weights, B = input rows): a lane's accumulators are 16 output
+//     channels of ONE voxel, so after one permlane32 swap every lane stores two 16-B chunks straight from
+//     registers (no LDS epilogue tile), and the residual is added in the same layout.
+// Data gradient = the same kernel with the flipped tap offsets and the [t][ci][co] weight pack.
+// Reference: F.conv3d in Conv3d.forward (unet3D.py:27) via NoBottleneck (:56-73) and its autograd.
+#include <cstdlib>
+#include <type_traits>
+
+#include "common.h"
+
+namespace u3d {
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+constexpr int RG_BH = 8, RG_BW = 32, RG_HH = RG_BH + 2, RG_HW = RG_BW + 2;
+constexpr int RG_NR = RG_HH * RG_HW;                 // 340 halo rows per plane
+constexpr int RG_PS = RG_NR * 16;                    // chunk-plane stride: 1360 dwords = 16 mod 64 banks
+constexpr int RG_SS = 4 * RG_PS;                     // ring slot stride
+constexpr int RG_NT = 512;
+constexpr int RG_LD = (RG_NR * 4 + RG_NT - 1) / RG_NT;  // 3 staged 16-B pieces per thread and plane
+constexpr int RG_NWR = 27 * 32;                      // weight rows (t, co)
+
+struct RGGeom {
+  int n, d, h, w;
+  int nbh, nbw;
+  long long planes;  // output planes = n * nbh * nbw * d
+  long long xbytes;  // bytes of x (and of the residual / y): < 2^31, the buffer-offset range
+  int per;           // output planes per workgroup
+  int gn_groups;
+};
+
+// One staged input plane: column (n, h0, w0), input depth zin (-1 / d = zero padding), and whether it is the
+// third plane of a triple (output zin - 1 follows it).
+struct RGPlane {
+  int n, h0, w0, zin;
+  bool valid, out;
+};
+
+// Walks the workgroup's output range [o, o_end) as a sequence of input planes: each maximal run of outputs
+// z0..z1-1 inside one column stages zin = z0-1 .. z1.
+struct RGWalk {
+  long long o_next, o_end;
+  int col, zin, zfirst, zlast;
+  bool done;
+  __device__ void start_run(const RGGeom& g) {
+    if (o_next >= o_end) { done = true; return; }
+    col = (int)(o_next / g.d);
+    zfirst = (int)(o_next - (long long)col * g.d);
+    zlast = (int)min<long long>(g.d, zfirst + (o_end - o_next));
+    o_next += zlast - zfirst;
+    zin = zfirst - 1;
+  }
+  __device__ RGPlane next(const RGGeom& g) {
+    RGPlane p{};
+    if (!done && zin > zlast) start_run(g);
+    if (done) return p;
+    int c = col;
+    const int bw_ = c % g.nbw; c /= g.nbw;
+    const int bh_ = c % g.nbh;
+    p.n = c / g.nbh;
+    p.h0 = bh_ * RG_BH;
+    p.w0 = bw_ * RG_BW;
+    p.zin = zin;
+    p.valid = true;
+    p.out = zin >= zfirst + 1;
+    ++zin;
+    return p;
+  }
+};
+
+template <bool FLIP, bool GN, bool RES, int KR>
+__global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
+                                                              bf16* __restrict__ y, const bf16* __restrict__ res,
+                                                              const float* __restrict__ gstat,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, RGGeom g) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024];
+  char* const ring = smem;
+  char* const wts = smem + 4 * RG_SS;
+  char* const junk = wts + 4 * RG_NWR * 16;  // target of the staging lanes past the plane's last row
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int ch = tid & 3;  // staging: fixed 8-channel chunk per thread (4 threads = one voxel's 64 B)
+
+  // XCD-aware range order: XCD x (= blockIdx % 8) runs a contiguous eighth of the output planes, so the
+  // columns it works on at a time are neighbours whose halo rows meet in its L2.
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  RGWalk walk{};
+  walk.o_next = (long long)bid * g.per;
+  walk.o_end = min(g.planes, walk.o_next + g.per);
+  walk.done = false;
+  walk.zin = 1;
+  walk.zlast = 0;  // forces start_run on the first next()
+
+  for (int i = tid; i < RG_NWR * 4; i += RG_NT) {  // weights: plane c, row t*32 + co
+    const int c = i / RG_NWR, row = i % RG_NWR;
+    *reinterpret_cast<u32x4*>(wts + (c * RG_NWR + row) * 16) = *reinterpret_cast<const u32x4*>(wpk + row * 32 + c * 8);
+  }
+  // k16 step st = (tap t = st >> 1, half s = st & 1): this lane's weight fragment is W[t][co = r][16s + 8h ..]
+  bf16x8 wreg[KR > 0 ? KR : 1];
+#pragma unroll
+  for (int st = 0; st < KR; ++st)
+    wreg[st] = *reinterpret_cast<const bf16x8*>(wpk + ((st >> 1) * 32 + r) * 32 + (st & 1) * 16 + 8 * h);
+
+  // buffer loads: out-of-range offsets return zeros with no branch around the load (no exec-masked paths whose
+  // merge would make the wait-count insertion pessimistic)
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)g.xbytes, 0x00020000);
+  const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, RES ? (int)g.xbytes : 0, 0x00020000);
+  f32x2 sc[4], sh[4];
+  int gn_n = -1;
+  // branch-free staging: out-of-volume rows load a valid dummy address and are zeroed when written
+  auto load_plane = [&](const RGPlane& p, u32x4 (&v)[RG_LD], unsigned& m) {
+    m = 0;
+#pragma unroll
+    for (int i = 0; i < RG_LD; ++i) {
+      const int row = (tid >> 2) + i * (RG_NT / 4);
+      const int hw = row % RG_HW, hh = row / RG_HW;
+      const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
+      const bool ok = p.valid && row < RG_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
+                      (unsigned)zw < (unsigned)g.w;
+      const unsigned off = ok ? (unsigned)((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * 64 + ch * 16) : 0xFFFFFFF0u;
+      v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      m |= (ok ? 1u : 0u) << i;
+    }
+  };
+  auto gn_table = [&](const RGPlane& p) {
+    if (GN && p.valid && p.n != gn_n) {
+      gn_n = p.n;
+      gn_coef8(gstat, gamma, beta, g.gn_groups, 32, p.n, ch * 8, sc, sh);
+    }
+  };
+  auto write_piece = [&](int i, const u32x4& v, unsigned m, int slot) {
+    const int row = (tid >> 2) + i * (RG_NT / 4);
+    u32x4 val = v;
+    if constexpr (GN) val = gn_relu8(v, sc, sh);
+    if constexpr (GN) if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
+    char* dst = row < RG_NR ? ring + slot * RG_SS + ch * RG_PS + row * 16 : junk + (tid & 63) * 16;
+    *reinterpret_cast<u32x4*>(dst) = val;
+  };
+
+  // A computed output plane waiting for its epilogue: the epilogue (bf16 pack, permlane swap, residual add,
+  // stores) of plane k runs between the MFMAs of plane k+1, so it is off the per-plane critical path.
+  struct Pending {
+    f32x16 acc;
+    u32x4 rv[2];
+    long long vox;
+    bool ok;
+  };
+  Pending pend;
+  pend.ok = false;
+  pend.vox = 0;
+  auto epilogue = [&](const Pending& p) {
+    // lane (r, h): acc[4q + e] = channel 8q + 4h + e of voxel r. Pack to bf16 pairs, then swap halves so that
+    // lane (r, h) holds channels 8h..8h+7 (pk[0..1]) and 16+8h..16+8h+7 (pk[2..3]).
+    uint32_t pk[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        pk[q][e] = pack_bf16x2(p.acc[4 * q + 2 * e], p.acc[4 * q + 2 * e + 1]);
+#pragma unroll
+    for (int q = 0; q < 4; q += 2)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(pk[q][e], pk[q + 1][e], false, false);
+        pk[q][e] = sw[0];
+        pk[q + 1][e] = sw[1];
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      u32x4 v = {pk[2 * u][0], pk[2 * u][1], pk[2 * u + 1][0], pk[2 * u + 1][1]};
+      if constexpr (RES) {
+        float a[8], c[8];
+        load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
+        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[u]), c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += c[e];
+        store16<bf16>(reinterpret_cast<bf16*>(&v), a);
+      }
+      if (p.ok) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
+    }
+  };
+
+  // output plane from the three slots s0 (z-1), s1 (z), s2 (z+1); the staging writes of the next plane and
+  // the previous plane's epilogue are issued between the MFMAs
+  auto compute = [&](const RGPlane& pc, int s0, int s1, int s2) {
+    const int zo = pc.zin - 1;
+    const int zh = pc.h0 + wave, zw = pc.w0 + r;
+    Pending nw;
+    nw.ok = zh < g.h && zw < g.w;
+    nw.vox = (((long long)pc.n * g.d + zo) * g.h + zh) * g.w + zw;
+    nw.rv[0] = nw.rv[1] = u32x4{0u, 0u, 0u, 0u};
+    if constexpr (RES) {
+      const unsigned ro = nw.ok ? (unsigned)(nw.vox * 64 + 16 * h) : 0xFFFFFFC0u;
+      nw.rv[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
+      nw.rv[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro + 32, 0, 0));
+    }
+    const int sl[3] = {FLIP ? s2 : s0, s1, FLIP ? s0 : s2};
+    const char* abase = ring + h * RG_PS + (wave * RG_HW + r) * 16;
+    const char* bbase = wts + (h * RG_NWR + r) * 16;
+    auto aoff = [&](int st) {
+      const int t = st >> 1, s = st & 1;
+      const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
+      const int oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
+      return sl[td] * RG_SS + (oh * RG_HW + ow) * 16 + 2 * s * RG_PS;
+    };
+    auto boff = [](int st) { return (2 * (st & 1) * RG_NWR + (st >> 1) * 32) * 16; };
+#pragma unroll
+    for (int e = 0; e < 16; ++e) nw.acc[e] = 0.f;
+    // fragments in flight: step st's MFMA consumes the reads issued LA steps earlier; one scheduling region
+    // per step (sched_barrier) keeps that order and spreads the staging writes / epilogue over the chain
+    constexpr int LA = 3;
+    bf16x8 fa[LA + 1], fb[LA + 1];
+    auto rd = [&](int st, int k) {
+      fa[k] = *reinterpret_cast<const bf16x8*>(abase + aoff(st));
+      if (st < KR)
+        fb[k] = wreg[st < KR ? st : 0];
+      else
+        fb[k] = *reinterpret_cast<const bf16x8*>(bbase + boff(st));
+    };
+#pragma unroll
+    for (int k = 0; k < LA; ++k) rd(k, k);
+    auto mstep = [&](auto stc) {
+      constexpr int st = decltype(stc)::value;
+      if constexpr (st + LA < 54) rd(st + LA, (st + LA) % (LA + 1));
+      if constexpr (st == 30) epilogue(pend);
+      __builtin_amdgcn_sched_barrier(0);
+      nw.acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[st % (LA + 1)], fa[st % (LA + 1)], nw.acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, 54>(mstep);
+    pend = nw;
+  };
+
+  // step s: load plane s+1 into registers, write plane s (loaded during step s-1) into slot s&3, compute the
+  // output whose triple ends at plane s-1, barrier. Unrolled by two so the register sets swap statically.
+  u32x4 va[RG_LD], vb[RG_LD];
+  unsigned ma = 0, mb = 0;
+  RGPlane pw = walk.next(g);  // plane 0
+  load_plane(pw, va, ma);
+  __syncthreads();            // weights visible
+  RGPlane pc{};               // plane s-1 (compute)
+  int s = 0;
+  // The staged plane is written at the start of the step, BEFORE the next plane's loads are issued: its loads
+  // (a full step old) are then the oldest in flight, so no wait inside the MFMA chain can fall on a young load.
+  auto step = [&](u32x4 (&cur)[RG_LD], unsigned& mcur, u32x4 (&nxt)[RG_LD], unsigned& mnxt) {
+    gn_table(pw);
+    const int slot = s & 3;
+    if (pw.valid) {
+#pragma unroll
+      for (int i = 0; i < RG_LD; ++i) write_piece(i, cur[i], mcur, slot);
+    }
+    const RGPlane pl = walk.next(g);  // plane s+1
+    load_plane(pl, nxt, mnxt);
+    if (pc.valid && pc.out) compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3);
+    __syncthreads();
+    pc = pw;
+    pw = pl;
+    ++s;
+  };
+  while (pw.valid || (pc.valid && pc.out)) {
+    step(va, ma, vb, mb);
+    if (!(pw.valid || (pc.valid && pc.out))) break;
+    step(vb, mb, va, ma);
+  }
+  epilogue(pend);  // the last computed plane (ok = false if none)
+}
+
+}  // namespace u3d
+
+using namespace u3d;
+
+static int ring_kr(int dflt) {  // U3D_RING_KR=0: no weight steps in registers (experiments)
+  static const int kr = [] {
+    const char* e = getenv("U3D_RING_KR");
+    return e ? atoi(e) : -1;
+  }();
+  return kr < 0 ? dflt : kr;
+}
+
+extern "C" int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
+                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                               const void* residual, void* y, u3d_stream_t stream) {
+  U3D_REQUIRE(x && wpk && y && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv32_ring: bad args");
+  U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0), "conv32_ring: bad GN");
+  RGGeom g{};
+  g.n = n; g.d = d; g.h = h; g.w = w;
+  g.nbh = cdiv(h, RG_BH); g.nbw = cdiv(w, RG_BW);
+  g.planes = (long long)n * g.nbh * g.nbw * d;
+  g.xbytes = (long long)n * d * h * w * 64;
+  U3D_REQUIRE(g.xbytes < (1LL << 31), "conv32_ring: tensor of %lld bytes beyond the 2 GiB buffer-offset range",
+              g.xbytes);
+  long long grid = std::min<long long>(256, g.planes);
+  g.per = (int)((g.planes + grid - 1) / grid);
+  grid = (g.planes + g.per - 1) / g.per;
+  g.gn_groups = gn_groups;
+  hipStream_t s = (hipStream_t)stream;
+#define RG_LAUNCH(F, G, R, K)                                                                                  \
+  hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K>), dim3((unsigned)grid), dim3(RG_NT), 0, s, (const bf16*)x, \
+                     (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g)
+#define RG_KR(F, G, R, K)                  \
+  do {                                     \
+    if (kr) RG_LAUNCH(F, G, R, K);         \
+    else RG_LAUNCH(F, G, R, 0);            \
+  } while (0)
+  U3D_REQUIRE(!(flip && (gn_stats || residual)), "conv32_ring: the data gradient takes no prologue / residual");
+  // register budget (2 waves per SIMD): the GroupNorm variants hold 16 weight steps, the others 27
+  const bool kr = ring_kr(1) != 0;
+  if (flip) RG_KR(true, false, false, 27);
+  else if (gn_stats && residual) RG_KR(false, true, true, 16);
+  else if (gn_stats) RG_KR(false, true, false, 16);
+  else if (residual) RG_KR(false, false, true, 27);
+  else RG_KR(false, false, false, 27);
+#undef RG_KR
+#undef RG_LAUNCH
+  return check_launch("conv32_ring_kernel");
+}

@@ -146,7 +146,7 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
     od, oh, ow = out_dim(d, k, stride), out_dim(h, k, stride), out_dim(w_, k, stride)
     y = torch.empty((n, od, oh, ow, cout), dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
     st, ga, be, G = gn if gn is not None else (None, None, None, 0)
-    if _use_conv32(x.dtype, cin, cout, k, stride, n, w_) and not out_f32 and bias is None:
+    if _use_conv32(x.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(x) and not out_f32 and bias is None:
         probe = PROBE is not None
         if probe:  # bench.py: HIP events around the dominant kernel, on the stream it runs on
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -181,12 +181,17 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
 SPLITK_WS_BYTES = 64 << 20
 PROBE = None  # list -> conv32_brick forward launches record (start, end, voxels) HIP events (bench.py roofline)
 USE_CONV32_BRICK = True
-CONV32_FN = "u3d_conv32_brick"
+CONV32_FN = "u3d_conv32_ring"   # "u3d_conv32_brick": the earlier halo-brick schedule (same results)
 
 
 def _use_conv32(dtype, cin, cout, k, stride, n, w=32):
-    return USE_CONV32_BRICK and dtype == torch.bfloat16 and cin == 32 and cout == 32 and k == 3 and stride == 1 \
-        and n <= 16 and w % 32 == 0
+    if not (USE_CONV32_BRICK and dtype == torch.bfloat16 and cin == 32 and cout == 32 and k == 3 and stride == 1):
+        return False
+    return CONV32_FN == "u3d_conv32_ring" or (n <= 16 and w % 32 == 0)
+
+
+def _conv32_fits(x):
+    return CONV32_FN != "u3d_conv32_ring" or x.numel() * x.element_size() < (1 << 31)  # 32-bit buffer offsets
 
 
 USE_SMALL_CONV = True
@@ -217,7 +222,7 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     n, d, h, w_ = in_shape
     cout = dy.shape[-1]
     dx = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
-    if _use_conv32(dy.dtype, cin, cout, k, stride, n, w_):
+    if _use_conv32(dy.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(dy):
         call(CONV32_FN, 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
              dx.data_ptr(), _stream())
         return dx

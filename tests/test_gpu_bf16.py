@@ -48,7 +48,7 @@ SHAPES = [(2, 32, 32, (12, 10, 16), 1), (1, 32, 32, (5, 9, 70), 1), (1, 32, 64, 
           (1, 256, 256, (6, 6, 6), 2), (1, 40, 48, (6, 10, 14), 2)]
 
 
-@pytest.fixture(params=["auto", "gen_brick", "igemm", "small"])
+@pytest.fixture(params=["auto", "gen_brick", "igemm", "small", "ring", "brick32"])
 def conv_path(request):
     """auto = production routing; gen_brick = force the generic halo-brick kernel; igemm = force implicit GEMM."""
     from u3d import ops
@@ -60,6 +60,10 @@ def conv_path(request):
         ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK, ops.USE_SMALL_CONV = False, False, False, False
     elif request.param == "small":
         ops.USE_CONV32_BRICK, ops.SMALL_MAX_VOX = False, 1 << 40
+    elif request.param == "ring":
+        ops.CONV32_FN, ops.USE_SMALL_CONV = "u3d_conv32_ring", False
+    elif request.param == "brick32":
+        ops.CONV32_FN, ops.USE_SMALL_CONV = "u3d_conv32_brick", False
     yield request.param
     (ops.BRICK_MIN_WG, ops.USE_CONV32_BRICK, ops.USE_GEN_BRICK, ops.USE_S2_BRICK, ops.USE_SMALL_CONV,
      ops.SMALL_MAX_VOX, ops.CONV32_FN) = saved
