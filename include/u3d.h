@@ -147,6 +147,14 @@ int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int w, const v
                     const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
                     u3d_stream_t stream);
 
+/* Stride-1 3^3 weight gradient, depth-streaming ring schedule (wgrad_ring.hip): same partial-slab contract as
+ * u3d_conv_wgrad_brick ([nsplit][27][cout_p][cin_p] fp32, summed by the caller in fixed order); a split is a
+ * contiguous range of 16x16-voxel output planes walked down d. */
+int u3d_conv_wgrad_ring_splits(int n, int cin, int d, int h, int w, int cout);
+int u3d_conv_wgrad_ring(const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout,
+                        const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                        float* partials, int nsplit, u3d_stream_t stream);
+
 /* bf16 3^3 stride-1 conv for any cin/cout (multiples of 8) in halo-brick form: 4x8x16-voxel bricks x 64-channel
  * co tiles, 32-channel input chunks staged once per brick (GN+ReLU prologue), weights streamed per tap plane.
  * flip/wpk as u3d_conv32_brick (for flip=1, cin/cout are the data-gradient's input/output channels). */

@@ -1,0 +1,323 @@
+// Weight gradient of the 3^3 stride-1 convolutions, depth-streaming ring form (gfx950).
+//
+//   dW[t][co][ci] = sum_{n, q} dy[n, q, co] * A[n, q + t - 1, ci],   A = relu(gn(x)) (prologue)
+//
+// Same contract as u3d_conv_wgrad_brick (fp32 partial slabs [split][27][cout_p][cin_p]), different schedule:
+//   * workgroup = one (32 co) x (32 ci) tile x a contiguous range of OUTPUT PLANES in (column, d) order, a
+//     column being (n, 16-row h tile, 16-voxel w tile); it walks down d, so each input plane (18 x 18 halo
+//     rows) is staged once for three output planes, and each dy plane once;
+//   * LDS: a ring of 4 input planes + 2 dy planes, rows channel-contiguous (64 B); the plane written at a step
+//     start (GroupNorm + ReLU applied once per element) is the one loaded a full step earlier, the next
+//     plane's loads then fly under the MFMAs; one barrier per output plane;
+//   * k = the 256 voxels of an output plane, 16 per MFMA (one 16-voxel w row): both operands are read
+//     transposed (ds_read_b64_tr_b16), every lane addressing its own (shifted) row, so the 27 tap windows
+//     come from the same staged planes with no data movement; wave w owns taps w, w+8, w+16 (, w+24) and
+//     shares its dy fragment between them.
+// Reference: autograd of F.conv3d in Conv3d.forward (unet3D.py:27).
+#include <type_traits>
+
+#include "common.h"
+
+namespace u3d {
+namespace {
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+__device__ __forceinline__ v4i16 trd(const char* lds_base, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4i16*)((__attribute__((address_space(3))) char*)lds_base + byte_off));
+}
+__device__ __forceinline__ bf16x8 frag2(v4i16 lo, v4i16 hi) {
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  v8i16 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+template <int I, int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<I + 1, N>(f);
+  }
+}
+
+constexpr int WR_PH = 16, WR_PW = 16, WR_HH = WR_PH + 2, WR_HW = WR_PW + 2;
+constexpr int WR_NR = WR_HH * WR_HW;  // 324 halo rows per input plane
+constexpr int WR_NV = WR_PH * WR_PW;  // 256 voxels per output plane = 16 k16 steps
+constexpr int WR_ROWB = 64;
+constexpr int WR_SLOT = WR_NR * WR_ROWB;
+constexpr int WR_DSLOT = WR_NV * WR_ROWB;
+constexpr int WR_NT = 512;
+constexpr int WR_LX = (WR_NR * 4 + WR_NT - 1) / WR_NT;  // 3 input pieces per thread and plane
+constexpr int WR_LY = WR_NV * 4 / WR_NT;                // 2 dy pieces
+
+struct WRGeom {
+  int n, d, h, w, cin, cout, cin_p, cout_p;
+  int nbh, nbw;
+  long long planes;  // output planes per channel tile = n * nbh * nbw * d
+  int per;           // output planes per split
+  int gn_groups;
+  long long xbytes, ybytes;
+};
+
+struct WRPlane {
+  int n, h0, w0, zin;
+  bool valid, out;
+};
+
+struct WRWalk {
+  long long o_next, o_end;
+  int col, zin, zfirst, zlast;
+  bool done;
+  __device__ void start_run(const WRGeom& g) {
+    if (o_next >= o_end) { done = true; return; }
+    col = (int)(o_next / g.d);
+    zfirst = (int)(o_next - (long long)col * g.d);
+    zlast = (int)min<long long>(g.d, zfirst + (o_end - o_next));
+    o_next += zlast - zfirst;
+    zin = zfirst - 1;
+  }
+  __device__ WRPlane next(const WRGeom& g) {
+    WRPlane p{};
+    if (!done && zin > zlast) start_run(g);
+    if (done) return p;
+    int c = col;
+    const int bw_ = c % g.nbw; c /= g.nbw;
+    const int bh_ = c % g.nbh;
+    p.n = c / g.nbh;
+    p.h0 = bh_ * WR_PH;
+    p.w0 = bw_ * WR_PW;
+    p.zin = zin;
+    p.valid = true;
+    p.out = zin >= zfirst + 1;
+    ++zin;
+    return p;
+  }
+};
+
+}  // namespace
+
+template <bool GN>
+__global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                             const float* __restrict__ gstat,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, float* __restrict__ part,
+                                                             WRGeom g) {
+  __shared__ __attribute__((aligned(16))) char lds[4 * WR_SLOT + 2 * WR_DSLOT + 1024];
+  char* const ring = lds;
+  char* const dyr = lds + 4 * WR_SLOT;
+  char* const junk = dyr + 2 * WR_DSLOT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = tid & 3;
+  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * 32;
+  int split = blockIdx.z;
+  if (gridDim.x * gridDim.y == 1) {  // XCD-aware: XCD x runs a contiguous eighth of the plane ranges
+    const int nwg = gridDim.z, q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.z & 7, loc = blockIdx.z >> 3;
+    split = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  WRWalk walk{};
+  walk.o_next = (long long)split * g.per;
+  walk.o_end = min(g.planes, walk.o_next + g.per);
+  walk.done = false;
+  walk.zin = 1;
+  walk.zlast = 0;
+
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)g.xbytes, 0x00020000);
+  const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)dy, 0, (int)g.ybytes, 0x00020000);
+  f32x2 sc[4], sh[4];
+  int gn_n = -1;
+  const bool cok = ci0 + ch * 8 < g.cin, dok = co0 + ch * 8 < g.cout;
+
+  auto load_plane = [&](const WRPlane& p, u32x4 (&vx)[WR_LX], u32x4 (&vy)[WR_LY], unsigned& m) {
+    m = 0;
+#pragma unroll
+    for (int i = 0; i < WR_LX; ++i) {
+      const int row = (tid >> 2) + i * (WR_NT / 4);
+      const int hw = row % WR_HW, hh = row / WR_HW;
+      const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
+      const bool ok = p.valid && cok && row < WR_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
+                      (unsigned)zw < (unsigned)g.w;
+      const unsigned off =
+          ok ? (unsigned)(((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * g.cin + ci0 + ch * 8) * 2) : 0xFFFFFFF0u;
+      vx[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      m |= (ok ? 1u : 0u) << i;
+    }
+#pragma unroll
+    for (int i = 0; i < WR_LY; ++i) {
+      const int v = (tid >> 2) + i * (WR_NT / 4);
+      const int zh = p.h0 + v / WR_PW, zw = p.w0 + v % WR_PW, zo = p.zin - 1;
+      const bool ok = p.valid && p.out && dok && zh < g.h && zw < g.w;
+      const unsigned off =
+          ok ? (unsigned)(((((p.n * g.d + zo) * g.h + zh) * g.w + zw) * g.cout + co0 + ch * 8) * 2) : 0xFFFFFFF0u;
+      vy[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0));
+    }
+  };
+  auto write_plane = [&](const WRPlane& p, const u32x4 (&vx)[WR_LX], const u32x4 (&vy)[WR_LY], unsigned m, int slot,
+                         int dslot) {
+    if (GN && p.n != gn_n) {
+      gn_n = p.n;
+      gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, p.n, ci0 + ch * 8, sc, sh);
+    }
+#pragma unroll
+    for (int i = 0; i < WR_LX; ++i) {
+      const int row = (tid >> 2) + i * (WR_NT / 4);
+      u32x4 val = vx[i];
+      if constexpr (GN) {
+        val = gn_relu8(val, sc, sh);
+        if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
+      }
+      char* dst = row < WR_NR ? ring + slot * WR_SLOT + row * WR_ROWB + ch * 16 : junk + (tid & 63) * 16;
+      *reinterpret_cast<u32x4*>(dst) = val;
+    }
+    if (p.out) {
+#pragma unroll
+      for (int i = 0; i < WR_LY; ++i) {
+        const int v = (tid >> 2) + i * (WR_NT / 4);
+        *reinterpret_cast<u32x4*>(dyr + dslot * WR_DSLOT + v * WR_ROWB + ch * 16) = vy[i];
+      }
+    }
+  };
+
+  constexpr int MAXT = 4;  // taps per wave: t = wave + 8j
+  f32x16 acc[MAXT];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+  int tap_row[MAXT], tap_d[MAXT];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    const int t = min(wave + 8 * j, 26);
+    tap_d[j] = t / 9;
+    tap_row[j] = (((t / 3) % 3) * WR_HW + t % 3) * WR_ROWB;
+  }
+  const int ntap = (27 - wave + 7) / 8;  // 4 for waves 0-2, 3 for 3-7
+  // fragment lane geometry: group gq = lane>>4, in-group lane i = lane&15 -> (q = i>>2, p = i&3)
+  const int hh = lane >> 5, gq = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int colb = (16 * (gq & 1) + 4 * pp) * 2;
+  int lrow[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) lrow[m] = (8 * hh + 4 * m + q) * WR_ROWB + colb;  // voxel k of a 16-voxel row
+
+  auto compute = [&](int dslot, int s0, int s1, int s2, auto ntc) {
+    constexpr int NTP = decltype(ntc)::value;
+    const int sl[3] = {s0, s1, s2};
+    int tb[NTP];
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) tb[j] = sl[tap_d[j]] * WR_SLOT + tap_row[j];
+    const char* dbase = dyr + dslot * WR_DSLOT;
+    constexpr int LA = GN ? 1 : 2;  // fragment lookahead (k16 steps); the GN variant's registers allow one
+    bf16x8 fa[LA + 1], fb[LA + 1][NTP];
+    auto rd = [&](int ks, int k) {
+      fa[k] = frag2(trd(dbase, ks * WR_PW * WR_ROWB + lrow[0]), trd(dbase, ks * WR_PW * WR_ROWB + lrow[1]));
+#pragma unroll
+      for (int j = 0; j < NTP; ++j)
+        fb[k][j] = frag2(trd(ring, tb[j] + ks * WR_HW * WR_ROWB + lrow[0]),
+                         trd(ring, tb[j] + ks * WR_HW * WR_ROWB + lrow[1]));
+    };
+#pragma unroll
+    for (int k = 0; k < LA; ++k) rd(k, k);
+    __builtin_amdgcn_sched_barrier(0);
+    sfor<0, WR_PH>([&](auto kc) {
+      constexpr int ks = decltype(kc)::value;
+      if constexpr (ks + LA < WR_PH) rd(ks + LA, (ks + LA) % (LA + 1));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NTP; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (LA + 1)], fb[ks % (LA + 1)][j], acc[j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+
+  u32x4 xa[WR_LX], xb[WR_LX], ya[WR_LY], yb[WR_LY];
+  unsigned ma = 0, mb = 0;
+  WRPlane pw = walk.next(g);
+  load_plane(pw, xa, ya, ma);
+  WRPlane pc{};
+  int s = 0;
+  auto step = [&](u32x4 (&cx)[WR_LX], u32x4 (&cy)[WR_LY], unsigned& mc, u32x4 (&nx)[WR_LX], u32x4 (&ny)[WR_LY],
+                  unsigned& mn) {
+    if (pw.valid) write_plane(pw, cx, cy, mc, s & 3, s & 1);
+    const WRPlane pl = walk.next(g);
+    load_plane(pl, nx, ny, mn);
+    if (pc.valid && pc.out) {
+      if (ntap == 4)
+        compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 4>{});
+      else
+        compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 3>{});
+    }
+    __syncthreads();
+    pc = pw;
+    pw = pl;
+    ++s;
+  };
+  while (pw.valid || (pc.valid && pc.out)) {
+    step(xa, ya, ma, xb, yb, mb);
+    if (!(pw.valid || (pc.valid && pc.out))) break;
+    step(xb, yb, mb, xa, ya, ma);
+  }
+  // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h
+  const int r = lane & 31;
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    if (j < ntap) {
+      const int tt = wave + 8 * j;
+      float* pq = part + ((long long)blockIdx.z * 27 + tt) * g.cout_p * g.cin_p;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int co = co0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        pq[(long long)co * g.cin_p + ci0 + r] = acc[j][i];
+      }
+    }
+  }
+}
+
+}  // namespace u3d
+
+using namespace u3d;
+
+static void wr_geom(int n, int cin, int d, int h, int w, int cout, WRGeom& g) {
+  g = WRGeom{};
+  g.n = n; g.d = d; g.h = h; g.w = w; g.cin = cin; g.cout = cout;
+  g.cin_p = round_up(cin, 32); g.cout_p = round_up(cout, 32);
+  g.nbh = cdiv(h, WR_PH); g.nbw = cdiv(w, WR_PW);
+  g.planes = (long long)n * g.nbh * g.nbw * d;
+  g.xbytes = (long long)n * d * h * w * cin * 2;
+  g.ybytes = (long long)n * d * h * w * cout * 2;
+}
+
+extern "C" int u3d_conv_wgrad_ring_splits(int n, int cin, int d, int h, int w, int cout) {
+  WRGeom g;
+  wr_geom(n, cin, d, h, w, cout, g);
+  const long long tiles = (long long)(g.cin_p / 32) * (g.cout_p / 32);
+  const long long want = std::max(1LL, std::min(g.planes, 256 / tiles));
+  const long long per = (g.planes + want - 1) / want;
+  return (int)((g.planes + per - 1) / per);  // every split receives planes: no zero-filled slabs
+}
+
+extern "C" int u3d_conv_wgrad_ring(const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout,
+                                   const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                                   float* partials, int nsplit, u3d_stream_t stream) {
+  U3D_REQUIRE(dy && x && partials && nsplit >= 1 && n >= 1, "wgrad_ring: bad args");
+  U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "wgrad_ring: channels must be multiples of 8");
+  U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "wgrad_ring: bad GN");
+  WRGeom g;
+  wr_geom(n, cin, d, h, w, cout, g);
+  U3D_REQUIRE(g.xbytes < (1LL << 31) && g.ybytes < (1LL << 31), "wgrad_ring: tensors beyond the 2 GiB offset range");
+  g.per = (int)((g.planes + nsplit - 1) / nsplit);
+  g.gn_groups = gn_groups;
+  const int ns_eff = (int)((g.planes + g.per - 1) / g.per);
+  hipStream_t s = (hipStream_t)stream;
+  if (ns_eff < nsplit)  // trailing slabs would stay unwritten
+    U3D_HIP(hipMemsetAsync(partials + (long long)ns_eff * 27 * g.cout_p * g.cin_p, 0,
+                           (size_t)(nsplit - ns_eff) * 27 * g.cout_p * g.cin_p * 4, s));
+  dim3 grid(g.cin_p / 32, g.cout_p / 32, ns_eff);
+  if (gn_stats)
+    hipLaunchKernelGGL(wgrad_ring_kernel<true>, grid, dim3(WR_NT), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats,
+                       gn_gamma, gn_beta, partials, g);
+  else
+    hipLaunchKernelGGL(wgrad_ring_kernel<false>, grid, dim3(WR_NT), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats,
+                       gn_gamma, gn_beta, partials, g);
+  return check_launch("wgrad_ring_kernel");
+}

@@ -246,6 +246,8 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
 
 
 USE_BRICK_WGRAD = True
+USE_RING_WGRAD = True      # stride-1 3^3 weight gradients: depth-streaming ring kernel (wgrad_ring.hip)
+RING_WGRAD_MIN_HW = 8      # h, w extents below this use the brick kernel (measured faster from 12^3 up)
 USE_S2_BRICK = True  # stride-2 3^3 bf16 data gradient: one-launch parity-merged kernel (dgrad_s2.hip)
 
 
@@ -256,6 +258,15 @@ def conv_wgrad(dy, x, k, stride, gn=None, brick=None):
     st, ga, be, G = gn if gn is not None else (None, None, None, 0)
     if brick is None:
         brick = USE_BRICK_WGRAD and x.dtype == torch.bfloat16
+        if brick and k == 3 and stride == 1 and USE_RING_WGRAD and min(h, w_) >= RING_WGRAD_MIN_HW:
+            brick = "ring"
+    if brick == "ring":
+        assert k == 3 and stride == 1 and x.dtype == torch.bfloat16
+        ns = query("u3d_conv_wgrad_ring_splits", n, cin, d, h, w_, cout)
+        part = torch.empty((ns, 27, round32(cout), round32(cin)), dtype=torch.float32, device=x.device)
+        call("u3d_conv_wgrad_ring", dy.data_ptr(), x.data_ptr(), n, cin, d, h, w_, cout, _ptr(st), _ptr(ga), _ptr(be),
+             G, part.data_ptr(), ns, _stream())
+        return part, ns
     if brick and k == 1:
         ns = query("u3d_conv_wgrad1_splits", n, cin, d, h, w_, cout, stride)
         part = torch.empty((ns, 1, round32(cout), round32(cin)), dtype=torch.float32, device=x.device)

@@ -73,7 +73,7 @@ def _dgrad(n, cin, cout, s, k, stride):
 
 def _wgrad(n, cin, cout, s, k, stride):
     x, pf, pd, g, r, dy, flop = conv_case(n, cin, cout, s, k, stride, True)
-    us = t_(lambda: ops.conv_wgrad(dy, x, k, stride, g))
+    us = t_(lambda: ops.conv_wgrad(dy, x, k, stride, g, brick={"ring": "ring", "brick": True}.get(os.environ.get("KB_WGRAD", ""))))
     return us, flop
 
 
