@@ -142,12 +142,12 @@ __global__ __launch_bounds__(GT) void gn_stats_kernel(const T* __restrict__ x, R
     for (int e = 0; e < VEC; ++e) shift[e] = to_f(xn[((j * VEC + e) / g.cpg) * g.cpg]);  // x[n, voxel 0, first ch of group]
     const long long v0 = (long long)blk * g.vpb, v1 = std::min<long long>(g.v, v0 + g.vpb);
     long long v = v0 + vl;
-    for (; v + 3 * g.vlanes < v1; v += 4 * g.vlanes) {  // 4 loads in flight per thread
-      float xv[4][VEC];
+    for (; v + 7 * g.vlanes < v1; v += 8 * g.vlanes) {  // 8 loads (64 KB per CU) in flight: HBM latency hidden
+      float xv[8][VEC];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) load16<T>(xn + (v + u * g.vlanes) * g.c + j * VEC, xv[u]);
+      for (int u = 0; u < 8; ++u) load16<T>(xn + (v + u * g.vlanes) * g.c + j * VEC, xv[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
           const float d = xv[u][e] - shift[e];
@@ -228,15 +228,15 @@ __global__ __launch_bounds__(GT) void gn_bwd_partial(const T* __restrict__ da, c
       }
     };
     long long v = v0 + vl;
-    for (; v + g.vlanes < v1; v += 2 * g.vlanes) {  // 4 loads in flight per thread
-      float xv[2][VEC], dv[2][VEC];
+    for (; v + 3 * g.vlanes < v1; v += 4 * g.vlanes) {  // 8 loads (64 KB per CU) in flight per thread
+      float xv[4][VEC], dv[4][VEC];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < 4; ++u) {
         load16<T>(x + base + (v + u * g.vlanes) * g.c + j * VEC, xv[u]);
         load16<T>(da + base + (v + u * g.vlanes) * g.c + j * VEC, dv[u]);
       }
-      step(xv[0], dv[0]);
-      step(xv[1], dv[1]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) step(xv[u], dv[u]);
     }
     for (; v < v1; v += g.vlanes) {
       float xv[VEC], dv[VEC];
