@@ -227,7 +227,9 @@ long long u3d_channel_sum_workspace_bytes(long long rows, int c);
 /* ---------------------------------------------------------------- partial-label Dice + BCE (A10, A11, A13)
  * EDiceLoss_partial(C)(logits, target, mask=[w], soft_max, uce), loss_partial.py:71-99 / DiceLoss :10-57.
  * logits fp32 [S][V][C] (NDHWC), labels fp32 [S][V] (integer-valued), weights fp32 [C] (= mask[0][:C]).
- * sums (fp64 [C][4]) = per class (sum p*t, sum p^2, sum t, sum BCE) over the whole batch; loss fp32[1]. */
+ * sums (fp64 [C][4]) = per class (sum p*t, sum p^2, sum t, sum BCE) over the whole batch; loss fp32[1].
+ * uce: 0 = Dice only, 1 = + sum_c w_c BCE_c (EDiceLoss_partial), 2 = + cross entropy of the logits (softmax only;
+ * nn.CrossEntropyLoss mean, unweighted: EDiceLoss_full, loss_partial.py:102-135). */
 long long u3d_loss_workspace_bytes(int S, long long V, int C);
 int u3d_partial_loss_fwd(const float* logits, const float* labels, int S, long long V, int C, int softmax,
                          const float* weights, int uce, double* sums, float* loss, float* ws, u3d_stream_t stream);
@@ -235,6 +237,11 @@ int u3d_partial_loss_fwd(const float* logits, const float* labels, int S, long l
 int u3d_partial_loss_bwd(int dtype_out, const float* logits, const float* labels, int S, long long V, int C,
                          int softmax, const float* weights, int uce, const double* sums, const float* grad_out,
                          void* dlogits, u3d_stream_t stream);
+
+/* Partial-label target (A12, train_amos_atlas_final.py:252-255): out = labels with every label l in [lmin, lmax]
+ * whose mask[s][l] == 0 set to 0; mask int64 [S][mask_stride] (mask_stride 0 = one vector for the batch), length M. */
+int u3d_partial_target(const float* labels, int S, long long V, const long long* mask, int mask_stride, int M,
+                       int lmin, int lmax, float* out, u3d_stream_t stream);
 
 /* ---------------------------------------------------------------- hard Dice metric (A14)
  * get_dice(preds, labels, t_id, atlas=None, num_class), evaluate_amos.py:128-154 with dice_score :92-102:

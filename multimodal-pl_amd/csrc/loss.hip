@@ -110,9 +110,11 @@ __global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restric
           acc[0][c] = fmaf(p, tc, acc[0][c]);
           acc[1][c] = fmaf(p, p, acc[1][c]);
           acc[2][c] += tc;
-          if (uce) {
+          if (uce == 1) {
             const float lq = hit ? x[c] - ls : __builtin_amdgcn_logf(s - e[c]) * LN2 - ls;
             acc[3][c] -= fmaxf(lq, -100.f);
+          } else if (uce == 2 && hit) {
+            acc[3][c] -= x[c] - ls;  // cross entropy: -log_softmax(x)[t] (nn.CrossEntropyLoss, no clamp)
           }
         }
     } else {
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restric
           acc[0][c] = fmaf(p[c], tc, acc[0][c]);
           acc[1][c] = fmaf(p[c], p[c], acc[1][c]);
           acc[2][c] += tc;
-          if (uce) acc[3][c] += bce_elem(p[c], tc);
+          if (uce == 1) acc[3][c] += bce_elem(p[c], tc);
         }
     }
   }
@@ -171,7 +173,7 @@ __global__ void loss_final_kernel(int C, const float* __restrict__ wt, int uce, 
       const double I = sums[c * 4 + 0], Z = sums[c * 4 + 1], Y = sums[c * 4 + 2], B = sums[c * 4 + 3];
       const float d = 1.f - (float)((2.0 * I + 1e-5) / (Z + Y + 1e-5));
       dice += (double)d * wt[c];
-      ce += (double)(float)(B / count) * wt[c];
+      ce += uce == 2 ? B / count : (double)(float)(B / count) * wt[c];
     }
     double l = dice / C;
     if (uce) l += ce;
@@ -195,7 +197,7 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
       // d(1 - num/den)/dp = -(2 t den - num * 2 p) / den^2  =  t * a + p * b
       a = (float)(-2.0 / den * scale);
       b = (float)(2.0 * num / (den * den) * scale);
-      e = uce ? (float)((double)wt[c] / count * gout[0]) : 0.f;
+      e = uce == 1 ? (float)((double)wt[c] / count * gout[0]) : uce == 2 ? (float)(1.0 / count * gout[0]) : 0.f;
     }
     kd_a[c] = a;
     kd_b[c] = b;
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
       if (c < C) {
         const float tc = (t == (float)c) ? 1.f : 0.f;
         float gc = fmaf(tc, kd_a[c], p[c] * kd_b[c]);
-        if (uce) gc += kb[c] * (p[c] - tc) * __builtin_amdgcn_rcpf(fmaxf((1.f - p[c]) * p[c], 1e-12f));
+        if (uce == 1) gc += kb[c] * (p[c] - tc) * __builtin_amdgcn_rcpf(fmaxf((1.f - p[c]) * p[c], 1e-12f));
         g[c] = gc;
         dot = fmaf(gc, p[c], dot);
       }
@@ -229,6 +231,11 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
 #pragma unroll
     for (int c = 0; c < NC; ++c)
       r[c] = softmax == 1 ? p[c] * (g[c] - dot) : softmax == 0 ? g[c] * (1.f - p[c]) * p[c] : g[c];
+    if (uce == 2) {  // cross entropy, in logit space: (softmax - onehot) / count
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c < C) r[c] += kb[c] * (p[c] - ((t == (float)c) ? 1.f : 0.f));
+    }
     if constexpr (NC == 16 && sizeof(TO) == 4) {
 #pragma unroll
       for (int c = 0; c < 16; c += 4)
@@ -238,6 +245,22 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
       for (int c = 0; c < NC; ++c)
         if (c < C) dl[v * C + c] = from_f<TO>(r[c]);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------- partial-label target
+// cmask = labels with every organ the sample's dataset does not annotate set to background
+// (train_amos_atlas_final.py:252-255: for l in 1..13, if not mask[l]: cmask[cmask == l] = 0).
+__global__ __launch_bounds__(LT) void partial_target_kernel(const float* __restrict__ lab, long long V, int S,
+                                                           const long long* __restrict__ mask, int mstride, int M,
+                                                           int lmin, int lmax, float* __restrict__ out) {
+  const long long total = (long long)S * V;
+  for (long long i = blockIdx.x * (long long)LT + threadIdx.x; i < total; i += (long long)gridDim.x * LT) {
+    const float t = lab[i];
+    const long long* m = mask + (i / V) * mstride;
+    bool drop = false;
+    for (int l = lmin; l <= lmax && l < M; ++l) drop |= (t == (float)l) && m[l] == 0;
+    out[i] = drop ? 0.f : t;
   }
 }
 
@@ -316,6 +339,8 @@ extern "C" int u3d_partial_loss_fwd(const float* logits, const float* labels, in
                                     u3d_stream_t stream) {
   U3D_REQUIRE(logits && labels && weights && sums && loss && ws, "partial_loss_fwd: null pointer");
   U3D_REQUIRE(C >= 1 && C <= CMAX && S >= 1 && V >= 1, "partial_loss_fwd: C=%d unsupported (max %d)", C, CMAX);
+  U3D_REQUIRE(uce >= 0 && uce <= 2 && (uce != 2 || softmax == 1), "partial_loss_fwd: uce=%d (2 = cross entropy, "
+              "softmax logits only)", uce);
   hipStream_t s = (hipStream_t)stream;
   const long long nvox = (long long)S * V;
   const int nb = loss_blocks(nvox);
@@ -333,6 +358,7 @@ extern "C" int u3d_partial_loss_bwd(int dtype_out, const float* logits, const fl
                                     const float* grad_out, void* dlogits, u3d_stream_t stream) {
   U3D_REQUIRE(logits && labels && weights && sums && grad_out && dlogits, "partial_loss_bwd: null pointer");
   U3D_REQUIRE(C >= 1 && C <= CMAX, "partial_loss_bwd: C=%d unsupported", C);
+  U3D_REQUIRE(uce >= 0 && uce <= 2 && (uce != 2 || softmax == 1), "partial_loss_bwd: bad uce=%d", uce);
   hipStream_t s = (hipStream_t)stream;
   const long long nvox = (long long)S * V;
   const int nb = (int)std::min<long long>(8192, (nvox + LT - 1) / LT);
@@ -367,4 +393,14 @@ extern "C" int u3d_dice_metric(const float* logits, const float* labels, int S, 
   hipLaunchKernelGGL(dice_final_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)counts, S, num_class,
                      metrics);
   return check_launch("dice_metric");
+}
+
+extern "C" int u3d_partial_target(const float* labels, int S, long long V, const long long* mask, int mask_stride,
+                                  int M, int lmin, int lmax, float* out, u3d_stream_t stream) {
+  U3D_REQUIRE(labels && mask && out && S >= 1 && V >= 1 && M >= 1 && mask_stride >= 0, "partial_target: bad args");
+  const long long total = (long long)S * V;
+  const int nb = (int)std::min<long long>(4096, (total + LT - 1) / LT);
+  hipLaunchKernelGGL(partial_target_kernel, dim3(nb), dim3(LT), 0, (hipStream_t)stream, labels, V, S, mask,
+                     mask_stride, M, lmin, lmax, out);
+  return check_launch("partial_target_kernel");
 }

@@ -51,13 +51,39 @@ class EDiceLoss_partial(nn.Module):
         return _L.partial_loss(inputs, target, w, mode=mode, uce=bool(uce))
 
 
+class EDiceLoss_full(nn.Module):
+    """Reference loss_partial.py:102-135: soft Dice over all classes (DiceLoss, weights 1) of softmax (or sigmoid)
+    probabilities + nn.CrossEntropyLoss of the logits when uce. One fused pass (uce=2: cross-entropy mode)."""
+
+    def __init__(self, n_classes):
+        super().__init__()
+        self.labels = ["ET", "TC", "WT"] + ["a"] * 20
+        self.device = "cpu"
+        self.n_classes = n_classes
+        self.diceloss = DiceLoss(n_classes=n_classes)
+        self.bce = nn.BCELoss()
+        self.mce = nn.CrossEntropyLoss()
+
+    def forward(self, inputs, target, logits="softmax", uce=True):
+        if logits == "extend":
+            raise NotImplementedError("EDiceLoss_full(logits='extend') is not on the native path")
+        C = inputs.shape[1]
+        assert C == self.n_classes, "predict & target shape do not match"
+        w = torch.ones(C, dtype=torch.float32, device=inputs.device)
+        if logits == "softmax":
+            return _L.partial_loss(inputs, target, w, mode=_L.MODE_SOFTMAX, uce=2 if uce else 0)
+        if uce:
+            raise NotImplementedError("EDiceLoss_full: sigmoid probabilities with the cross-entropy term")
+        return _L.partial_loss(inputs, target, w, mode=_L.MODE_SIGMOID, uce=0)
+
+
 def _next_row(name):
     class _Missing(nn.Module):
         def __init__(self, *a, **k):
-            raise NotImplementedError(f"{name}: refiner/consistency loss, SURVEY.md §8(f) row f3 — not built yet")
+            raise NotImplementedError(f"{name}: consistency loss over the feam3 attention maps, SURVEY.md §8(f) "
+                                      "rows f2/f3 — not built yet")
     _Missing.__name__ = name
     return _Missing
 
 
-EDiceLoss_full = _next_row("EDiceLoss_full")
 EDiceLoss_full2 = _next_row("EDiceLoss_full2")

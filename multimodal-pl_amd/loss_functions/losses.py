@@ -1,6 +1,7 @@
 """Drop-in for the reference loss_functions/losses.py: the pre-train branch of get_loss (losses.py:107-113,
-179-182), which is what train_amos_atlas_final.py:303-304 calls for epoch < pretrain_epoch."""
-from loss_functions.loss_partial import EDiceLoss_partial
+179-182), which is what train_amos_atlas_final.py:303-304 calls for epoch < pretrain_epoch, and the refiner
+loss get_loss_refine (:46-62)."""
+from loss_functions.loss_partial import EDiceLoss_full, EDiceLoss_partial
 
 
 def get_loss(output, cm, deep_out, target, mask=None, catlas=None, attns=None, refine_output=None, label_t=None,
@@ -14,5 +15,23 @@ def get_loss(output, cm, deep_out, target, mask=None, catlas=None, attns=None, r
     return dice_loss, confi_
 
 
-def get_loss_refine(*a, **k):
-    raise NotImplementedError("get_loss_refine: refiner loss, SURVEY.md §8(f) row f3 — not built yet")
+def get_loss_refine(output, label, dlist, aug_mask=1):
+    """Reference losses.py:46-62: sum over the refiner's samples of EDiceLoss_full(2) (uce=False) against the
+    binary mask of that sample's organ (label == l + 1); with aug_mask > 1 the batch holds aug_mask copies."""
+    from u3d import ops
+    ops.require_device(output, label)
+    loss = 0.
+    cedice = EDiceLoss_full(2)
+    reps = aug_mask if aug_mask > 1 else 1
+    for kk in range(reps):
+        start = kk * len(dlist)
+        for idx, l in enumerate(dlist):
+            loss += cedice(output[start + idx:start + idx + 1], (label == (l + 1)).squeeze(1), uce=False)
+    return loss
+
+
+def make_partial_target(labels, sup_mask):
+    """train_amos_atlas_final.py:252-255: cmask = labels with organs 1..13 the dataset does not annotate (mask[l]
+    == 0) set to background, one device pass (u3d_partial_target) instead of 13 masked writes."""
+    from u3d import ops
+    return ops.partial_target(labels, sup_mask, 1, 13).reshape(labels.shape)

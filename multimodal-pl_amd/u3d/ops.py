@@ -431,6 +431,24 @@ def channel_sum(x, out=None, accumulate=False):
 
 
 # ------------------------------------------------------------------------------------------ loss / metric
+def partial_target(labels, mask, lmin=1, lmax=13):
+    """labels fp32 (any shape, leading dim S) with organs the mask marks unlabelled set to 0 (A12)."""
+    require_device(labels)
+    lab = labels.float().contiguous()
+    m = torch.as_tensor(mask).to(device=labels.device, dtype=torch.int64)
+    S = lab.shape[0]
+    V = lab.numel() // S
+    if m.dim() == 1:
+        stride, M = 0, m.numel()
+    else:
+        assert m.shape[0] == S, "one mask row per sample"
+        stride, M = m.shape[1], m.shape[1]
+    m = m.contiguous()
+    out = torch.empty_like(lab)
+    call("u3d_partial_target", lab.data_ptr(), S, V, m.data_ptr(), stride, M, lmin, lmax, out.data_ptr(), _stream())
+    return out
+
+
 def partial_loss_fwd(logits, labels, weights, softmax=True, uce=True):
     """logits fp32 [S, ..., C] NDHWC-contiguous, labels fp32 [S, ...] -> (loss fp32[1], sums fp64[C,4])."""
     S, C = logits.shape[0], logits.shape[-1]

@@ -148,6 +148,42 @@ def edice_partial(inputs, target, mask=None, soft_max=True, uce=True):
 
 
 # ------------------------------------------------------------------------------------------------- A14
+def _soft_dice(p, t):
+    """DiceLoss._dice_loss, loss_partial.py:24-36, mask all ones: 1 - (2 sum pt + 1e-5) / (sum p^2 + sum t^2 + 1e-5)."""
+    return 1 - (2 * torch.sum(p * t) + 1e-5) / (torch.sum(p * p) + torch.sum(t * t) + 1e-5)
+
+
+def edice_full(inputs, target, logits="softmax", uce=True):
+    """EDiceLoss_full.forward, loss_partial.py:119-135 (DiceLoss over all C classes, weights 1, / C) + the
+    cross entropy of the logits (nn.CrossEntropyLoss, mean) when uce."""
+    C = inputs.shape[1]
+    p = torch.softmax(inputs, 1) if logits == "softmax" else torch.sigmoid(inputs)
+    t = target.long()
+    dice = sum(_soft_dice(p[:, i], (t == i).float()) for i in range(C)) / C
+    if uce:
+        dice = dice + F.cross_entropy(inputs.float(), t)
+    return dice
+
+
+def get_loss_refine(output, label, dlist, aug_mask=1):
+    """losses.py:46-62: sum over samples of EDiceLoss_full(2)(output[i:i+1], label == l+1, uce=False)."""
+    loss = 0.
+    for kk in range(aug_mask if aug_mask > 1 else 1):
+        start = kk * len(dlist)
+        for idx, l in enumerate(dlist):
+            loss = loss + edice_full(output[start + idx:start + idx + 1], (label == (l + 1)).squeeze(1), uce=False)
+    return loss
+
+
+def partial_target(labels, sup_mask):
+    """train_amos_atlas_final.py:252-255 (numpy): for l in 1..13, if not mask[l]: cmask[cmask == l] = 0."""
+    cm = np.array(labels, dtype=np.float32, copy=True)
+    for l in range(1, 14):
+        if not sup_mask[l]:
+            cm[cm == l] = 0
+    return cm
+
+
 def get_dice(preds, labels, num_class=13):
     """evaluate_amos.py:92-154 (atlas=None branch): argmax of softmax; per class l=1..num_class per-sample
     dice 2*sum(P*T)/(sum P + sum T + 1), sensitivity sum(P*T)/(sum T + 1), precision sum(P*T)/(sum P + 1),

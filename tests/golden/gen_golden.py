@@ -254,6 +254,31 @@ def g5():
          amin=logits.amin((0, 2, 3, 4)).numpy(), amax=logits.amax((0, 2, 3, 4)).numpy())
 
 
+def g7():
+    """f3: EDiceLoss_full (loss_partial.py:102-135) and get_loss_refine (losses.py:46-62) values + dlogits."""
+    from loss_functions import losses as RL
+    rng = np.random.default_rng([7, 99])
+    sp = (12, 10, 8)
+    out = {}
+    lab = torch.from_numpy(rng.integers(0, 14, (1, 1) + sp).astype(np.float32))
+    for tag, n in (("a1", 3), ("a2", 6)):
+        lg = torch.from_numpy((rng.standard_normal((n, 2) + sp) * 2).astype(np.float32)).requires_grad_(True)
+        v = RL.get_loss_refine(lg, lab, [2, 5, 7], 1 if tag == "a1" else 2)
+        v.backward()
+        out[f"ref_{tag}_logits"], out[f"ref_{tag}_value"], out[f"ref_{tag}_dlogits"] = \
+            lg.detach().numpy(), v.detach().numpy(), lg.grad.numpy()
+    out["ref_labels"] = lab.numpy()
+    for tag, C, lgt, uce in (("s2u", 2, "softmax", True), ("s2n", 2, "softmax", False), ("g2n", 2, "sigmoid", False),
+                             ("s4u", 4, "softmax", True)):
+        lg = torch.from_numpy((rng.standard_normal((2, C) + sp) * 2).astype(np.float32)).requires_grad_(True)
+        t = torch.from_numpy(rng.integers(0, C, (2,) + sp).astype(np.int64))
+        v = RLP.EDiceLoss_full(C)(lg, t, logits=lgt, uce=uce)
+        v.backward()
+        out[f"full_{tag}_logits"], out[f"full_{tag}_target"] = lg.detach().numpy(), t.numpy()
+        out[f"full_{tag}_value"], out[f"full_{tag}_dlogits"] = v.detach().numpy(), lg.grad.numpy()
+    save("g7_refine_losses.npz", **out)
+
+
 def g6():
     """Gaussian importance map of predict_sliding (evaluate_amos.py:184-197) for the 64x192x192 tile."""
     g = REV._get_gaussian((64, 192, 192), sigma_scale=1.0 / 8)
@@ -264,6 +289,6 @@ def g6():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7"]
     for w in which:
         globals()[w]()

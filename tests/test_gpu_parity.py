@@ -261,3 +261,41 @@ def test_cpu_tensor_raises(gpu):
     m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], 16, True)
     with pytest.raises(U3DError):
         m(torch.zeros(1, 1, 16, 16, 16))
+
+
+# ------------------------------------------------------------------------------------ f3 refiner losses
+def test_g7_get_loss_refine_and_edice_full(gpu):
+    """loss_functions.losses.get_loss_refine / loss_partial.EDiceLoss_full (fused HIP loss, cross-entropy mode)
+    against the reference's own values and dlogits (G7)."""
+    from loss_functions import losses, loss_partial
+    g = golden("g7_refine_losses.npz")
+    lab = torch.from_numpy(g["ref_labels"]).to(gpu)
+    for tag, aug in (("a1", 1), ("a2", 2)):
+        lg = torch.from_numpy(g[f"ref_{tag}_logits"]).to(gpu).requires_grad_(True)
+        v = losses.get_loss_refine(lg, lab, [2, 5, 7], aug)
+        v.backward()
+        np.testing.assert_allclose(float(v), float(g[f"ref_{tag}_value"]), rtol=1e-4)
+        np.testing.assert_allclose(lg.grad.cpu().numpy(), g[f"ref_{tag}_dlogits"], rtol=1e-3, atol=1e-7)
+    for tag, C, lgt, uce in (("s2u", 2, "softmax", True), ("s2n", 2, "softmax", False), ("g2n", 2, "sigmoid", False),
+                             ("s4u", 4, "softmax", True)):
+        lg = torch.from_numpy(g[f"full_{tag}_logits"]).to(gpu).requires_grad_(True)
+        t = torch.from_numpy(g[f"full_{tag}_target"]).to(gpu)
+        v = loss_partial.EDiceLoss_full(C)(lg, t, logits=lgt, uce=uce)
+        v.backward()
+        np.testing.assert_allclose(float(v), float(g[f"full_{tag}_value"]), rtol=1e-4)
+        np.testing.assert_allclose(lg.grad.cpu().numpy(), g[f"full_{tag}_dlogits"], rtol=1e-3, atol=1e-7)
+
+
+def test_partial_target_vs_oracle(gpu):
+    """A12 (train_amos_atlas_final.py:252-255) as one device pass, batch mask and per-sample masks."""
+    from loss_functions import losses
+    from u3d import ops
+    rng = np.random.default_rng(3)
+    lab = rng.integers(0, 16, (2, 1, 9, 10, 11)).astype(np.float32)
+    mask = rng.integers(0, 2, 15).astype(np.int64)
+    got = losses.make_partial_target(torch.from_numpy(lab).to(gpu), torch.from_numpy(mask)).cpu().numpy()
+    np.testing.assert_array_equal(got, O.partial_target(lab, mask))
+    masks = rng.integers(0, 2, (2, 15)).astype(np.int64)
+    got = ops.partial_target(torch.from_numpy(lab).to(gpu), torch.from_numpy(masks)).cpu().numpy()
+    ref = np.stack([O.partial_target(lab[i:i + 1], masks[i])[0] for i in range(2)])
+    np.testing.assert_array_equal(got.reshape(ref.shape), ref)

@@ -171,3 +171,31 @@ def test_f1_gaussian_product_vs_scipy_and_oracle():
         ref[ref == 0] = ref[ref != 0].min()
         np.testing.assert_allclose(O.gaussian_map(ts), ref, rtol=1e-6, atol=0)
         np.testing.assert_allclose(E._get_gaussian(ts), ref, rtol=1e-6, atol=0)
+
+
+def test_g7_refine_losses():
+    """f3: oracle restatements of EDiceLoss_full and get_loss_refine vs the reference's own values and grads."""
+    g = golden("g7_refine_losses.npz")
+    lab = torch.from_numpy(g["ref_labels"])
+    for tag, aug in (("a1", 1), ("a2", 2)):
+        lg = torch.from_numpy(g[f"ref_{tag}_logits"]).requires_grad_(True)
+        v = O.get_loss_refine(lg, lab, [2, 5, 7], aug)
+        v.backward()
+        np.testing.assert_allclose(float(v), float(g[f"ref_{tag}_value"]), rtol=1e-5)
+        np.testing.assert_allclose(lg.grad.numpy(), g[f"ref_{tag}_dlogits"], rtol=1e-4, atol=1e-9)
+    for tag, lgt, uce in (("s2u", "softmax", True), ("s2n", "softmax", False), ("g2n", "sigmoid", False),
+                          ("s4u", "softmax", True)):
+        lg = torch.from_numpy(g[f"full_{tag}_logits"]).requires_grad_(True)
+        v = O.edice_full(lg, torch.from_numpy(g[f"full_{tag}_target"]), logits=lgt, uce=uce)
+        v.backward()
+        np.testing.assert_allclose(float(v), float(g[f"full_{tag}_value"]), rtol=1e-5)
+        np.testing.assert_allclose(lg.grad.numpy(), g[f"full_{tag}_dlogits"], rtol=1e-4, atol=1e-9)
+
+
+def test_partial_target_known_answer():
+    """A12 restatement: organs the dataset does not annotate (mask 0, labels 1..13) become background; labels
+    >= 14 and the background are untouched."""
+    lab = np.array([[0, 1, 2, 3, 13, 14, 15, 2]], dtype=np.float32)
+    mask = np.ones(15, dtype=np.int64)
+    mask[[2, 13, 14]] = 0
+    np.testing.assert_array_equal(O.partial_target(lab, mask), [[0, 1, 0, 3, 0, 14, 15, 0]])
