@@ -255,6 +255,91 @@ def predict_sliding(pred_fn, image, tile_size, classes, tta=False):
     return full / count
 
 
+# ---------------------------------------------------------------------------------------------- next f2
+def eam_attn(P, pre, x, token, num_heads=4):
+    """EAM.forward, unet3D.py:186-212, up to the returned ``attn`` (q k^T before the scaled softmax) — the only
+    output unet3D_with_feam3 uses (its ``cm`` is discarded, :1134). x [B, N, C], token [1, Nt, C]. The kv / q
+    reshapes use the TOKEN's batch (:189, :198), so B > 1 raises exactly as in the reference."""
+    B, N, C = x.shape
+    Bt, Nt, _ = token.shape
+    xn = F.layer_norm(x, (C,), P[pre + "norm2.weight"], P[pre + "norm2.bias"], 1e-5)
+    tn = F.layer_norm(token, (C,), P[pre + "norm3.weight"], P[pre + "norm3.bias"], 1e-5)
+    kv = F.linear(xn, P[pre + "kv.weight"]).reshape(Bt, N, 2, num_heads, C // num_heads).permute(2, 0, 3, 1, 4)
+    q = F.linear(tn, P[pre + "q.weight"]).reshape(Bt, Nt, num_heads, C // num_heads).permute(0, 2, 1, 3)
+    return q @ kv[0].transpose(-2, -1)
+
+
+def feam3_forward(P, tokens, x, num_classes, deep_up=False, use_cm=(True, True, True), training=True):
+    """unet3D_with_feam3.forward, unet3D.py:1095-1190 (layers [1,2,2,2,2], GN 16): trunk + deep-supervision heads
+    deepout1-3 (GN, ReLU, 1^3 conv + bias, :969-993) + EAM attention maps against the detached class tokens
+    (:1131-1175; x8/x4/x2 upsampled to full size when deep_up) + detached feature copies. ``tokens`` =
+    [class_token1 (nc-1 x 128), class_token2 (x 64), class_token3 (x 32)]."""
+    x = conv(x, P["conv1.weight"], 1)
+    skips = []
+    for i, name in enumerate(["layer0", "layer1", "layer2", "layer3", "layer4"]):
+        x = layer(P, name, x, (1, 2, 2, 2, 2)[i], 1 if i == 0 else 2, 16)
+        skips.append(x)
+    x = conv(gn_relu(x, 16, P["fusionConv.0.weight"], P["fusionConv.0.bias"]), P["fusionConv.2.weight"], 1)
+    atten, deep, feats = [], [], []
+    scales = [8, 4, 2]
+    for k, (name, skip, eam) in enumerate(zip(["x8_resb", "x4_resb", "x2_resb"], skips[3:0:-1],
+                                               ["eam84", "eam42", "eam21"])):
+        x = layer(P, name, upsample2x(x) + skip, 1, 1, 16)
+        pre = f"deepout{k + 1}."
+        deep.append(F.conv3d(gn_relu(x, 16, P[pre + "0.weight"], P[pre + "0.bias"]), P[pre + "2.weight"],
+                             P[pre + "2.bias"]))
+        feats.append(x.detach().clone())
+        if use_cm[k]:
+            B, C = x.shape[:2]
+            xt = x.reshape(B, C, -1).permute(0, 2, 1)
+            cattn = eam_attn(P, eam + ".", xt, tokens[k].reshape(1, num_classes - 1, C).detach())
+            a = cattn.mean(1).reshape((B, num_classes - 1) + tuple(x.shape[2:]))
+            atten.append(F.interpolate(a, scale_factor=scales[k], mode="trilinear") if deep_up else a)
+    x = layer(P, "x1_resb", upsample2x(x) + skips[0], 1, 1, 16)
+    logits = precls(P, x, 16)
+    return (logits, atten, deep, feats) if training else logits
+
+
+def renew_token(tokens, features, mask, num_classes, alpha=0.01):
+    """unet3D_with_feam3.renew_token, unet3D.py:1051-1068, in place on ``tokens``: for every class l with voxels
+    in ``mask`` (== l+1), nearest-resized to each feature's size, token[l] <- (1-a) token[l] + a * mean. The mean
+    is taken over ``x[cmask].reshape(C, -1)`` rows exactly as written (for B > 1 the rows are not channels)."""
+    for index, x in enumerate(features):
+        for l in range(num_classes):
+            if (mask == (l + 1)).sum() != 0:
+                cmask = F.interpolate((mask == (l + 1)).float(), x.shape[2:], mode="nearest").bool()
+                cmask = cmask.repeat(1, x.shape[1], 1, 1, 1)
+                if cmask.sum() == 0:
+                    continue
+                m = x[:, :][cmask].reshape(x.shape[1], -1).mean(-1).detach()
+                tokens[index][l] = tokens[index][l] * (1 - alpha) + m * alpha
+    return tokens
+
+
+def state_shapes_feam3(num_classes=14):
+    """Ordered (key, shape) list of the unet3D_with_feam3([1,2,2,2,2]) state_dict (registration order :949-1004)."""
+    base = dict(state_shapes_baseline(num_classes))
+    order = [k for k, _ in state_shapes_baseline(num_classes)]
+    i8 = order.index("x8_resb.0.gn1.weight")
+    head = [(k, base[k]) for k in order[:i8]]
+
+    def blk(name):
+        return [(k, base[k]) for k in order if k.startswith(name + ".")]
+
+    def extra(k, c):
+        e = [(f"deepout{k}.0.weight", (c,)), (f"deepout{k}.0.bias", (c,)),
+             (f"deepout{k}.2.weight", (num_classes, c, 1, 1, 1)), (f"deepout{k}.2.bias", (num_classes,))]
+        pre = {1: "eam84", 2: "eam42", 3: "eam21"}[k] + "."
+        e += [(pre + "kv.weight", (2 * c, c)), (pre + "q.weight", (c, c)), (pre + "proj.weight", (c, c)),
+              (pre + "proj.bias", (c,)), (pre + "norm2.weight", (c,)), (pre + "norm2.bias", (c,)),
+              (pre + "norm3.weight", (c,)), (pre + "norm3.bias", (c,))]
+        return e
+
+    out = head + blk("x8_resb") + extra(1, 128) + blk("x4_resb") + extra(2, 64) + blk("x2_resb") + extra(3, 32)
+    out += blk("x1_resb") + blk("precls_conv")
+    return out
+
+
 def params_from_module_dict(sd):
     return {k: v.detach().float().cpu() for k, v in sd.items()}
 

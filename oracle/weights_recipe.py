@@ -9,6 +9,8 @@ and the recipe, never the 69 MB of weights, and the same tensors come out on any
 * 5-D conv weight  ``[Cout, Cin/groups, k, k, k]``  ->  N(0,1) / sqrt(Cin/groups * k^3)
 * 1-D ``*.weight`` (GroupNorm gamma)               ->  1 + 0.1 N(0,1)
 * 1-D ``*.bias``   (GroupNorm beta, conv bias)     ->  0.1 N(0,1)
+* 2-D Linear weight ``[out, in]``                   ->  N(0,1) / sqrt(in)
+* class tokens (plain tensors, not state_dict)      ->  N(0,1)   (``torch.randn``, unet3D.py:1016-1021)
 """
 import zlib
 
@@ -22,6 +24,10 @@ def param_array(key: str, shape, seed: int = 0) -> np.ndarray:
     if len(shape) == 5:
         fan_in = shape[1] * shape[2] * shape[3] * shape[4]
         out = z / np.sqrt(fan_in)
+    elif len(shape) == 2 and key.startswith("class_token"):
+        out = z
+    elif len(shape) == 2:
+        out = z / np.sqrt(shape[1])
     elif len(shape) == 1 and key.endswith("weight"):
         out = 1.0 + 0.1 * z
     elif len(shape) == 1 and key.endswith("bias"):

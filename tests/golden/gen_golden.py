@@ -288,7 +288,93 @@ def g6():
          gmin=g.min(), gmax=g.max(), pts=pts, vals=g[pts[:, 0], pts[:, 1], pts[:, 2]])
 
 
+def g8():
+    """f2: unet3D_with_feam3 (unet3D.py:938-1190) — train-mode outputs (logits, attention maps with and without
+    deep_up, deep-supervision maps, stored features), parameter gradients of a seeded projection of every output,
+    eval-mode logits, renew_token (B = 1) and the renew_token row quirk at B = 2 (use_cm off, :1064)."""
+    from weights_recipe import param_array
+    nc = 14
+    out = {}
+    x = torch.from_numpy(input_volume((1, 1, 32, 32, 32), seed=80, kind="normal"))
+    for tag, deep_up in (("nd", False), ("du", True)):
+        m = R.unet3D_with_feam3([1, 2, 2, 2, 2], num_classes=nc, weight_std=True, deep_up=deep_up)
+        apply_recipe(m, seed=0)
+        for k in (1, 2, 3):
+            setattr(m, f"class_token{k}", torch.from_numpy(param_array(f"class_token{k}",
+                                                                       getattr(m, f"class_token{k}").shape, 0)))
+        m.train()
+        logits, att, deep, feats = m(x)
+        rng = np.random.default_rng([81, 1 if deep_up else 0])
+        proj = [logits] + att + deep
+        ups = [torch.from_numpy(rng.standard_normal(t.shape).astype(np.float32)) for t in proj]
+        sum((t * u).sum() for t, u in zip(proj, ups)).backward()
+        # the projections are regenerated by the tests from the same seed (not stored); full-size maps sampled
+        if not deep_up:
+            out[f"{tag}_logits"] = logits.detach().numpy()
+            for i in range(3):
+                out[f"{tag}_att{i}"], out[f"{tag}_deep{i}"] = att[i].detach().numpy(), deep[i].detach().numpy()
+        else:
+            for i in range(3):
+                flat = att[i].detach().reshape(-1)
+                idx = np.random.default_rng([84, i]).integers(0, flat.numel(), size=SAMPLE_N)
+                out[f"{tag}_att{i}_idx"], out[f"{tag}_att{i}_val"] = idx, flat[torch.from_numpy(idx)].numpy()
+                out[f"{tag}_att{i}_sum"] = att[i].detach().double().sum().numpy()
+        names, norms, gidx, gval = [], [], [], []
+        for i, (k, p) in enumerate(m.named_parameters()):
+            names.append(k)
+            if p.grad is None:                      # eamXX.proj.* : the EAM's x output is discarded (:1134)
+                norms.append(-1.0)
+                gidx.append(np.zeros(16, np.int64))
+                gval.append(np.zeros(16))
+                continue
+            g = p.grad.detach().reshape(-1).double()
+            idx = np.random.default_rng([1234, i]).integers(0, g.numel(), size=16)
+            norms.append(g.norm().item())
+            gidx.append(idx)
+            gval.append(g[torch.from_numpy(idx)].numpy())
+        out[f"{tag}_gnames"], out[f"{tag}_gnorm"] = np.array(names), np.array(norms)
+        out[f"{tag}_gidx"], out[f"{tag}_gval"] = np.stack(gidx), np.stack(gval)
+        if not deep_up:
+            for i in range(3):
+                out[f"feat{i}"] = feats[i].numpy()
+            # renew_token with a label volume missing some classes (B = 1)
+            lab = np.random.default_rng([82, 0]).integers(0, nc, size=(1, 1, 32, 32, 32))
+            lab[np.isin(lab, [3, 7])] = 0
+            lab[:, :, :16][lab[:, :, :16] == 5] = 0
+            lab[lab == 9] = 0                            # class 9 only at odd (d, h, w): nearest resizing picks
+            lab[:, :, 1::10, 1::6, 1::4] = 9             # even source indices, so it vanishes at every feature size
+            fmask = torch.from_numpy(lab.astype(np.float32))
+            m.renew_token(feats, fmask)
+            out["renew_mask"] = lab.astype(np.float32)
+            for k in (1, 2, 3):
+                out[f"renew_tok{k}"] = getattr(m, f"class_token{k}").numpy()
+            m.eval()
+            with torch.no_grad():
+                out["eval_minus_train"] = (m(x) - logits.detach()).abs().max().numpy()
+    # the renew_token reshape quirk at B = 2 (rows of x[cmask].reshape(C, -1) are not channels)
+    m = R.unet3D_with_feam3([1, 2, 2, 2, 2], num_classes=nc, weight_std=True)
+    rng = np.random.default_rng([83, 0])
+    feats = [torch.from_numpy(rng.standard_normal((2, c, s, s, s)).astype(np.float32))
+             for c, s in ((128, 2), (64, 4), (32, 8))]
+    lab = rng.integers(0, 5, size=(2, 1, 16, 16, 16)).astype(np.float32)
+    lab[0][lab[0] == 2] = 0
+    toks = [torch.from_numpy(param_array(f"class_token{k}", (nc - 1, c), 0)) for k, c in ((1, 128), (2, 64), (3, 32))]
+    for k in (1, 2, 3):
+        setattr(m, f"class_token{k}", toks[k - 1].clone())
+    m.renew_token(feats, torch.from_numpy(lab))
+    for i in range(3):
+        out[f"q_feat{i}"] = feats[i].numpy()
+        out[f"q_tok{i + 1}"] = getattr(m, f"class_token{i + 1}").numpy()
+    out["q_mask"] = lab
+    try:
+        m(torch.zeros(2, 1, 16, 16, 16))
+        out["b2_raises"] = np.array(0)
+    except RuntimeError:
+        out["b2_raises"] = np.array(1)
+    save("g8_feam3_32.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8"]
     for w in which:
         globals()[w]()

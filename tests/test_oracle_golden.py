@@ -1,10 +1,11 @@
 """Pin the CPU oracle (oracle/ref_cpu.py) against the golden vectors generated from the reference itself."""
 import numpy as np
+import pytest
 import torch
 
 from conftest import golden
 from oracle import ref_cpu as O
-from oracle.weights_recipe import recipe_state_dict
+from oracle.weights_recipe import input_volume, recipe_state_dict
 
 torch.set_num_threads(min(8, torch.get_num_threads()))
 
@@ -46,8 +47,10 @@ def test_g1_unet3d_dynconv_backward():
     for i, k in enumerate(g["gnames"]):
         gr = params[k].grad.reshape(-1).double()
         np.testing.assert_allclose(gr.norm().item(), g["gnorm"][i], rtol=1e-3, atol=1e-6)
+        # entries: 1e-4 of the tensor's norm — the CPU summation order (thread count, BLAS build) moves single
+        # entries of the shallow layers' gradients by up to ~1%; the norms above stay at 1e-3
         np.testing.assert_allclose(gr[torch.from_numpy(g["gidx"][i])].numpy(), g["gval"][i], rtol=2e-3,
-                                   atol=2e-5 * max(1.0, g["gnorm"][i]))
+                                   atol=1e-4 * max(1.0, g["gnorm"][i]))
 
 
 def test_g2_unet3d_g():
@@ -199,3 +202,71 @@ def test_partial_target_known_answer():
     mask = np.ones(15, dtype=np.int64)
     mask[[2, 13, 14]] = 0
     np.testing.assert_array_equal(O.partial_target(lab, mask), [[0, 1, 0, 3, 0, 14, 15, 0]])
+
+
+# ------------------------------------------------------------------------------------------- f2: feam3
+def feam3_tokens(seed=0, nc=14):
+    from oracle.weights_recipe import param_array
+    return [torch.from_numpy(param_array(f"class_token{k}", (nc - 1, c), seed)) for k, c in ((1, 128), (2, 64), (3, 32))]
+
+
+def feam3_projections(deep_up, shapes):
+    """The seeded projections gen_golden.g8 contracted every output with (same generator, same order)."""
+    rng = np.random.default_rng([81, 1 if deep_up else 0])
+    return [torch.from_numpy(rng.standard_normal(s).astype(np.float32)) for s in shapes]
+
+
+def test_g8_feam3_state_dict_order():
+    g = golden("g8_feam3_32.npz")
+    assert list(g["nd_gnames"]) == [k for k, _ in O.state_shapes_feam3(14)]
+
+
+@pytest.mark.parametrize("deep_up", [False, True])
+def test_g8_feam3_forward_backward(deep_up):
+    g = golden("g8_feam3_32.npz")
+    tag = "du" if deep_up else "nd"
+    params = {k: v.requires_grad_(True) for k, v in P(O.state_shapes_feam3(14)).items()}
+    x = torch.from_numpy(input_volume((1, 1, 32, 32, 32), seed=80, kind="normal"))
+    logits, att, deep, feats = O.feam3_forward(params, feam3_tokens(), x, 14, deep_up=deep_up)
+    if deep_up:
+        for i in range(3):
+            flat = att[i].detach().reshape(-1)
+            np.testing.assert_allclose(flat[torch.from_numpy(g[f"du_att{i}_idx"])].numpy(), g[f"du_att{i}_val"],
+                                       rtol=1e-4, atol=1e-4)
+    else:
+        assert np.abs(logits.detach().numpy() - g["nd_logits"]).max() < 1e-4
+        for i in range(3):
+            np.testing.assert_allclose(att[i].detach().numpy(), g[f"nd_att{i}"], rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(deep[i].detach().numpy(), g[f"nd_deep{i}"], rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(feats[i].numpy(), g[f"feat{i}"], rtol=1e-4, atol=1e-4)
+    outs = [logits] + att + deep
+    ups = feam3_projections(deep_up, [tuple(t.shape) for t in outs])
+    sum((t * u).sum() for t, u in zip(outs, ups)).backward()
+    for i, k in enumerate(g[f"{tag}_gnames"]):
+        if g[f"{tag}_gnorm"][i] < 0:
+            assert params[k].grad is None, k
+            continue
+        gr = params[k].grad.reshape(-1).double()
+        np.testing.assert_allclose(gr.norm().item(), g[f"{tag}_gnorm"][i], rtol=1e-3, atol=1e-6, err_msg=k)
+
+
+def test_g8_renew_token_and_row_quirk():
+    g = golden("g8_feam3_32.npz")
+    toks = feam3_tokens()
+    feats = [torch.from_numpy(g[f"feat{i}"]) for i in range(3)]
+    O.renew_token(toks, feats, torch.from_numpy(g["renew_mask"]), 14)
+    for k in range(3):
+        np.testing.assert_allclose(toks[k].numpy(), g[f"renew_tok{k + 1}"], rtol=1e-6, atol=1e-6)
+    toks = feam3_tokens()
+    feats = [torch.from_numpy(g[f"q_feat{i}"]) for i in range(3)]
+    O.renew_token(toks, feats, torch.from_numpy(g["q_mask"]), 14)
+    for k in range(3):
+        np.testing.assert_allclose(toks[k].numpy(), g[f"q_tok{k + 1}"], rtol=1e-6, atol=1e-6)
+
+
+def test_g8_feam3_batch2_raises_like_reference():
+    g = golden("g8_feam3_32.npz")
+    assert int(g["b2_raises"]) == 1
+    params = P(O.state_shapes_feam3(14))
+    with pytest.raises(RuntimeError):
+        O.feam3_forward(params, feam3_tokens(), torch.zeros(2, 1, 16, 16, 16), 14)
