@@ -282,6 +282,45 @@ int u3d_dyn_controller_bwd(int dtype, const float* feat, int n, int kf, const lo
                            const float* dparams, int m, float* dw, float* db, int accumulate, long long v, void* dA,
                            u3d_stream_t stream);
 
+/* ---------------------------------------------------------------- unet3D_with_feam3 attention branch (f2)
+ * EAM (unet3D.py:142-212) as used by unet3D_with_feam3.forward (:1131-1175): only `attn` = q k^T is kept, averaged
+ * over the heads (cattn.mean(1)), which equals sum_c M[t][c] LN2(x_n)[c] with M = (1/h) q Wk.
+ * u3d_eam_prep: per token t: zhat = LN3 normalised token (eps 1e-5), q = Wq (zhat g3 + b3), M = inv_heads q Wk
+ * (Wk = kv.weight rows 0..c-1). tok/zhat/q/m [nt][c] fp32; wq, wk [c][c]. nt <= 16, c <= 256. */
+int u3d_eam_prep(const float* tok, int nt, int c, const float* g3, const float* b3, const float* wq, const float* wk,
+                 float inv_heads, float* zhat, float* q, float* m, u3d_stream_t stream);
+/* att[n][t][v] (fp32, NCDHW) = sum_c M[t][c] LayerNorm(x[n][v][:]; g2, b2)[c]; x NDHWC dtype, c % 8 == 0 */
+int u3d_eam_attn_fwd(int dtype, const void* x, int n, long long v, int c, const float* g2, const float* b2,
+                     const float* m, int nt, float* out, u3d_stream_t stream);
+/* Backward of u3d_eam_attn_fwd from gout [n][nt][v]: dx (dtype NDHWC, += when accumulate), dM [nt][c], dg2/db2
+ * ([c], += when acc_params). part: u3d_eam_attn_bwd_part_floats(...) floats (fixed-order block partials). c in
+ * {32, 64, 128}. */
+int u3d_eam_attn_bwd_blocks(int n, long long v);
+long long u3d_eam_attn_bwd_part_floats(int n, long long v, int c, int nt);
+int u3d_eam_attn_bwd(int dtype, const void* x, int n, long long v, int c, const float* g2, const float* b2,
+                     const float* m, int nt, const float* gout, void* dx, int accumulate, float* part, float* dm,
+                     float* dg2, float* db2, int acc_params, u3d_stream_t stream);
+/* Token-side backward: from dM -> dWq [c][c], d(kv.weight) [2c][c] (v half = 0), dg3, db3 (norm3). dq_ws, dz_ws
+ * [nt][c] scratch. The token itself is detached (:1134). */
+int u3d_eam_param_bwd(const float* dm, int nt, int c, const float* zhat, const float* g3, const float* b3,
+                      const float* wq, const float* wk, const float* q, float inv_heads, float* dq_ws, float* dz_ws,
+                      float* dwq, float* dkv, float* dg3, float* db3, int accumulate, u3d_stream_t stream);
+/* nn.Upsample(scale_factor=s, mode='trilinear'), align_corners=False (unet3D.py:963-965, deep_up maps): NCDHW fp32
+ * x [nc][d][h][w] -> y [nc][sd][sh][sw]; backward by three separable gather passes (ws: *_bwd_ws_floats). */
+int u3d_upsample_trilinear(const float* x, long long nc, int d, int h, int w, int s, float* y, u3d_stream_t stream);
+long long u3d_upsample_trilinear_bwd_ws_floats(long long nc, int d, int h, int w, int s);
+int u3d_upsample_trilinear_bwd(const float* dy, long long nc, int d, int h, int w, int s, float* dx, int accumulate,
+                               float* ws, u3d_stream_t stream);
+/* renew_token (unet3D.py:1051-1068) for one feature level x ([n][v][c] with element strides sv (voxel), sc
+ * (channel); batch stride v*c: NDHWC sv=c,sc=1; NCDHW sv=1,sc=v) and the full-size label mask [n][md][mh][mw]
+ * (nearest-resized): token[l] (ntok rows of c) <- (1-alpha) token[l] + alpha * mean of row r of x[:,:][mask==l+1]
+ * reshaped (c, -1) (B > 1 row quirk kept), for every class l < ncls with selected voxels. ws:
+ * u3d_renew_token_ws_bytes. */
+long long u3d_renew_token_ws_bytes(int n, int d, int h, int w, int ncls, int c);
+int u3d_renew_token(int dtype, const void* x, long long sv, long long sc, int n, int d, int h, int w, int c,
+                    const float* mask, int md, int mh, int mw, int ncls, int ntok, float alpha, float* tok, void* ws,
+                    u3d_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

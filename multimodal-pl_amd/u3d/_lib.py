@@ -67,8 +67,20 @@ _SIGS = {
     "u3d_dynhead_bwd_blocks": [L],
     "u3d_dynhead_bwd": [P, P, P, I, L, P, P, P, P],
     "u3d_dyn_controller_bwd": [I, P, I, I, P, I, P, P, I, P, P, I, L, P, P],
+    "u3d_eam_prep": [P, I, I, P, P, P, P, F, P, P, P, P],
+    "u3d_eam_attn_fwd": [I, P, I, L, I, P, P, P, I, P, P],
+    "u3d_eam_attn_bwd_blocks": [I, L],
+    "u3d_eam_attn_bwd_part_floats": [I, L, I, I],
+    "u3d_eam_attn_bwd": [I, P, I, L, I, P, P, P, I, P, P, I, P, P, P, P, I, P],
+    "u3d_eam_param_bwd": [P, I, I, P, P, P, P, P, P, F, P, P, P, P, P, P, I, P],
+    "u3d_upsample_trilinear": [P, L, I, I, I, I, P, P],
+    "u3d_upsample_trilinear_bwd_ws_floats": [L, I, I, I, I],
+    "u3d_upsample_trilinear_bwd": [P, L, I, I, I, I, P, I, P, P],
+    "u3d_renew_token_ws_bytes": [I, I, I, I, I, I],
+    "u3d_renew_token": [I, P, L, L, I, I, I, I, I, P, I, I, I, I, I, F, P, P, P],
 }
-_RESTYPE = {"u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L}
+_RESTYPE = {"u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
+            "u3d_eam_attn_bwd_part_floats": L, "u3d_upsample_trilinear_bwd_ws_floats": L, "u3d_renew_token_ws_bytes": L}
 
 _lib = None
 

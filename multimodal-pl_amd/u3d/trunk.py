@@ -82,6 +82,7 @@ class Tape:
         for pre in blocks:
             plan += [(pre + c, std, True) for c in ("conv1", "downsample.2", "conv2")]
         plan += [("fusionConv.2", std, True), ("precls_conv.2", False, True)]
+        plan += [(f"deepout{k}.2", False, True) for k in (1, 2, 3)]  # unet3D_with_feam3 deep supervision
         return plan
 
     def pend_wgrad(self, part, ns, W, st, std, name):
@@ -267,9 +268,11 @@ class Tape:
             skips.append(t)
         f = self.gn_conv(t, "fusionConv.2", 1, 1, gn_key="fusionConv.0", G=cfg.fusion_groups)
         bott = f
+        self.dec = []  # decoder features after x8/x4/x2/x1_resb (unet3D_with_feam3 heads read the first three)
         for name, s in zip(["x8_resb", "x4_resb", "x2_resb", "x1_resb"], [skips[3], skips[2], skips[1], skips[0]]):
             u = self.up_add(f, s)
             f = self.block(u, name + ".0.", 1, cfg.groups)
+            self.dec.append(f)
         return f, bott
 
     def head(self, f, cfg):

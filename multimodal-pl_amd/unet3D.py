@@ -221,8 +221,100 @@ def _next_row(name, row):
     return ctor
 
 
+class EAM(nn.Module):
+    """Reference unet3D.py:142-212 (same parameters: kv, q, proj, norm2, norm3). Inside unet3D_with_feam3 its
+    attention map runs natively (u3d.feam: only ``attn`` is used there, :1134); called on its own it raises."""
+
+    def __init__(self, dim, input_resolution, num_heads, mlp_ratio=4., qkv_bias=True, qk_scale=None, drop=0.,
+                 attn_drop=0., drop_path=0., norm_layer=nn.LayerNorm, upsample=None, use_checkpoint=False):
+        super().__init__()
+        self.dim = dim
+        self.input_resolution = input_resolution
+        self.use_checkpoint = use_checkpoint
+        self.num_heads = num_heads
+        head_dim = dim // num_heads
+        self.scale = qk_scale or head_dim ** -0.5
+        self.kv = nn.Linear(dim, dim * 2, bias=False)
+        self.q = nn.Linear(dim, dim, bias=False)
+        self.softmax = nn.Softmax(dim=-1)
+        self.proj = nn.Linear(dim, dim)
+        self.norm2 = norm_layer(dim)
+        self.norm3 = norm_layer(dim)
+
+    def forward(self, x, modality_token):
+        raise U3DError("EAM: the native path runs it inside unet3D_with_feam3 (u3d.feam); standalone use is not "
+                       "on the hot path")
+
+
+class unet3D_with_feam3(_TrunkMixin, nn.Module):
+    """Reference unet3D.py:938-1190 (the model train_amos_atlas_final.py:118 trains): the trunk + deep-supervision
+    heads deepout1-3 + EAM attention maps against EMA class tokens. forward(input, mask=None) -> train:
+    (logits, atten_map[<=3], deep_map[3], feature_stored[3]); eval: logits. Batch 1 when use_cm (the reference's
+    EAM reshapes with the token's batch of 1 and raises otherwise)."""
+
+    def __init__(self, layers, num_classes=12, weight_std=False, ema=False, use_cm=[True, True, True],  # noqa: B006
+                 deep_up=False):
+        self.inplanes = 128
+        self.weight_std = weight_std
+        self.num_classes = num_classes
+        self.use_cm = use_cm
+        self.alpha = 0.01
+        self.deep_up = deep_up
+        super().__init__()
+        mk = lambda cin, cout, n, s: _make_layer(self, NoBottleneck, cin, cout, n, stride=s)  # noqa: E731
+        self.conv1 = conv3x3x3(1, 32, stride=[1, 1, 1], weight_std=self.weight_std)
+        self.layer0 = mk(32, 32, layers[0], (1, 1, 1))
+        self.layer1 = mk(32, 64, layers[1], (2, 2, 2))
+        self.layer2 = mk(64, 128, layers[2], (2, 2, 2))
+        self.layer3 = mk(128, 256, layers[3], (2, 2, 2))
+        self.layer4 = mk(256, 256, layers[4], (2, 2, 2))
+        self.fusionConv = nn.Sequential(
+            nn.GroupNorm(16, 256), nn.ReLU(inplace=in_place),
+            conv3x3x3(256, 256, kernel_size=(1, 1, 1), padding=(0, 0, 0), weight_std=self.weight_std))
+        self.upsamplex2 = nn.Upsample(scale_factor=2, mode="trilinear")
+        self.upsamplex3 = nn.Upsample(scale_factor=4, mode="trilinear")
+        self.upsamplex4 = nn.Upsample(scale_factor=8, mode="trilinear")
+        head = lambda c: nn.Sequential(nn.GroupNorm(16, c), nn.ReLU(inplace=in_place),  # noqa: E731
+                                       nn.Conv3d(c, num_classes, kernel_size=1))
+        self.x8_resb = mk(256, 128, 1, (1, 1, 1))
+        self.deepout1 = head(128)
+        self.eam84 = EAM(128, input_resolution=None, num_heads=4)
+        self.x4_resb = mk(128, 64, 1, (1, 1, 1))
+        self.deepout2 = head(64)
+        self.eam42 = EAM(64, input_resolution=None, num_heads=4)
+        self.x2_resb = mk(64, 32, 1, (1, 1, 1))
+        self.deepout3 = head(32)
+        self.eam21 = EAM(32, input_resolution=None, num_heads=4)
+        self.x1_resb = mk(32, 32, 1, (1, 1, 1))
+        self.precls_conv = head(32)
+        # class tokens: plain tensors (not parameters / buffers, so not in the state_dict), :1016-1021
+        self.class_token1 = torch.randn(num_classes - 1, 128)
+        self.class_token2 = torch.randn(num_classes - 1, 64)
+        self.class_token3 = torch.randn(num_classes - 1, 32)
+        self._u3d_cfg = trunk.TrunkCfg(layers=tuple(layers), weight_std=bool(self.weight_std))
+        if ema:
+            for param in self.parameters():
+                param.detach_()
+
+    def renew_token(self, features, mask):
+        """EMA update of the class tokens from the stored features (:1051-1068), on the device."""
+        from u3d import feam
+        dev = mask.device
+        self.class_token1 = self.class_token1.to(dev)
+        self.class_token2 = self.class_token2.to(dev)
+        self.class_token3 = self.class_token3.to(dev)
+        feam.renew_token([self.class_token1, self.class_token2, self.class_token3], features, mask,
+                         self.num_classes, self.alpha)
+
+    def forward(self, input, mask=None):
+        from u3d import feam
+        self.class_token1 = self.class_token1.to(input.device)
+        self.class_token2 = self.class_token2.to(input.device)
+        self.class_token3 = self.class_token3.to(input.device)
+        return feam.run_feam3(self, input)
+
+
 # Method-specific variants and discriminators (SURVEY.md §2 rows 3-4): next rows, not on the trunk path.
-unet3D_with_feam3 = _next_row("unet3D_with_feam3", "f2")
 unet3D_with_feam2 = _next_row("unet3D_with_feam2", "f2")
 unet3D_with_feam = _next_row("unet3D_with_feam", "f2")
 unet3D_with_eam = _next_row("unet3D_with_eam", "f2")

@@ -1,0 +1,159 @@
+"""f2: unet3D_with_feam3 on the native path (u3d.feam, eam.hip) against the reference's G8 golden vectors and the
+CPU oracle. fp32 parity mode: logits / deep maps / features <= 1e-3 max-abs (north_star), attention maps <= 1e-3
+relative to their scale, parameter-gradient norms rtol 2e-3 (as the trunk parity tests), renew_token tokens
+<= 1e-5. bf16 mode: the attention / deep maps of the bf16 run against fp32 within 3e-2 norm-wise."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import ref_cpu as O
+from oracle.weights_recipe import apply_recipe, input_volume, param_array
+
+pytestmark = pytest.mark.gpu
+NC = 14
+
+
+def _model(gpu, deep_up=False, use_cm=(True, True, True)):
+    import unet3D
+    m = unet3D.unet3D_with_feam3([1, 2, 2, 2, 2], num_classes=NC, weight_std=True, use_cm=list(use_cm),
+                                 deep_up=deep_up)
+    apply_recipe(m, seed=0)
+    for k, c in ((1, 128), (2, 64), (3, 32)):
+        setattr(m, f"class_token{k}", torch.from_numpy(param_array(f"class_token{k}", (NC - 1, c), 0)))
+    return m.to(gpu).train()
+
+
+def _x(gpu):
+    return torch.from_numpy(input_volume((1, 1, 32, 32, 32), seed=80, kind="normal")).to(gpu)
+
+
+def _projections(deep_up, shapes):
+    rng = np.random.default_rng([81, 1 if deep_up else 0])
+    return [torch.from_numpy(rng.standard_normal(s).astype(np.float32)) for s in shapes]
+
+
+def test_feam3_state_dict_matches_reference_keys():
+    import unet3D
+    m = unet3D.unet3D_with_feam3([1, 2, 2, 2, 2], num_classes=NC, weight_std=True)
+    assert [(k, tuple(v.shape)) for k, v in m.state_dict().items()] == \
+        [(k, tuple(s)) for k, s in O.state_shapes_feam3(NC)]
+
+
+@pytest.mark.parametrize("deep_up", [False, True])
+def test_feam3_forward_backward_vs_golden(gpu, deep_up):
+    g = golden("g8_feam3_32.npz")
+    tag = "du" if deep_up else "nd"
+    m = _model(gpu, deep_up)
+    logits, att, deep, feats = m(_x(gpu))
+    assert len(att) == 3 and len(deep) == 3 and len(feats) == 3
+    if deep_up:
+        for i in range(3):
+            assert att[i].shape == (1, NC - 1, 32, 32, 32)
+            flat = att[i].detach().reshape(-1).cpu()
+            ref = g[f"du_att{i}_val"]
+            err = np.abs(flat[torch.from_numpy(g[f"du_att{i}_idx"])].numpy() - ref).max()
+            assert err < 1e-3 * max(1.0, np.abs(ref).max()), (i, err)
+    else:
+        assert np.abs(logits.detach().cpu().numpy() - g["nd_logits"]).max() < 1e-3
+        for i in range(3):
+            ref = g[f"nd_att{i}"]
+            err = np.abs(att[i].detach().cpu().numpy() - ref).max()
+            assert err < 1e-3 * max(1.0, np.abs(ref).max()), (i, err)
+            assert np.abs(deep[i].detach().cpu().numpy() - g[f"nd_deep{i}"]).max() < 1e-3
+            assert np.abs(feats[i].float().cpu().numpy() - g[f"feat{i}"]).max() < 1e-3
+            assert not feats[i].requires_grad
+    outs = [logits] + att + deep
+    ups = _projections(deep_up, [tuple(t.shape) for t in outs])
+    sum((t * u.to(gpu)).sum() for t, u in zip(outs, ups)).backward()
+    named = dict(m.named_parameters())
+    for i, k in enumerate(g[f"{tag}_gnames"]):
+        p = named[str(k)]
+        if g[f"{tag}_gnorm"][i] < 0:
+            assert p.grad is None, k               # eamXX.proj: unused in the reference too
+            continue
+        gn = p.grad.double().norm().item()
+        np.testing.assert_allclose(gn, g[f"{tag}_gnorm"][i], rtol=2e-3, atol=1e-5, err_msg=str(k))
+
+
+def test_feam3_only_logits_grad_matches_baseline_path(gpu):
+    """Pre-train branch (losses.py:179-182): only the logits carry gradient; attention / deep maps get None."""
+    m = _model(gpu)
+    logits, att, deep, _ = m(_x(gpu))
+    (logits * 1e-3).sum().backward()
+    assert m.eam84.kv.weight.grad is None and m.deepout1[2].weight.grad is None
+    assert torch.isfinite(m.conv1.weight.grad).all()
+
+
+def test_feam3_eval_returns_logits(gpu):
+    g = golden("g8_feam3_32.npz")
+    m = _model(gpu).eval()
+    with torch.no_grad():
+        y = m(_x(gpu))
+    assert torch.is_tensor(y) and y.shape == (1, NC, 32, 32, 32)
+    assert np.abs(y.cpu().numpy() - g["nd_logits"]).max() < 1e-3
+
+
+def test_feam3_batch2_raises_like_reference(gpu):
+    m = _model(gpu)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(2, 1, 32, 32, 32, device=gpu))
+    m2 = _model(gpu, use_cm=(False, False, False))
+    logits, att, deep, feats = m2(torch.zeros(2, 1, 32, 32, 32, device=gpu))
+    assert att == [] and len(deep) == 3 and logits.shape[0] == 2
+
+
+def test_renew_token_vs_golden(gpu):
+    g = golden("g8_feam3_32.npz")
+    m = _model(gpu)
+    feats = [torch.from_numpy(g[f"feat{i}"]).to(gpu) for i in range(3)]
+    m.renew_token(feats, torch.from_numpy(g["renew_mask"]).to(gpu))
+    for k in range(3):
+        np.testing.assert_allclose(getattr(m, f"class_token{k + 1}").cpu().numpy(), g[f"renew_tok{k + 1}"],
+                                   rtol=1e-5, atol=1e-5)
+    # the B = 2 row quirk of x[:,:][cmask].reshape(C, -1) (unet3D.py:1064)
+    m = _model(gpu)
+    feats = [torch.from_numpy(g[f"q_feat{i}"]).to(gpu) for i in range(3)]
+    m.renew_token(feats, torch.from_numpy(g["q_mask"]).to(gpu))
+    for k in range(3):
+        np.testing.assert_allclose(getattr(m, f"class_token{k + 1}").cpu().numpy(), g[f"q_tok{k + 1}"],
+                                   rtol=1e-5, atol=1e-5)
+
+
+def test_renew_token_on_native_features(gpu):
+    """renew_token on the model's own (NDHWC-stored) features equals the oracle on the same values."""
+    g = golden("g8_feam3_32.npz")
+    m = _model(gpu)
+    _, _, _, feats = m(_x(gpu))
+    mask = torch.from_numpy(g["renew_mask"])
+    toks = [getattr(m, f"class_token{k}").cpu().clone() for k in (1, 2, 3)]
+    O.renew_token(toks, [f.float().cpu() for f in feats], mask, NC)
+    m.renew_token(feats, mask.to(gpu))
+    for k in range(3):
+        np.testing.assert_allclose(getattr(m, f"class_token{k + 1}").cpu().numpy(), toks[k].numpy(), rtol=1e-5,
+                                   atol=1e-5)
+
+
+@pytest.mark.parametrize("s", [2, 4, 8])
+def test_upsample_trilinear_scale(gpu, s):
+    from u3d import feam
+    torch.manual_seed(s)
+    x = torch.randn(2, 3, 3, 5, 4)
+    y = feam.upsample_trilinear(x.to(gpu), s)
+    ref = torch.nn.functional.interpolate(x, scale_factor=s, mode="trilinear")
+    assert (y.cpu() - ref).abs().max() < 1e-5
+    xr = x.clone().requires_grad_(True)
+    up = torch.randn(ref.shape)
+    (torch.nn.functional.interpolate(xr, scale_factor=s, mode="trilinear") * up).sum().backward()
+    dx = feam.upsample_trilinear_bwd(up.to(gpu), tuple(x.shape), s)
+    assert (dx.cpu() - xr.grad).abs().max() < 1e-4
+
+
+def test_feam3_bf16_attention_close_to_fp32(gpu):
+    m = _model(gpu)
+    with torch.no_grad():
+        _, att32, deep32, _ = m(_x(gpu))
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        _, att16, deep16, _ = m(_x(gpu))
+    for a, b in zip(att32 + deep32, att16 + deep16):   # norm-wise: bf16 activations through the whole trunk
+        assert ((a - b.float()).norm() / a.norm()).item() < 3e-2
