@@ -321,6 +321,31 @@ int u3d_renew_token(int dtype, const void* x, long long sv, long long sc, int n,
                     const float* mask, int md, int mh, int mw, int ncls, int ntok, float alpha, float* tok, void* ws,
                     u3d_stream_t stream);
 
+/* ---------------------------------------------------------------- consistency branch of get_loss (f2/f3)
+ * losses.py:131-178: for every organ g with label_t[g] == 0 and every map k (natt attention maps through a sigmoid,
+ * then softmax(logits)[g+1]) the soft Dice vs t = softmax(refine[g])[1] over the refiner-confident voxels
+ * (t > 1-confi or t < confi), weighted [0.125,0.25,0.5,1][k] * weight_feature / (nt - supcount). Layouts by element
+ * strides: att maps (organ att_sc, voxel att_sv), logits (voxel lsv, class lsc), refine (organ rsn, class rsc,
+ * voxel rsv). Outputs: aux[1] (the weighted sum), dice [nt][4], coef [nt][4][2] (for the backward). Batch 1. */
+long long u3d_consistency_ws_bytes(int nt);
+int u3d_consistency_fwd(const float* att0, const float* att1, const float* att2, int natt, long long att_sc,
+                        long long att_sv, const float* logits, long long lsv, long long lsc, int C, const float* refine,
+                        long long rsn, long long rsc, long long rsv, const float* label_t, int nt, long long V,
+                        float confi, float weight_feature, float* aux, float* dice, float* coef, void* ws,
+                        u3d_stream_t stream);
+/* gradients (scaled by grad_out[0]): datt_k [nt][V] contiguous, dlogits [V][C] contiguous (NDHWC) */
+int u3d_consistency_bwd(const float* att0, const float* att1, const float* att2, int natt, long long att_sc,
+                        long long att_sv, const float* logits, long long lsv, long long lsc, int C, const float* refine,
+                        long long rsn, long long rsc, long long rsv, const float* label_t, int nt, long long V,
+                        float confi, const float* coef, const float* grad_out, float* datt0, float* datt1,
+                        float* datt2, float* dlogits, u3d_stream_t stream);
+/* EDiceLoss_full2 (loss_partial.py:137-170) on contiguous x, t, m (nullable) of V elements: masked soft dice of
+ * sigmoid(x) (or x) vs t, + mean BCEWithLogits(x, t) when uce. ws: 128*4 doubles. coef[3] feeds the backward. */
+int u3d_edice_full2_fwd(const float* x, const float* t, const float* m, long long V, int sigmoid, int uce,
+                        float* loss, float* coef, void* ws, u3d_stream_t stream);
+int u3d_edice_full2_bwd(const float* x, const float* t, const float* m, long long V, int sigmoid, const float* coef,
+                        const float* grad_out, float* dx, u3d_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,13 +77,17 @@ class EDiceLoss_full(nn.Module):
         return _L.partial_loss(inputs, target, w, mode=_L.MODE_SIGMOID, uce=0)
 
 
-def _next_row(name):
-    class _Missing(nn.Module):
-        def __init__(self, *a, **k):
-            raise NotImplementedError(f"{name}: consistency loss over the feam3 attention maps, SURVEY.md §8(f) "
-                                      "rows f2/f3 — not built yet")
-    _Missing.__name__ = name
-    return _Missing
+class EDiceLoss_full2(nn.Module):
+    """Reference loss_partial.py:137-170 (binary soft Dice on sigmoid(inputs) or inputs vs a soft target over the
+    mask, + BCEWithLogits when uce): one fused device pass each way (u3d_edice_full2_fwd/_bwd)."""
 
+    def __init__(self, n_classes):
+        super().__init__()
+        self.labels = ["ET", "TC", "WT"] + ["a"] * 20
+        self.device = "cpu"
+        self.n_classes = n_classes
+        self.diceloss = DiceLoss(n_classes=n_classes)
 
-EDiceLoss_full2 = _next_row("EDiceLoss_full2")
+    def forward(self, inputs, target, uce=True, mask=None, sigmoid=True):
+        from u3d import loss as L
+        return L.edice_full2(inputs, target, uce=uce, mask=mask, sigmoid=sigmoid)

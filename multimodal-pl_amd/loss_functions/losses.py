@@ -1,18 +1,30 @@
-"""Drop-in for the reference loss_functions/losses.py: the pre-train branch of get_loss (losses.py:107-113,
-179-182), which is what train_amos_atlas_final.py:303-304 calls for epoch < pretrain_epoch, and the refiner
-loss get_loss_refine (:46-62)."""
+"""Drop-in for the reference loss_functions/losses.py: get_loss — the pre-train branch (losses.py:107-113,
+179-182, train_amos_atlas_final.py:303-304) and the refiner-consistency branch over the feam3 attention maps
+(:131-178, train_amos_atlas_final.py:312) — and the refiner loss get_loss_refine (:46-62)."""
+import torch
+
 from loss_functions.loss_partial import EDiceLoss_full, EDiceLoss_partial
 
 
 def get_loss(output, cm, deep_out, target, mask=None, catlas=None, attns=None, refine_output=None, label_t=None,
              discard=0.05, confi_=0.10, aux_weight=1, weight_feature=0.1):
-    """Returns (EDiceLoss_partial(C)(output, target.squeeze(1), soft_max=True, mask=mask), confi_)."""
-    if len(deep_out) != 0 or refine_output is not None:
-        raise NotImplementedError("get_loss: deep supervision / refiner-consistency branches are SURVEY.md §8(f) "
-                                  "rows f2/f3 — not built yet")
+    """EDiceLoss_partial(C)(output, target.squeeze(1), soft_max=True, mask=mask); with ``refine_output`` plus the
+    consistency term: masked soft Dice of every attention map (sigmoid) and of softmax(output)[:, 1:] against the
+    refiner's confident foreground for the organs label_t marks unsupervised (u3d.loss.consistency_aux, one fused
+    pass). ``refine_label`` (:134-157) is never read by the reference and is not built; ``refine_output`` carries
+    no gradient (the driver computes it under no_grad, train_amos_atlas_final.py:285-287). Returns (loss, 0.10)."""
+    if len(deep_out) != 0:
+        raise NotImplementedError("get_loss: the deep_out branch (losses.py:119-129) is never used by the driver "
+                                  "(train_amos_atlas_final.py:304, 312 pass []) and is not built")
     edice = EDiceLoss_partial(output.shape[1])
     dice_loss = edice(output, target.squeeze(1), soft_max=True, mask=mask)
-    return dice_loss, confi_
+    if refine_output is None:
+        return dice_loss, confi_
+    from u3d import loss as L
+    if not torch.is_tensor(label_t):
+        label_t = torch.tensor(label_t, dtype=torch.float32)
+    aux = L.consistency_aux(output, list(attns), refine_output, label_t, weight_feature, confi=0.10)
+    return dice_loss + aux * aux_weight, 0.10
 
 
 def get_loss_refine(output, label, dlist, aug_mask=1):

@@ -78,9 +78,15 @@ _SIGS = {
     "u3d_upsample_trilinear_bwd": [P, L, I, I, I, I, P, I, P, P],
     "u3d_renew_token_ws_bytes": [I, I, I, I, I, I],
     "u3d_renew_token": [I, P, L, L, I, I, I, I, I, P, I, I, I, I, I, F, P, P, P],
+    "u3d_consistency_ws_bytes": [I],
+    "u3d_consistency_fwd": [P, P, P, I, L, L, P, L, L, I, P, L, L, L, P, I, L, F, F, P, P, P, P, P],
+    "u3d_consistency_bwd": [P, P, P, I, L, L, P, L, L, I, P, L, L, L, P, I, L, F, P, P, P, P, P, P, P],
+    "u3d_edice_full2_fwd": [P, P, P, L, I, I, P, P, P, P],
+    "u3d_edice_full2_bwd": [P, P, P, L, I, P, P, P, P],
 }
 _RESTYPE = {"u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
-            "u3d_eam_attn_bwd_part_floats": L, "u3d_upsample_trilinear_bwd_ws_floats": L, "u3d_renew_token_ws_bytes": L}
+            "u3d_eam_attn_bwd_part_floats": L, "u3d_upsample_trilinear_bwd_ws_floats": L, "u3d_renew_token_ws_bytes": L,
+            "u3d_consistency_ws_bytes": L}
 
 _lib = None
 

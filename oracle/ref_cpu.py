@@ -340,6 +340,49 @@ def state_shapes_feam3(num_classes=14):
     return out
 
 
+def _dice_loss_masked(score, target, mask):
+    """DiceLoss._dice_loss, loss_partial.py:24-36: score[mask], target[mask.squeeze(1)], smooth 1e-5."""
+    s = score[mask.bool()]
+    t = target.float()[mask.squeeze(1).bool()]
+    return 1 - (2 * torch.sum(s * t) + 1e-5) / (torch.sum(s * s) + torch.sum(t * t) + 1e-5)
+
+
+def edice_full2(inputs, target, uce=True, mask=None, sigmoid=True):
+    """EDiceLoss_full2.forward, loss_partial.py:150-170: masked soft dice of sigmoid(inputs) (or inputs) vs the
+    soft target; + BCEWithLogits(inputs.squeeze(0), target) (mean, unmasked) when uce."""
+    s = torch.sigmoid(inputs) if sigmoid else inputs
+    if mask is None:
+        mask = torch.ones_like(target).unsqueeze(0)
+    d = _dice_loss_masked(s, target, mask)
+    if uce:
+        d = d + F.binary_cross_entropy_with_logits(inputs.float().squeeze(0), target.float())
+    return d
+
+
+def get_loss_consistency(output, target, mask, attns, refine_output, label_t, confi_=0.10, aux_weight=1,
+                         weight_feature=0.1):
+    """get_loss, losses.py:107-113 + 131-178 (refine_output given, no deep_out): EDiceLoss_partial(output) +
+    sum over maps (3 attention maps, then softmax(output)[:, 1:]) and unsupervised organs gan (label_t[gan] == 0)
+    of EDiceLoss_full2(map[:, gan], softmax(refine)[gan, 1], mask = refiner confident (p > 1-confi or p < confi),
+    sigmoid except for the softmax map) / (num_classes - supcount) * [0.125, .25, .5, 1][idx] * weight_feature.
+    ``refine_label`` (:134-157) is built by the reference but never read, so it is not restated."""
+    dice_loss = edice_partial(output, target.squeeze(1), mask=mask)
+    num_classes = output.shape[1] - 1
+    weights = [0.125, 0.25, 0.5, 1]
+    p = torch.softmax(refine_output, 1)
+    confi = torch.logical_or(p > (1 - confi_), p < confi_).float()
+    supcount = int(sum(1 for l in range(refine_output.shape[0]) if label_t[l]))
+    maps = list(attns) + [torch.softmax(output, 1)[:, 1:]]
+    aux = 0.0
+    for idx, l in enumerate(maps):
+        for gan in range(num_classes):
+            if not label_t[gan]:
+                cd = edice_full2(l[:, gan:gan + 1], p[gan:gan + 1, 1], uce=False, sigmoid=idx != 3,
+                                 mask=confi[gan:gan + 1, 1:])
+                aux = aux + cd / (num_classes - supcount) * weights[idx] * weight_feature
+    return dice_loss + aux * aux_weight
+
+
 def params_from_module_dict(sd):
     return {k: v.detach().float().cpu() for k, v in sd.items()}
 

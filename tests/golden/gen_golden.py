@@ -374,7 +374,50 @@ def g8():
     save("g8_feam3_32.npz", **out)
 
 
+def g9():
+    """f2/f3: the consistency branch of get_loss (losses.py:107-113, 131-178: EDiceLoss_partial + masked
+    EDiceLoss_full2 between each attention map / the output's softmax and the refiner's confident foreground) and
+    EDiceLoss_full2 itself (loss_partial.py:137-170): values + gradients w.r.t. output and attention maps."""
+    from loss_functions import losses as RL
+    rng = np.random.default_rng([9, 9])
+    sp = (12, 10, 8)
+    out = {}
+    C = 14
+    for tag, lt in (("mix", [1, 0, 0, 1, 0, 1, 1, 0, 0, 0, 1, 0, 0]), ("none", [0] * 13), ("all", [1] * 13)):
+        lg = torch.from_numpy((rng.standard_normal((1, C) + sp) * 2).astype(np.float32)).requires_grad_(True)
+        lab = torch.from_numpy(rng.integers(0, C, (1, 1) + sp).astype(np.float32))
+        mvec = torch.from_numpy(np.concatenate([[1], rng.integers(0, 2, 14)]).astype(np.int64))
+        att = [torch.from_numpy((rng.standard_normal((1, C - 1) + sp) * 3).astype(np.float32)).requires_grad_(True)
+               for _ in range(3)]
+        ref = torch.from_numpy((rng.standard_normal((C - 1, 2) + sp) * 3).astype(np.float32))
+        label_t = torch.tensor(lt).float()
+        attl = list(att)
+        v, conf = RL.get_loss(lg, 0, [], lab, [mvec], None, attl, ref, label_t, weight_feature=0.07)
+        assert len(attl) == 3
+        v.backward()
+        out[f"{tag}_logits"], out[f"{tag}_labels"], out[f"{tag}_mask"] = lg.detach().numpy(), lab.numpy(), mvec.numpy()
+        out[f"{tag}_refine"], out[f"{tag}_label_t"] = ref.numpy(), label_t.numpy()
+        out[f"{tag}_value"], out[f"{tag}_dlogits"] = v.detach().numpy(), lg.grad.numpy()
+        for i in range(3):
+            gr = att[i].grad   # None when every organ is supervised (no aux term touches the maps)
+            out[f"{tag}_att{i}"] = att[i].detach().numpy()
+            out[f"{tag}_datt{i}"] = gr.numpy() if gr is not None else np.zeros(att[i].shape, np.float32)
+    # EDiceLoss_full2 alone: sigmoid / identity, with and without mask, uce on/off
+    x = torch.from_numpy((rng.standard_normal((1, 1) + sp) * 2).astype(np.float32))
+    t = torch.from_numpy(rng.uniform(0, 1, (1,) + sp).astype(np.float32))
+    m = torch.from_numpy((rng.uniform(0, 1, (1, 1) + sp) > 0.4).astype(np.float32))
+    out["f2_x"], out["f2_t"], out["f2_m"] = x.numpy(), t.numpy(), m.numpy()
+    for tag, kw in (("sig_m", dict(uce=False, mask=m)), ("sig_nom", dict(uce=False)),
+                    ("id_m", dict(uce=False, mask=m, sigmoid=False)), ("sig_uce", dict(uce=True, mask=m))):
+        xi = (torch.sigmoid(x) if tag.startswith("id") else x).clone().requires_grad_(True)
+        v = RLP.EDiceLoss_full2(2)(xi, t, **kw)
+        v.backward()
+        out[f"f2_{tag}_in"], out[f"f2_{tag}_value"], out[f"f2_{tag}_grad"] = xi.detach().numpy(), \
+            v.detach().numpy(), xi.grad.numpy()
+    save("g9_consistency.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9"]
     for w in which:
         globals()[w]()

@@ -299,3 +299,65 @@ def test_partial_target_vs_oracle(gpu):
     got = ops.partial_target(torch.from_numpy(lab).to(gpu), torch.from_numpy(masks)).cpu().numpy()
     ref = np.stack([O.partial_target(lab[i:i + 1], masks[i])[0] for i in range(2)])
     np.testing.assert_array_equal(got.reshape(ref.shape), ref)
+
+
+# ------------------------------------------------------------- f2/f3: consistency branch of get_loss (G9)
+@pytest.mark.parametrize("tag", ["mix", "none", "all"])
+def test_g9_get_loss_consistency(gpu, tag):
+    from loss_functions.losses import get_loss
+    g = golden("g9_consistency.npz")
+    lg = torch.from_numpy(g[f"{tag}_logits"]).to(gpu).requires_grad_(True)
+    att = [torch.from_numpy(g[f"{tag}_att{i}"]).to(gpu).requires_grad_(True) for i in range(3)]
+    attl = list(att)
+    v, conf = get_loss(lg, 0, [], torch.from_numpy(g[f"{tag}_labels"]).to(gpu),
+                       [torch.from_numpy(g[f"{tag}_mask"]).to(gpu)], None, attl,
+                       torch.from_numpy(g[f"{tag}_refine"]).to(gpu), torch.from_numpy(g[f"{tag}_label_t"]),
+                       weight_feature=0.07)
+    assert len(attl) == 3 and conf == 0.10
+    np.testing.assert_allclose(float(v), float(g[f"{tag}_value"]), rtol=1e-4)
+    v.backward()
+    ref = g[f"{tag}_dlogits"]
+    np.testing.assert_allclose(lg.grad.cpu().numpy(), ref, rtol=1e-3, atol=1e-4 * np.abs(ref).max())
+    for i in range(3):
+        ref = g[f"{tag}_datt{i}"]
+        got = att[i].grad.cpu().numpy() if att[i].grad is not None else np.zeros_like(ref)
+        np.testing.assert_allclose(got, ref, rtol=1e-3, atol=1e-4 * max(np.abs(ref).max(), 1e-12))
+
+
+def test_g9_edice_full2(gpu):
+    from loss_functions.loss_partial import EDiceLoss_full2
+    g = golden("g9_consistency.npz")
+    t, m = torch.from_numpy(g["f2_t"]).to(gpu), torch.from_numpy(g["f2_m"]).to(gpu)
+    for tag, kw in (("sig_m", dict(uce=False, mask=m)), ("sig_nom", dict(uce=False)),
+                    ("id_m", dict(uce=False, mask=m, sigmoid=False)), ("sig_uce", dict(uce=True, mask=m))):
+        xi = torch.from_numpy(g[f"f2_{tag}_in"]).to(gpu).requires_grad_(True)
+        v = EDiceLoss_full2(2)(xi, t, **kw)
+        np.testing.assert_allclose(float(v), float(g[f"f2_{tag}_value"]), rtol=1e-4)
+        v.backward()
+        ref = g[f"f2_{tag}_grad"]
+        np.testing.assert_allclose(xi.grad.cpu().numpy(), ref, rtol=1e-3, atol=1e-4 * np.abs(ref).max())
+
+
+def test_consistency_on_native_feam3_outputs(gpu):
+    """End to end: feam3 (deep_up) outputs + a native refiner's output -> get_loss consistency branch, gradients
+    through the attention maps into the model, against the oracle on the same values."""
+    import unet3D
+    from loss_functions.losses import get_loss
+    torch.manual_seed(3)
+    m = unet3D.unet3D_with_feam3([1, 2, 2, 2, 2], num_classes=14, weight_std=True, deep_up=True)
+    apply_recipe(m, seed=0)
+    m = m.to(gpu).train()
+    x = torch.from_numpy(input_volume((1, 1, 32, 32, 32), seed=5, kind="normal")).to(gpu)
+    logits, att, _, _ = m(x)
+    refine = torch.randn(13, 2, 32, 32, 32, device=gpu) * 3
+    lab = torch.from_numpy(label_volume((1, 1, 32, 32, 32), 14, seed=6)).to(gpu)
+    mvec = torch.ones(15, dtype=torch.int64, device=gpu)
+    lt = torch.tensor([1, 0, 0, 1, 0, 1, 1, 0, 0, 0, 1, 0, 0]).float()
+    v, _ = get_loss(logits, 0, [], lab, [mvec], None, att, refine, lt, weight_feature=0.1)
+    lgc = logits.detach().cpu().requires_grad_(True)
+    atc = [a.detach().cpu().requires_grad_(True) for a in att]
+    vr = O.get_loss_consistency(lgc, lab.cpu(), [mvec.cpu()], atc, refine.cpu(), lt, weight_feature=0.1)
+    np.testing.assert_allclose(float(v), float(vr), rtol=1e-4)
+    v.backward()
+    vr.backward()
+    assert torch.isfinite(m.eam21.kv.weight.grad).all() and m.eam21.kv.weight.grad.abs().sum() > 0

@@ -268,3 +268,32 @@ def test_g8_feam3_batch2_raises_like_reference():
     params = P(O.state_shapes_feam3(14))
     with pytest.raises(RuntimeError):
         O.feam3_forward(params, feam3_tokens(), torch.zeros(2, 1, 16, 16, 16), 14)
+
+
+# ------------------------------------------------------------------------------- f2/f3: consistency loss
+@pytest.mark.parametrize("tag", ["mix", "none", "all"])
+def test_g9_consistency_loss(tag):
+    g = golden("g9_consistency.npz")
+    lg = torch.from_numpy(g[f"{tag}_logits"]).requires_grad_(True)
+    att = [torch.from_numpy(g[f"{tag}_att{i}"]).requires_grad_(True) for i in range(3)]
+    v = O.get_loss_consistency(lg, torch.from_numpy(g[f"{tag}_labels"]), [torch.from_numpy(g[f"{tag}_mask"])], att,
+                               torch.from_numpy(g[f"{tag}_refine"]), torch.from_numpy(g[f"{tag}_label_t"]),
+                               weight_feature=0.07)
+    np.testing.assert_allclose(float(v), float(g[f"{tag}_value"]), rtol=1e-5)
+    v.backward()
+    np.testing.assert_allclose(lg.grad.numpy(), g[f"{tag}_dlogits"], rtol=1e-4, atol=1e-9)
+    for i in range(3):
+        gr = att[i].grad.numpy() if att[i].grad is not None else np.zeros(att[i].shape, np.float32)
+        np.testing.assert_allclose(gr, g[f"{tag}_datt{i}"], rtol=1e-4, atol=1e-9)
+
+
+def test_g9_edice_full2():
+    g = golden("g9_consistency.npz")
+    t, m = torch.from_numpy(g["f2_t"]), torch.from_numpy(g["f2_m"])
+    for tag, kw in (("sig_m", dict(uce=False, mask=m)), ("sig_nom", dict(uce=False)),
+                    ("id_m", dict(uce=False, mask=m, sigmoid=False)), ("sig_uce", dict(uce=True, mask=m))):
+        xi = torch.from_numpy(g[f"f2_{tag}_in"]).requires_grad_(True)
+        v = O.edice_full2(xi, t, **kw)
+        np.testing.assert_allclose(float(v), float(g[f"f2_{tag}_value"]), rtol=1e-5)
+        v.backward()
+        np.testing.assert_allclose(xi.grad.numpy(), g[f"f2_{tag}_grad"], rtol=1e-4, atol=1e-9)
