@@ -347,8 +347,39 @@ __device__ __forceinline__ Lin lin_src(int dst, int n_in, float inv_s) {
   return r;
 }
 
+// four consecutive outputs along w per thread (one 16-B store); the d/h weights and the two source rows are shared
 __global__ __launch_bounds__(256) void up_tri_fwd_kernel(const float* __restrict__ x, long long nc, int d, int h, int w,
                                                         int s, float* __restrict__ y) {
+  const int od = d * s, oh = h * s, ow = w * s, ow4 = ow >> 2;
+  const float inv = 1.f / (float)s;
+  const long long total = nc * od * oh * ow4;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long row = e / ow4;
+    const int xw0 = (int)(e - row * ow4) * 4;
+    const int xh = (int)(row % oh);
+    const long long r2 = row / oh;
+    const int xd = (int)(r2 % od);
+    const long long ch = r2 / od;
+    const float* src = x + ch * d * h * w;
+    const Lin ld = lin_src(xd, d, inv), lh = lin_src(xh, h, inv);
+    const float* r00 = src + ((long long)ld.i0 * h + lh.i0) * w;
+    const float* r01 = src + ((long long)ld.i0 * h + lh.i1) * w;
+    const float* r10 = src + ((long long)ld.i1 * h + lh.i0) * w;
+    const float* r11 = src + ((long long)ld.i1 * h + lh.i1) * w;
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const Lin lw = lin_src(xw0 + j, w, inv);
+      const float v0 = lh.l0 * (lw.l0 * r00[lw.i0] + lw.l1 * r00[lw.i1]) + lh.l1 * (lw.l0 * r01[lw.i0] + lw.l1 * r01[lw.i1]);
+      const float v1 = lh.l0 * (lw.l0 * r10[lw.i0] + lw.l1 * r10[lw.i1]) + lh.l1 * (lw.l0 * r11[lw.i0] + lw.l1 * r11[lw.i1]);
+      o[j] = ld.l0 * v0 + ld.l1 * v1;
+    }
+    *reinterpret_cast<f32x4*>(y + row * ow + xw0) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void up_tri_fwd1_kernel(const float* __restrict__ x, long long nc, int d, int h, int w,
+                                                         int s, float* __restrict__ y) {
   const int od = d * s, oh = h * s, ow = w * s;
   const float inv = 1.f / (float)s;
   const long long total = nc * od * oh * ow;
@@ -508,35 +539,42 @@ __global__ __launch_bounds__(RT_CHUNK) void renew_partial_kernel(const T* __rest
   }
 }
 
-// one block per class; thread per row r: sum the runs that land in r (fixed order over sample, channel, chunk),
-// token[l][r] = token[l][r] (1 - alpha) + alpha * sum / L
-__global__ void renew_update_kernel(const float* __restrict__ part, int n, int nchunk, int ncls, int C, int ntok,
-                                    const int* __restrict__ off, const long long* __restrict__ K,
-                                    const long long* __restrict__ base, const long long* __restrict__ L, float alpha,
-                                    float* __restrict__ tok) {
-  const int l = blockIdx.x;
+// one block per (class l, row r): token[l][r] = token[l][r] (1 - alpha) + alpha * sum / L, the sum over the runs
+// that land in row r — (sample, channel) segments covering r (uniform test), their chunks strided over the
+// threads, then a fixed-order block reduction (deterministic)
+__global__ __launch_bounds__(256) void renew_update_kernel(const float* __restrict__ part, int n, int nchunk, int ncls,
+                                                          int C, int ntok, const int* __restrict__ off,
+                                                          const long long* __restrict__ K,
+                                                          const long long* __restrict__ base,
+                                                          const long long* __restrict__ L, float alpha,
+                                                          float* __restrict__ tok) {
+  const int l = blockIdx.x, r = blockIdx.y;
   const long long Ll = L[l];
   if (Ll == 0 || l >= ntok) return;  // no voxel of class l+1 at this size (:1055-1058)
-  for (int r = threadIdx.x; r < C; r += blockDim.x) {
-    double s = 0;
-    for (int b = 0; b < n; ++b) {
-      const long long Kb = K[b * ncls + l];
-      if (Kb == 0) continue;
-      for (int c_ = 0; c_ < C; ++c_) {
-        const long long seg0 = row_start(base[b * ncls + l], c_, Kb, 0, C);
-        const long long ra = seg0 / Ll, rb = (seg0 + Kb - 1) / Ll;
-        if (r < ra || r > rb) continue;
-        for (int chk = 0; chk < nchunk; ++chk) {
-          const long long kf = off[((long long)b * nchunk + chk) * ncls + l];
-          const long long p0 = seg0 + kf;
-          const long long r0 = p0 / Ll;
-          const float* pp = part + ((((long long)b * nchunk + chk) * ncls + l) * C + c_) * 2;
-          if (r0 == r) s += pp[0];
-          else if (r0 + 1 == r) s += pp[1];
-        }
+  double s = 0;
+  for (int b = 0; b < n; ++b) {
+    const long long Kb = K[b * ncls + l];
+    if (Kb == 0) continue;
+    for (int c_ = 0; c_ < C; ++c_) {
+      const long long seg0 = row_start(base[b * ncls + l], c_, Kb, 0, C);
+      if (r < seg0 / Ll || r > (seg0 + Kb - 1) / Ll) continue;
+      for (int chk = threadIdx.x; chk < nchunk; chk += blockDim.x) {
+        const long long r0 = (seg0 + off[((long long)b * nchunk + chk) * ncls + l]) / Ll;
+        const float* pp = part + ((((long long)b * nchunk + chk) * ncls + l) * C + c_) * 2;
+        if (r0 == r) s += pp[0];
+        else if (r0 + 1 == r) s += pp[1];
       }
     }
-    const float mean = (float)(s / (double)Ll);
+  }
+  __shared__ double red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float mean = (float)(red[0] / (double)Ll);
     tok[l * C + r] = tok[l * C + r] * (1.f - alpha) + mean * alpha;
   }
 }
@@ -629,8 +667,13 @@ extern "C" int u3d_upsample_trilinear(const float* x, long long nc, int d, int h
                                       u3d_stream_t stream) {
   U3D_REQUIRE(x && y && nc > 0 && d > 0 && h > 0 && w > 0 && s >= 1, "upsample_trilinear: bad args");
   const long long total = nc * (long long)d * h * w * s * s * s;
-  const int nb = (int)std::min<long long>(8192, (total + 255) / 256);
-  hipLaunchKernelGGL(up_tri_fwd_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, x, nc, d, h, w, s, y);
+  if ((w * s) % 4 == 0) {
+    const int nb = (int)std::min<long long>(8192, (total / 4 + 255) / 256);
+    hipLaunchKernelGGL(up_tri_fwd_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, x, nc, d, h, w, s, y);
+  } else {
+    const int nb = (int)std::min<long long>(8192, (total + 255) / 256);
+    hipLaunchKernelGGL(up_tri_fwd1_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, x, nc, d, h, w, s, y);
+  }
   return check_launch("up_tri_fwd_kernel");
 }
 
@@ -691,7 +734,7 @@ extern "C" int u3d_renew_token(int dtype, const void* x, long long sv, long long
   else
     hipLaunchKernelGGL(renew_partial_kernel<float>, dim3(nchunk, n), dim3(RT_CHUNK), 0, s, (const float*)x, sv, sc,
                        mask, d, h, w, md, mh, mw, ncls, c, nchunk, cnt, off, K, base, L, part);
-  hipLaunchKernelGGL(renew_update_kernel, dim3(ncls), dim3(256), 0, s, part, n, nchunk, ncls, c, ntok, off, K, base, L,
-                     alpha, tok);
+  hipLaunchKernelGGL(renew_update_kernel, dim3(ncls, c), dim3(256), 0, s, part, n, nchunk, ncls, c, ntok, off, K, base,
+                     L, alpha, tok);
   return check_launch("renew_token");
 }
