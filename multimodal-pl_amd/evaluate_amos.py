@@ -12,6 +12,7 @@ import math
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from u3d import ops
 from u3d.loss import ndhwc_view
@@ -93,27 +94,17 @@ def _as_ndhwc(pred):
     return p if p.is_contiguous() else p.contiguous()
 
 
-def predict_sliding(args, net_list, image, tile_size, classes, task_id, tta=False):
-    """Reference evaluate_amos.py:198-279. Returns full_probs [N, classes, D, H, W] as a device fp32 tensor (the
-    reference returns a float64 CPU tensor)."""
-    from u3d import _lib
-    dev = next(net_list[0].parameters()).device
-    img_all = torch.as_tensor(image).to(device=dev, dtype=torch.float32)
-    ops.require_device(img_all)
-    image_size = img_all.shape
+def tile_plan(image_size, tile_size):
+    """The reference's tile sequence (evaluate_amos.py:205-236): overlap 1/4, ceil strides, tiles clamped to the
+    volume. Returns [(d1, d2, y1, y2, x1, x2)] in the reference's dep/row/col order."""
     overlap = 1 / 4
     strideHW = math.ceil(tile_size[1] * (1 - overlap))
     strideD = math.ceil(tile_size[0] * (1 - overlap))
-    tile_deps = int(math.ceil((image_size[2] - tile_size[0]) / strideD) + 1)
-    tile_rows = int(math.ceil((image_size[3] - tile_size[1]) / strideHW) + 1)
-    tile_cols = int(math.ceil((image_size[4] - tile_size[2]) / strideHW) + 1)
-    N, D, H, W = image_size[0], image_size[2], image_size[3], image_size[4]
-    full = torch.zeros((N, classes, D, H, W), dtype=torch.float32, device=dev)
-    count = torch.zeros((N, D, H, W), dtype=torch.float32, device=dev)
-    (pd, ph, pw), gmin = _gaussian_profiles(tile_size)
-    gd, gh, gw = (torch.tensor(p, dtype=torch.float32, device=dev) for p in (pd, ph, pw))
-    flip_sets = [()] + ([(2,), (3,), (4,), (2, 3), (2, 4), (3, 4), (2, 3, 4)] if tta else [])
-    scale = 1.0 / (len(net_list) * len(flip_sets))
+    D, H, W = image_size[-3], image_size[-2], image_size[-1]
+    tile_deps = int(math.ceil((D - tile_size[0]) / strideD) + 1)
+    tile_rows = int(math.ceil((H - tile_size[1]) / strideHW) + 1)
+    tile_cols = int(math.ceil((W - tile_size[2]) / strideHW) + 1)
+    plan = []
     for dep in range(tile_deps):
         for row in range(tile_rows):
             for col in range(tile_cols):
@@ -122,19 +113,55 @@ def predict_sliding(args, net_list, image, tile_size, classes, task_id, tta=Fals
                 x2 = min(x1 + tile_size[2], W)
                 y2 = min(y1 + tile_size[1], H)
                 d1, x1, y1 = max(int(d2 - tile_size[0]), 0), max(int(x2 - tile_size[2]), 0), max(int(y2 - tile_size[1]), 0)
-                img = img_all[:, :, d1:d2, y1:y2, x1:x2].contiguous()
-                first = 1
-                for dims in flip_sets:
-                    inp = torch.flip(img, dims) if dims else img
-                    flags = sum({2: 1, 3: 2, 4: 4}[d] for d in dims)
-                    for net in net_list:
-                        p = _as_ndhwc(net(inp, task_id))
-                        if p.shape[-1] != classes or tuple(p.shape[1:4]) != (d2 - d1, y2 - y1, x2 - x1):
-                            raise ValueError(f"predict_sliding: prediction {tuple(p.shape)} does not match the tile "
-                                             f"({d2 - d1}, {y2 - y1}, {x2 - x1}) x {classes} classes")
-                        _lib.call("u3d_window_accumulate", p.data_ptr(), N, classes, d2 - d1, y2 - y1, x2 - x1,
-                                  gd.data_ptr(), gh.data_ptr(), gw.data_ptr(), float(gmin), float(scale),
-                                  full.data_ptr(), count.data_ptr(), D, H, W, d1, y1, x1, flags, first, ops._stream())
-                        first = 0
+                plan.append((d1, d2, y1, y2, x1, x2))
+    return plan
+
+
+def shard_tiles(plan, rank, world):
+    """Tiles are independent: rank r takes tiles r, r + world, ... (round-robin keeps the ranks'
+    shares within one tile of each other for any tile count)."""
+    return plan[rank::world]
+
+
+def predict_sliding(args, net_list, image, tile_size, classes, task_id, tta=False, group=None):
+    """Reference evaluate_amos.py:198-279. Returns full_probs [N, classes, D, H, W] as a device fp32 tensor (the
+    reference returns a float64 CPU tensor). With a process ``group`` of world size > 1 (one process per GPU) the
+    tiles are sharded round-robin over the ranks and the weighted sums / counts are summed with one all-reduce
+    each (RCCL), then normalised: every rank returns the full volume."""
+    from u3d import _lib
+    dev = next(net_list[0].parameters()).device
+    img_all = torch.as_tensor(image).to(device=dev, dtype=torch.float32)
+    ops.require_device(img_all)
+    image_size = img_all.shape
+    N, D, H, W = image_size[0], image_size[2], image_size[3], image_size[4]
+    plan = tile_plan(image_size, tile_size)
+    world = 1
+    if group is not None or (dist.is_available() and dist.is_initialized() and getattr(args, "shard_tiles", False)):
+        world = dist.get_world_size(group)
+        plan = shard_tiles(plan, dist.get_rank(group), world)
+    full = torch.zeros((N, classes, D, H, W), dtype=torch.float32, device=dev)
+    count = torch.zeros((N, D, H, W), dtype=torch.float32, device=dev)
+    (pd, ph, pw), gmin = _gaussian_profiles(tile_size)
+    gd, gh, gw = (torch.tensor(p, dtype=torch.float32, device=dev) for p in (pd, ph, pw))
+    flip_sets = [()] + ([(2,), (3,), (4,), (2, 3), (2, 4), (3, 4), (2, 3, 4)] if tta else [])
+    scale = 1.0 / (len(net_list) * len(flip_sets))
+    for d1, d2, y1, y2, x1, x2 in plan:
+        img = img_all[:, :, d1:d2, y1:y2, x1:x2].contiguous()
+        first = 1
+        for dims in flip_sets:
+            inp = torch.flip(img, dims) if dims else img
+            flags = sum({2: 1, 3: 2, 4: 4}[d] for d in dims)
+            for net in net_list:
+                p = _as_ndhwc(net(inp, task_id))
+                if p.shape[-1] != classes or tuple(p.shape[1:4]) != (d2 - d1, y2 - y1, x2 - x1):
+                    raise ValueError(f"predict_sliding: prediction {tuple(p.shape)} does not match the tile "
+                                     f"({d2 - d1}, {y2 - y1}, {x2 - x1}) x {classes} classes")
+                _lib.call("u3d_window_accumulate", p.data_ptr(), N, classes, d2 - d1, y2 - y1, x2 - x1,
+                          gd.data_ptr(), gh.data_ptr(), gw.data_ptr(), float(gmin), float(scale),
+                          full.data_ptr(), count.data_ptr(), D, H, W, d1, y1, x1, flags, first, ops._stream())
+                first = 0
+    if world > 1:
+        dist.all_reduce(full, group=group)
+        dist.all_reduce(count, group=group)
     _lib.call("u3d_window_normalize", full.data_ptr(), count.data_ptr(), N, classes, D * H * W, ops._stream())
     return full

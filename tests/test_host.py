@@ -181,3 +181,64 @@ def test_ddp_bucketer_gloo_world2():
             expect = 0.0 if n == "p2" else (1 + 2) / 2 * (1 + i)  # mean over ranks of (rank+1)*(1+i)
             assert np.allclose(v, expect), (n, v[:3], expect)
     assert np.allclose(out[0][2], out[1][2])  # init broadcast: identical weights on both ranks
+
+
+# ------------------------------------------------------------- f1: sliding-window tiles sharded over ranks
+def test_tile_plan_matches_reference_tiling_and_shards_partition_it():
+    from evaluate_amos import shard_tiles, tile_plan
+    plan = tile_plan((1, 1, 256, 512, 512), (64, 192, 192))
+    assert len(plan) == 80                                   # 5 x 4 x 4 tiles
+    assert plan[0] == (0, 64, 0, 192, 0, 192) and plan[-1] == (192, 256, 320, 512, 320, 512)
+    for world in (1, 2, 3, 8):
+        shards = [shard_tiles(plan, r, world) for r in range(world)]
+        assert sorted(t for s in shards for t in s) == sorted(plan)
+        assert max(map(len, shards)) - min(map(len, shards)) <= 1
+    small = tile_plan((1, 1, 40, 50, 30), (16, 24, 24))      # ragged: last tiles clamped back into the volume
+    assert all(d2 - d1 == 16 and y2 - y1 == 24 and x2 - x1 == 24 for d1, d2, y1, y2, x1, x2 in small)
+
+
+def _tile_pred(img):
+    """Deterministic stand-in network for the sharding test: per-class affine maps of the tile."""
+    return np.concatenate([img * (k + 1) - k for k in range(3)], axis=1)
+
+
+def _window_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from evaluate_amos import shard_tiles, tile_plan
+    from oracle.ref_cpu import gaussian_map
+    rng = np.random.default_rng(5)
+    image = rng.standard_normal((1, 1, 40, 50, 30))
+    tile = (16, 24, 24)
+    g = gaussian_map(tile).astype(np.float64)
+    full = torch.zeros((1, 3, 40, 50, 30), dtype=torch.float64)
+    count = torch.zeros((1, 3, 40, 50, 30), dtype=torch.float64)
+    for d1, d2, y1, y2, x1, x2 in shard_tiles(tile_plan(image.shape, tile), rank, world):
+        pred = _tile_pred(image[:, :, d1:d2, y1:y2, x1:x2])
+        full[:, :, d1:d2, y1:y2, x1:x2] += torch.from_numpy(pred * g)
+        count[:, :, d1:d2, y1:y2, x1:x2] += torch.from_numpy(g)
+    dist.all_reduce(full)     # the product path's two all-reduces (evaluate_amos.predict_sliding)
+    dist.all_reduce(count)
+    q.put((rank, (full / count).numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sliding_window_sharded_gloo_world2_matches_oracle():
+    from oracle.ref_cpu import predict_sliding
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_window_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=60) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    image = np.random.default_rng(5).standard_normal((1, 1, 40, 50, 30))
+    ref = predict_sliding(_tile_pred, image, (16, 24, 24), 3)
+    for _, got in out:
+        np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
