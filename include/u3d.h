@@ -146,6 +146,14 @@ int u3d_conv32_brick(int flip, const void* x, int n, int d, int h, int w, const 
 int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
                     const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
                     u3d_stream_t stream);
+/* u3d_conv32_ring forward with the GroupNorm prologue that also returns the GroupNorm(16, 32) statistics of its
+ * (stored, bf16) output — (mean, rstd) [n][16][2], eps 1e-5 — accumulated in the epilogue, so the next GroupNorm
+ * (NoBottleneck gn2 / the next block's gn1, unet3D.py:44-53) needs no statistics pass. stats_ws:
+ * u3d_conv32_ring_stats_ws_floats(n) floats. */
+int u3d_conv32_ring_stats_ws_floats(int n);
+int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
+                          const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
+                          float* stats_out, float* stats_ws, u3d_stream_t stream);
 
 /* Stride-1 3^3 weight gradient, depth-streaming ring schedule (wgrad_ring.hip): same partial-slab contract as
  * u3d_conv_wgrad_brick ([nsplit][27][cout_p][cin_p] fp32, summed by the caller in fixed order); a split is a

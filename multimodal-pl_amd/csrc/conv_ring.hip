@@ -47,6 +47,8 @@ struct RGGeom {
   long long xbytes;  // bytes of x (and of the residual / y): < 2^31, the buffer-offset range
   int per;           // output planes per workgroup
   int gn_groups;
+  long long pps;     // output planes per sample; workgroups never straddle samples (per-sample GN statistics)
+  int wps;           // workgroups per sample
 };
 
 // One staged input plane: column (n, h0, w0), input depth zin (-1 / d = zero padding), and whether it is the
@@ -93,7 +95,8 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
                                                               bf16* __restrict__ y, const bf16* __restrict__ res,
                                                               const float* __restrict__ gstat,
                                                               const float* __restrict__ gamma,
-                                                              const float* __restrict__ beta, RGGeom g) {
+                                                              const float* __restrict__ beta, float* __restrict__ spart,
+                                                              RGGeom g) {
   __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024];
   char* const ring = smem;
   char* const wts = smem + 4 * RG_SS;
@@ -110,8 +113,9 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
   }
   RGWalk walk{};
-  walk.o_next = (long long)bid * g.per;
-  walk.o_end = min(g.planes, walk.o_next + g.per);
+  const int smp = bid / g.wps, jw = bid - smp * g.wps;
+  walk.o_next = (long long)smp * g.pps + (long long)jw * g.per;
+  walk.o_end = min((long long)(smp + 1) * g.pps, walk.o_next + g.per);
   walk.done = false;
   walk.zin = 1;
   walk.zlast = 0;  // forces start_run on the first next()
@@ -173,6 +177,12 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   Pending pend;
   pend.ok = false;
   pend.vox = 0;
+  // GroupNorm(16, 32) statistics of the stored output (GN variants = the forward convs whose outputs feed the next
+  // GroupNorm): lane (r, h) holds channels 16u + 8h + e, i.e. groups 8u + 4h + e/2 -> 8 (sum, sum of squares)
+  // pairs per lane, accumulated in fp32 over the lane's voxels, reduced per workgroup at the end
+  float gs[8], gq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) gs[j] = gq[j] = 0.f;
   auto epilogue = [&](const Pending& p) {
     // lane (r, h): acc[4q + e] = channel 8q + 4h + e of voxel r. Pack to bf16 pairs, then swap halves so that
     // lane (r, h) holds channels 8h..8h+7 (pk[0..1]) and 16+8h..16+8h+7 (pk[2..3]).
@@ -202,6 +212,17 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         store16<bf16>(reinterpret_cast<bf16*>(&v), a);
       }
       if (p.ok) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
+      if constexpr (GN) {
+        if (p.ok) {
+          float a[8];
+          load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            gs[4 * u + (e >> 1)] += a[e];
+            gq[4 * u + (e >> 1)] = fmaf(a[e], a[e], gq[4 * u + (e >> 1)]);
+          }
+        }
+      }
     }
   };
 
@@ -289,6 +310,57 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     step(vb, mb, va, ma);
   }
   epilogue(pend);  // the last computed plane (ok = false if none)
+  if constexpr (GN) {
+    if (spart == nullptr) return;
+    // lanes with the same h hold the same groups: reduce over r (xor within 32-lane halves), then over the waves in
+    // fixed order through LDS (the ring is idle: every step ended with a barrier)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        gs[j] += __shfl_xor(gs[j], o);
+        gq[j] += __shfl_xor(gq[j], o);
+      }
+    float* red = reinterpret_cast<float*>(ring);  // [wave][group 16][2]
+    if (r == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int grp = 8 * (j >> 2) + 4 * h + (j & 3);
+        red[(wave * 16 + grp) * 2] = gs[j];
+        red[(wave * 16 + grp) * 2 + 1] = gq[j];
+      }
+    }
+    __syncthreads();
+    if (tid < 32) {
+      float t = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < RG_NT / 64; ++wv) t += red[wv * 32 + tid];
+      spart[(long long)bid * 32 + tid] = t;  // [sample][wps][group][2]: bid = sample * wps + jw
+    }
+  }
+}
+
+// stats[n][16] = (mean, rstd) of GroupNorm(16, 32) from the ring kernel's per-workgroup partials: one wave per
+// (n, group), lanes strided over the workgroups, fp64 butterfly in fixed order (deterministic)
+__global__ __launch_bounds__(64) void ring_gn_finalize_kernel(const float* __restrict__ spart, int n, int wps, double m,
+                                                             float* __restrict__ stats) {
+  const int p = blockIdx.x, nn = p / 16, gr = p % 16;
+  double s1 = 0, s2 = 0;
+  for (int w = threadIdx.x; w < wps; w += 64) {
+    s1 += spart[((long long)nn * wps + w) * 32 + gr * 2];
+    s2 += spart[((long long)nn * wps + w) * 32 + gr * 2 + 1];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  if (threadIdx.x == 0) {
+    const double mean = s1 / m;
+    double var = s2 / m - mean * mean;
+    if (var < 0) var = 0;
+    stats[p * 2] = (float)mean;
+    stats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+  }
 }
 
 }  // namespace u3d
@@ -303,26 +375,31 @@ static int ring_kr(int dflt) {  // U3D_RING_KR=0: no weight steps in registers (
   return kr < 0 ? dflt : kr;
 }
 
-extern "C" int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
-                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                               const void* residual, void* y, u3d_stream_t stream) {
+static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
+                            const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                            const void* residual, void* y, float* stats_out, float* stats_ws, u3d_stream_t stream) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv32_ring: bad args");
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0), "conv32_ring: bad GN");
+  U3D_REQUIRE(!stats_out || (gn_stats && stats_ws), "conv32_ring: output statistics need the GN prologue + ws");
   RGGeom g{};
   g.n = n; g.d = d; g.h = h; g.w = w;
   g.nbh = cdiv(h, RG_BH); g.nbw = cdiv(w, RG_BW);
-  g.planes = (long long)n * g.nbh * g.nbw * d;
+  g.pps = (long long)g.nbh * g.nbw * d;
+  g.planes = (long long)n * g.pps;
   g.xbytes = (long long)n * d * h * w * 64;
   U3D_REQUIRE(g.xbytes < (1LL << 31), "conv32_ring: tensor of %lld bytes beyond the 2 GiB buffer-offset range",
               g.xbytes);
-  long long grid = std::min<long long>(256, g.planes);
-  g.per = (int)((g.planes + grid - 1) / grid);
-  grid = (g.planes + g.per - 1) / g.per;
+  // ~256 persistent workgroups, split evenly per sample (no workgroup straddles two samples)
+  const long long wps0 = std::max<long long>(1, std::min<long long>(g.pps, 256 / n));
+  g.per = (int)((g.pps + wps0 - 1) / wps0);
+  g.wps = (int)((g.pps + g.per - 1) / g.per);
+  const long long grid = (long long)n * g.wps;
   g.gn_groups = gn_groups;
   hipStream_t s = (hipStream_t)stream;
+  float* sp = stats_out ? stats_ws : nullptr;
 #define RG_LAUNCH(F, G, R, K)                                                                                  \
   hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K>), dim3((unsigned)grid), dim3(RG_NT), 0, s, (const bf16*)x, \
-                     (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g)
+                     (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, sp, g)
 #define RG_KR(F, G, R, K)                  \
   do {                                     \
     if (kr) RG_LAUNCH(F, G, R, K);         \
@@ -338,5 +415,25 @@ extern "C" int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int
   else RG_KR(false, false, false, 27);
 #undef RG_KR
 #undef RG_LAUNCH
+  if (stats_out)
+    hipLaunchKernelGGL(ring_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, stats_ws, n, g.wps, 2.0 * d * h * w,
+                       stats_out);
   return check_launch("conv32_ring_kernel");
+}
+
+extern "C" int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
+                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                               const void* residual, void* y, u3d_stream_t stream) {
+  return conv32_ring_impl(flip, x, n, d, h, w, wpk, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, nullptr,
+                          nullptr, stream);
+}
+
+extern "C" int u3d_conv32_ring_stats_ws_floats(int n) { return 32 * std::max(256, n); }
+
+extern "C" int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
+                                     const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual,
+                                     void* y, float* stats_out, float* stats_ws, u3d_stream_t stream) {
+  U3D_REQUIRE(stats_out && stats_ws, "conv32_ring_stats: null statistics output / workspace");
+  return conv32_ring_impl(0, x, n, d, h, w, wpk, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_out,
+                          stats_ws, stream);
 }

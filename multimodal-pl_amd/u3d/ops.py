@@ -1,6 +1,7 @@
 """Tensor-level wrappers over the libu3d C ABI. Torch is only the allocator / stream provider here: every
 value is computed by a HIP kernel. All activations are NDHWC tensors of shape [n, d, h, w, c]."""
 import ctypes
+import os
 
 import torch
 
@@ -178,6 +179,30 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
     return y
 
 
+def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
+    """conv_fwd that also returns the GroupNorm(16) statistics [n,16,2] of its output when the 32->32 ring kernel
+    runs with a GN prologue (epilogue-accumulated); otherwise (conv_fwd(...), None)."""
+    n, d, h, w_, cin = x.shape
+    if (RING_STATS and gn is not None and cout == 32 and CONV32_FN == "u3d_conv32_ring"
+            and _use_conv32(x.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(x)):
+        st, ga, be, G = gn
+        y = torch.empty((n, d, h, w_, cout), dtype=x.dtype, device=x.device)
+        stats = torch.empty((n, 16, 2), dtype=torch.float32, device=x.device)
+        ws = WS.get(4 * query("u3d_conv32_ring_stats_ws_floats", n), x.device, slot=9)
+        probe = PROBE is not None
+        if probe:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        call("u3d_conv32_ring_stats", x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
+             be.data_ptr(), G, _ptr(residual), y.data_ptr(), stats.data_ptr(), ws.data_ptr(), _stream())
+        if probe:
+            e1.record()
+            PROBE.append((e0, e1, n * d * h * w_))
+        return y, stats
+    return conv_fwd(x, wpk, cout, k, stride, gn, residual), None
+
+
+RING_STATS = os.environ.get("U3D_RING_STATS", "1") != "0"  # GroupNorm statistics from the ring conv epilogue (False: separate u3d_gn_stats pass)
 SPLITK_WS_BYTES = 64 << 20
 PROBE = None  # list -> conv32_brick forward launches record (start, end, voxels) HIP events (bench.py roofline)
 USE_CONV32_BRICK = True

@@ -187,11 +187,16 @@ class Tape:
             gn = (self.stats(x, G), self.P[gn_key + ".weight"], self.P[gn_key + ".bias"], G)
         b = self.P[key + ".bias"] if bias else None
         head = out_f32 and residual is None and ops.use_head(x.t.dtype, cin, cout, k, stride)
+        st16 = None
         if head:  # precls_conv: streaming MFMA head (head.hip)
             y = ops.head_fwd(x.t, pf, cout, b, gn)
+        elif gn is not None and b is None and not out_f32 and cout == 32:
+            y, st16 = ops.conv_fwd_stats(x.t, pf, cout, k, stride, gn, residual.t if residual is not None else None)
         else:
             y = ops.conv_fwd(x.t, pf, cout, k, stride, gn, residual.t if residual is not None else None, b, out_f32)
         out = Act(y)
+        if st16 is not None:
+            out.stats[16] = st16  # GroupNorm(16) statistics from the conv epilogue (consumed by the next GN)
         if self.record:
             def bwd():
                 dy = out.grad
