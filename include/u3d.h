@@ -146,14 +146,16 @@ int u3d_conv32_brick(int flip, const void* x, int n, int d, int h, int w, const 
 int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
                     const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
                     u3d_stream_t stream);
-/* u3d_conv32_ring forward with the GroupNorm prologue that also returns the GroupNorm(16, 32) statistics of its
- * (stored, bf16) output — (mean, rstd) [n][16][2], eps 1e-5 — accumulated in the epilogue, so the next GroupNorm
- * (NoBottleneck gn2 / the next block's gn1, unet3D.py:44-53) needs no statistics pass. stats_ws:
- * u3d_conv32_ring_stats_ws_floats(n) floats. */
+/* u3d_conv32_ring forward with the GroupNorm prologue that also accumulates the GroupNorm(16, 32) statistics of
+ * its (stored, bf16) output in the epilogue (per-workgroup partials in stats_ws, u3d_conv32_ring_stats_ws_floats(n)
+ * floats); u3d_conv32_ring_stats_finalize turns them into (mean, rstd) [n][16][2], eps 1e-5 — so the next GroupNorm
+ * (NoBottleneck gn2 / the next block's gn1, unet3D.py:44-53) needs no statistics pass over the output. */
 int u3d_conv32_ring_stats_ws_floats(int n);
 int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
                           const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
-                          float* stats_out, float* stats_ws, u3d_stream_t stream);
+                          float* stats_ws, u3d_stream_t stream);
+int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
+                                   u3d_stream_t stream);
 
 /* Stride-1 3^3 weight gradient, depth-streaming ring schedule (wgrad_ring.hip): same partial-slab contract as
  * u3d_conv_wgrad_brick ([nsplit][27][cout_p][cin_p] fp32, summed by the caller in fixed order); a split is a

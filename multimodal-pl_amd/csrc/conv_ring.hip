@@ -415,9 +415,6 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
   else RG_KR(false, false, false, 27);
 #undef RG_KR
 #undef RG_LAUNCH
-  if (stats_out)
-    hipLaunchKernelGGL(ring_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, stats_ws, n, g.wps, 2.0 * d * h * w,
-                       stats_out);
   return check_launch("conv32_ring_kernel");
 }
 
@@ -432,8 +429,20 @@ extern "C" int u3d_conv32_ring_stats_ws_floats(int n) { return 32 * std::max(256
 
 extern "C" int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
                                      const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual,
-                                     void* y, float* stats_out, float* stats_ws, u3d_stream_t stream) {
-  U3D_REQUIRE(stats_out && stats_ws, "conv32_ring_stats: null statistics output / workspace");
-  return conv32_ring_impl(0, x, n, d, h, w, wpk, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_out,
+                                     void* y, float* stats_ws, u3d_stream_t stream) {
+  U3D_REQUIRE(stats_ws, "conv32_ring_stats: null statistics workspace");
+  return conv32_ring_impl(0, x, n, d, h, w, wpk, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
                           stats_ws, stream);
+}
+
+extern "C" int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
+                                              u3d_stream_t stream) {
+  U3D_REQUIRE(stats_ws && stats_out && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv32_ring_stats_finalize: bad args");
+  const long long pps = (long long)cdiv(h, RG_BH) * cdiv(w, RG_BW) * d;  // same split as conv32_ring_impl
+  const long long wps0 = std::max<long long>(1, std::min<long long>(pps, 256 / n));
+  const long long per = (pps + wps0 - 1) / wps0;
+  const int wps = (int)((pps + per - 1) / per);
+  hipLaunchKernelGGL(ring_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, (hipStream_t)stream, stats_ws, n, wps,
+                     2.0 * d * h * w, stats_out);
+  return check_launch("ring_gn_finalize_kernel");
 }

@@ -194,10 +194,11 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         call("u3d_conv32_ring_stats", x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
-             be.data_ptr(), G, _ptr(residual), y.data_ptr(), stats.data_ptr(), ws.data_ptr(), _stream())
+             be.data_ptr(), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), _stream())
         if probe:
             e1.record()
             PROBE.append((e0, e1, n * d * h * w_))
+        call("u3d_conv32_ring_stats_finalize", ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
         return y, stats
     return conv_fwd(x, wpk, cout, k, stride, gn, residual), None
 
