@@ -10,6 +10,8 @@
 //
 // Workspace (u3d_gn_workspace_bytes): [256 B completion counters][partials n x nblk x 2 x c f32][coef n x 5 x c
 // f32]. It must be zero-filled when first allocated; every launch leaves its counter at zero again.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace u3d {
@@ -23,6 +25,15 @@ struct RedGeom {
   long long v;
 };
 
+// reduction blocks over all samples (U3D_GN_MAXBLK overrides, for experiments)
+static long long gn_max_blocks() {
+  static const long long m = [] {
+    const char* e = getenv("U3D_GN_MAXBLK");
+    return e ? atoll(e) : 256LL;
+  }();
+  return m;
+}
+
 static RedGeom make_geom(int n, int c, long long v, int groups, int vec) {
   RedGeom g{};
   g.n = n;
@@ -35,18 +46,46 @@ static RedGeom make_geom(int n, int c, long long v, int groups, int vec) {
   // blocks in all ~ bytes / 64 KB, 16..256 (512 threads, 32 KB of loads in flight each): every CU streams on
   // the big tensors, and the partials stay few enough for a one-round last-block combine
   const long long bytes = v * n * c * (vec == 8 ? 2 : 4);
-  const long long nb = std::min<long long>(256, std::max<long long>(16, bytes >> 16));
+  const long long nb = std::min<long long>(gn_max_blocks(), std::max<long long>(16, bytes >> 16));
   long long want = std::max<long long>((long long)g.vlanes * 4, (v * n + nb - 1) / nb);
   g.vpb = (int)((want + g.vlanes - 1) / g.vlanes * g.vlanes);
   g.nblk = (int)((v + g.vpb - 1) / g.vpb);
   return g;
 }
 
-// Block-level per-channel reduction of VEC-wide per-thread partials into out[c] for c < C.
+// Block-level per-channel reduction of VEC-wide per-thread partials into out[c] for c < C. Thread t holds chunk
+// j = t % chn of voxel lane t / chn. When chn divides the wave (64 % chn == 0) the lanes of one chunk are chn apart
+// inside a wave: an xor-shuffle tree over offsets chn..32 reduces them, then the 8 waves' rows are summed through
+// LDS in wave order (log2(64/chn) shuffles + 8 LDS reads instead of a serial walk over the voxel lanes).
+// Deterministic either way (fixed tree / order).
 template <int VEC, int NV>
 __device__ __forceinline__ void block_channel_reduce(float (&acc)[NV][VEC], float* lds, const RedGeom& g,
                                                      float* out /*[NV][C]*/) {
   const int tid = threadIdx.x;
+  constexpr int NW = GT / 64;
+  if (g.chn <= 64 && (64 % g.chn) == 0 && NW * NV * g.c <= GT * VEC) {
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int o = g.chn; o < 64; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[k][e] += __shfl_xor(acc[k][e], o);
+    __syncthreads();  // lds may still be read by a previous reduction
+    if (lane < g.chn)
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) lds[(wave * NV + k) * g.c + lane * VEC + e] = acc[k][e];
+    __syncthreads();
+    for (int i = tid; i < NV * g.c; i += GT) {
+      const int k = i / g.c, c = i - k * g.c;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += lds[(w * NV + k) * g.c + c];
+      __hip_atomic_store(out + k * g.c + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: write-through
+    }
+    return;
+  }
   const int active = g.vlanes * g.chn;
   for (int k = 0; k < NV; ++k) {
     __syncthreads();
