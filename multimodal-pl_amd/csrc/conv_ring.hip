@@ -177,13 +177,24 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   Pending pend;
   pend.ok = false;
   pend.vox = 0;
-  // GroupNorm(16, 32) statistics of the stored output (GN variants = the forward convs whose outputs feed the next
-  // GroupNorm): lane (r, h) holds channels 16u + 8h + e, i.e. groups 8u + 4h + e/2 -> 8 (sum, sum of squares)
-  // pairs per lane, accumulated in fp32 over the lane's voxels, reduced per workgroup at the end
+  // GroupNorm(16, 32) statistics of the output (GN variants = the forward convs whose outputs feed the next
+  // GroupNorm), from the fp32 values just before the final bf16 rounding (no unpack; the voxel's in-volume flag
+  // selects): 8 (sum, sum of squares) pairs per lane, fp32 over the lane's voxels, reduced per workgroup at
+  // the end. Without residual the lane's accumulators acc[4q + e] are channels 8q + 4h + e -> slot 2q + e/2 =
+  // group 4q + 2h + e/2; with residual the post-swap values are channels 16u + 8h + e -> slot 4u + e/2 = group
+  // 8u + 4h + e/2.
   float gs[8], gq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) gs[j] = gq[j] = 0.f;
   auto epilogue = [&](const Pending& p) {
+    if constexpr (GN && !RES) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float t = p.ok ? p.acc[k] : 0.f;  // select, not a multiply: rows past the volume may hold non-finite
+        gs[2 * (k >> 2) + ((k & 3) >> 1)] += t;
+        gq[2 * (k >> 2) + ((k & 3) >> 1)] = fmaf(t, t, gq[2 * (k >> 2) + ((k & 3) >> 1)]);
+      }
+    }
     // lane (r, h): acc[4q + e] = channel 8q + 4h + e of voxel r. Pack to bf16 pairs, then swap halves so that
     // lane (r, h) holds channels 8h..8h+7 (pk[0..1]) and 16+8h..16+8h+7 (pk[2..3]).
     uint32_t pk[4][2];
@@ -209,20 +220,17 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[u]), c);
 #pragma unroll
         for (int e = 0; e < 8; ++e) a[e] += c[e];
+        if constexpr (GN) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float t = p.ok ? a[e] : 0.f;
+            gs[4 * u + (e >> 1)] += t;
+            gq[4 * u + (e >> 1)] = fmaf(t, t, gq[4 * u + (e >> 1)]);
+          }
+        }
         store16<bf16>(reinterpret_cast<bf16*>(&v), a);
       }
       if (p.ok) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
-      if constexpr (GN) {
-        if (p.ok) {
-          float a[8];
-          load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            gs[4 * u + (e >> 1)] += a[e];
-            gq[4 * u + (e >> 1)] = fmaf(a[e], a[e], gq[4 * u + (e >> 1)]);
-          }
-        }
-      }
     }
   };
 
@@ -325,7 +333,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     if (r == 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int grp = 8 * (j >> 2) + 4 * h + (j & 3);
+        const int grp = RES ? 8 * (j >> 2) + 4 * h + (j & 3) : 4 * (j >> 1) + 2 * h + (j & 1);
         red[(wave * 16 + grp) * 2] = gs[j];
         red[(wave * 16 + grp) * 2 + 1] = gq[j];
       }
@@ -406,10 +414,10 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
     else RG_LAUNCH(F, G, R, 0);            \
   } while (0)
   U3D_REQUIRE(!(flip && (gn_stats || residual)), "conv32_ring: the data gradient takes no prologue / residual");
-  // register budget (2 waves per SIMD): the GroupNorm variants hold 16 weight steps, the others 27
+  // register budget (2 waves per SIMD): GN + residual holds 12 weight steps, GN 16, the others 27
   const bool kr = ring_kr(1) != 0;
   if (flip) RG_KR(true, false, false, 27);
-  else if (gn_stats && residual) RG_KR(false, true, true, 16);
+  else if (gn_stats && residual) RG_KR(false, true, true, 12);  // + the statistics accumulators: 12 steps
   else if (gn_stats) RG_KR(false, true, false, 16);
   else if (residual) RG_KR(false, false, true, 27);
   else RG_KR(false, false, false, 27);

