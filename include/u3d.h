@@ -214,6 +214,13 @@ int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v, int groups
 int u3d_gn_bwd(int dtype, const void* da, const void* x, int n, int c, long long v, int groups,
                const float* stats, const float* gamma, const float* beta, void* dx, int accumulate,
                float* dgamma, float* dbeta, int accumulate_params, float* ws, u3d_stream_t stream);
+/* Backward of two GroupNorm+ReLU consumers of the same x with the same statistics (NoBottleneck gn1 and the
+ * downsample GN of a stage's first block, unet3D.py:44-53, :1666-1686): dx (+)= GN-bwd(dA1; gamma1, beta1) +
+ * GN-bwd(dA2; gamma2, beta2) in one partial pass and one apply pass; dgamma/dbeta of both (+= when acc). */
+int u3d_gn_bwd2(int dtype, const void* da1, const void* da2, const void* x, int n, int c, long long v, int groups,
+                const float* stats, const float* gamma1, const float* beta1, const float* gamma2, const float* beta2,
+                void* dx, int accumulate, float* dgamma1, float* dbeta1, float* dgamma2, float* dbeta2,
+                int accumulate_params, float* ws, u3d_stream_t stream);
 
 /* ---------------------------------------------------------------- trilinear x2 upsample + skip (A6)
  * nn.Upsample(scale_factor=2, mode='trilinear') (align_corners=False) then `+ skip`

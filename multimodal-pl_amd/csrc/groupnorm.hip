@@ -121,7 +121,8 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 
 // Last-block combine, phase 1: cs[p] = (sum_b P[n][b][0][c], sum_b P[n][b][1][c]) in fp64 for p = n*C + c.
 // Threads run along channels (coalesced partial rows) and over block slices; slices combine in fixed order.
-__device__ __forceinline__ void combine_channels(const float* __restrict__ ws, const RedGeom& g, double (*cs)[2]) {
+__device__ __forceinline__ void combine_channels(const float* __restrict__ ws, const RedGeom& g, double (*cs)[2],
+                                                 int nv = 2, int k0 = 0) {
   __shared__ double part[GT][2];
   const int tid = threadIdx.x, npairs = g.n * g.c;
   const int spl = npairs >= GT ? 1 : GT / npairs;
@@ -130,14 +131,15 @@ __device__ __forceinline__ void combine_channels(const float* __restrict__ ws, c
     double s1 = 0, s2 = 0;
     if (p < npairs && sl < spl) {
       const int nn = p / g.c, c = p % g.c;
-      const float* q = ws + (long long)nn * g.nblk * 2 * g.c + c;  // partials of other blocks: sc1 loads only
+      // partials of other blocks (rows of nv x C per block; this pass reads rows k0, k0 + 1): sc1 loads only
+      const float* q = ws + (long long)nn * g.nblk * nv * g.c + k0 * g.c + c;
       int b = sl;
       for (; b + 31 * spl < g.nblk; b += 32 * spl) {  // 64 loads in flight: the combine is one latency round
         float a[32], bb[32];
 #pragma unroll
         for (int u = 0; u < 32; ++u) {
-          a[u] = ld_sc1(q + (long long)(b + u * spl) * 2 * g.c);
-          bb[u] = ld_sc1(q + (long long)(b + u * spl) * 2 * g.c + g.c);
+          a[u] = ld_sc1(q + (long long)(b + u * spl) * nv * g.c);
+          bb[u] = ld_sc1(q + (long long)(b + u * spl) * nv * g.c + g.c);
         }
 #pragma unroll
         for (int u = 0; u < 32; ++u) {
@@ -146,8 +148,8 @@ __device__ __forceinline__ void combine_channels(const float* __restrict__ ws, c
         }
       }
       for (; b < g.nblk; b += spl) {
-        s1 += ld_sc1(q + (long long)b * 2 * g.c);
-        s2 += ld_sc1(q + (long long)b * 2 * g.c + g.c);
+        s1 += ld_sc1(q + (long long)b * nv * g.c);
+        s2 += ld_sc1(q + (long long)b * nv * g.c + g.c);
       }
     }
     part[tid][0] = s1;
@@ -356,6 +358,157 @@ __global__ __launch_bounds__(GT) void gn_bwd_apply(const T* __restrict__ da, con
 }
 
 
+// Two GroupNorm consumers of the SAME activation x with the same statistics (NoBottleneck gn1 and the downsample
+// GN of the first block of a stage, unet3D.py:44-53 + _make_layer :1666-1686): one partial pass over x, dA1, dA2
+// (per set k: s1_k = sum m_k dA_k, s2_k = sum m_k dA_k xhat) and one apply writing
+//   dx (+)= alpha1 m1 dA1 + alpha2 m2 dA2 + (bx1 + bx2) x + (d1 + d2)
+// instead of two full backward passes (x read 4 times, dx written twice). coef2 [2][n][5][C].
+template <typename T>
+__global__ __launch_bounds__(GT) void gn_bwd2_partial(const T* __restrict__ da1, const T* __restrict__ da2,
+                                                     const T* __restrict__ x, RedGeom g, const float* __restrict__ stats,
+                                                     const float* __restrict__ gamma1, const float* __restrict__ beta1,
+                                                     const float* __restrict__ gamma2, const float* __restrict__ beta2,
+                                                     float* __restrict__ ws, unsigned* __restrict__ cnt,
+                                                     float* __restrict__ coef, float* __restrict__ dgamma1,
+                                                     float* __restrict__ dbeta1, float* __restrict__ dgamma2,
+                                                     float* __restrict__ dbeta2, int accp) {
+  constexpr int VEC = 16 / sizeof(T);
+  __shared__ float lds[GT * VEC];
+  __shared__ double cs[GN_PAIRS_MAX][2];
+  const int n = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
+  const long long base = (long long)n * g.v * g.c;
+  const int j = tid % g.chn, vl = tid / g.chn;
+  float acc[4][VEC];
+  for (int e = 0; e < VEC; ++e) acc[0][e] = acc[1][e] = acc[2][e] = acc[3][e] = 0.f;
+  if (vl < g.vlanes) {
+    float mu[VEC], rs[VEC], sc1[VEC], sh1[VEC], sc2[VEC], sh2[VEC];
+    for (int e = 0; e < VEC; ++e) {
+      const int c = j * VEC + e, gr = c / g.cpg;
+      mu[e] = stats[(n * g.groups + gr) * 2];
+      rs[e] = stats[(n * g.groups + gr) * 2 + 1];
+      sc1[e] = rs[e] * gamma1[c];
+      sh1[e] = beta1[c] - mu[e] * sc1[e];
+      sc2[e] = rs[e] * gamma2[c];
+      sh2[e] = beta2[c] - mu[e] * sc2[e];
+    }
+    const long long v0 = (long long)blk * g.vpb, v1 = std::min<long long>(g.v, v0 + g.vpb);
+    auto step = [&](const float (&xv)[VEC], const float (&d1)[VEC], const float (&d2)[VEC]) {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float xh = (xv[e] - mu[e]) * rs[e];
+        const float g1 = fmaf(xv[e], sc1[e], sh1[e]) > 0.f ? d1[e] : 0.f;
+        const float g2 = fmaf(xv[e], sc2[e], sh2[e]) > 0.f ? d2[e] : 0.f;
+        acc[0][e] += g1;
+        acc[1][e] = fmaf(g1, xh, acc[1][e]);
+        acc[2][e] += g2;
+        acc[3][e] = fmaf(g2, xh, acc[3][e]);
+      }
+    };
+    long long v = v0 + vl;
+    for (; v + 1 * g.vlanes < v1; v += 2 * g.vlanes) {  // 6 loads in flight per thread
+      float xv[2][VEC], d1[2][VEC], d2[2][VEC];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const long long off = base + (v + u * g.vlanes) * g.c + j * VEC;
+        load16<T>(x + off, xv[u]);
+        load16<T>(da1 + off, d1[u]);
+        load16<T>(da2 + off, d2[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) step(xv[u], d1[u], d2[u]);
+    }
+    for (; v < v1; v += g.vlanes) {
+      float xv[VEC], d1[VEC], d2[VEC];
+      const long long off = base + v * g.c + j * VEC;
+      load16<T>(x + off, xv);
+      load16<T>(da1 + off, d1);
+      load16<T>(da2 + off, d2);
+      step(xv, d1, d2);
+    }
+  }
+  block_channel_reduce<VEC, 4>(acc, lds, g, ws + ((long long)n * g.nblk + blk) * 4 * g.c);
+  if (!block_is_last(cnt, (unsigned)(g.n * g.nblk))) return;
+  const int npairs = g.n * g.c;
+  const double M = (double)g.v * g.cpg;
+  for (int k = 0; k < 2; ++k) {
+    const float* gamma = k ? gamma2 : gamma1;
+    const float* beta = k ? beta2 : beta1;
+    combine_channels(ws, g, cs, 4, 2 * k);
+    for (int p = tid; p < npairs; p += GT) {
+      const int nn = p / g.c, c = p % g.c, gr = c / g.cpg;
+      double a = 0, bb = 0;
+      for (int q = 0; q < g.cpg; ++q) {
+        const int cc = gr * g.cpg + q;
+        a += (double)gamma[cc] * cs[nn * g.c + cc][0];
+        bb += (double)gamma[cc] * cs[nn * g.c + cc][1];
+      }
+      const float ca = (float)(a / M), cb = (float)(bb / M);
+      const float mu = stats[(nn * g.groups + gr) * 2], rs = stats[(nn * g.groups + gr) * 2 + 1];
+      const float scv = rs * gamma[c];
+      float* o = coef + ((long long)k * g.n + nn) * 5 * g.c;
+      o[c] = scv;
+      o[g.c + c] = beta[c] - mu * scv;
+      o[2 * g.c + c] = rs * gamma[c];
+      o[3 * g.c + c] = -rs * rs * cb;
+      o[4 * g.c + c] = -rs * ca + rs * rs * cb * mu;
+    }
+    float* dg = k ? dgamma2 : dgamma1;
+    float* db = k ? dbeta2 : dbeta1;
+    for (int c = tid; c < g.c; c += GT) {
+      double tg = 0, tb = 0;
+      for (int nn = 0; nn < g.n; ++nn) {
+        tb += cs[nn * g.c + c][0];
+        tg += cs[nn * g.c + c][1];
+      }
+      if (dg) dg[c] = (accp ? dg[c] : 0.f) + (float)tg;
+      if (db) db[c] = (accp ? db[c] : 0.f) + (float)tb;
+    }
+    __syncthreads();  // cs is rebuilt for the second set
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(GT) void gn_bwd2_apply(const T* __restrict__ da1, const T* __restrict__ da2,
+                                                   const T* __restrict__ x, RedGeom g, const float* __restrict__ coef,
+                                                   T* __restrict__ dx, int accum) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int n = blockIdx.y;
+  const int first = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;  // chn | blockDim
+  const int j = first % g.chn;
+  float sc1[VEC], sh1[VEC], al1[VEC], sc2[VEC], sh2[VEC], al2[VEC], bx[VEC], dd[VEC];
+  const float* c1 = coef + (long long)n * 5 * g.c + j * VEC;
+  const float* c2 = coef + ((long long)g.n + n) * 5 * g.c + j * VEC;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    sc1[e] = c1[e];
+    sh1[e] = c1[g.c + e];
+    al1[e] = c1[2 * g.c + e];
+    sc2[e] = c2[e];
+    sh2[e] = c2[g.c + e];
+    al2[e] = c2[2 * g.c + e];
+    bx[e] = c1[3 * g.c + e] + c2[3 * g.c + e];
+    dd[e] = c1[4 * g.c + e] + c2[4 * g.c + e];
+  }
+  const long long nb = (long long)n * g.v * g.c + j * VEC;
+  const int vstep = stride / g.chn;
+  for (long long vox = first / g.chn; vox < g.v; vox += vstep) {
+    const long long off = nb + vox * g.c;
+    float xv[VEC], d1[VEC], d2[VEC], o[VEC];
+    load16<T>(x + off, xv);
+    load16<T>(da1 + off, d1);
+    load16<T>(da2 + off, d2);
+    if (accum) load16<T>(dx + off, o);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const float g1 = fmaf(xv[e], sc1[e], sh1[e]) > 0.f ? d1[e] : 0.f;
+      const float g2 = fmaf(xv[e], sc2[e], sh2[e]) > 0.f ? d2[e] : 0.f;
+      const float r = fmaf(al1[e], g1, fmaf(al2[e], g2, fmaf(bx[e], xv[e], dd[e])));
+      o[e] = accum ? o[e] + r : r;
+    }
+    store16<T>(dx + off, o);
+  }
+}
+
 // y = relu(x * scale[n,c] + shift[n,c]) materialised (8 channels per thread): used ahead of the implicit
 // GEMM on the small deep-layer activations so its K loop carries no GroupNorm arithmetic.
 template <typename T>
@@ -384,12 +537,12 @@ using namespace u3d;
 extern "C" long long u3d_gn_workspace_bytes(int n, int c, long long v) {
   long long nb = 0;
   for (int vec : {4, 8}) nb = std::max<long long>(nb, make_geom(n, c, v, 1, vec).nblk);
-  return GN_CNT_BYTES + (long long)n * nb * 2 * c * 4 + 256 + (long long)n * c * 5 * 4;
+  return GN_CNT_BYTES + (long long)n * nb * 4 * c * 4 + 256 + 2LL * n * c * 5 * 4;  // room for u3d_gn_bwd2
 }
 
 static float* gn_coef_ptr(float* ws, const RedGeom& g) {
   return reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GN_CNT_BYTES +
-                                  (((long long)g.n * g.nblk * 2 * g.c * 4 + 255) / 256) * 256);
+                                  (((long long)g.n * g.nblk * 4 * g.c * 4 + 255) / 256) * 256);
 }
 static float* gn_part_ptr(float* ws) { return reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GN_CNT_BYTES); }
 
@@ -456,4 +609,38 @@ extern "C" int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v,
     hipLaunchKernelGGL(gn_apply_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)x, (float*)y, n, c, v,
                        groups, stats, gamma, beta);
   return check_launch("gn_apply_kernel");
+}
+
+extern "C" int u3d_gn_bwd2(int dtype, const void* da1, const void* da2, const void* x, int n, int c, long long v,
+                           int groups, const float* stats, const float* gamma1, const float* beta1,
+                           const float* gamma2, const float* beta2, void* dx, int accumulate, float* dgamma1,
+                           float* dbeta1, float* dgamma2, float* dbeta2, int accumulate_params, float* ws,
+                           u3d_stream_t stream) {
+  U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "gn_bwd2: bad dtype");
+  U3D_REQUIRE(da1 && da2 && x && stats && gamma1 && beta1 && gamma2 && beta2 && dx && ws && groups > 0 &&
+              c % groups == 0, "gn_bwd2: bad args");
+  const int vec = dtype == U3D_BF16 ? 8 : 4;
+  U3D_REQUIRE(c % vec == 0 && c <= 256, "gn_bwd2: channels %d unsupported", c);
+  U3D_REQUIRE(n * c <= GN_PAIRS_MAX, "gn_bwd2: n * c must be <= %d", GN_PAIRS_MAX);
+  RedGeom g = make_geom(n, c, v, groups, vec);
+  hipStream_t s = (hipStream_t)stream;
+  unsigned* cnt = reinterpret_cast<unsigned*>(ws) + 2;
+  float* coef = gn_coef_ptr(ws, g);
+  const long long nvec = v * g.chn;
+  const int athr = GT / g.chn * g.chn;
+  const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + athr - 1) / athr);
+  if (dtype == U3D_BF16) {
+    hipLaunchKernelGGL(gn_bwd2_partial<bf16>, dim3(g.nblk, n), dim3(GT), 0, s, (const bf16*)da1, (const bf16*)da2,
+                       (const bf16*)x, g, stats, gamma1, beta1, gamma2, beta2, gn_part_ptr(ws), cnt, coef, dgamma1,
+                       dbeta1, dgamma2, dbeta2, accumulate_params);
+    hipLaunchKernelGGL(gn_bwd2_apply<bf16>, dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da1, (const bf16*)da2,
+                       (const bf16*)x, g, coef, (bf16*)dx, accumulate);
+  } else {
+    hipLaunchKernelGGL(gn_bwd2_partial<float>, dim3(g.nblk, n), dim3(GT), 0, s, (const float*)da1,
+                       (const float*)da2, (const float*)x, g, stats, gamma1, beta1, gamma2, beta2, gn_part_ptr(ws),
+                       cnt, coef, dgamma1, dbeta1, dgamma2, dbeta2, accumulate_params);
+    hipLaunchKernelGGL(gn_bwd2_apply<float>, dim3(ablk, n), dim3(athr), 0, s, (const float*)da1, (const float*)da2,
+                       (const float*)x, g, coef, (float*)dx, accumulate);
+  }
+  return check_launch("gn_bwd2");
 }

@@ -409,6 +409,24 @@ def gn_bwd(da, x, stats, gamma, beta, groups, dx=None, accumulate=False, dgamma=
     return dx
 
 
+def gn_bwd2(da1, da2, x, stats, gn1, gn2, groups, dx=None, accumulate=False, dparams1=(None, None),
+            dparams2=(None, None)):
+    """Two GroupNorm+ReLU consumers of x (same statistics): gn_k = (gamma_k, beta_k); one fused backward."""
+    n, c = x.shape[0], x.shape[-1]
+    v = x.numel() // (n * c)
+    if dx is None:
+        dx = torch.empty_like(x)
+        accumulate = False
+    call("u3d_gn_bwd2", dt_code(x.dtype), da1.data_ptr(), da2.data_ptr(), x.data_ptr(), n, c, v, groups,
+         stats.data_ptr(), gn1[0].data_ptr(), gn1[1].data_ptr(), gn2[0].data_ptr(), gn2[1].data_ptr(), dx.data_ptr(),
+         int(accumulate), _ptr(dparams1[0]), _ptr(dparams1[1]), _ptr(dparams2[0]), _ptr(dparams2[1]), 0,
+         _gn_ws(n, c, v, x.device).data_ptr(), _stream())
+    return dx
+
+
+GN_BWD_PAIRS = os.environ.get("U3D_GN_PAIRS", "1") != "0"  # fuse gn1 + downsample-GN backward of a block
+
+
 # ------------------------------------------------------------------------------------------ upsample
 def upsample2x_add(x, skip=None):
     n, d, h, w_, c = x.shape

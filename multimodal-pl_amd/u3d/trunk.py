@@ -44,12 +44,13 @@ USE_SIDE_STREAM = os.environ.get("U3D_SIDE_STREAM", "0") != "0"  # measured slow
 
 class Act:
     """An NDHWC activation, its cached GroupNorm statistics and its accumulated gradient."""
-    __slots__ = ("t", "stats", "grad")
+    __slots__ = ("t", "stats", "grad", "gn_pend")
 
     def __init__(self, t):
         self.t = t
         self.stats = {}
         self.grad = None
+        self.gn_pend = None  # the parked (dA, gn, key) of a block's downsample GN until gn1's backward fuses both
 
 
 class Tape:
@@ -176,7 +177,7 @@ class Tape:
         return out
 
     def gn_conv(self, x, key, k, stride, gn_key=None, G=0, residual=None, bias=False, out_f32=False,
-                standardize=None):
+                standardize=None, pair=None):
         """conv(relu(gn(x))) [+ residual] [+ bias] — Conv3d/conv3x3x3 :16-35 behind GN+ReLU :44-53."""
         std = self.std if standardize is None else standardize
         W = self.P[key + ".weight"]
@@ -201,6 +202,9 @@ class Tape:
             def bwd():
                 dy = out.grad
                 if dy is None:
+                    if pair == "finish" and x.gn_pend:  # the parked partner still owes its GN backward
+                        dA2, gn2, key2 = x.gn_pend.pop()
+                        self.gn_bwd_one(x, dA2, gn2, key2, G)
                     return
                 if head:  # dA, bf16 dy and the bias gradient in one pass over the fp32 dlogits
                     db = self.grad_out(key + ".bias", b) if bias else None
@@ -219,18 +223,34 @@ class Tape:
                 self.pend_wgrad(part, ns, W, st, std, key + ".weight")
                 if not head:
                     dA = ops.conv_dgrad(dyT, pd, cin, x.t.shape[:4], k, stride)
-                if gn is not None:
-                    dg = self.grad_out(gn_key + ".weight", gn[1])
-                    db = self.grad_out(gn_key + ".bias", gn[2])
+                if gn is not None and pair == "park":
+                    x.gn_pend = [(dA, gn, gn_key)]  # the block's gn1 backward (runs next) finishes the pair
+                elif gn is not None and pair == "finish" and x.gn_pend:
+                    dA2, gn2, key2 = x.gn_pend.pop()
+                    dps = []
+                    for key_, g_ in ((gn_key, gn), (key2, gn2)):
+                        dps.append((self.grad_out(key_ + ".weight", g_[1]), self.grad_out(key_ + ".bias", g_[2])))
                     self.before_write(x.grad)
-                    x.grad = ops.gn_bwd(dA, x.t, gn[0], gn[1], gn[2], G, dx=x.grad,
-                                        accumulate=x.grad is not None, dgamma=dg, dbeta=db)
-                    self.grad_done(gn_key + ".weight")
-                    self.grad_done(gn_key + ".bias")
+                    x.grad = ops.gn_bwd2(dA, dA2, x.t, gn[0], (gn[1], gn[2]), (gn2[1], gn2[2]), G, dx=x.grad,
+                                         accumulate=x.grad is not None, dparams1=dps[0], dparams2=dps[1])
+                    for key_ in (gn_key, key2):
+                        self.grad_done(key_ + ".weight")
+                        self.grad_done(key_ + ".bias")
+                elif gn is not None:
+                    self.gn_bwd_one(x, dA, gn, gn_key, G)
                 else:
                     self.acc_grad(x, dA)
             self.ops.append(bwd)
         return out
+
+    def gn_bwd_one(self, x, dA, gn, gn_key, G):
+        dg = self.grad_out(gn_key + ".weight", gn[1])
+        db = self.grad_out(gn_key + ".bias", gn[2])
+        self.before_write(x.grad)
+        x.grad = ops.gn_bwd(dA, x.t, gn[0], gn[1], gn[2], G, dx=x.grad,
+                            accumulate=x.grad is not None, dgamma=dg, dbeta=db)
+        self.grad_done(gn_key + ".weight")
+        self.grad_done(gn_key + ".bias")
 
     def up_add(self, x, skip):
         """upsamplex2 (trilinear, align_corners=False) + skip, unet3D.py:1646 / :1764-1783."""
@@ -249,9 +269,13 @@ class Tape:
 
     def block(self, x, pre, stride, G):
         """NoBottleneck.forward, unet3D.py:56-73."""
-        h = self.gn_conv(x, pre + "conv1", 3, stride, gn_key=pre + "gn1", G=G)
+        # gn1 and the downsample GN read x with the same statistics: their backward runs as one fused pass (the
+        # downsample's backward runs first in the reversed tape and parks its dA, gn1's finishes the pair)
+        pair = pre + "downsample.2.weight" in self.P and ops.GN_BWD_PAIRS
+        h = self.gn_conv(x, pre + "conv1", 3, stride, gn_key=pre + "gn1", G=G, pair="finish" if pair else None)
         if pre + "downsample.2.weight" in self.P:
-            r = self.gn_conv(x, pre + "downsample.2", 1, stride, gn_key=pre + "downsample.0", G=G)
+            r = self.gn_conv(x, pre + "downsample.2", 1, stride, gn_key=pre + "downsample.0", G=G,
+                             pair="park" if pair else None)
         else:
             r = x
         return self.gn_conv(h, pre + "conv2", 3, 1, gn_key=pre + "gn2", G=G, residual=r)
