@@ -2,7 +2,11 @@
 tile 64x192x192, overlap 1/4 (80 tiles, evaluate_amos.py:211-221), the 16-organ unet3D_baseline trunk, forward
 only, bf16 activations (the config names fp16; the native path computes bf16 with fp32 accumulation), device
 Gaussian accumulation. Prints one JSON line: volume voxels/s, per-tile ms and the conv-stack MFMA fraction
-(1025.7 GFLOP per tile forward)."""
+(1025.7 GFLOP per tile forward).
+
+Multi-GPU (one process per GPU, `python -m torch.distributed.run --nproc-per-node N bench_infer.py`): the tiles are
+sharded round-robin over the ranks (predict_sliding(..., group=WORLD), two RCCL all-reduces at the end); the time
+is the max over ranks between barriers; the value is whole-volume voxels/s."""
 import argparse
 import json
 import os
@@ -30,7 +34,16 @@ def main():
     import unet3D
     import evaluate_amos as E
     from oracle.weights_recipe import apply_recipe
-    dev = torch.device("cuda:0")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", device_id=dev)
+        group = dist.group.WORLD
+    else:
+        dev = torch.device("cuda:0")
     m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=a.classes, weight_std=True)
     apply_recipe(m, seed=0)
     m = m.to(dev).eval()
@@ -39,15 +52,23 @@ def main():
     D, H, W = a.volume
     vol = ((torch.rand((1, 1, D, H, W), generator=g) * 2000 - 1000).clamp(-325, 325) / 325).to(dev)
     with torch.no_grad():
-        out = E.predict_sliding(None, [m], vol, a.tile, a.classes, None, tta=a.tta)    # warm-up volume
+        out = E.predict_sliding(None, [m], vol, a.tile, a.classes, None, tta=a.tta, group=group)  # warm-up
         torch.cuda.synchronize()
         del out
         ts = []
         for _ in range(a.reps):
-            t0 = time.perf_counter()
-            out = E.predict_sliding(None, [m], vol, a.tile, a.classes, None, tta=a.tta)
+            if group is not None:
+                dist.barrier()
             torch.cuda.synchronize()
-            ts.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            out = E.predict_sliding(None, [m], vol, a.tile, a.classes, None, tta=a.tta, group=group)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if group is not None:
+                tt = torch.tensor([dt], device=dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                dt = float(tt)
+            ts.append(dt)
             del out
     import math
     sHW, sD = math.ceil(a.tile[1] * 0.75), math.ceil(a.tile[0] * 0.75)
@@ -55,12 +76,18 @@ def main():
              * (math.ceil((W - a.tile[2]) / sHW) + 1)) * (8 if a.tta else 1)
     t = min(ts)
     gflop = GFLOP_PER_TILE * tiles * (a.tile[0] * a.tile[1] * a.tile[2]) / (64 * 192 * 192)
+    if group is not None and dist.get_rank() != 0:
+        dist.destroy_process_group()
+        return
     print(json.dumps({"metric": "sliding-window inference voxels/sec (configs[4])", "value": D * H * W / t,
+                      "n_gpus": world,
                       "unit": "voxels/s", "s_per_volume": t, "tiles": tiles, "ms_per_tile": 1e3 * t / tiles,
                       "dtype": a.dtype, "data": "synthetic CT-like volume, random-init weights",
                       "conv_tflops": gflop / t / 1e3, "mfma_frac": gflop / t / 1e3 / PEAK_BF16_TFLOPS,
                       "config": {"workload": "unet3D_baseline(16) predict_sliding", "volume": a.volume,
                                  "tile": a.tile, "tta": a.tta}}))
+    if group is not None:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -11,28 +11,36 @@
 
 namespace u3d {
 
+// grid (w chunks, tile rows td*th, n): one output voxel per thread along w, no 64-bit div/mod; the prediction row
+// (C contiguous fp32 per voxel) is read as 16-B vectors when C % 4 == 0
 __global__ __launch_bounds__(256) void window_acc_kernel(const float* __restrict__ pred, int C, int td, int th, int tw,
                                                         const float* __restrict__ gd, const float* __restrict__ gh,
                                                         const float* __restrict__ gw, float gmin, float scale,
                                                         float* __restrict__ full, float* __restrict__ count, int D,
                                                         int H, int W, int d1, int y1, int x1, int flips,
                                                         int add_count) {
-  const int n = blockIdx.y;
-  const long long tv = (long long)td * th * tw;
+  const int n = blockIdx.z, row = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= tw) return;
+  const int a = row / th, b = row - a * th;
   const long long DHW = (long long)D * H * W;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < tv; i += (long long)gridDim.x * 256) {
-    const int e = (int)(i % tw);
-    const long long t = i / tw;
-    const int b = (int)(t % th), a = (int)(t / th);
-    float g = gd[a] * gh[b] * gw[e];
-    if (g == 0.f) g = gmin;
-    const long long vox = ((long long)(d1 + a) * H + (y1 + b)) * W + (x1 + e);
-    if (add_count) count[n * DHW + vox] += g;
-    // the prediction of the flipped input is flipped back: read the mirrored tile voxel
-    const int pa = (flips & 1) ? td - 1 - a : a, pb = (flips & 2) ? th - 1 - b : b, pe = (flips & 4) ? tw - 1 - e : e;
-    const float* pv = pred + ((((long long)n * td + pa) * th + pb) * tw + pe) * C;
-    const float gs = g * scale;
-    for (int c = 0; c < C; ++c) full[((long long)n * C + c) * DHW + vox] += pv[c] * gs;
+  float g = gd[a] * gh[b] * gw[e];
+  if (g == 0.f) g = gmin;
+  const long long vox = ((long long)(d1 + a) * H + (y1 + b)) * W + (x1 + e);
+  if (add_count) count[n * DHW + vox] += g;
+  // the prediction of the flipped input is flipped back: read the mirrored tile voxel
+  const int pa = (flips & 1) ? td - 1 - a : a, pb = (flips & 2) ? th - 1 - b : b, pe = (flips & 4) ? tw - 1 - e : e;
+  const float* pv = pred + ((((long long)n * td + pa) * th + pb) * tw + pe) * C;
+  const float gs = g * scale;
+  float* fo = full + (long long)n * C * DHW + vox;
+  if ((C & 3) == 0) {
+    for (int c = 0; c < C; c += 4) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(pv + c);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) fo[(long long)(c + k) * DHW] += q[k] * gs;
+    }
+  } else {
+    for (int c = 0; c < C; ++c) fo[(long long)c * DHW] += pv[c] * gs;
   }
 }
 
@@ -55,10 +63,9 @@ extern "C" int u3d_window_accumulate(const float* pred, int n, int C, int td, in
   U3D_REQUIRE(d1 >= 0 && y1 >= 0 && x1 >= 0 && d1 + td <= D && y1 + th <= H && x1 + tw <= W,
               "window_accumulate: tile [%d+%d, %d+%d, %d+%d] outside the volume %dx%dx%d", d1, td, y1, th, x1, tw, D,
               H, W);
-  const long long tv = (long long)td * th * tw;
-  const int nb = (int)std::min<long long>(8192, (tv + 255) / 256);
-  hipLaunchKernelGGL(window_acc_kernel, dim3(nb, n), dim3(256), 0, (hipStream_t)stream, pred, C, td, th, tw, gd, gh,
-                     gw, gmin, scale, full, count, D, H, W, d1, y1, x1, flips, add_count);
+  U3D_REQUIRE((long long)td * th <= 65535 && n <= 65535, "window_accumulate: tile rows %d x %d beyond the grid", td, th);
+  hipLaunchKernelGGL(window_acc_kernel, dim3(cdiv(tw, 256), td * th, n), dim3(256), 0, (hipStream_t)stream, pred, C,
+                     td, th, tw, gd, gh, gw, gmin, scale, full, count, D, H, W, d1, y1, x1, flips, add_count);
   return check_launch("window_acc_kernel");
 }
 

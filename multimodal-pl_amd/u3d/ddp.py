@@ -124,6 +124,8 @@ class U3DDataParallel(torch.nn.Module):
             with torch.no_grad():  # start from identical weights on every rank (DDP's init broadcast)
                 for p in module.parameters():
                     dist.broadcast(p.data, 0, group=group)
+            from . import ops
+            ops.WEIGHT_GEN[0] += 1  # .data writes bump no autograd version: invalidate cached weight packs
 
     def forward(self, *args, **kwargs):
         if self.bucketer is None or not torch.is_grad_enabled():

@@ -74,11 +74,37 @@ def wstd_fwd(w, dtype, standardize=True, need_dgrad=True):
     return pf, pd, st
 
 
+WEIGHT_GEN = [0]     # bumped by every native in-place weight update (u3d.optim.SGD, DDP init broadcast)
+_PACK_CACHE = {}     # inference only: standardised packs keyed by (weights, their versions, WEIGHT_GEN)
+PACK_CACHE_OK = [os.environ.get("U3D_PACK_CACHE", "1") != "0"]  # off once an optimizer step is graph-captured
+
+
+def _pack_key(items, dtype):
+    return (dtype, WEIGHT_GEN[0], tuple((w.data_ptr(), w._version, tuple(w.shape), bool(s), bool(d))
+                                        for w, s, d in items))
+
+
 def wstd_fwd_batch(items, dtype):
     """Batched wstd_fwd over [(w, standardize, need_dgrad)]: one launch per 48 convs; packs and stats are
-    views of three flat buffers. Returns [(pf, pd, st)] in item order."""
+    views of three flat buffers. Returns [(pf, pd, st)] in item order. Under no_grad (inference, e.g. the 80
+    sliding-window tiles of one volume) the packs of unchanged weights are reused: the key holds every weight's
+    pointer and autograd version plus WEIGHT_GEN, which the native in-place updates bump."""
     if not items:
         return []
+    if not torch.is_grad_enabled() and PACK_CACHE_OK[0] and not torch.cuda.is_current_stream_capturing():
+        key = _pack_key(items, dtype)
+        hit = _PACK_CACHE.get(key)
+        if hit is not None:
+            return hit
+        out = _wstd_fwd_batch(items, dtype)
+        if len(_PACK_CACHE) >= 4:
+            _PACK_CACHE.clear()
+        _PACK_CACHE[key] = out
+        return out
+    return _wstd_fwd_batch(items, dtype)
+
+
+def _wstd_fwd_batch(items, dtype):
     dev = items[0][0].device
     shp = []
     nf = ns = 0

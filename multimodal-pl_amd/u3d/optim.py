@@ -53,6 +53,11 @@ class SGD(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         capturing = torch.cuda.is_current_stream_capturing()
+        from . import ops as _ops
+        _ops.WEIGHT_GEN[0] += 1          # the native update does not bump autograd versions: invalidate packs
+        if capturing:                    # replays update the weights without running this code: no pack cache
+            _ops.PACK_CACHE_OK[0] = False
+            _ops._PACK_CACHE.clear()
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:

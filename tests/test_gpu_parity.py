@@ -361,3 +361,43 @@ def test_consistency_on_native_feam3_outputs(gpu):
     v.backward()
     vr.backward()
     assert torch.isfinite(m.eam21.kv.weight.grad).all() and m.eam21.kv.weight.grad.abs().sum() > 0
+
+
+def test_inference_pack_cache_tracks_weight_updates(gpu):
+    """no_grad forwards reuse the standardised weight packs only while the weights are unchanged: a native SGD
+    step, an in-place torch update and load_state_dict each invalidate them (results equal an uncached run)."""
+    import unet3D
+    from u3d import ops
+    from u3d.optim import SGD
+    m = _model("baseline", C=16).to(gpu)
+    x = torch.from_numpy(input_volume((1, 1, 16, 16, 16), seed=3, kind="ct")).to(gpu)
+
+    def fwd():
+        with torch.no_grad():
+            return m.eval()(x).clone()
+
+    def uncached():
+        ops.PACK_CACHE_OK[0] = False
+        try:
+            return fwd()
+        finally:
+            ops.PACK_CACHE_OK[0] = True
+
+    y0 = fwd()
+    assert torch.equal(fwd(), y0)                                   # cache hit: same result
+    m.train()
+    opt = SGD(m.parameters(), lr=0.5, momentum=0.9)
+    lg, _, _ = m(x)
+    (lg.float() ** 2).mean().backward()
+    opt.step()                                                      # native in-place update
+    y1 = fwd()
+    assert not torch.equal(y1, y0) and torch.equal(y1, uncached())
+    with torch.no_grad():
+        m.layer2[0].conv1.weight.mul_(1.5)                          # torch in-place update (version bump)
+    y2 = fwd()
+    assert not torch.equal(y2, y1) and torch.equal(y2, uncached())
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd["conv1.weight"].neg_()
+    m.load_state_dict(sd)
+    y3 = fwd()
+    assert torch.equal(y3, uncached())
