@@ -2,6 +2,8 @@
 // stride-2 conv0 of unet3D_g (in_channel -> init_filter, :1514). K = 27*cin is far below one MFMA
 // K-block, so this is a direct VALU conv: one thread per output voxel keeps all cout accumulators in
 // registers; the standardised weights sit in LDS as fp32. Input is the model's fp32 NCDHW volume.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace u3d {
@@ -56,6 +58,77 @@ __global__ __launch_bounds__(ST) void stem_fwd_kernel(const float* __restrict__ 
       for (int c = 0; c < ncol; ++c) yr[c] = from_f<T>(acc[c]);
     }
   }
+}
+
+// cin = 1, stride 1, cout = 32 (conv1 of every trunk, unet3D.py:1632): a thread computes FOUR consecutive w voxels
+// x 32 channels, so each tap's 32 weights (8 LDS vector reads) serve four voxels and the 3 x 6 input row window is
+// read once for them (the one-voxel form was LDS-bound: 216 vector reads per voxel). Same fp32 FMA chain per output
+// as stem_fwd_kernel (x fp32, weights from the packed bf16/f32 image), so results are bitwise those of the generic
+// kernel. One thread per (output row, group of four w voxels).
+template <typename T>
+__global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__ x, const T* __restrict__ wpk,
+                                                      T* __restrict__ y, int d, int h, int w, int cin_p,
+                                                      long long rows) {
+  __shared__ f32x4 wl[27 * 8];  // [t][co/4]
+  for (int i = threadIdx.x; i < 27 * 32; i += ST) {
+    const int co = i % 32, t = i / 32;
+    reinterpret_cast<float*>(wl)[i] = to_f(wpk[((long long)t * 32 + co) * cin_p]);
+  }
+  __syncthreads();
+  const int w4 = w >> 2;
+  const long long item = (long long)blockIdx.x * ST + threadIdx.x;  // (output row, 4-voxel group)
+  const long long row = item / w4;
+  if (row >= rows) return;
+  const int q = (int)(item - row * w4);
+  const int yy = (int)(row % h);
+  const long long nz = row / h;
+  const int z = (int)(nz % d);
+  const long long nn = nz / d;
+  const int x0 = 4 * q;
+  const float* xb = x + nn * d * h * w;
+  float acc[4][32];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int c = 0; c < 32; ++c) acc[j][c] = 0.f;
+#pragma unroll 1
+  for (int kd = 0; kd < 3; ++kd) {
+    const int zd = z + kd - 1;
+#pragma unroll 1
+    for (int kh = 0; kh < 3; ++kh) {
+      const int zh = yy + kh - 1;
+      const bool rowok = (unsigned)zd < (unsigned)d && (unsigned)zh < (unsigned)h;
+      float in[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int zw = x0 + k - 1;
+        in[k] = rowok && (unsigned)zw < (unsigned)w ? xb[((long long)zd * h + zh) * w + zw] : 0.f;
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int t = (kd * 3 + kh) * 3 + kw;
+#pragma unroll
+        for (int c4 = 0; c4 < 8; ++c4) {
+          const f32x4 wv = wl[t * 8 + c4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[j][4 * c4 + e] = fmaf(in[j + kw], wv[e], acc[j][4 * c4 + e]);
+        }
+      }
+    }
+  }
+  T* yr = y + (row * w + x0) * 32;
+  constexpr int VEC = 16 / sizeof(T);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int c = 0; c < 32; c += VEC) {
+      float v[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) v[e] = acc[j][c + e];
+      store16<T>(yr + j * 32 + c, v);
+    }
 }
 
 // dW[t][co][ci] partial over a voxel split: thread per (t, ci, co) output, loop over the split's voxels.
@@ -253,6 +326,14 @@ using namespace u3d;
 
 static int sdim(int d, int s) { return (d - 1) / s + 1; }  // k3 pad1: (d + 2 - 3)/s + 1
 
+static bool stem1_on() {  // U3D_STEM1=0: the generic one-voxel kernel (A/B experiments)
+  static const bool on = [] {
+    const char* e = getenv("U3D_STEM1");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                             int stride, void* y, u3d_stream_t stream) {
   U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "stem_fwd: bad dtype");
@@ -260,6 +341,17 @@ extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, in
   hipStream_t s = (hipStream_t)stream;
   const int od = sdim(d, stride), oh = sdim(h, stride), ow = sdim(w, stride);
   const long long total = (long long)n * od * oh * ow;
+  if (cin == 1 && stride == 1 && cout == 32 && w % 4 == 0 && (long long)n * d * h < 2147483647LL && stem1_on()) {
+    const long long rows = (long long)n * d * h, items = rows * (w / 4);
+    const dim3 grid((unsigned)((items + ST - 1) / ST));
+    if (dtype == U3D_BF16)
+      hipLaunchKernelGGL(stem1_fwd_kernel<bf16>, grid, dim3(ST), 0, s, x, (const bf16*)wpk, (bf16*)y, d, h, w,
+                         round_up(cin, 32), rows);
+    else
+      hipLaunchKernelGGL(stem1_fwd_kernel<float>, grid, dim3(ST), 0, s, x, (const float*)wpk, (float*)y, d, h, w,
+                         round_up(cin, 32), rows);
+    return check_launch("stem1_fwd_kernel");
+  }
   const int nb = (int)std::min<long long>(8192, (total + ST - 1) / ST);
   for (int co0 = 0; co0 < cout; co0 += SCO) {
     if (dtype == U3D_BF16)

@@ -283,3 +283,18 @@ def test_ring_epilogue_gn_stats_match_stats_pass(gpu, n, dims, res):
     scale = y.float().abs().max().item()
     assert (s16[..., 0] - ref[..., 0]).abs().max().item() < 1e-4 * scale
     assert ((s16[..., 1] - ref[..., 1]).abs() / ref[..., 1]).max().item() < 5e-4
+
+
+@pytest.mark.parametrize("dims", [(5, 7, 16), (3, 9, 20), (4, 4, 6)])
+def test_stem_fwd_fp32_four_voxel_kernel(gpu, dims):
+    """cin=1 stride-1 32-channel stem: the four-voxels-per-thread kernel (w % 4 == 0) and the generic one (w = 6)
+    against fp64 on the same fp32 operands."""
+    from u3d import ops
+    torch.manual_seed(4)
+    x = torch.randn((2, 1) + dims, device=gpu)
+    w = torch.randn(32, 1, 3, 3, 3, device=gpu)
+    pf, _, _ = ops.wstd_fwd(w, torch.float32, True, need_dgrad=False)
+    y = ops.stem_fwd(x, pf, 32, 1, torch.float32)
+    wq = pf.cpu()[:, :32, :1].permute(1, 2, 0).reshape(32, 1, 3, 3, 3).double()
+    ref = F.conv3d(x.cpu().double(), wq, padding=1).permute(0, 2, 3, 4, 1)
+    assert (y.double().cpu() - ref).abs().max().item() < 1e-5 * ref.abs().max().item()
