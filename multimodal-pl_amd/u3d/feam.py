@@ -106,7 +106,9 @@ def eam_op(tape, f, key, token, up):
     return out
 
 
-def _feam3_forward(tape, cfg, x, tokens, use_cm, deep_up, heads=True):
+def _feam3_forward(tape, cfg, x, tokens, use_cm, deep_up, heads=True, renew=None):
+    """renew = (mask, num_classes, alpha): unet3D_with_feam2's in-forward class-token update of each level, before
+    that level's attention (unet3D.py:869-878, 896-903, 919-926)."""
     f, _ = tape.trunk(x, cfg)
     lg = tape.head(f, cfg)
     att, deep, feats = [], [], []
@@ -116,6 +118,8 @@ def _feam3_forward(tape, cfg, x, tokens, use_cm, deep_up, heads=True):
             deep.append(tape.gn_conv(fk, f"deepout{k + 1}.2", 1, 1, gn_key=f"deepout{k + 1}.0", G=16, bias=True,
                                      out_f32=True, standardize=False))
             feats.append(fk.t.detach().clone())
+            if renew is not None:
+                renew_token([tokens[k]], [fk.t.permute(0, 4, 1, 2, 3)], renew[0], renew[1], renew[2])
             if use_cm[k]:
                 att.append(eam_op(tape, fk, EAM_KEYS[k], tokens[k], UP_SCALE[k] if deep_up else 1))
     return lg, att, deep, feats
@@ -163,8 +167,9 @@ class _Feam3Fn(torch.autograd.Function):
         return (None, None, None, None, None, None, None, *pg)
 
 
-def run_feam3(model, x):
-    """model: unet3D.unet3D_with_feam3. Returns train: (logits, atten_map, deep_map, feature_stored); eval: logits."""
+def run_feam3(model, x, renew=None):
+    """model: unet3D.unet3D_with_feam3 (or _feam2). Returns train: (logits, atten_map, deep_map, feature_stored);
+    eval: logits."""
     ops.require_device(x)
     cfg = model._u3d_cfg
     dtype = trunk.compute_dtype(getattr(model, "compute_dtype", None))
@@ -178,12 +183,14 @@ def run_feam3(model, x):
             lg, _, _, _ = _feam3_forward(tape, cfg, x, tokens, use_cm, model.deep_up, heads=False)
         return _ncdhw(lg.t)
     if torch.is_grad_enabled() and any(p.requires_grad for _, p in named):
+        if renew is not None:
+            raise RuntimeError("a leaf Variable that requires grad is being used in an in-place operation.")
         outs = _Feam3Fn.apply(cfg, dtype, use_cm, bool(model.deep_up), [nm for nm, _ in named], x, tokens,
                               *[p for _, p in named])
     else:
         with torch.no_grad():
             tape = trunk.Tape(dict(named), dtype, record=False)
-            lg, att, deep, feats = _feam3_forward(tape, cfg, x, tokens, use_cm, model.deep_up)
+            lg, att, deep, feats = _feam3_forward(tape, cfg, x, tokens, use_cm, model.deep_up, renew=renew)
         outs = [_ncdhw(lg.t)] + [a.t for a in att] + [_ncdhw(d.t) for d in deep] + [_ncdhw(ft) for ft in feats]
     na = sum(use_cm)
     return outs[0], list(outs[1:1 + na]), list(outs[1 + na:4 + na]), list(outs[4 + na:7 + na])

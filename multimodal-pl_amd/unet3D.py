@@ -314,8 +314,37 @@ class unet3D_with_feam3(_TrunkMixin, nn.Module):
         return feam.run_feam3(self, input)
 
 
+class unet3D_with_feam2(unet3D_with_feam3):
+    """Reference unet3D.py:721-936 — the model evaluate_amos.py:571 builds. Same modules as unet3D_with_feam3; the
+    class tokens are nn.Parameters (in the state_dict, registered last, :788-793) updated INSIDE forward in train
+    mode (each level before its attention). forward(input, mask=None) -> train: (logits, atten_map, deep_map);
+    eval: logits. As in the reference, a train-mode forward with a mask updates the tokens in place, which
+    autograd refuses while they require grad (it works with ema=True), and mask=None fails at ``(mask == l+1)``."""
+
+    def __init__(self, layers, num_classes=12, weight_std=False, ema=False, use_cm=[True, True, True],  # noqa: B006
+                 deep_up=False):
+        super().__init__(layers, num_classes, weight_std, False, use_cm, deep_up)
+        self.class_token1 = nn.Parameter(torch.randn(num_classes - 1, 128))
+        self.class_token2 = nn.Parameter(torch.randn(num_classes - 1, 64))
+        self.class_token3 = nn.Parameter(torch.randn(num_classes - 1, 32))
+        if ema:
+            for param in self.parameters():
+                param.detach_()
+
+    def _trunk_named(self):
+        return [(n, p) for n, p in self.named_parameters() if not n.startswith("class_token")]
+
+    def forward(self, input, mask=None):
+        from u3d import feam
+        if not self.training:
+            return feam.run_feam3(self, input)
+        if mask is None:
+            raise AttributeError("'bool' object has no attribute 'sum'")  # (None == l+1).sum(), unet3D.py:870
+        outs = feam.run_feam3(self, input, renew=(mask, self.num_classes, self.alpha))
+        return outs[0], outs[1], outs[2]
+
+
 # Method-specific variants and discriminators (SURVEY.md §2 rows 3-4): next rows, not on the trunk path.
-unet3D_with_feam2 = _next_row("unet3D_with_feam2", "f2")
 unet3D_with_feam = _next_row("unet3D_with_feam", "f2")
 unet3D_with_eam = _next_row("unet3D_with_eam", "f2")
 unet3D_with_eam_baseline = _next_row("unet3D_with_eam_baseline", "f2")

@@ -417,7 +417,47 @@ def g9():
     save("g9_consistency.npz", **out)
 
 
+def g10():
+    """unet3D_with_feam2 (unet3D.py:721-936, the model evaluate_amos.py:571 builds): state_dict order, eval logits,
+    and the ema=True train forward with a mask (in-forward class-token updates before each level's attention)."""
+    from weights_recipe import param_array
+    nc = 14
+    out = {}
+    x = torch.from_numpy(input_volume((1, 1, 32, 32, 32), seed=80, kind="normal"))
+    lab = np.random.default_rng([82, 0]).integers(0, nc, size=(1, 1, 32, 32, 32))
+    lab[np.isin(lab, [3, 7])] = 0
+    mask = torch.from_numpy(lab.astype(np.float32))
+    for tag, ema in (("eval", False), ("ema", True)):
+        m = R.unet3D_with_feam2([1, 2, 2, 2, 2], num_classes=nc, weight_std=True, ema=ema, deep_up=True)
+        apply_recipe(m, seed=0)   # class tokens are parameters here: the recipe's 2-D class_token rule applies
+        if tag == "eval":
+            out["keys"] = np.array(list(m.state_dict().keys()))
+            m.eval()
+            with torch.no_grad():   # the logits never depend on the tokens: G8's (same weights, same input)
+                g8 = np.load(os.path.join(OUT, "g8_feam3_32.npz"))["nd_logits"]
+                out["eval_minus_g8"] = np.abs(m(x).numpy() - g8).max()
+        else:
+            m.train()
+            logits, att, deep = m(x, mask)
+            out["ema_minus_g8"] = np.abs(logits.detach().numpy() - g8).max()
+            for i in range(3):
+                flat = att[i].detach().reshape(-1)
+                idx = np.random.default_rng([85, i]).integers(0, flat.numel(), size=SAMPLE_N)
+                out[f"ema_att{i}_idx"], out[f"ema_att{i}_val"] = idx, flat[torch.from_numpy(idx)].numpy()
+                out[f"ema_deep{i}"] = deep[i].detach().numpy()
+                out[f"ema_tok{i + 1}"] = getattr(m, f"class_token{i + 1}").detach().numpy()
+    # train mode without ema: the in-place token update on a leaf that requires grad raises
+    m = R.unet3D_with_feam2([1, 2, 2, 2, 2], num_classes=nc, weight_std=True)
+    try:
+        m.train()(x, mask)
+        out["noema_raises"] = np.array(0)
+    except RuntimeError:
+        out["noema_raises"] = np.array(1)
+    out["mask"] = lab.astype(np.float32)
+    save("g10_feam2_32.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9", "g10"]
     for w in which:
         globals()[w]()

@@ -157,3 +157,45 @@ def test_feam3_bf16_attention_close_to_fp32(gpu):
         _, att16, deep16, _ = m(_x(gpu))
     for a, b in zip(att32 + deep32, att16 + deep16):   # norm-wise: bf16 activations through the whole trunk
         assert ((a - b.float()).norm() / a.norm()).item() < 8e-2
+
+
+# ------------------------------------------------------------------ unet3D_with_feam2 (evaluate_amos.py:571)
+def _feam2(gpu, ema):
+    import unet3D
+    m = unet3D.unet3D_with_feam2([1, 2, 2, 2, 2], num_classes=NC, weight_std=True, ema=ema, deep_up=True)
+    apply_recipe(m, seed=0)
+    return m.to(gpu)
+
+
+def test_feam2_state_dict_and_eval_vs_golden(gpu):
+    g, g8 = golden("g10_feam2_32.npz"), golden("g8_feam3_32.npz")
+    m = _feam2(gpu, False)
+    assert list(m.state_dict().keys()) == list(g["keys"])
+    assert float(g["eval_minus_g8"]) == 0.0
+    with torch.no_grad():
+        y = m.eval()(_x(gpu))
+    assert np.abs(y.cpu().numpy() - g8["nd_logits"]).max() < 1e-3
+
+
+def test_feam2_ema_train_tokens_attention_vs_golden(gpu):
+    g, g8 = golden("g10_feam2_32.npz"), golden("g8_feam3_32.npz")
+    m = _feam2(gpu, True).train()
+    logits, att, deep = m(_x(gpu), torch.from_numpy(g["mask"]).to(gpu))
+    assert np.abs(logits.detach().cpu().numpy() - g8["nd_logits"]).max() < 1e-3
+    for i in range(3):
+        ref = g[f"ema_att{i}_val"]
+        got = att[i].detach().reshape(-1).cpu()[torch.from_numpy(g[f"ema_att{i}_idx"])].numpy()
+        assert np.abs(got - ref).max() < 1e-3 * max(1.0, np.abs(ref).max()), i
+        assert np.abs(deep[i].detach().cpu().numpy() - g[f"ema_deep{i}"]).max() < 1e-3
+        np.testing.assert_allclose(getattr(m, f"class_token{i + 1}").detach().cpu().numpy(), g[f"ema_tok{i + 1}"],
+                                   rtol=1e-5, atol=1e-5)
+
+
+def test_feam2_train_errors_like_reference(gpu):
+    g = golden("g10_feam2_32.npz")
+    assert int(g["noema_raises"]) == 1
+    m = _feam2(gpu, False).train()
+    with pytest.raises(RuntimeError):
+        m(_x(gpu), torch.from_numpy(g["mask"]).to(gpu))
+    with pytest.raises(AttributeError):
+        m(_x(gpu))
