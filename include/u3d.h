@@ -276,6 +276,13 @@ int u3d_window_normalize(float* full, const float* count, int n, int C, long lon
 int u3d_dice_metric(const float* logits, const float* labels, int S, long long V, int C, int num_class,
                     long long* counts, float* metrics, long long* argmax /* nullable, [S][V] */,
                     u3d_stream_t stream);
+/* get_dice2 (evaluate_amos.py:156-182, atlas=None): refine [nt organs][2 classes][V] by element strides (organ
+ * rsn, class rsc, voxel rsv), labels [V] (one volume); per organ l the binary prediction argmax(softmax) == 1 vs
+ * labels == l+1: counts [nt][3] int64 (TP, P, T), metrics [nt][3] fp32 (dice, sensitivity, precision as
+ * dice_score / senc_score / spec_score compute them), argmax [nt][V] int64 (nullable). nt <= 64. */
+int u3d_dice_metric_binary(const float* refine, int nt, long long V, long long rsn, long long rsc, long long rsv,
+                           const float* labels, long long* counts, float* metrics, long long* argmax,
+                           u3d_stream_t stream);
 
 /* ---------------------------------------------------------------- DynConv 8,8,2 head of UNet3D (A8, A9)
  * GAP (unet3D.py:1659-1663): out[n][c] = mean_v relu(group_norm(x))[n][v][c] */

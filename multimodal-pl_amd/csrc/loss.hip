@@ -314,6 +314,37 @@ __global__ void dice_final_kernel(const unsigned long long* __restrict__ cnt, in
   m[l * 3 + 2] = sp / (float)S;
 }
 
+// get_dice2 (evaluate_amos.py:156-182, atlas=None): the refiner's output holds one 2-class prediction per organ
+// (sample l = organ l); per organ the binary prediction argmax(softmax(ref[l])) == 1 is scored against the shared
+// label volume == l+1. Element strides for the refiner layout (organ rsn, class rsc, voxel rsv).
+__global__ __launch_bounds__(LT) void dice_binary_count_kernel(const float* __restrict__ ref, long long rsn,
+                                                              long long rsc, long long rsv,
+                                                              const float* __restrict__ lab, long long V,
+                                                              unsigned long long* __restrict__ cnt,
+                                                              long long* __restrict__ amap) {
+  __shared__ unsigned int h[3];
+  if (threadIdx.x < 3) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int l = blockIdx.y;
+  unsigned int a = 0, b = 0, c = 0;
+  for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < V; v += (long long)gridDim.x * LT) {
+    const float r0 = ref[l * rsn + v * rsv], r1 = ref[l * rsn + rsc + v * rsv];
+    const float m = fmaxf(r0, r1);
+    const float e0 = expf(r0 - m), e1 = expf(r1 - m), inv = 1.f / (e0 + e1);
+    const int am = e1 * inv > e0 * inv ? 1 : 0;  // torch.argmax: the first maximum on ties
+    if (amap) amap[(long long)l * V + v] = am;
+    const int t = lab[v] == (float)(l + 1);
+    a += am & t;
+    b += am;
+    c += t;
+  }
+  atomicAdd(&h[0], a);  // integer: order-independent
+  atomicAdd(&h[1], b);
+  atomicAdd(&h[2], c);
+  __syncthreads();
+  if (threadIdx.x < 3 && h[threadIdx.x]) atomicAdd(&cnt[l * 3 + threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
 static int loss_blocks(long long nvox) { return (int)std::min<long long>(1024, std::max<long long>(1, (nvox + LT - 1) / LT)); }
 
 // dispatch on the class count: exact instantiations for the model heads, a guarded 32-wide fallback
@@ -403,4 +434,19 @@ extern "C" int u3d_partial_target(const float* labels, int S, long long V, const
   hipLaunchKernelGGL(partial_target_kernel, dim3(nb), dim3(LT), 0, (hipStream_t)stream, labels, V, S, mask,
                      mask_stride, M, lmin, lmax, out);
   return check_launch("partial_target_kernel");
+}
+
+extern "C" int u3d_dice_metric_binary(const float* refine, int nt, long long V, long long rsn, long long rsc,
+                                      long long rsv, const float* labels, long long* counts, float* metrics,
+                                      long long* argmax, u3d_stream_t stream) {
+  U3D_REQUIRE(refine && labels && counts && metrics && nt >= 1 && nt <= 64 && V >= 1, "dice_metric_binary: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  U3D_HIP(hipMemsetAsync(counts, 0, (size_t)nt * 3 * 8, s));
+  const int nb = (int)std::min<long long>(1024, (V + LT - 1) / LT);
+  hipLaunchKernelGGL(dice_binary_count_kernel, dim3(nb, nt), dim3(LT), 0, s, refine, rsn, rsc, rsv, labels, V,
+                     (unsigned long long*)counts, argmax);
+  // per organ (a batch of one each): the reference's ratios from the integer counts = dice_final_kernel with one
+  // sample and nt "classes"
+  hipLaunchKernelGGL(dice_final_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)counts, 1, nt, metrics);
+  return check_launch("dice_metric_binary");
 }

@@ -57,6 +57,38 @@ def get_dice(preds, labels, t_id, atlas=None, num_class=13):
     return dices, senc, spec, am
 
 
+def get_dice2(preds, labels, t_id, atlas=None, num_class=13):
+    """Reference evaluate_amos.py:156-182 (the refiner's metric, train_amos_atlas_final.py:294): preds = the
+    refiner output [num_class organs, 2, D, H, W]; organ l's binary prediction argmax(softmax(preds[l])) == 1 is
+    scored against labels == l+1. One fused pass (u3d_dice_metric_binary). Returns (dices, senc, spec, argmax)."""
+    if atlas is not None:
+        raise NotImplementedError("get_dice2 atlas branch (evaluate_amos.py:170-180) is not on the native path")
+    from u3d._lib import call
+    from u3d.loss import _voxel_strides
+    ops.require_device(preds, labels)
+    if preds.shape[0] < num_class or preds.shape[1] != 2:
+        raise AssertionError("predict & target batch size don't match")  # dice_score on an empty slice
+    ref, (rsn, rsc, rsv) = _voxel_strides(preds.float(), 2)
+    V = ref[0, 0].numel()
+    lab = labels.float().reshape(-1).contiguous()
+    if lab.numel() != V:
+        raise RuntimeError(f"get_dice2: labels {tuple(labels.shape)} vs prediction volume {tuple(preds.shape[2:])}")
+    counts = torch.empty((num_class, 3), dtype=torch.int64, device=preds.device)
+    metrics = torch.empty((num_class, 3), dtype=torch.float32, device=preds.device)
+    am = torch.empty((preds.shape[0],) + tuple(preds.shape[2:]), dtype=torch.int64, device=preds.device)
+    call("u3d_dice_metric_binary", ref.data_ptr(), num_class, V, rsn, rsc, rsv, lab.data_ptr(), counts.data_ptr(),
+         metrics.data_ptr(), am.data_ptr(), ops._stream())
+    if preds.shape[0] > num_class:  # the reference's argmax covers every organ of the batch
+        call("u3d_dice_metric_binary", ref.data_ptr(), preds.shape[0], V, rsn, rsc, rsv, lab.data_ptr(),
+             torch.empty((preds.shape[0], 3), dtype=torch.int64, device=preds.device).data_ptr(),
+             torch.empty((preds.shape[0], 3), dtype=torch.float32, device=preds.device).data_ptr(), am.data_ptr(),
+             ops._stream())
+    dices = [metrics[l, 0] for l in range(num_class)]
+    senc = [metrics[l, 1] for l in range(num_class)]
+    spec = [metrics[l, 2] for l in range(num_class)]
+    return dices, senc, spec, am
+
+
 def _gaussian_profiles(patch_size, sigma_scale=1.0 / 8):
     """The 1-D factors of _get_gaussian (evaluate_amos.py:184-197): scipy.ndimage.gaussian_filter (truncate 4.0,
     mode 'constant') of a centred delta is the product of three normalised 1-D kernels; each factor is scaled

@@ -2,6 +2,8 @@
 179-182, train_amos_atlas_final.py:303-304) and the refiner-consistency branch over the feam3 attention maps
 (:131-178, train_amos_atlas_final.py:312) — and the refiner loss get_loss_refine (:46-62)."""
 import torch
+import torch.nn.functional as F
+from torch.nn.modules.loss import _WeightedLoss
 
 from loss_functions.loss_partial import EDiceLoss_full, EDiceLoss_partial
 
@@ -47,3 +49,37 @@ def make_partial_target(labels, sup_mask):
     == 0) set to background, one device pass (u3d_partial_target) instead of 13 masked writes."""
     from u3d import ops
     return ops.partial_target(labels, sup_mask, 1, 13).reshape(labels.shape)
+
+
+class SmoothCrossEntropyLoss(_WeightedLoss):
+    """Reference losses.py:441-469 — the style discriminator's loss (the discriminators are out of scope, SURVEY
+    §2; this tiny [B, K] loss is kept so the driver's import line and its calls work): cross entropy against
+    label-smoothed one-hot targets (smoothing / (K-1) off-target), optional class weights, mean / sum / none."""
+
+    def __init__(self, weight=None, reduction="mean", smoothing=0.):
+        super().__init__(weight=weight, reduction=reduction)
+        self.smoothing = smoothing
+        self.weight = weight
+        self.reduction = reduction
+
+    def k_one_hot(self, targets, n_classes, smoothing=0.0):
+        with torch.no_grad():
+            t = torch.full((targets.size(0), n_classes), smoothing / (n_classes - 1), device=targets.device)
+            return t.scatter_(1, targets.data.unsqueeze(1), 1. - smoothing)
+
+    def reduce_loss(self, loss):
+        return loss.mean() if self.reduction == "mean" else loss.sum() if self.reduction == "sum" else loss
+
+    def forward(self, inputs, targets):
+        assert 0 <= self.smoothing < 1
+        targets = self.k_one_hot(targets, inputs.size(-1), self.smoothing)
+        log_preds = F.log_softmax(inputs, -1)
+        if self.weight is not None:
+            log_preds = log_preds * self.weight.unsqueeze(0)
+        return self.reduce_loss(-(targets * log_preds).sum(dim=-1))
+
+
+def bce_loss(y_pred, y_label):
+    """Reference losses.py:471-475: SmoothCrossEntropyLoss against a constant class label for the whole batch."""
+    y = torch.full((y_pred.shape[0],), float(y_label), device=y_pred.device).long()
+    return SmoothCrossEntropyLoss()(y_pred, y)

@@ -65,6 +65,7 @@ _SIGS = {
     "u3d_partial_loss_fwd": [P, P, I, L, I, I, P, I, P, P, P, P],
     "u3d_partial_loss_bwd": [I, P, P, I, L, I, I, P, I, P, P, P, P],
     "u3d_dice_metric": [P, P, I, L, I, I, P, P, P, P],
+    "u3d_dice_metric_binary": [P, I, L, L, L, L, P, P, P, P, P],
     "u3d_gn_relu_mean": [I, P, I, I, L, I, P, P, P, P, P],
     "u3d_dyn_controller": [P, I, I, P, I, P, P, I, P, P],
     "u3d_dynhead_fwd": [P, P, I, L, P, P],

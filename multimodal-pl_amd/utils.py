@@ -3,6 +3,7 @@ extant_file :62-70, all_reduce_tensor :72-74, seedfix :116-149, get_logger :43-5
 import argparse
 import os
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -50,6 +51,19 @@ def all_reduce_tensor(tensor, world_size=1, norm=True):
             t.div_(dist.get_world_size())
         return t
     return torch.mean(tensor)
+
+
+def mask_aug(mask, aug_times=2):
+    """Reference utils.py:76-114: [B, 1, D, H, W] -> [B * aug_times, 1, D, H, W], each sample repeated aug_times
+    times in a row (sample-major). Host-side numpy as in the reference: the output is np.zeros(..., dtype=mask.dtype),
+    so a torch tensor argument raises TypeError there exactly as it does in the reference."""
+    if aug_times <= 1:
+        return mask
+    out = np.zeros((mask.shape[0] * aug_times,) + tuple(mask.shape[1:]), dtype=mask.dtype)
+    for i in range(mask.shape[0]):
+        for j in range(aug_times):
+            out[i * aug_times + j] = mask[i]
+    return out
 
 
 def seedfix(seed):

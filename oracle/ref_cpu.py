@@ -201,6 +201,21 @@ def get_dice(preds, labels, num_class=13):
     return np.array(dices), np.array(senc), np.array(spec)
 
 
+def get_dice2(preds, labels, num_class=13):
+    """evaluate_amos.py:156-182 (atlas=None): organ l's prediction argmax(softmax(preds[l])) == 1 against
+    labels == l+1, per organ dice 2PT/(P+T+1), sensitivity PT/(T+1), precision PT/(P+1)."""
+    am = torch.argmax(torch.softmax(preds, 1), 1)
+    d, se, sp = [], [], []
+    for l in range(num_class):
+        P = (am[l:l + 1] == 1).reshape(1, -1).double()
+        T = (labels == l + 1).reshape(1, -1).double()
+        num = (P * T).sum(1)
+        d.append((2 * num / (P.sum(1) + T.sum(1) + 1)).mean().item())
+        se.append((num / (T.sum(1) + 1)).mean().item())
+        sp.append((num / (P.sum(1) + 1)).mean().item())
+    return np.array(d), np.array(se), np.array(sp), am
+
+
 # ---------------------------------------------------------------------------------------------- next f1
 def gaussian_map(patch_size, sigma_scale=1.0 / 8):
     """_get_gaussian, evaluate_amos.py:184-197: scipy gaussian_filter (truncate 4.0, mode constant) of a centred

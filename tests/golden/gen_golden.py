@@ -457,7 +457,43 @@ def g10():
     save("g10_feam2_32.npz", **out)
 
 
+def g11():
+    """get_dice2 (evaluate_amos.py:156-182): the refiner's per-organ binary Dice / sensitivity / precision."""
+    rng = np.random.default_rng([11, 11])
+    sp = (12, 10, 8)
+    ref = torch.from_numpy((rng.standard_normal((13, 2) + sp) * 2).astype(np.float32))
+    ref[3, 1] = ref[3, 0]                        # exact ties: argmax takes class 0
+    lab = torch.from_numpy(rng.integers(0, 14, (1, 1) + sp).astype(np.float32))
+    d, se, spc, am = REV.get_dice2(ref, lab, 1, num_class=13)
+    save("g11_dice2.npz", refine=ref.numpy(), labels=lab.numpy(), dice=np.array([float(v) for v in d]),
+         senc=np.array([float(v) for v in se]), spec=np.array([float(v) for v in spc]), argmax=am.numpy())
+
+
+def g12():
+    """Driver helpers on the import line (train_amos_atlas_final.py:34-35): utils.mask_aug and the discriminator
+    losses SmoothCrossEntropyLoss / bce_loss (values + gradients)."""
+    import utils as RU
+    from loss_functions import losses as RL
+    rng = np.random.default_rng([12, 12])
+    m = rng.standard_normal((3, 1, 2, 3, 4)).astype(np.float32)
+    out = {"aug_in": m, "aug_out": RU.mask_aug(m, 2), "aug_out3": RU.mask_aug(m, 3)}
+    x = torch.from_numpy(rng.standard_normal((5, 2)).astype(np.float32)).requires_grad_(True)
+    t = torch.from_numpy(rng.integers(0, 2, 5).astype(np.int64))
+    for tag, kw in (("plain", {}), ("smooth", dict(smoothing=0.2)), ("sum", dict(reduction="sum"))):
+        x.grad = None
+        v = RL.SmoothCrossEntropyLoss(**kw)(x, t)
+        v.backward()
+        out[f"sce_{tag}_value"], out[f"sce_{tag}_grad"] = v.detach().numpy(), x.grad.numpy().copy()
+    out["sce_x"], out["sce_t"] = x.detach().numpy(), t.numpy()
+    x.grad = None
+    xb = x.detach().clone().requires_grad_(True)
+    y_pred = xb * 1.0
+    y_pred.get_device = lambda: "cpu"   # the reference moves the labels with .to(y_pred.get_device())
+    out["bce1_value"] = RL.bce_loss(y_pred, 1).detach().numpy()
+    save("g12_driver_helpers.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9", "g10"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12"]
     for w in which:
         globals()[w]()

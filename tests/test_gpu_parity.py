@@ -401,3 +401,15 @@ def test_inference_pack_cache_tracks_weight_updates(gpu):
     m.load_state_dict(sd)
     y3 = fwd()
     assert torch.equal(y3, uncached())
+
+
+def test_g11_get_dice2(gpu):
+    """The refiner's metric (train_amos_atlas_final.py:294) against the reference's own values (incl. exact ties)."""
+    from evaluate_amos import get_dice2
+    g = golden("g11_dice2.npz")
+    d, se, sp, am = get_dice2(torch.from_numpy(g["refine"]).to(gpu), torch.from_numpy(g["labels"]).to(gpu), 1,
+                              num_class=13)
+    np.testing.assert_allclose([float(v) for v in d], g["dice"], atol=1e-6)
+    np.testing.assert_allclose([float(v) for v in se], g["senc"], atol=1e-6)
+    np.testing.assert_allclose([float(v) for v in sp], g["spec"], atol=1e-6)
+    assert np.array_equal(am.cpu().numpy(), g["argmax"])

@@ -69,7 +69,7 @@ def test_reference_names_exported():
     for n in ["DiceLoss", "EDiceLoss_partial", "EDiceLoss_full", "EDiceLoss_full2"]:
         assert hasattr(loss_partial, n)
     assert hasattr(losses, "get_loss")
-    for n in ["dice_score", "spec_score", "senc_score", "get_dice", "predict_sliding"]:
+    for n in ["dice_score", "spec_score", "senc_score", "get_dice", "get_dice2", "predict_sliding"]:
         assert hasattr(evaluate_amos, n)
 
 
@@ -242,3 +242,40 @@ def test_sliding_window_sharded_gloo_world2_matches_oracle():
     ref = predict_sliding(_tile_pred, image, (16, 24, 24), 3)
     for _, got in out:
         np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_driver_helpers_match_reference_fixture():
+    """utils.mask_aug and the discriminator losses on the driver's import line (train_amos_atlas_final.py:34-35)
+    against the reference's own outputs (G12)."""
+    from loss_functions.losses import SmoothCrossEntropyLoss, bce_loss
+    from utils import mask_aug
+    g = golden("g12_driver_helpers.npz")
+    assert np.array_equal(mask_aug(g["aug_in"], 2), g["aug_out"])
+    assert np.array_equal(mask_aug(g["aug_in"], 3), g["aug_out3"])
+    assert mask_aug(g["aug_in"], 1) is g["aug_in"] or np.array_equal(mask_aug(g["aug_in"], 1), g["aug_in"])
+    with pytest.raises(TypeError):       # np.zeros(dtype=torch.float32), as in the reference
+        mask_aug(torch.zeros(1, 1, 2, 2, 2), 2)
+    t = torch.from_numpy(g["sce_t"])
+    for tag, kw in (("plain", {}), ("smooth", dict(smoothing=0.2)), ("sum", dict(reduction="sum"))):
+        x = torch.from_numpy(g["sce_x"]).requires_grad_(True)
+        v = SmoothCrossEntropyLoss(**kw)(x, t)
+        v.backward()
+        np.testing.assert_allclose(float(v), float(g[f"sce_{tag}_value"]), rtol=1e-6)
+        np.testing.assert_allclose(x.grad.numpy(), g[f"sce_{tag}_grad"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(float(bce_loss(torch.from_numpy(g["sce_x"]), 1)), float(g["bce1_value"]), rtol=1e-6)
+
+
+def test_driver_import_line_resolves():
+    """Every name train_amos_atlas_final.py imports from the drop-in modules exists (:19, :27, :29, :34, :35)."""
+    import engine
+    import evaluate_amos
+    import unet3D
+    import utils
+    from loss_functions import losses
+    for mod, names in ((unet3D, ["unet3D_with_feam3", "get_style_discriminator_output", "norm_style_discriminator_output",
+                                 "deep_style_discriminator_output", "unet3D_with_deepsup", "unet3D_g"]),
+                       (evaluate_amos, ["predict_sliding", "get_dice", "get_dice2"]), (engine, ["Engine"]),
+                       (utils, ["adjust_learning_rate", "mask_aug", "seedfix"]),
+                       (losses, ["get_loss_refine", "get_loss", "SmoothCrossEntropyLoss", "bce_loss"])):
+        for n in names:
+            assert hasattr(mod, n), (mod.__name__, n)

@@ -297,3 +297,12 @@ def test_g9_edice_full2():
         np.testing.assert_allclose(float(v), float(g[f"f2_{tag}_value"]), rtol=1e-5)
         v.backward()
         np.testing.assert_allclose(xi.grad.numpy(), g[f"f2_{tag}_grad"], rtol=1e-4, atol=1e-9)
+
+
+def test_g11_get_dice2():
+    g = golden("g11_dice2.npz")
+    d, se, sp, am = O.get_dice2(torch.from_numpy(g["refine"]), torch.from_numpy(g["labels"]), 13)
+    np.testing.assert_allclose(d, g["dice"], atol=1e-6)
+    np.testing.assert_allclose(se, g["senc"], atol=1e-6)
+    np.testing.assert_allclose(sp, g["spec"], atol=1e-6)
+    assert np.array_equal(am.numpy(), g["argmax"])
