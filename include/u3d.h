@@ -156,6 +156,19 @@ int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, const void*
                           float* stats_ws, u3d_stream_t stream);
 int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
                                    u3d_stream_t stream);
+/* Data gradient of the 32->32 conv (u3d_conv32_ring flip) that also accumulates the partial sums of the backward
+ * of the GroupNorm + ReLU in front of the forward conv (x = that GroupNorm's input, gn_* its statistics and affine;
+ * unet3D.py:44-53) into part_ws (u3d_conv32_ring_stats_ws_floats(n) floats); u3d_conv32_ring_gn_bwd_coef turns
+ * them into the apply coefficients coef [n][5][32] + dgamma/dbeta (+= when accumulate_params), and
+ * u3d_gn_bwd_apply_coef writes dx (+)= alpha m dA + bx x + d — the separate partial pass over dA and x is gone. */
+int u3d_conv32_ring_dgrad_gn(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad, const void* x,
+                             const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                             void* dx, float* part_ws, u3d_stream_t stream);
+int u3d_conv32_ring_gn_bwd_coef(const float* part_ws, int n, int d, int h, int w, int gn_groups,
+                                const float* gn_stats, const float* gn_gamma, const float* gn_beta, float* coef,
+                                float* dgamma, float* dbeta, int accumulate_params, u3d_stream_t stream);
+int u3d_gn_bwd_apply_coef(int dtype, const void* da, const void* x, int n, int c, long long v, const float* coef,
+                          void* dx, int accumulate, u3d_stream_t stream);
 
 /* Stride-1 3^3 weight gradient, depth-streaming ring schedule (wgrad_ring.hip): same partial-slab contract as
  * u3d_conv_wgrad_brick ([nsplit][27][cout_p][cin_p] fp32, summed by the caller in fixed order); a split is a

@@ -297,6 +297,36 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     return dx
 
 
+DGRAD_GN = os.environ.get("U3D_DGRAD_GN", "0") != "0"  # GN-bwd partials in the ring dgrad epilogue (measured: -0.3%, off)
+
+
+def dgrad_gn_ok(dy, cin, k, stride, x_shape, G):
+    n, d, h, w_ = x_shape
+    return (DGRAD_GN and CONV32_FN == "u3d_conv32_ring" and dy.dtype == torch.bfloat16 and n <= 16 and 32 % G == 0
+            and _use_conv32(dy.dtype, cin, dy.shape[-1], k, stride, n, w_) and _conv32_fits(dy))
+
+
+def conv_dgrad_gn_bwd(dy, wpk_dgrad, x, gn, dx=None, accumulate=False, dgamma=None, dbeta=None):
+    """Ring data gradient of the 32->32 conv + the backward of the GroupNorm+ReLU in front of it, with the GN
+    partial sums taken in the dgrad epilogue: returns the gradient w.r.t. the GN input x (written into / added to
+    ``dx``)."""
+    st, ga, be, G = gn
+    n, d, h, w_, c = x.shape
+    dA = torch.empty_like(x)
+    ws = WS.get(4 * query("u3d_conv32_ring_stats_ws_floats", n), x.device, slot=10)
+    call("u3d_conv32_ring_dgrad_gn", dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), x.data_ptr(), st.data_ptr(),
+         ga.data_ptr(), be.data_ptr(), G, dA.data_ptr(), ws.data_ptr(), _stream())
+    coef = torch.empty((n, 5, 32), dtype=torch.float32, device=x.device)
+    call("u3d_conv32_ring_gn_bwd_coef", ws.data_ptr(), n, d, h, w_, G, st.data_ptr(), ga.data_ptr(), be.data_ptr(),
+         coef.data_ptr(), _ptr(dgamma), _ptr(dbeta), 0, _stream())
+    if dx is None:
+        dx = torch.empty_like(x)
+        accumulate = False
+    call("u3d_gn_bwd_apply_coef", dt_code(x.dtype), dA.data_ptr(), x.data_ptr(), n, c, d * h * w_, coef.data_ptr(),
+         dx.data_ptr(), int(accumulate), _stream())
+    return dx
+
+
 USE_BRICK_WGRAD = True
 USE_RING_WGRAD = True      # stride-1 3^3 weight gradients: depth-streaming ring kernel (wgrad_ring.hip)
 RING_WGRAD_MIN_HW = 8      # h, w extents below this use the brick kernel (measured faster from 12^3 up)

@@ -221,6 +221,17 @@ class Tape:
                 part, ns = self.wgrad_async(lambda: ops.conv_wgrad(dyT, x.t, k, stride, gn), dyT, x.t,
                                             gn[0] if gn is not None else None)
                 self.pend_wgrad(part, ns, W, st, std, key + ".weight")
+                if (not head and gn is not None and pair is None
+                        and ops.dgrad_gn_ok(dyT, cin, k, stride, x.t.shape[:4], G)):
+                    # the GN backward's partial sums come from the dgrad epilogue: one apply pass remains
+                    dg = self.grad_out(gn_key + ".weight", gn[1])
+                    db = self.grad_out(gn_key + ".bias", gn[2])
+                    self.before_write(x.grad)
+                    x.grad = ops.conv_dgrad_gn_bwd(dyT, pd, x.t, gn, dx=x.grad, accumulate=x.grad is not None,
+                                                   dgamma=dg, dbeta=db)
+                    self.grad_done(gn_key + ".weight")
+                    self.grad_done(gn_key + ".bias")
+                    return
                 if not head:
                     dA = ops.conv_dgrad(dyT, pd, cin, x.t.shape[:4], k, stride)
                 if gn is not None and pair == "park":
