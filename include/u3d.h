@@ -383,6 +383,26 @@ int u3d_edice_full2_fwd(const float* x, const float* t, const float* m, long lon
 int u3d_edice_full2_bwd(const float* x, const float* t, const float* m, long long V, int sigmoid, const float* coef,
                         const float* grad_out, float* dx, u3d_stream_t stream);
 
+/* ---------------------------------------------------------------- training data path (f4, MOTSDataset.py)
+ * u3d_volume_stats: [mean, population std, min, max] of x[0..V) followed by count - V zeros (the padding of
+ * pad_image, which truncate's np.mean / np.std see), fp64, fixed order; ws u3d_volume_stats_ws_bytes.
+ * u3d_crop_transpose: out[c][dd][hh][ww] = f(src[c][b0+hh][c0+ww][a0+dd]) (zero outside src = pad_image), f = copy /
+ * CT truncate (clip +-325, /325) / MRI (x - stats[0]) / stats[1] (truncate :171-186, crop :364-371, transpose
+ * :376-378). u3d_aug_*: the batchgenerators intensity transforms of my_collate (:33-52) with host-drawn
+ * parameters: additive Gaussian noise (counter-based RNG), one separable pass of scipy's gaussian_filter ('reflect',
+ * fp64 accumulation) along the middle axis of [outer][L][inner], x*mul + add, contrast around the mean with the
+ * range preserved (stats from u3d_volume_stats). */
+long long u3d_volume_stats_ws_bytes(void);
+int u3d_volume_stats(const float* x, long long V, long long count, float* out4, void* ws, u3d_stream_t stream);
+int u3d_crop_transpose(const float* src, int C, int sh, int sw, int sd, int b0, int c0, int a0, int ch, int cw, int cd,
+                       int mode, const float* stats, float* out, u3d_stream_t stream);
+int u3d_aug_noise(float* x, long long V, float sigma, unsigned long long seed, u3d_stream_t stream);
+int u3d_aug_blur_axis(const float* x, float* y, long long outer, int L, long long inner, const float* w, int radius,
+                      u3d_stream_t stream);
+int u3d_aug_affine(float* x, long long V, float mul, float add, u3d_stream_t stream);
+int u3d_aug_contrast(float* x, long long V, float factor, const float* stats, int preserve_range,
+                     u3d_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,10 +91,17 @@ _SIGS = {
     "u3d_consistency_bwd": [P, P, P, I, L, L, P, L, L, I, P, L, L, L, P, I, L, F, P, P, P, P, P, P, P],
     "u3d_edice_full2_fwd": [P, P, P, L, I, I, P, P, P, P],
     "u3d_edice_full2_bwd": [P, P, P, L, I, P, P, P, P],
+    "u3d_volume_stats_ws_bytes": [],
+    "u3d_volume_stats": [P, L, L, P, P, P],
+    "u3d_crop_transpose": [P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
+    "u3d_aug_noise": [P, L, F, ctypes.c_ulonglong, P],
+    "u3d_aug_blur_axis": [P, P, L, I, L, P, I, P],
+    "u3d_aug_affine": [P, L, F, F, P],
+    "u3d_aug_contrast": [P, L, F, P, I, P],
 }
 _RESTYPE = {"u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
             "u3d_eam_attn_bwd_part_floats": L, "u3d_upsample_trilinear_bwd_ws_floats": L, "u3d_renew_token_ws_bytes": L,
-            "u3d_consistency_ws_bytes": L}
+            "u3d_consistency_ws_bytes": L, "u3d_volume_stats_ws_bytes": L}
 
 _lib = None
 

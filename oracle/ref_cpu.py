@@ -398,6 +398,62 @@ def get_loss_consistency(output, target, mask, attns, refine_output, label_t, co
     return dice_loss + aux * aux_weight
 
 
+# ---------------------------------------------------------------------------------------------- next f4
+def truncate(ct, name):
+    """AMOSDataSet_newatlas.truncate, MOTSDataset.py:171-186: CT (case id < 500) clipped to [-325, 325] and / 325;
+    MRI z-scored with np.mean / np.std (population) of the whole (padded) array. float64 as numpy computes it."""
+    ct = np.array(ct, dtype=np.float64, copy=True)
+    if float(name) < 500:
+        ct[ct <= -325] = -325
+        ct[ct >= 325] = 325
+        return (ct - 0) / 325.
+    ct = ct - np.mean(ct)
+    return ct / np.std(ct)
+
+
+def pad_image(img, target, lead=0):
+    """pad_image / pad_image2, MOTSDataset.py:269-297: zero-pad the trailing three dims up to target."""
+    pads = [(0, 0)] * lead + [(0, max(0, int(math.ceil(t - n)))) for t, n in zip(target, img.shape[lead:])]
+    return np.pad(img, pads, "constant")
+
+
+def get_item_tensors(image, label, catlas, name, crop_size, rng, usage="train"):
+    """The tensor part of AMOSDataSet_newatlas.__getitem__ (MOTSDataset.py:355-384) after the file reads and the
+    atlas resize: pad to crop + 5, truncate, random crop (rng.randint in the order b, c, a), (H, W, D) -> (D, H, W)."""
+    cd, ch, cw = crop_size
+    tgt = [ch + 5, cw + 5, cd + 5]
+    image, label = pad_image(image, tgt), pad_image(label, tgt)
+    catlas = pad_image(catlas, tgt, lead=1)
+    image = truncate(image, name)
+    if usage == "train":
+        b = rng.randint(label.shape[0] - ch)
+        c = rng.randint(label.shape[1] - cw)
+        a = rng.randint(label.shape[2] - cd)
+        image = image[b:b + ch, c:c + cw, a:a + cd]
+        label = label[b:b + ch, c:c + cw, a:a + cd]
+        catlas = catlas[:, b:b + ch, c:c + cw, a:a + cd]
+    image = image[np.newaxis].transpose((0, 3, 1, 2)).astype(np.float32)
+    label = label[np.newaxis].transpose((0, 3, 1, 2)).astype(np.float32)
+    catlas = catlas.transpose((0, 3, 1, 2))
+    return image, label, catlas
+
+
+def aug_blur(x, sigma):
+    """batchgenerators augment_gaussian_blur on one channel: scipy.ndimage.gaussian_filter(x, sigma, order=0)."""
+    from scipy.ndimage import gaussian_filter
+    return gaussian_filter(np.asarray(x, dtype=np.float64), sigma, order=0).astype(np.float32)
+
+
+def aug_contrast(x, factor, preserve_range=True):
+    """batchgenerators augment_contrast on one channel: (x - mean) * factor + mean, clipped to the original range."""
+    x = np.asarray(x, dtype=np.float64)
+    mn, lo, hi = x.mean(), x.min(), x.max()
+    y = (x - mn) * factor + mn
+    if preserve_range:
+        y = np.clip(y, lo, hi)
+    return y.astype(np.float32)
+
+
 def params_from_module_dict(sd):
     return {k: v.detach().float().cpu() for k, v in sd.items()}
 
