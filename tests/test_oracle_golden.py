@@ -236,7 +236,10 @@ def test_g8_feam3_forward_backward(deep_up):
         for i in range(3):
             np.testing.assert_allclose(att[i].detach().numpy(), g[f"nd_att{i}"], rtol=1e-4, atol=1e-4)
             np.testing.assert_allclose(deep[i].detach().numpy(), g[f"nd_deep{i}"], rtol=1e-4, atol=1e-4)
-            np.testing.assert_allclose(feats[i].numpy(), g[f"feat{i}"], rtol=1e-4, atol=1e-4)
+            # The stored features are unnormalised decoder sums (|x| up to ~1e2): values near zero come from
+            # cancellation, so the bound is relative to the tensor's scale (1e-5 x max|x|), not per element.
+            ref = g[f"feat{i}"]
+            np.testing.assert_allclose(feats[i].numpy(), ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())
     outs = [logits] + att + deep
     ups = feam3_projections(deep_up, [tuple(t.shape) for t in outs])
     sum((t * u).sum() for t, u in zip(outs, ups)).backward()
@@ -245,7 +248,9 @@ def test_g8_feam3_forward_backward(deep_up):
             assert params[k].grad is None, k
             continue
         gr = params[k].grad.reshape(-1).double()
-        np.testing.assert_allclose(gr.norm().item(), g[f"{tag}_gnorm"][i], rtol=1e-3, atol=1e-6, err_msg=k)
+        # rtol 2e-3 (as the device test): the fp32 CPU conv accumulation order differs between host CPUs and the
+        # backward through the attention maps amplifies it (1.2e-3 seen on one GroupNorm bias across hosts).
+        np.testing.assert_allclose(gr.norm().item(), g[f"{tag}_gnorm"][i], rtol=2e-3, atol=1e-6, err_msg=k)
 
 
 def test_g8_renew_token_and_row_quirk():
