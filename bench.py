@@ -94,7 +94,7 @@ def dominant_kernel_roofline(device, batch, patch, live=None, reps=20):
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_source": tsrc, "algorithmic_bytes": 3 * batch * patch ** 3 * 32 * 2,
             "avg_launch_ms": round(ms, 4), "timing": src, "standalone_launch_ms": round(ms_alone, 4),
-            "flop_per_launch": flops}
+            "flop_per_launch": flops, "rocprof_check": timing_check(batch, patch, flops)}
 
 
 def pmc_traffic(batch, patch):
@@ -107,6 +107,22 @@ def pmc_traffic(batch, patch):
         return None, None
     with open(files[-1]) as f:
         return int(json.load(f)["traffic_bytes"]), os.path.relpath(files[-1], REPO)
+
+
+def timing_check(batch, patch, flops):
+    """The newest committed cross-check of the live event timing against the rocprofv3 kernel trace of the same
+    run (profiles/rNN_conv32_timing_check.json, tools/timing_check.py): reported beside `achieved`, with the
+    roofline fraction the trace's in-step average gives. Only valid for the configuration it was measured on."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_conv32_timing_check.json")))
+    if not files or (batch, patch) != (2, 96):
+        return None
+    with open(files[-1]) as f:
+        c = json.load(f)
+    return {"file": os.path.relpath(files[-1], REPO), "in_step_events_us": c["in_step_events_us"],
+            "in_step_trace_us": c["in_step_trace_us"], "standalone_events_us": c["standalone_events_us"],
+            "standalone_trace_us": c["standalone_trace_us"],
+            "frac_at_trace_in_step": round(flops / (c["in_step_trace_us"] * 1e-6) / 1e12 / PEAK_BF16_TFLOPS, 4)}
 
 
 def cpu_baseline(patch):
