@@ -94,7 +94,8 @@ def dominant_kernel_roofline(device, batch, patch, live=None, reps=20):
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_source": tsrc, "algorithmic_bytes": 3 * batch * patch ** 3 * 32 * 2,
             "avg_launch_ms": round(ms, 4), "timing": src, "standalone_launch_ms": round(ms_alone, 4),
-            "flop_per_launch": flops, "rocprof_check": timing_check(batch, patch, flops)}
+            "flop_per_launch": flops, "rocprof_check": timing_check(batch, patch, flops),
+            "peak_measured": measured_peak(achieved)}
 
 
 def pmc_traffic(batch, patch):
@@ -107,6 +108,19 @@ def pmc_traffic(batch, patch):
         return None, None
     with open(files[-1]) as f:
         return int(json.load(f)["traffic_bytes"]), os.path.relpath(files[-1], REPO)
+
+
+def measured_peak(achieved):
+    """The newest committed on-box calibration (profiles/rNN_peaks.json, tools/peak.hip: back-to-back bf16 MFMA on
+    every CU at the clock held under load; HBM read/copy). `peak` stays the guide's dense figure; this is beside it."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_peaks.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        c = json.load(f)
+    return {"file": os.path.relpath(files[-1], REPO), "mfma_bf16_tflops": c["mfma_bf16_dense_tflops"],
+            "hbm_read_gbs": c["hbm_read_gbs"], "frac_of_measured": round(achieved / c["mfma_bf16_dense_tflops"], 4)}
 
 
 def timing_check(batch, patch, flops):

@@ -12,8 +12,14 @@ import statistics
 import sys
 
 kt, log, steps, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-db = glob.glob(f"{kt}/**/*.db", recursive=True)[0]
-rows = list(sqlite3.connect(db).execute("select name, start, end, grid_x from kernels order by start"))
+dbs = glob.glob(f"{kt}/**/*.db", recursive=True)
+if dbs:
+    rows = list(sqlite3.connect(dbs[0]).execute("select name, start, end, grid_x from kernels order by start"))
+else:  # --output-format csv
+    import csv
+    rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Grid_Size_X"]))
+                   for r in csv.DictReader(open(glob.glob(f"{kt}/**/*kernel_trace.csv", recursive=True)[0]))),
+                  key=lambda r: r[1])
 fwd = [i for i, r in enumerate(rows) if "conv32_ring_kernel<false, true" in r[0] and r[3] >= 256 * 512]
 alone, in_step = fwd[-23:], fwd[:-23][-5 * steps:]
 dur = lambda i: (rows[i][2] - rows[i][1]) / 1e3  # noqa: E731
