@@ -249,9 +249,12 @@ def main():
     _ops.PROBE = None
     live = None
     try:  # dominant kernel timed live over the timed region (eager: every launch; graph: the last replay)
-        durs = [e0.elapsed_time(e1) for e0, e1, _ in probes]
+        # only the full-patch launches: the trunk also runs a 32->32 ring conv at half resolution, whose shorter
+        # launch must not enter an average priced at the full-patch FLOPs
+        full = a.batch * a.patch ** 3
+        durs = [e0.elapsed_time(e1) for e0, e1, v in probes if v == full]
         if durs:
-            live = (sum(durs) / len(durs), len(durs), probes[0][2],
+            live = (sum(durs) / len(durs), len(durs), full,
                     "every launch of the timed steps" if a.eager else "the last timed hipGraph replay")
     except Exception as e:  # noqa: BLE001 - event nodes not timeable on this runtime: fall back below
         print(f"[bench] live kernel timing unavailable ({e}); using the standalone measurement", file=sys.stderr)

@@ -1,8 +1,8 @@
 """Cross-check of the bench's live HIP-event timing of the dominant kernel against the rocprofv3 kernel trace of the
 same run (`tools/gpu_check.sh TAG prof`: bench.py --steps K --warmup W under rocprofv3 --kernel-trace).
 
-In-step launches = the 96^3 conv32 ring forward launches (GN prologue, with or without residual: the ones
-ops.PROBE wraps) of the K timed steps; standalone = the trailing 3 + 20 launches of bench.dominant_kernel_roofline
+In-step launches = the full-patch (2x96^3, 256-workgroup) conv32 ring forward launches (GN prologue, with or
+without residual: the ones bench.py averages) of the K timed steps; standalone = the trailing 3 + 20 launches of bench.dominant_kernel_roofline
 (each followed by its statistics finalize; the events there bracket both).
 Usage: python tools/timing_check.py gpurun_out/TAG/kt gpurun_out/TAG/bench_kt.log STEPS OUT.json"""
 import glob
@@ -21,10 +21,11 @@ else:  # --output-format csv
                    for r in csv.DictReader(open(glob.glob(f"{kt}/**/*kernel_trace.csv", recursive=True)[0]))),
                   key=lambda r: r[1])
 fwd = [i for i, r in enumerate(rows) if "conv32_ring_kernel<false, true" in r[0] and r[3] >= 256 * 512]
-alone, in_step = fwd[-23:], fwd[:-23][-5 * steps:]
-dur = lambda i: (rows[i][2] - rows[i][1]) / 1e3  # noqa: E731
 line = json.loads([l for l in open(log) if l.startswith("{")][-1])
 roof = line["roofline"]
+nev = int(roof["timing"].split(",")[1].split()[0])  # "HIP events, N launches, ..." (full-patch launches only)
+alone, in_step = fwd[-23:], fwd[:-23][-nev:]
+dur = lambda i: (rows[i][2] - rows[i][1]) / 1e3  # noqa: E731
 t_alone = [(rows[i + 1][2] - rows[i][1]) / 1e3 for i in alone[3:]]  # conv + finalize, as the events bracket them
 res = {
     "source": {"trace": kt, "bench_line": log},
