@@ -7,7 +7,8 @@ synthetic CT-like volumes, random-init weights. One step = forward + EDiceLoss_p
 
 Prints ONE JSON line on rank 0. `roofline` is the dominant kernel (the 32->32 3^3 conv at 96^3, 50.9% of
 forward FLOPs) timed with HIP events on the stream it is launched on; `cpu_baseline` times the oracle
-(plain-PyTorch fp32 restatement) on this host's cores on a bounded sample (one 1x96^3 training step).
+(plain-PyTorch fp32 restatement) on this host's cores on the same 2x96^3 step (warm-up + median of 3).
+`--gpus N` without WORLD_SIZE in the environment starts the N ranks itself (one process per GPU).
 """
 import argparse
 import json
@@ -39,6 +40,7 @@ def parse():
                         "(MOTSDataset.py:171-185), the batch's mask[0] applied to both (loss_partial.py:87)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--print-rank-env", action="store_true", help=argparse.SUPPRESS)  # launcher test (no GPU)
     p.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph (~1%% faster at "
                    "N=1; the roofline kernel then falls back to a standalone timing: graph event nodes are not "
                    "timeable)")
@@ -139,33 +141,75 @@ def timing_check(batch, patch, flops):
             "frac_at_trace_in_step": round(flops / (c["in_step_trace_us"] * 1e-6) / 1e12 / PEAK_BF16_TFLOPS, 4)}
 
 
-def cpu_baseline(patch):
-    """Oracle (plain PyTorch fp32 CPU restatement) timed on one 1x1xpatch^3 training step on this host."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(batch, patch, reps=3):
+    """Oracle (plain PyTorch fp32 CPU restatement, oracle/ref_cpu.py) timed on this host: SURVEY §8(d) procedure —
+    the same workload as the GPU step (batch x 1 x patch^3, fwd + EDiceLoss_partial + bwd), one full-size warm-up,
+    then the median of ``reps`` steps. Threads: every core of this process's affinity mask, capped by the
+    OMP_NUM_THREADS share the box grants (16 per GPU on the pool; os.cpu_count() shows the whole machine there)."""
+    import statistics
     from oracle import ref_cpu as O
     from oracle.weights_recipe import recipe_state_dict
     ncpu = len(os.sched_getaffinity(0))
-    torch.set_num_threads(max(1, min(ncpu, 32)))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    torch.set_num_threads(max(1, min(ncpu, share) if share > 0 else ncpu))
     P = {k: torch.from_numpy(v).requires_grad_(True) for k, v in recipe_state_dict(O.state_shapes_baseline(16)).items()}
-    x, lab, mask = synthetic(1, patch, "cpu", 7)
+    x, lab, mask = synthetic(batch, patch, "cpu", 7)
 
-    def step(xx, ll):
-        y = O.baseline_forward(P, xx)
-        loss = O.edice_partial(y, ll.squeeze(1), mask=[mask])
+    def step():
+        for p in P.values():
+            p.grad = None
+        t0 = time.perf_counter()
+        y = O.baseline_forward(P, x)
+        loss = O.edice_partial(y, lab.squeeze(1), mask=[mask])
         loss.backward()
-        return loss
+        return time.perf_counter() - t0
 
-    xs, ls, _ = synthetic(1, 32, "cpu", 8)
-    step(xs, ls)  # warm-up (small)
-    t0 = time.perf_counter()
-    step(x, lab)
-    dt = time.perf_counter() - t0
-    return {"value": round(patch ** 3 / dt, 1), "unit": "voxels/s", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"1 training step (fwd+EDiceLoss_partial+bwd, fp32) at 1x1x{patch}^3, "
-                                      f"{dt:.2f} s, oracle/ref_cpu.py"}
+    warm = step()
+    ts = [step() for _ in range(reps)]
+    dt = statistics.median(ts)
+    return {"value": round(batch * patch ** 3 / dt, 1), "unit": "voxels/s", "cores": torch.get_num_threads(),
+            "cpu_model": _cpu_model(), "affinity_cores": ncpu, "kind": "port",
+            "sample": f"{batch}x1x{patch}^3 training step (fwd+EDiceLoss_partial+bwd, fp32, oracle/ref_cpu.py): "
+                      f"1 warm-up ({warm:.2f} s) + median of {reps} ({', '.join('%.2f' % t for t in ts)} s)"}
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N child ranks (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous on
+    127.0.0.1) before this process touches the GPU, pass their output through, exit with the worst status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))
+    if a.print_rank_env:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}))
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -173,6 +217,7 @@ def main():
     device = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
+        assert dist.get_world_size() == world
 
     import unet3D
     from loss_functions.loss_partial import EDiceLoss_partial
@@ -268,7 +313,7 @@ def main():
         step_gflop = STEP_GFLOP_PER_SAMPLE * a.batch * (a.patch / 96) ** 3
         roof["step_mfma_frac"] = round(step_gflop / (ms * 1e-3) / 1e3 / PEAK_BF16_TFLOPS, 4)
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(a.patch)
+        cpu = cpu_baseline(a.batch, a.patch)
     if rank == 0:
         out = {
             "metric": "train voxels/sec at 96^3 patch, 1/2/4/8 MI355X; fwd+bwd step ms",
@@ -277,7 +322,9 @@ def main():
             "dtype": a.dtype, "data": "synthetic (CT-normalised random volumes, random labels, random-init weights)",
             "config": {"workload": "unet3D_baseline([1,2,2,2,2],16,weight_std) fwd+EDiceLoss_partial+bwd+SGD",
                        "model": "unet3D_baseline-16", "global_batch": world * a.batch, "seq_len": a.patch ** 3,
-                       "patch": [a.patch] * 3, "parallelism": f"dp{world}"},
+                       "patch": [a.patch] * 3, "parallelism": f"dp{world}",
+                       "backend": dist.get_backend() if world > 1 else None,
+                       "world_size_seen": dist.get_world_size() if world > 1 else 1},
             "loss": round(loss_v, 6), "launch": "eager" if a.eager else "hipgraph",
             "roofline": roof, "cpu_baseline": cpu,
         }

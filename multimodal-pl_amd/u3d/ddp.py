@@ -51,11 +51,13 @@ class GradBucketer:
             self.buckets.append((cur, cur_n))
         self.device = params[0][1].device if params else None
         self.active = False
+        self.synced = set()
 
     def begin(self):
         self.bufs = [torch.empty(nel, dtype=torch.float32, device=self.device) for _, nel in self.buckets]
         self.left = [len(names) for names, _ in self.buckets]
         self.done_names = set()
+        self.synced = set()
         self.works = [None] * len(self.buckets)
         self.active = True
 
@@ -109,26 +111,54 @@ class GradBucketer:
             w.wait()
             if not self.avg_native:
                 self.bufs[b].div_(self.world)
+        self.synced = set(self.done_names)  # averaged here: the post-accumulate hooks skip these
         self.active = False
+
+    def average(self, t):
+        """Synchronous mean over ranks of one gradient the native backward did not produce."""
+        if self.avg_native:
+            dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            t.div_(self.world)
 
 
 class U3DDataParallel(torch.nn.Module):
-    """DDP-style wrapper: ``.module`` is the wrapped model (train_amos_atlas_final.py:391 uses it)."""
+    """DDP-style wrapper: ``.module`` is the wrapped model (train_amos_atlas_final.py:391 uses it).
+
+    Gradients written by the native tapes (trunk, dynamic head, feam heads) are averaged in buckets from inside
+    the backward. Any other parameter gradient (plain torch autograd, a subgraph the tapes do not cover) is caught
+    by a post-accumulate hook and averaged there, synchronously, so no rank is ever left with an unsynchronised
+    gradient."""
 
     def __init__(self, module, group=None, bucket_mb=25.0):
         super().__init__()
         self.module = module
         self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
         self.bucketer = GradBucketer(module.named_parameters(), bucket_mb, group) if self.distributed else None
+        self.fallback_names = []  # parameters averaged by the hook in the last backward (tests / diagnostics)
         if self.distributed:
             with torch.no_grad():  # start from identical weights on every rank (DDP's init broadcast)
                 for p in module.parameters():
                     dist.broadcast(p.data, 0, group=group)
             from . import ops
             ops.WEIGHT_GEN[0] += 1  # .data writes bump no autograd version: invalidate cached weight packs
+            for name, p in module.named_parameters():
+                if p.requires_grad:
+                    p.register_post_accumulate_grad_hook(self._hook(name))
+
+    def _hook(self, name):
+        def fn(p):
+            if name in self.bucketer.synced:  # averaged in its bucket: exempt this one accumulation
+                self.bucketer.synced.discard(name)
+                return
+            self.bucketer.average(p.grad)
+            self.fallback_names.append(name)
+        return fn
 
     def forward(self, *args, **kwargs):
         if self.bucketer is None or not torch.is_grad_enabled():
             return self.module(*args, **kwargs)
+        self.fallback_names = []
         with use_sink(self.bucketer):
             return self.module(*args, **kwargs)

@@ -1,0 +1,122 @@
+"""Data-parallel equivalence of the native training step ("N-GPU step == 1-GPU step on the concatenated
+batch"; reference: engine.data_parallel + DDP, train_amos_atlas_final.py:141-144,375; run_amos_atlas_final.sh:2).
+
+Two ranks share cuda:0 (the pool's boxes have one GPU; RCCL refuses two ranks on one device), so the collective is
+gloo on device tensors. What runs is the production data-parallel machinery: U3DDataParallel around
+unet3D_baseline(16), the native backward writing parameter gradients straight into flat bucket views, the
+bucket-ordered weight-gradient flush (u3d/trunk.py Tape.backward: needs_flush -> flush_wgrads) with 1 MB buckets so
+that ~70 buckets complete one after another inside the backward, the SUM + divide branch of the averaging, and the
+post-accumulate hook that averages a gradient the native tape did not produce (an extra parameter used by plain
+torch autograd). Rank r trains on sample r of a batch of two; the single-process reference trains on the whole
+batch with the loss averaged over the two samples (the partial-label Dice is a sum over the batch, so each rank's
+loss is the per-sample term and the mean of the rank gradients is the gradient of the mean).
+
+Tolerance: fp32 parity mode; the only difference is the summation order of the two samples' contributions (inside
+the weight-gradient split partials vs across the all-reduce). Weight standardisation's backward cancels most of a
+raw weight gradient (the conv inputs are ReLU outputs, >= 0), which amplifies that fp32 reordering noise (measured
+3.2e-4 worst rel L2): per-parameter relative L2 <= 2e-3, far below what a missing or doubled average gives (O(1)),
+and after one SGD step (lr 0.1, momentum 0.9, wd 1e-4, u3d.optim.SGD) every weight within 1e-6 of the reference."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+MASK = [1, 1, 0, 1, 1, 0, 1, 1, 1, 0, 1, 1, 1, 1, 0, 1]
+
+
+def _build(dev):
+    import unet3D
+    from oracle.weights_recipe import apply_recipe
+    m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=16, weight_std=True)
+    apply_recipe(m, seed=0)
+    m.register_parameter("extra_scale", torch.nn.Parameter(torch.tensor(1.25)))
+    return m.to(dev).train()
+
+
+def _data(dev):
+    from oracle.weights_recipe import input_volume, label_volume
+    x = torch.from_numpy(input_volume((2, 1, 32, 32, 32), seed=51, kind="ct")).to(dev)
+    lab = torch.from_numpy(label_volume((2, 32, 32, 32), 16, seed=52)).to(dev)
+    return x, lab
+
+
+def _step(m, net, x, lab, samples):
+    from loss_functions.loss_partial import EDiceLoss_partial
+    from u3d.optim import SGD
+    crit = EDiceLoss_partial(16)
+    mask = [torch.tensor(MASK)]
+    opt = SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    opt.zero_grad(set_to_none=True)
+    lg, _, _ = net(x)
+    lg = lg * m.extra_scale
+    loss = sum(crit(lg[i:i + 1], lab[i:i + 1], mask=mask) for i in range(len(samples))) / len(samples)
+    loss.backward()
+    grads = {k: p.grad.detach().cpu() for k, p in m.named_parameters()}
+    opt.step()
+    return grads, {k: p.detach().cpu() for k, p in m.named_parameters()}
+
+
+def _worker(rank, world, port, ref_path, q):
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import torch.distributed as dist
+    try:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from u3d.ddp import U3DDataParallel
+        m = _build(dev)
+        net = U3DDataParallel(m, bucket_mb=1.0)
+        assert net.bucketer is not None and len(net.bucketer.buckets) > 20
+        x, lab = _data(dev)
+        grads, weights = _step(m, net, x[rank:rank + 1], lab[rank:rank + 1], [rank])
+        torch.cuda.synchronize()
+        ref = torch.load(ref_path, weights_only=True)
+        gerr = max((((grads[k].double() - ref["g"][k].double()).norm()
+                     / ref["g"][k].double().norm().clamp_min(1e-30)).item(), k) for k in grads)
+        werr = max((weights[k] - ref["w"][k]).abs().max().item() for k in weights)
+        q.put((rank, gerr, werr, sorted(net.fallback_names), None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 - report to the parent instead of hanging its queue
+        import traceback
+        q.put((rank, None, None, None, traceback.format_exc()))
+        raise
+
+
+def test_u3d_data_parallel_world2_equals_concatenated_batch(gpu, tmp_path):
+    x, lab = _data(gpu)
+    m = _build(gpu)
+    g, w = _step(m, m, x, lab, [0, 1])
+    ref_path = str(tmp_path / "ref.pt")
+    torch.save({"g": g, "w": w}, ref_path)
+    del m
+    torch.cuda.synchronize()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, ref_path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=100) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for rank, gerr, werr, fallback, tb in out:
+        assert tb is None, tb
+        print(f"rank {rank}: worst gradient rel L2 {gerr[0]:.3e} ({gerr[1]}), weights {werr:.3e}")
+        assert gerr[0] <= 2e-3, f"rank {rank}: worst parameter-gradient rel L2 vs the concatenated batch {gerr}"
+        assert werr <= 1e-6, f"rank {rank}: post-SGD weights off by {werr:.3e}"
+        assert fallback == ["extra_scale"], fallback  # everything else went through the native buckets
+    for p in procs:
+        assert p.exitcode == 0

@@ -183,6 +183,64 @@ def test_ddp_bucketer_gloo_world2():
     assert np.allclose(out[0][2], out[1][2])  # init broadcast: identical weights on both ranks
 
 
+def _fallback_worker(rank, world, port, q):
+    """Plain torch autograd parameters (no native tape) under U3DDataParallel: every gradient reaches the
+    post-accumulate hook and is averaged; equals one process on the concatenated batch."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from u3d.ddp import U3DDataParallel
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 2))
+    net = U3DDataParallel(m)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 6, generator=g)
+    net(x[2 * rank:2 * rank + 2]).square().mean().backward()
+    grads = {k: p.grad.tolist() for k, p in m.named_parameters()}
+    q.put((rank, grads, sorted(net.fallback_names)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_fallback_hook_averages_non_native_grads_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fallback_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=60) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 2))
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 6, generator=g)
+    (0.5 * (m(x[:2]).square().mean() + m(x[2:]).square().mean())).backward()
+    for rank, grads, fallback in out:
+        assert fallback == sorted(k for k, _ in m.named_parameters())
+        for k, p in m.named_parameters():
+            assert np.allclose(grads[k], p.grad.numpy(), rtol=1e-6, atol=1e-7), (rank, k)
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus N` (the driver's SCALE command shape, no torchrun) starts N ranks itself, each with
+    its own RANK / LOCAL_RANK / WORLD_SIZE and a 127.0.0.1 rendezvous, before any GPU call."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3", "--print-rank-env"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = sorted((json.loads(s) for s in r.stdout.strip().splitlines()), key=lambda d: d["RANK"])
+    assert [(d["RANK"], d["LOCAL_RANK"], d["WORLD_SIZE"], d["MASTER_ADDR"]) for d in lines] == \
+        [(str(i), str(i), "3", "127.0.0.1") for i in range(3)]
+
+
 # ------------------------------------------------------------- f1: sliding-window tiles sharded over ranks
 def test_tile_plan_matches_reference_tiling_and_shards_partition_it():
     from evaluate_amos import shard_tiles, tile_plan
