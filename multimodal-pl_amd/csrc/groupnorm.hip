@@ -511,23 +511,28 @@ __global__ __launch_bounds__(GT) void gn_bwd2_apply(const T* __restrict__ da1, c
 
 // y = relu(x * scale[n,c] + shift[n,c]) materialised (8 channels per thread): used ahead of the implicit
 // GEMM on the small deep-layer activations so its K loop carries no GroupNorm arithmetic.
+// grid (blocks, n): one sample per grid row; the grid stride (blocks x 256 vectors) is a
+// multiple of c / 8 (c <= 256 divides 2048), so a thread's 8-channel chunk and its GroupNorm coefficients are fixed
+// for the whole loop (no per-element 64-bit index division or coefficient reloads)
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, T* __restrict__ y, int n, int c,
                                                        long long v, int groups, const float* __restrict__ st,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta) {
   constexpr int VEC = 8;
-  const int c8 = c / VEC;
-  const long long per = v * c8, total = per * n;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int nn = (int)(i / per), cc = (int)(i % c8) * VEC;
-    f32x2 sc[4], sh[4];
-    gn_coef8(st, gamma, beta, groups, c, nn, cc, sc, sh);
+  const int c8 = c / VEC, nn = blockIdx.y;
+  const long long per = v * c8;
+  const long long i0 = blockIdx.x * 256LL + threadIdx.x, stride = (long long)gridDim.x * 256;
+  f32x2 sc[4], sh[4];
+  gn_coef8(st, gamma, beta, groups, c, nn, (int)(i0 % c8) * VEC, sc, sh);
+  const T* xs = x + (long long)nn * per * VEC;
+  T* ys = y + (long long)nn * per * VEC;
+  for (long long i = i0; i < per; i += stride) {
     float a[VEC];
-    loadv<T, VEC>(x + i * VEC, a);
+    loadv<T, VEC>(xs + i * VEC, a);
 #pragma unroll
     for (int e = 0; e < VEC; ++e) a[e] = fmaxf(0.f, fmaf(a[e], sc[e >> 1][e & 1], sh[e >> 1][e & 1]));
-    storev<T, VEC>(y + i * VEC, a);
+    storev<T, VEC>(ys + i * VEC, a);
   }
 }
 }  // namespace u3d
@@ -599,14 +604,16 @@ extern "C" int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v,
   U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "gn_apply: bad dtype");
   U3D_REQUIRE(x && y && stats && gamma && beta && n >= 1 && c % 8 == 0 && groups > 0 && c % groups == 0,
               "gn_apply: bad args (c %% 8 == 0)");
-  const long long total = (long long)n * v * (c / 8);
-  const int grid = (int)std::min<long long>(4096, (total + 255) / 256);
+  U3D_REQUIRE(c <= 256, "gn_apply: channels %d > 256", c);
+  const long long per = v * (c / 8);
+  const dim3 grid((unsigned)std::max<long long>(1, std::min<long long>(std::max(1, 2048 / n), (per + 255) / 256)),
+                  (unsigned)n);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == U3D_BF16)
-    hipLaunchKernelGGL(gn_apply_kernel<bf16>, dim3(grid), dim3(256), 0, s, (const bf16*)x, (bf16*)y, n, c, v, groups,
+    hipLaunchKernelGGL(gn_apply_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, (bf16*)y, n, c, v, groups,
                        stats, gamma, beta);
   else
-    hipLaunchKernelGGL(gn_apply_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)x, (float*)y, n, c, v,
+    hipLaunchKernelGGL(gn_apply_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (float*)y, n, c, v,
                        groups, stats, gamma, beta);
   return check_launch("gn_apply_kernel");
 }

@@ -317,3 +317,27 @@ def test_ring_dgrad_gn_backward_matches_separate_passes(gpu, n, dims):
     dx2 = ops.gn_bwd(dA, x, st, ga, be, G, dx=prev.clone(), accumulate=True, dgamma=dg2, dbeta=db2)
     for a, b in ((dx1.float(), dx2.float()), (dg1, dg2), (db1, db2)):
         assert (a - b).abs().max().item() < 2e-3 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n,c,dims", [(2, 64, (6, 7, 9)), (3, 256, (5, 4, 3)), (1, 32, (9, 11, 13)), (2, 128, (24, 24, 24))])
+def test_gn_apply_materialised(gpu, dt, n, c, dims):
+    """relu(gn(x)) materialised (u3d_gn_apply, sample-per-grid-row kernel) against the prologue formula."""
+    from u3d import ops
+    torch.manual_seed(9)
+    x = (torch.randn((n,) + dims + (c,), device=gpu) * 1.5 + 0.3).to(dt)
+    st = ops.gn_stats(x, 16)
+    ga = 1 + 0.1 * torch.randn(c, device=gpu)
+    be = 0.1 * torch.randn(c, device=gpu)
+    y = ops.gn_apply(x, st, ga, be, 16)
+    if dt == torch.float32:
+        xf = x.cpu()
+        g = torch.arange(c) // (c // 16)
+        s = st.cpu()
+        sc = s[:, g, 1] * ga.cpu()[None]
+        sh = be.cpu()[None] - s[:, g, 0] * sc
+        ref = torch.clamp_min(xf * sc.view(n, 1, 1, 1, c) + sh.view(n, 1, 1, 1, c), 0).double()
+        assert (y.double().cpu() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    else:
+        ref = _act_ref(x, st, ga, be, 16)
+        assert (y.double().cpu() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
