@@ -156,6 +156,22 @@ int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, const void*
                           float* stats_ws, u3d_stream_t stream);
 int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
                                    u3d_stream_t stream);
+/* Work-stealing form of u3d_conv32_ring / u3d_conv32_ring_stats (same operation, same outputs bitwise): each
+ * workgroup claims the sub-chunks of its static range of output planes front to back and, once done, steals
+ * sub-chunks from the back of other ranges (64-bit compare-and-swap per claim), so workgroups that start late (CUs
+ * held by a concurrent kernel, e.g. an RCCL all-reduce overlapping the backward) leave no full-range tail.
+ * queue = u3d_conv32_ring_q_queue_bytes(n, d, h, w) bytes of caller-owned device memory, zero on entry; the kernel
+ * leaves it zero (one queue per concurrently running launch). stats_ws (nullable; needs the GN prologue) receives
+ * per-(sub-chunk, wave) GroupNorm(16) partials of the output, u3d_conv32_ring_q_stats_ws_floats(n, d, h, w)
+ * floats, turned into (mean, rstd) [n][16][2] by u3d_conv32_ring_q_stats_finalize (fixed order, fp64:
+ * deterministic whatever the assignment). */
+int u3d_conv32_ring_q_queue_bytes(int n, int d, int h, int w);
+int u3d_conv32_ring_q_stats_ws_floats(int n, int d, int h, int w);
+int u3d_conv32_ring_q(int flip, const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
+                      const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
+                      float* stats_ws, int* queue, u3d_stream_t stream);
+int u3d_conv32_ring_q_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
+                                     u3d_stream_t stream);
 /* Data gradient of the 32->32 conv (u3d_conv32_ring flip) that also accumulates the partial sums of the backward
  * of the GroupNorm + ReLU in front of the forward conv (x = that GroupNorm's input, gn_* its statistics and affine;
  * unet3D.py:44-53) into part_ws (u3d_conv32_ring_stats_ws_floats(n) floats); u3d_conv32_ring_gn_bwd_coef turns
@@ -245,6 +261,9 @@ int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d, int h, in
 
 /* ---------------------------------------------------------------- small elementwise / reductions */
 int u3d_add_inplace(int dtype, void* y, const void* x, long long numel, u3d_stream_t stream);
+/* Diagnostics (tools/kbench.py, concurrency tests): nwg single-CU workgroups spinning iters dependent FMAs — the
+ * one-GPU stand-in for an RCCL all-reduce holding CUs while the backward's persistent kernels run. */
+int u3d_diag_occupy(int nwg, long long iters, float* out, u3d_stream_t stream);
 /* y[r][c] = c < cin ? x[r][c] : 0, c < cout, converted between U3D_F32 / U3D_BF16 (fp32 logit gradients ->
  * the head's GEMM operand, channel-padded to a multiple of 8) */
 int u3d_cast(int dtype_in, const void* x, int dtype_out, void* y, long long rows, int cin, int cout,

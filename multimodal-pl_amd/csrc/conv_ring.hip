@@ -49,6 +49,7 @@ struct RGGeom {
   int gn_groups;
   long long pps;     // output planes per sample; workgroups never straddle samples (per-sample GN statistics)
   int wps;           // workgroups per sample
+  int sc, rmax;      // work-stealing mode: output planes per sub-chunk, sub-chunks per (full) range
 };
 
 // One staged input plane: column (n, h0, w0), input depth zin (-1 / d = zero padding), and whether it is the
@@ -56,6 +57,7 @@ struct RGGeom {
 struct RGPlane {
   int n, h0, w0, zin;
   bool valid, out;
+  int chunk;  // work-stealing mode: the sub-chunk the plane's output belongs to (statistics slot)
 };
 
 // Walks the workgroup's output range [o, o_end) as a sequence of input planes: each maximal run of outputs
@@ -96,13 +98,21 @@ struct RGWalk {
 // residual slot; gstat/gamma/beta = that GroupNorm) into spart[wg][32][2]; s2 = sum m dA xhat = rstd (s3 - mean s1)
 // is formed per group in fp64 by the coefficient kernel. No separate partial pass over dA and x is needed
 // (u3d_gn_bwd_apply_coef finishes the backward).
-template <bool FLIP, bool GN, bool RES, int KR, bool BG = false>
+// Q (work-stealing mode): each workgroup still owns the static range of output planes, split into sub-chunks of g.sc
+// planes, and claims them front to back (one 64-bit compare-and-swap per sub-chunk on its range's word (front,
+// stolen), lane 0, vector atomics) while walking the range as before; a workgroup whose range is exhausted steals
+// sub-chunks from the BACK of other ranges. A workgroup that starts late (CUs held by a concurrent kernel, e.g.
+// RCCL's all-reduce during the data-parallel backward) finds the back of its range already done by others, so the
+// tail is one sub-chunk instead of a whole range; uncontended, the walk is the static one. GroupNorm statistics go
+// to per-(sub-chunk, wave) slots (fixed-order finalize: deterministic whatever the assignment). The last workgroup
+// to exit resets the words and the exit counter to zero for the next launch.
+template <bool FLIP, bool GN, bool RES, int KR, bool BG = false, bool Q = false>
 __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                               bf16* __restrict__ y, const bf16* __restrict__ res,
                                                               const float* __restrict__ gstat,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float* __restrict__ spart,
-                                                              RGGeom g) {
+                                                              RGGeom g, int* __restrict__ queue = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024 + 512];
   char* const ring = smem;
   char* const wts = smem + 4 * RG_SS;
@@ -119,12 +129,65 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
   }
   RGWalk walk{};
-  const int smp = bid / g.wps, jw = bid - smp * g.wps;
-  walk.o_next = (long long)smp * g.pps + (long long)jw * g.per;
-  walk.o_end = min((long long)(smp + 1) * g.pps, walk.o_next + g.per);
-  walk.done = false;
-  walk.zin = 1;
-  walk.zlast = 0;  // forces start_run on the first next()
+  int* const qslot = reinterpret_cast<int*>(smem + 4 * RG_SS + 4 * RG_NWR * 16 + 1024 + 256);  // claim broadcast
+  unsigned long long* const words = reinterpret_cast<unsigned long long*>(queue);
+  // range b = (sample, jw) of the static schedule: [o0, o0 + len), sub-chunks of g.sc planes
+  auto range_len = [&](int b) {
+    const int jw_ = b % g.wps;
+    return (int)min<long long>(g.per, g.pps - (long long)jw_ * g.per);
+  };
+  auto range_o0 = [&](int b) { return (long long)(b / g.wps) * g.pps + (long long)(b % g.wps) * g.per; };
+  auto nsub = [&](int b) { return (range_len(b) + g.sc - 1) / g.sc; };
+  // Claims are single 64-bit atomic adds on the range's word (front | stolen << 32); the returned old value decides:
+  // the owner's add of 1 wins sub-chunk `front` iff front + stolen < R, a thief's add of 2^32 wins sub-chunk
+  // R - 1 - stolen under the same test. Adds serialise, so no sub-chunk is won twice; a losing add only overshoots
+  // a counter of a range that is exhausted anyway. The owner's add is fire-and-forget (lane 0 keeps the old value
+  // and publishes the verdict a step later), so claiming never stalls the walk.
+  auto claim_ok = [&](unsigned long long old, int b) {
+    return (unsigned)old + (unsigned)(old >> 32) < (unsigned)nsub(b);
+  };
+  // wave 0 only (all 64 lanes): steal the last unclaimed sub-chunk of another range, scanning 64 ranges per load
+  // round; returns the global sub-chunk id (lane-uniform) or -1
+  auto steal = [&]() -> int {
+    const int nwg = (int)gridDim.x;
+    for (int base = 1; base < nwg; base += 64) {
+      for (;;) {
+        const int v = (bid + base + lane) % nwg;
+        bool cand = false;
+        if (base + lane < nwg) {
+          const unsigned long long w = __hip_atomic_load(&words[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          cand = claim_ok(w, v);
+        }
+        const unsigned long long m = __ballot(cand);
+        if (!m) break;  // nothing left in these 64 ranges
+        const int l = __builtin_ctzll(m), vv = (bid + base + l) % nwg;
+        int got = -1;
+        if (lane == 0) {
+          const unsigned long long old = atomicAdd(&words[vv], 1ull << 32);
+          if (claim_ok(old, vv)) got = vv * g.rmax + (int)((unsigned)nsub(vv) - 1 - (unsigned)(old >> 32));
+        }
+        got = __shfl(got, 0);
+        if (got >= 0) return got;  // else lost a race on vv: rescan
+      }
+    }
+    return -1;
+  };
+  bool own = true;        // walking the own range (claims pending at sub-chunk boundaries)
+  int claimed = -1;       // own sub-chunks claimed so far: 0..claimed
+  int issued = -1;        // own claim in flight (lane 0 holds the old word in claim_old)
+  int check = -1;         // own claim whose verdict is in qslot[1] after this step's barrier
+  unsigned long long claim_old = 0;
+  int nxt = -1;           // steal mode: stolen sub-chunk waiting to be walked (-1: none)
+  if constexpr (Q) {
+    if (tid == 0) qslot[0] = claim_ok(atomicAdd(&words[bid], 1ull), bid);
+  } else {
+    const int smp = bid / g.wps, jw = bid - smp * g.wps;
+    walk.o_next = (long long)smp * g.pps + (long long)jw * g.per;
+    walk.o_end = min((long long)(smp + 1) * g.pps, walk.o_next + g.per);
+    walk.done = false;
+    walk.zin = 1;
+    walk.zlast = 0;  // forces start_run on the first next()
+  }
 
   for (int i = tid; i < RG_NWR * 4; i += RG_NT) {  // weights: plane c, row t*32 + co
     const int c = i / RG_NWR, row = i % RG_NWR;
@@ -191,10 +254,12 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     u32x4 rv[2];
     long long vox;
     bool ok;
+    int chunk;
   };
   Pending pend;
   pend.ok = false;
   pend.vox = 0;
+  pend.chunk = -1;
   // GroupNorm(16, 32) statistics of the output (GN variants = the forward convs whose outputs feed the next
   // GroupNorm), from the fp32 values just before the final bf16 rounding (no unpack; the voxel's in-volume flag
   // selects): 8 (sum, sum of squares) pairs per lane, fp32 over the lane's voxels, reduced per workgroup at
@@ -207,7 +272,35 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   float b1[BG ? 16 : 1], b2[BG ? 16 : 1];  // BG: channels 16u + 8h + e -> slot 8u + e
 #pragma unroll
   for (int j = 0; j < (BG ? 16 : 1); ++j) b1[j] = b2[j] = 0.f;
-  auto epilogue = [&](const Pending& p) {
+  int acc_chunk = -1;
+  // work-queue mode: the statistics of one chunk, per wave: reduce over the wave's voxels (xor within the 32-lane
+  // halves) and write slot (chunk, wave); no barrier, so it can run inside the MFMA chain
+  auto flush = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        gs[j] += __shfl_xor(gs[j], o);
+        gq[j] += __shfl_xor(gq[j], o);
+      }
+    if (r == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int grp = RES ? 8 * (j >> 2) + 4 * h + (j & 3) : 4 * (j >> 1) + 2 * h + (j & 1);
+        spart[((long long)c * (RG_NT / 64) + wave) * 32 + grp * 2] = gs[j];
+        spart[((long long)c * (RG_NT / 64) + wave) * 32 + grp * 2 + 1] = gq[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gs[j] = gq[j] = 0.f;
+  };
+  auto epilogue = [&](const Pending& p) __attribute__((always_inline)) {
+    if constexpr (Q && GN) {
+      if (spart != nullptr && p.chunk != acc_chunk) {
+        if (acc_chunk >= 0) flush(acc_chunk);
+        acc_chunk = p.chunk;
+      }
+    }
     if constexpr (GN && !RES) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
@@ -270,10 +363,11 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
 
   // output plane from the three slots s0 (z-1), s1 (z), s2 (z+1); the staging writes of the next plane and
   // the previous plane's epilogue are issued between the MFMAs
-  auto compute = [&](const RGPlane& pc, int s0, int s1, int s2) {
+  auto compute = [&](const RGPlane& pc, int s0, int s1, int s2) __attribute__((always_inline)) {
     const int zo = pc.zin - 1;
     const int zh = pc.h0 + wave, zw = pc.w0 + r;
     Pending nw;
+    nw.chunk = pc.chunk;
     nw.ok = zh < g.h && zw < g.w;
     nw.vox = (((long long)pc.n * g.d + zo) * g.h + zh) * g.w + zw;
     nw.rv[0] = nw.rv[1] = u32x4{0u, 0u, 0u, 0u};
@@ -324,22 +418,122 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   // output whose triple ends at plane s-1, barrier. Unrolled by two so the register sets swap statically.
   u32x4 va[RG_LD], vb[RG_LD];
   unsigned ma = 0, mb = 0;
-  RGPlane pw = walk.next(g);  // plane 0
+  auto set_range = [&](long long o0, long long o1) {
+    walk.o_next = o0;
+    walk.o_end = o1;
+    walk.done = false;
+    walk.zin = 1;
+    walk.zlast = 0;
+  };
+  // statistics slot of the next output plane, tracked incrementally (no divisions in the walk): own mode counts the
+  // range's outputs (sub-chunk k = count / sc), a stolen range is one sub-chunk
+  int own_cnt = 0, own_k = 0, stolen_id = -1;
+  auto start_stolen = [&](int id) {  // walk sub-chunk id (= range * rmax + k)
+    stolen_id = id;
+    const int b = id / g.rmax, k = id - b * g.rmax;
+    const long long o0 = range_o0(b) + (long long)k * g.sc;
+    set_range(o0, min(range_o0(b) + range_len(b), o0 + g.sc));
+  };
+  if constexpr (Q) {
+    __syncthreads();  // the claim of sub-chunk 0
+    if (qslot[0]) {
+      claimed = 0;
+      set_range(range_o0(bid), range_o0(bid) + range_len(bid));
+    } else {  // the whole range was stolen before this workgroup started
+      own = false;
+      walk.done = true;
+      if (wave == 0) {
+        const int st_ = steal();
+        if (lane == 0) qslot[2] = st_;
+      }
+      __syncthreads();
+      nxt = qslot[2];
+    }
+  }
+  // next input plane of the walk. Own mode: staging the first plane whose output starts own sub-chunk k issues the
+  // claim of k (result read at the next step, two steps before that output is computed). Steal mode: a finished
+  // range hands over to the stolen sub-chunk fetched one ahead, and lane 0 steals the one after it.
+  auto next_plane = [&]() __attribute__((always_inline)) {
+    RGPlane p = walk.next(g);
+    if constexpr (Q) {
+      if (own && !p.valid) {  // own range done: from now on steal (uniform branch; one extra barrier per workgroup)
+        own = false;
+        if (wave == 0) {
+          const int st_ = steal();
+          if (lane == 0) qslot[3] = st_;
+        }
+        __syncthreads();
+        nxt = qslot[3];
+      }
+      if (!own && !p.valid && nxt >= 0) {  // next stolen range; steal the one after it now (wave 0)
+        start_stolen(nxt);
+        nxt = -2;
+        if (wave == 0) {
+          const int st_ = steal();
+          if (lane == 0) qslot[2] = st_;
+        }
+        p = walk.next(g);
+      }
+      if (p.valid && p.out) {
+        if (own) {
+          const int k = own_k;
+          p.chunk = bid * g.rmax + k;
+          if (++own_cnt == g.sc) {
+            own_cnt = 0;
+            ++own_k;
+          }
+          if (k > claimed && issued < 0 && check < 0) {
+            issued = k;
+            if (tid == 0) claim_old = atomicAdd(&words[bid], 1ull);
+          }
+        } else {
+          p.chunk = stolen_id;
+        }
+      }
+    }
+    return p;
+  };
+  RGPlane pw = next_plane();  // plane 0
   load_plane(pw, va, ma);
   __syncthreads();            // weights visible
   RGPlane pc{};               // plane s-1 (compute)
   int s = 0;
   // The staged plane is written at the start of the step, BEFORE the next plane's loads are issued: its loads
   // (a full step old) are then the oldest in flight, so no wait inside the MFMA chain can fall on a young load.
-  auto step = [&](u32x4 (&cur)[RG_LD], unsigned& mcur, u32x4 (&nxt)[RG_LD], unsigned& mnxt) {
+  auto step = [&](u32x4 (&vcur)[RG_LD], unsigned& mcur, u32x4 (&vnxt)[RG_LD], unsigned& mnxt) {
+    if constexpr (Q) {
+      if (nxt == -2) nxt = qslot[2];
+      if (check >= 0) {  // verdict of the claim issued two steps ago; its first plane is pc now
+        if (qslot[1]) {
+          claimed = check;
+        } else {  // sub-chunks check.. were stolen: the own range ends before pc's output
+          pc.out = false;
+          pw.out = false;
+          walk.done = true;
+          own = false;
+          if (wave == 0) {
+            const int st_ = steal();
+            if (lane == 0) qslot[2] = st_;
+          }
+          __syncthreads();
+          nxt = qslot[2];
+        }
+        check = -1;
+      }
+      if (issued >= 0) {  // publish last step's claim (its atomic has long returned); read after this barrier
+        if (tid == 0) qslot[1] = claim_ok(claim_old, bid);
+        check = issued;
+        issued = -1;
+      }
+    }
     gn_table(pw);
     const int slot = s & 3;
     if (pw.valid) {
 #pragma unroll
-      for (int i = 0; i < RG_LD; ++i) write_piece(i, cur[i], mcur, slot);
+      for (int i = 0; i < RG_LD; ++i) write_piece(i, vcur[i], mcur, slot);
     }
-    const RGPlane pl = walk.next(g);  // plane s+1
-    load_plane(pl, nxt, mnxt);
+    const RGPlane pl = next_plane();  // plane s+1
+    load_plane(pl, vnxt, mnxt);
     if (pc.valid && pc.out) compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3);
     __syncthreads();
     pc = pw;
@@ -352,6 +546,21 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     step(vb, mb, va, ma);
   }
   epilogue(pend);  // the last computed plane (ok = false if none)
+  if constexpr (Q) {
+    if constexpr (GN) {
+      if (spart != nullptr && acc_chunk >= 0) flush(acc_chunk);
+    }
+    int* const exits = reinterpret_cast<int*>(words + gridDim.x);
+    // a claim issued in the last step(s) may still be in flight: consume its result (waits for the atomic) so that
+    // every claim of this workgroup has landed before its exit is counted (device-scope atomics of one lane, in
+    // order; no fence: an agent-scope release would write back the XCD's whole L2)
+    if (tid == 0 && issued >= 0) qslot[1] = claim_ok(claim_old, bid);
+    if (tid == 0 && atomicAdd(exits, 1) == (int)gridDim.x - 1) {  // every workgroup is past its last claim
+      for (unsigned b = 0; b < gridDim.x; ++b) atomicExch(&words[b], 0ull);
+      atomicExch(exits, 0);
+    }
+    return;
+  }
   if constexpr (BG) {
     if (spart == nullptr) return;
 #pragma unroll
@@ -840,6 +1049,127 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
 #undef RG_KR
 #undef RG_LAUNCH
   return check_launch("conv32_ring_kernel");
+}
+
+// ------------------------------------------------------------------------------------------- work-stealing mode
+static int ring_sc_env() {  // U3D_RING_SC: output planes per sub-chunk (experiments; 0 = default)
+  static const int v = [] {
+    const char* e = getenv("U3D_RING_SC");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// the static split of conv32_ring_impl (~256 workgroups, ranges of `per` planes never straddling samples), each
+// range cut into sub-chunks of about a ninth of it (>= 3 planes); a third when the launch accumulates GroupNorm
+// statistics (each sub-chunk boundary costs a per-wave reduction inside the MFMA chain)
+static void ring_q_geom(int n, int d, int h, int w, RGGeom& g, bool stats = false) {
+  g = RGGeom{};
+  g.n = n; g.d = d; g.h = h; g.w = w;
+  g.nbh = cdiv(h, RG_BH); g.nbw = cdiv(w, RG_BW);
+  g.pps = (long long)g.nbh * g.nbw * d;
+  g.planes = (long long)n * g.pps;
+  g.xbytes = (long long)n * d * h * w * 64;
+  const long long wps0 = std::max<long long>(1, std::min<long long>(g.pps, ring_wgs() / n));
+  g.per = (int)((g.pps + wps0 - 1) / wps0);
+  g.wps = (int)((g.pps + g.per - 1) / g.per);
+  const int env = ring_sc_env();
+  // >= 3 planes: a claim's verdict (two steps after its first plane is staged) lands before the next boundary
+  const int parts = stats ? 3 : 9;
+  g.sc = std::min(g.per, std::max(3, env > 0 ? env : (g.per + parts - 1) / parts));
+  g.rmax = (g.per + g.sc - 1) / g.sc;
+}
+
+extern "C" int u3d_conv32_ring_q_stats_ws_floats(int n, int d, int h, int w) {
+  RGGeom g;
+  ring_q_geom(n, d, h, w, g, true);
+  return n * g.wps * g.rmax * (RG_NT / 64) * 32;
+}
+
+extern "C" int u3d_conv32_ring_q_queue_bytes(int n, int d, int h, int w) {
+  RGGeom g;
+  ring_q_geom(n, d, h, w, g);
+  return 8 * (n * g.wps + 1);
+}
+
+extern "C" int u3d_conv32_ring_q(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
+                                 const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                                 const void* residual, void* y, float* stats_ws, int* queue, u3d_stream_t stream) {
+  U3D_REQUIRE(x && wpk && y && queue && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv32_ring_q: bad args");
+  U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0), "conv32_ring_q: bad GN");
+  U3D_REQUIRE(!stats_ws || gn_stats, "conv32_ring_q: output statistics need the GN prologue");
+  U3D_REQUIRE(!(flip && (gn_stats || residual)), "conv32_ring_q: the data gradient takes no prologue / residual");
+  RGGeom g;
+  ring_q_geom(n, d, h, w, g, stats_ws != nullptr);
+  U3D_REQUIRE(g.xbytes < (1LL << 31), "conv32_ring_q: tensor of %lld bytes beyond the 2 GiB buffer-offset range",
+              g.xbytes);
+  g.gn_groups = gn_groups;
+  const unsigned grid = (unsigned)(n * g.wps);
+  hipStream_t s = (hipStream_t)stream;
+#define RQ_LAUNCH(F, G, R, K)                                                                                     \
+  hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K, false, true>), dim3(grid), dim3(RG_NT), 0, s, (const bf16*)x, \
+                     (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, stats_ws, g, queue)
+  // register budget: the claim state costs the weight steps of the static variants a few registers
+  if (flip) RQ_LAUNCH(true, false, false, 24);
+  else if (gn_stats && residual) RQ_LAUNCH(false, true, true, 4);
+  else if (gn_stats) RQ_LAUNCH(false, true, false, 8);
+  else if (residual) RQ_LAUNCH(false, false, true, 16);
+  else RQ_LAUNCH(false, false, false, 24);
+#undef RQ_LAUNCH
+  return check_launch("conv32_ring_kernel (work stealing)");
+}
+
+// stats[n][16] from the per-(sub-chunk, wave) partials of the work-stealing ring: one 256-thread block per sample,
+// each thread sums whole slot rows (16 groups x 2) of its slots in index order (slots of sub-chunks a short last
+// range does not have are skipped), then the threads' fp64 rows are combined in a fixed-order LDS tree
+__global__ __launch_bounds__(256) void ring_gn_finalize_q_kernel(const float* __restrict__ spart, RGGeom g, double m,
+                                                                float* __restrict__ stats) {
+  __shared__ double red[256][33];
+  const int nn = blockIdx.x, t = threadIdx.x;
+  constexpr int NW = RG_NT / 64;
+  double acc[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) acc[e] = 0;
+  const int per_range = g.rmax * NW, nslot = g.wps * per_range;
+  const float* row0 = spart + (long long)nn * nslot * 32;
+  for (int i = t; i < nslot; i += 256) {  // independent loads: the slots of all ranges at once
+    const int jw = i / per_range, k = (i - jw * per_range) / NW;
+    const int len = (int)std::min<long long>(g.per, g.pps - (long long)jw * g.per);
+    if (k * g.sc >= len) continue;
+    const f32x4* r = reinterpret_cast<const f32x4*>(row0 + (long long)i * 32);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const f32x4 v = r[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[4 * q + e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 32; ++e) red[t][e] = acc[e];
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (t < st)
+#pragma unroll
+      for (int e = 0; e < 32; ++e) red[t][e] += red[t + st][e];
+    __syncthreads();
+  }
+  if (t < 16) {
+    const double mean = red[0][2 * t] / m;
+    double var = red[0][2 * t + 1] / m - mean * mean;
+    if (var < 0) var = 0;
+    stats[(nn * 16 + t) * 2] = (float)mean;
+    stats[(nn * 16 + t) * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+  }
+}
+
+extern "C" int u3d_conv32_ring_q_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
+                                                u3d_stream_t stream) {
+  U3D_REQUIRE(stats_ws && stats_out && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv32_ring_q_stats_finalize: bad args");
+  RGGeom g;
+  ring_q_geom(n, d, h, w, g, true);
+  hipLaunchKernelGGL(ring_gn_finalize_q_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, stats_ws, g,
+                     2.0 * d * h * w, stats_out);
+  return check_launch("ring_gn_finalize_q_kernel");
 }
 
 extern "C" int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int w, const void* wpk,

@@ -141,3 +141,24 @@ extern "C" int u3d_cast(int dtype_in, const void* x, int dtype_out, void* y, lon
     hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(nb), dim3(256), 0, s, (const bf16*)x, (bf16*)y, rows, cin, cout);
   return check_launch("cast_kernel");
 }
+
+// Diagnostics: nwg workgroups that each hold one CU (48 KB of LDS: no 143 KB ring workgroup fits beside one) and
+// spin iters dependent FMAs, e.g. on a side stream while a persistent kernel runs on another — the one-GPU stand-in
+// for RCCL's all-reduce kernels taking CUs during the data-parallel backward. out[0] receives a value only if the
+// chain hits an impossible result (keeps the loop alive).
+namespace u3d {
+__global__ __launch_bounds__(64) void occupy_kernel(long long iters, float* out) {
+  __shared__ float pad[12288];
+  float v = 1.f + threadIdx.x * 1e-3f;
+  for (long long i = 0; i < iters; ++i) v = fmaf(v, 0.999999f, 1e-6f);
+  pad[threadIdx.x] = v;
+  __syncthreads();
+  if (pad[(threadIdx.x + 1) & 63] == -12345.f) out[0] = v;
+}
+}  // namespace u3d
+
+extern "C" int u3d_diag_occupy(int nwg, long long iters, float* out, u3d_stream_t stream) {
+  U3D_REQUIRE(nwg >= 1 && nwg <= 4096 && iters >= 0 && out, "diag_occupy: bad args");
+  hipLaunchKernelGGL(occupy_kernel, dim3(nwg), dim3(64), 0, (hipStream_t)stream, iters, out);
+  return check_launch("occupy_kernel");
+}

@@ -13,6 +13,8 @@ import threading
 import torch
 import torch.distributed as dist
 
+from . import ops
+
 _local = threading.local()
 
 
@@ -76,6 +78,7 @@ class GradBucketer:
     def _launch(self, b):
         op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
         self.works[b] = dist.all_reduce(self.bufs[b], op=op, group=self.group, async_op=True)
+        ops.COLLECTIVE_IN_FLIGHT[0] = True  # the ring data gradients switch to work stealing until finish()
 
     def needs_flush(self, pending):
         """True if producing the ``pending`` gradients would complete a bucket (so they must be written now)."""
@@ -113,6 +116,7 @@ class GradBucketer:
                 self.bufs[b].div_(self.world)
         self.synced = set(self.done_names)  # averaged here: the post-accumulate hooks skip these
         self.active = False
+        ops.COLLECTIVE_IN_FLIGHT[0] = False
 
     def average(self, t):
         """Synchronous mean over ranks of one gradient the native backward did not produce."""
@@ -141,7 +145,6 @@ class U3DDataParallel(torch.nn.Module):
             with torch.no_grad():  # start from identical weights on every rank (DDP's init broadcast)
                 for p in module.parameters():
                     dist.broadcast(p.data, 0, group=group)
-            from . import ops
             ops.WEIGHT_GEN[0] += 1  # .data writes bump no autograd version: invalidate cached weight packs
             for name, p in module.named_parameters():
                 if p.requires_grad:

@@ -178,8 +178,12 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
         if probe:  # bench.py: HIP events around the dominant kernel, on the stream it runs on
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        call(CONV32_FN, 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
-             _ptr(residual), y.data_ptr(), _stream())
+        if _ring_queue():
+            call("u3d_conv32_ring_q", 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
+                 _ptr(residual), y.data_ptr(), None, _queue(x.device, (n, d, h, w_)), _stream())
+        else:
+            call(CONV32_FN, 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
+                 _ptr(residual), y.data_ptr(), _stream())
         if probe:
             e1.record()
             PROBE.append((e0, e1, n * d * h * w_))
@@ -214,19 +218,48 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
         st, ga, be, G = gn
         y = torch.empty((n, d, h, w_, cout), dtype=x.dtype, device=x.device)
         stats = torch.empty((n, 16, 2), dtype=torch.float32, device=x.device)
-        ws = WS.get(4 * query("u3d_conv32_ring_stats_ws_floats", n), x.device, slot=9)
+        q = _ring_queue()
+        nws = query("u3d_conv32_ring_q_stats_ws_floats", n, d, h, w_) if q else query("u3d_conv32_ring_stats_ws_floats", n)
+        ws = WS.get(4 * nws, x.device, slot=9)
         probe = PROBE is not None
         if probe:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        call("u3d_conv32_ring_stats", x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
-             be.data_ptr(), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), _stream())
+        if q:
+            call("u3d_conv32_ring_q", 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
+                 be.data_ptr(), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), _queue(x.device, (n, d, h, w_)), _stream())
+        else:
+            call("u3d_conv32_ring_stats", x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
+                 be.data_ptr(), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), _stream())
         if probe:
             e1.record()
             PROBE.append((e0, e1, n * d * h * w_))
-        call("u3d_conv32_ring_stats_finalize", ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
+        fin = "u3d_conv32_ring_q_stats_finalize" if q else "u3d_conv32_ring_stats_finalize"
+        call(fin, ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
         return y, stats
     return conv_fwd(x, wpk, cout, k, stride, gn, residual), None
+
+
+# Work-stealing ring (u3d_conv32_ring_q): robust to a concurrent kernel holding CUs (a late workgroup's range is
+# taken over by the others instead of doubling the launch), but 10-25% slower alone (tools/concurrency.py,
+# profiles/r02_concurrency.json). Used for the data-gradient ring while a gradient all-reduce may be running
+# (COLLECTIVE_IN_FLIGHT, set by u3d.ddp between the first bucket launch and finish()); U3D_RING_QUEUE=1 forces it
+# for every ring launch.
+RING_QUEUE = os.environ.get("U3D_RING_QUEUE", "0") != "0"
+COLLECTIVE_IN_FLIGHT = [False]
+
+
+def _ring_queue(dgrad=False):
+    return CONV32_FN == "u3d_conv32_ring" and (RING_QUEUE or (dgrad and COLLECTIVE_IN_FLIGHT[0]))
+
+
+QUEUE_SLOT = 40  # workspace slot of the ring claim words (used by nothing else: the words must stay zero between launches)
+
+
+def _queue(device, shape):
+    """Zeroed claim words for the work-stealing ring kernels (left zero by every launch; one queue: launches are
+    stream-ordered on the caller's stream)."""
+    return WS.get(query("u3d_conv32_ring_q_queue_bytes", *shape), device, slot=QUEUE_SLOT).data_ptr()
 
 
 RING_STATS = os.environ.get("U3D_RING_STATS", "1") != "0"  # GroupNorm statistics from the ring conv epilogue (False: separate u3d_gn_stats pass)
@@ -275,8 +308,12 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     cout = dy.shape[-1]
     dx = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
     if _use_conv32(dy.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(dy):
-        call(CONV32_FN, 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
-             dx.data_ptr(), _stream())
+        if _ring_queue(dgrad=True):
+            call("u3d_conv32_ring_q", 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
+                 dx.data_ptr(), None, _queue(dy.device, (n, d, h, w_)), _stream())
+        else:
+            call(CONV32_FN, 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
+                 dx.data_ptr(), _stream())
         return dx
     if USE_S2_BRICK and dy.dtype == torch.bfloat16 and k == 3 and stride == 2:
         call("u3d_conv_dgrad_s2", dy.data_ptr(), n, cout, wpk_dgrad.data_ptr(), cin, d, h, w_, dx.data_ptr(),

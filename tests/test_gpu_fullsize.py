@@ -284,3 +284,41 @@ def test_bf16_training_step_2x96_tracks_fp32(gpu):
         assert r <= 1.5 * rt + 1e-2, f"{k}: gradient rel L2 {r:.3e} vs autocast {rt:.3e}"
         if k.endswith("weight") and g32[k].dim() == 5:
             assert cos >= 0.9, f"{k}: gradient cosine {cos:.4f}"
+
+
+# ------------------------------------------------------------------------------------------ work-queue ring
+def query_bytes(n, dims):
+    from u3d._lib import query
+    return query("u3d_conv32_ring_q_queue_bytes", n, *dims)
+
+
+@pytest.mark.parametrize("n,dims", PER2 + [(2, (96, 96, 96))])
+def test_ring_work_queue_matches_static_schedule(gpu, n, dims):
+    """u3d_conv32_ring_q (chunks of output planes taken from an atomic counter) computes every output voxel exactly
+    as the static schedule (bitwise: same per-voxel MFMA chain), for the forward with the GN prologue + residual and
+    for the data gradient; its per-(chunk, wave) GroupNorm statistics equal the static per-workgroup ones to fp32
+    rounding of a different summation grouping (<= 1e-5 relative), and the queue counters are left at zero."""
+    from u3d import ops
+    x, w, gn = _operands(gpu, n, 32, 32, dims, 24)
+    pf, pd, _ = ops.wstd_fwd(w, torch.bfloat16, True)
+    r = (torch.randn((n,) + dims + (32,), device=gpu) + 0.5).to(torch.bfloat16)
+    saved = ops.RING_QUEUE
+    try:
+        out = {}
+        for q in (False, True):
+            ops.RING_QUEUE = q
+            y, s16 = ops.conv_fwd_stats(x, pf, 32, 3, 1, gn, residual=r)
+            y2, _ = ops.conv_fwd_stats(x, pf, 32, 3, 1, gn, residual=None)
+            dx = ops.conv_dgrad(x, pd, 32, (n,) + dims, 3, 1)
+            out[q] = (y, s16, y2, dx)
+        torch.cuda.synchronize()
+        qb = ops.WS.get(256, gpu, slot=ops.QUEUE_SLOT)[:query_bytes(n, dims)].view(torch.int32).cpu()
+        nz = torch.nonzero(qb).flatten()
+        assert nz.numel() == 0, (qb.numel(), nz[:16].tolist(), qb[nz[:16]].tolist())
+    finally:
+        ops.RING_QUEUE = saved
+    for a, b in zip(out[False], out[True]):
+        if a.dtype == torch.float32:
+            assert ((a - b).abs() <= 1e-5 * a.abs() + 1e-7).all()
+        else:
+            assert torch.equal(a, b)

@@ -99,6 +99,21 @@ CASES["fwd96_nogn"] = lambda: _fwd(2, 32, 32, 96, 3, 1, False, True)
 CASES["fwd96_plain"] = lambda: _fwd(2, 32, 32, 96, 3, 1, False, False)
 CASES["head96"] = lambda: _fwd(2, 32, 16, 96, 1, 1, True, False)
 
+
+def _queue(fn):
+    def run():
+        saved = ops.RING_QUEUE
+        ops.RING_QUEUE = True
+        try:
+            return fn()
+        finally:
+            ops.RING_QUEUE = saved
+    return run
+
+
+CASES["fwd96q"] = _queue(CASES["fwd96"])
+CASES["dgrad96q"] = _queue(CASES["dgrad96"])
+
 if __name__ == "__main__":
     names = sys.argv[1:] or list(CASES)
     for nm in names:
