@@ -493,7 +493,47 @@ def g12():
     save("g12_driver_helpers.npz", **out)
 
 
+def g13():
+    """predict_sliding (evaluate_amos.py:211-279) itself, run here on CPU: its only device call, the per-tile
+    ``torch.from_numpy(img).cuda()`` (:242), is shimmed to the identity (Tensor.cuda -> self) for the call. The
+    networks are deterministic stand-ins with the module call signature net(img, task_id): a 3^3 convolution with
+    fixed asymmetric weights (so tile borders and the TTA flips change the result) plus a per-class bias and a
+    tanh. Cases: one net without TTA on a ragged volume; two nets with the 8-flip TTA (multi_net's mean, :198-209);
+    a volume of exactly one tile. The weights are stored with the outputs (float64 full_probs, as returned)."""
+    rng = np.random.default_rng([13, 13])
+
+    class StandIn(torch.nn.Module):
+        def __init__(self, w, b):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.from_numpy(w))
+            self.b = torch.nn.Parameter(torch.from_numpy(b))
+
+        def forward(self, x, task_id):
+            return torch.tanh(F.conv3d(x, self.w, padding=1) + self.b.view(1, -1, 1, 1, 1))
+
+    out = {}
+    cases = [("a", (14, 27, 29), (8, 16, 16), 1, False), ("b", (14, 27, 29), (8, 16, 16), 2, True),
+             ("c", (8, 16, 16), (8, 16, 16), 2, True)]
+    cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    try:
+        for tag, vol, tile, nnets, tta in cases:
+            C = 3
+            ws = [(rng.standard_normal((C, 1, 3, 3, 3)) * 0.5).astype(np.float32) for _ in range(nnets)]
+            bs = [(rng.standard_normal(C) * 0.2).astype(np.float32) for _ in range(nnets)]
+            nets = [StandIn(w, b).eval() for w, b in zip(ws, bs)]
+            img = rng.standard_normal((1, 1) + vol).astype(np.float32)
+            with torch.no_grad():
+                full = REV.predict_sliding(None, nets, img, tile, C, 0, tta=tta)
+            out[f"{tag}_img"], out[f"{tag}_w"], out[f"{tag}_b"] = img, np.stack(ws), np.stack(bs)
+            out[f"{tag}_tile"], out[f"{tag}_tta"] = np.array(tile), np.array(int(tta))
+            out[f"{tag}_full"] = full.numpy()
+    finally:
+        torch.Tensor.cuda = cuda
+    save("g13_predict_sliding.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12", "g13"]
     for w in which:
         globals()[w]()

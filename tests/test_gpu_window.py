@@ -78,3 +78,32 @@ def test_predict_sliding_baseline_model(gpu):
     got = out.double().cpu().numpy()
     np.testing.assert_allclose(got, ref, atol=WIN_TOL * np.abs(ref).max(), rtol=0)
 
+
+
+class _StandIn(torch.nn.Module):
+    """The deterministic network of fixture G13 (tests/golden/gen_golden.py g13): tanh(conv3d 3^3 + bias)."""
+
+    def __init__(self, w, b):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.from_numpy(w))
+        self.b = torch.nn.Parameter(torch.from_numpy(b))
+
+    def forward(self, x, task_id=None):
+        return torch.tanh(torch.nn.functional.conv3d(x, self.w, padding=1) + self.b.view(1, -1, 1, 1, 1))
+
+
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
+def test_predict_sliding_vs_reference_fixture(gpu, tag):
+    """evaluate_amos.predict_sliding on the device against the REFERENCE's own predict_sliding output (G13: ragged
+    volume without TTA; two nets with the 8-flip TTA; a one-tile volume), same stand-in networks: <= WIN_TOL of the
+    volume's max |probability| (fp32 device accumulation vs the reference's float64 host arrays)."""
+    from conftest import golden
+    from evaluate_amos import predict_sliding
+    g = golden("g13_predict_sliding.npz")
+    nets = [_StandIn(w, b).to(gpu).eval() for w, b in zip(g[f"{tag}_w"], g[f"{tag}_b"])]
+    tile = tuple(int(v) for v in g[f"{tag}_tile"])
+    ref = g[f"{tag}_full"]
+    with torch.no_grad():
+        out = predict_sliding(None, nets, g[f"{tag}_img"], tile, ref.shape[1], 0, tta=bool(g[f"{tag}_tta"]))
+    err = np.abs(out.double().cpu().numpy() - ref).max()
+    assert err <= WIN_TOL * np.abs(ref).max(), err

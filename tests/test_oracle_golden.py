@@ -311,3 +311,26 @@ def test_g11_get_dice2():
     np.testing.assert_allclose(se, g["senc"], atol=1e-6)
     np.testing.assert_allclose(sp, g["spec"], atol=1e-6)
     assert np.array_equal(am.numpy(), g["argmax"])
+
+
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
+def test_g13_predict_sliding_oracle_vs_reference(tag):
+    """oracle.ref_cpu.predict_sliding (the float64 restatement of evaluate_amos.py:211-279 that the GPU window tests
+    use) against the reference's own predict_sliding on the same stand-in networks (G13): tiling, clamping, the flip
+    TTA, multi_net's mean, the Gaussian weights and full /= count. Tolerance 1e-6 of max: the reference averages
+    the nets / flips in float32 tensors, the restatement in float64."""
+    import torch
+    import torch.nn.functional as F
+    from oracle import ref_cpu as O
+    g = golden("g13_predict_sliding.npz")
+    ws, bs = g[f"{tag}_w"], g[f"{tag}_b"]
+
+    def pred_fn(t):
+        x = torch.from_numpy(np.ascontiguousarray(t)).float()
+        outs = [torch.tanh(F.conv3d(x, torch.from_numpy(w), padding=1) + torch.from_numpy(b).view(1, -1, 1, 1, 1))
+                for w, b in zip(ws, bs)]
+        return (sum(outs) / len(outs)).double().numpy()
+    ref = g[f"{tag}_full"]
+    out = O.predict_sliding(pred_fn, g[f"{tag}_img"], tuple(int(v) for v in g[f"{tag}_tile"]), ref.shape[1],
+                            tta=bool(g[f"{tag}_tta"]))
+    assert np.abs(out - ref).max() <= 1e-6 * np.abs(ref).max()
