@@ -217,6 +217,12 @@ int u3d_conv_wgrad1(const void* dy, const void* x, int n, int cin, int d, int h,
 
 /* Stem conv with cin <= 4 (conv1 1->32, unet3D.py:1632; conv0 2->f stride 2, :1514): fp32 NCDHW input,
  * direct VALU conv (K = 27*cin is too short for MFMA), NDHWC output. */
+/* bf16 stem conv (cin 1 -> 32, 3^3, stride 1, w % 4 == 0) that also returns the GroupNorm(16) statistics (mean,
+ * rstd) [n][16][2] of its stored output (layer0's gn1, unet3D.py:56-73) from the epilogue (fp64 across blocks,
+ * fixed order). ws = u3d_stem_fwd_stats_ws_bytes(n, d, h, w) bytes, zero on first use (left reusable). */
+long long u3d_stem_fwd_stats_ws_bytes(int n, int d, int h, int w);
+int u3d_stem_fwd_stats(const float* x, int n, int d, int h, int w, const void* wpk, void* y, float* stats, void* ws,
+                       u3d_stream_t stream);
 int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                  int stride, void* y, u3d_stream_t stream);
 /* split count for u3d_stem_wgrad given its dtype/channels (the bf16 1->32 stride-1 stem runs on MFMA) */
@@ -256,6 +262,13 @@ int u3d_gn_bwd2(int dtype, const void* da1, const void* da2, const void* x, int 
  * (unet3D.py:1646, 1764-1783). x [n][d][h][w][c] -> y [n][2d][2h][2w][c]; skip nullable. */
 int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
                        u3d_stream_t stream);
+/* u3d_upsample2x_add (bf16) that also returns the GroupNorm(16) statistics (mean, rstd) [n][16][2] of its stored
+ * output — the decoder block's gn1 / downsample-GN input (unet3D.py:56-73) — accumulated in the epilogue (fp64
+ * per-block partials, fixed-order last-block combine). c a power of two in [16, 256]. ws =
+ * u3d_upsample2x_stats_ws_bytes(n, c, d) bytes, zero on first use (left reusable). */
+long long u3d_upsample2x_stats_ws_bytes(int n, int c, int d);
+int u3d_upsample2x_add_stats(const void* x, int n, int c, int d, int h, int w, const void* skip, void* y, float* stats,
+                             void* ws, u3d_stream_t stream);
 int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d, int h, int w, void* dx, int accumulate,
                        u3d_stream_t stream);
 

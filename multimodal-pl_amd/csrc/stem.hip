@@ -5,6 +5,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "gnpart.h"
 
 namespace u3d {
 
@@ -65,10 +66,15 @@ __global__ __launch_bounds__(ST) void stem_fwd_kernel(const float* __restrict__ 
 // read once for them (the one-voxel form was LDS-bound: 216 vector reads per voxel). Same fp32 FMA chain per output
 // as stem_fwd_kernel (x fp32, weights from the packed bf16/f32 image), so results are bitwise those of the generic
 // kernel. One thread per (output row, group of four w voxels).
-template <typename T>
+// STATS: also the GroupNorm(16, 32) statistics of the stored output (layer0's gn1 input, unet3D.py:56-73):
+// per-thread fp32 sums of its 4 voxels x 2 channels per group, fp64 across the block (xor tree + waves in order)
+// and the blocks (gnpart.h last-block combine).
+template <typename T, bool STATS = false>
 __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__ x, const T* __restrict__ wpk,
                                                       T* __restrict__ y, int d, int h, int w, int cin_p,
-                                                      long long rows) {
+                                                      long long rows, double* __restrict__ part = nullptr,
+                                                      unsigned* __restrict__ cnt = nullptr,
+                                                      float* __restrict__ stats = nullptr, int n = 0) {
   __shared__ f32x4 wl[27 * 8];  // [t][co/4]
   for (int i = threadIdx.x; i < 27 * 32; i += ST) {
     const int co = i % 32, t = i / 32;
@@ -77,8 +83,10 @@ __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__
   __syncthreads();
   const int w4 = w >> 2;
   const long long item = (long long)blockIdx.x * ST + threadIdx.x;  // (output row, 4-voxel group)
-  const long long row = item / w4;
-  if (row >= rows) return;
+  const long long row0 = item / w4;
+  const bool live = row0 < rows;
+  if (!STATS && !live) return;
+  const long long row = live ? row0 : rows - 1;
   const int q = (int)(item - row * w4);
   const int yy = (int)(row % h);
   const long long nz = row / h;
@@ -120,15 +128,97 @@ __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__
   }
   T* yr = y + (row * w + x0) * 32;
   constexpr int VEC = 16 / sizeof(T);
+  if (live) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int c = 0; c < 32; c += VEC) {
-      float v[VEC];
+      for (int c = 0; c < 32; c += VEC) {
+        float v[VEC];
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) v[e] = acc[j][c + e];
-      store16<T>(yr + j * 32 + c, v);
+        for (int e = 0; e < VEC; ++e) v[e] = acc[j][c + e];
+        store16<T>(yr + j * 32 + c, v);
+      }
+  }
+  if constexpr (STATS) {
+    // a block may straddle two samples: partials per (block, which sample); a thread's rows belong to sample
+    // nn = row / (d * h). fp32 within a wave (512 values), fp64 across waves and blocks.
+    __shared__ double red[ST / 64][2][32];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long long nn = row / ((long long)d * h);
+    const long long nfirst = ((long long)blockIdx.x * ST / w4) / ((long long)d * h);
+    const int which = (int)(nn - nfirst);  // 0 or 1: a block spans at most two samples (d * h * w / 4 >= ST)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int gq = 0; gq < 16; ++gq) {
+        float s1 = 0.f, s2 = 0.f;
+        if (live && which == q) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const float t = to_f(from_f<T>(acc[j][2 * gq + e]));  // the stored value
+              s1 += t;
+              s2 = fmaf(t, t, s2);
+            }
+        }
+        for (int o = 1; o < 64; o <<= 1) {
+          s1 += __shfl_xor(s1, o);
+          s2 += __shfl_xor(s2, o);
+        }
+        if (lane == 0) {
+          red[wave][q][2 * gq] = s1;
+          red[wave][q][2 * gq + 1] = s2;
+        }
+      }
     }
+    __syncthreads();
+    // part[block][which][16][2] (which = 0: the first sample the block touches, 1: the next one, zeros if none)
+    const int nblk = gridDim.x;
+    if (threadIdx.x < 64) {
+      const int q = threadIdx.x >> 5, k = threadIdx.x & 31;
+      double v = 0;
+      for (int wv = 0; wv < ST / 64; ++wv) v += red[wv][q][k];
+      __hip_atomic_store(part + ((long long)blockIdx.x * 2 + q) * 32 + k, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!gn_part_is_last(cnt, (unsigned)nblk)) return;
+    // sample s is touched by the contiguous blocks b_lo..b_hi; block b holds it in slot s - (first sample of b)
+    __shared__ double fin[ST][2];
+    const long long ips = (long long)d * h * w4;  // items per sample
+    const int npairs = n * 16, spl = npairs >= ST ? 1 : ST / npairs;
+    for (int p0 = 0; p0 < npairs; p0 += ST) {
+      const int p = p0 + threadIdx.x % min(npairs, ST), sl = threadIdx.x / min(npairs, ST);
+      double s1 = 0, s2 = 0;
+      if (p < npairs && sl < spl) {
+        const int smp = p / 16, gq = p % 16;
+        const int lo = (int)((smp * ips) / ST), hi = (int)(((smp + 1) * ips - 1) / ST);
+        const int b0 = lo + (int)((long long)(hi - lo + 1) * sl / spl), b1 = lo + (int)((long long)(hi - lo + 1) * (sl + 1) / spl);
+        for (int bb = b0; bb < b1; ++bb) {
+          const int which = smp - (int)(((long long)bb * ST / w4) / ((long long)d * h));
+          const double* q = part + ((long long)bb * 2 + which) * 32 + 2 * gq;
+          s1 += __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s2 += __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      fin[threadIdx.x][0] = s1;
+      fin[threadIdx.x][1] = s2;
+      __syncthreads();
+      if (threadIdx.x < min(npairs, ST) && p < npairs) {
+        double t1 = 0, t2 = 0;
+        for (int k = 0; k < spl; ++k) {
+          t1 += fin[k * min(npairs, ST) + threadIdx.x][0];
+          t2 += fin[k * min(npairs, ST) + threadIdx.x][1];
+        }
+        const double M = (double)d * h * w * 2, mean = t1 / M;
+        double var = t2 / M - mean * mean;
+        if (var < 0) var = 0;
+        stats[p * 2] = (float)mean;
+        stats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+      }
+      __syncthreads();
+    }
+  }
 }
 
 // dW[t][co][ci] partial over a voxel split: thread per (t, ci, co) output, loop over the split's voxels.
@@ -332,6 +422,26 @@ static bool stem1_on() {  // U3D_STEM1=0: the generic one-voxel kernel (A/B expe
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+extern "C" long long u3d_stem_fwd_stats_ws_bytes(int n, int d, int h, int w) {
+  const long long items = (long long)n * d * h * (w / 4);
+  return 256 + ((items + ST - 1) / ST) * 2 * 32 * 8;
+}
+
+extern "C" int u3d_stem_fwd_stats(const float* x, int n, int d, int h, int w, const void* wpk, void* y, float* stats,
+                                  void* ws, u3d_stream_t stream) {
+  U3D_REQUIRE(x && wpk && y && stats && ws && n >= 1 && d >= 1 && h >= 1 && w % 4 == 0 && w >= 4,
+              "stem_fwd_stats: bad args (cin 1 -> 32, stride 1, w %% 4 == 0)");
+  U3D_REQUIRE((long long)d * h * (w / 4) >= ST, "stem_fwd_stats: volume too small (a block must span <= 2 samples)");
+  const long long rows = (long long)n * d * h, items = rows * (w / 4);
+  U3D_REQUIRE(rows < 2147483647LL, "stem_fwd_stats: volume too large");
+  const dim3 grid((unsigned)((items + ST - 1) / ST));
+  unsigned* cnt = reinterpret_cast<unsigned*>(ws);
+  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
+  hipLaunchKernelGGL((stem1_fwd_kernel<bf16, true>), grid, dim3(ST), 0, (hipStream_t)stream, x, (const bf16*)wpk,
+                     (bf16*)y, d, h, w, 32, rows, part, cnt, stats, n);
+  return check_launch("stem1_fwd_kernel (statistics)");
 }
 
 extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
