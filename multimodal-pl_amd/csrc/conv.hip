@@ -767,13 +767,26 @@ static int launch_igemm(Geom g, int n, const T* x, const T* wpk, TO* y, const T*
                         hipStream_t s) {
   const int Mq = g.qd * g.qh * g.qw;
   if (Mq <= 0) return U3D_OK;
-  const int BN = g.cout_p <= 32 ? 32 : (sizeof(T) == 2 && g.cout_p >= 128) ? 128 : 64;
+  static const int env_bn = [] { const char* e = getenv("U3D_IGEMM_BN"); return e ? atoi(e) : 0; }();
+  static const int env_ns = [] { const char* e = getenv("U3D_IGEMM_NS"); return e ? atoi(e) : 0; }();
+  static const int env_target = [] { const char* e = getenv("U3D_IGEMM_TARGET"); return e ? atoi(e) : 512; }();
+  int BN = g.cout_p <= 32 ? 32 : (sizeof(T) == 2 && g.cout_p >= 128) ? 128 : 64;
+  static const bool auto_bn = [] { const char* e = getenv("U3D_IGEMM_AUTO"); return !e || atoi(e) != 0; }();
+  if (sizeof(T) == 2 && auto_bn) {
+    // too few output tiles to fill the CUs: narrower N tiles before splitting K (measured, tools/igemm_sweep.sh:
+    // 48^3 64->128 s2 91 -> 66 us at BN 64, 12^3 256->256 s2 50 -> 37 us at BN 32)
+    auto ntile = [&](int bn) { return (long long)cdiv(Mq, 128) * cdiv(g.cout, bn) * n; };
+    if (BN > 32 && ntile(BN) < 256) BN /= 2;
+    if (BN > 32 && ntile(BN) < 64) BN /= 2;
+  }
+  if (env_bn && sizeof(T) == 2 && env_bn <= g.cout_p) BN = env_bn;  // experiments
   const long long tiles = (long long)cdiv(Mq, 128) * cdiv(g.cout, BN) * n;
   const int nk = g.ntaps * (g.cin_p / BK);
   // split K when the output tiles cannot fill the 256 CUs (deep, small-volume layers)
   int ns = 1;
   if (ws && tiles < 256 && nk >= 8) {
-    ns = (int)std::min<long long>(nk / 4, (512 + tiles - 1) / tiles);
+    ns = (int)std::min<long long>(nk / 4, (env_target + tiles - 1) / tiles);
+    if (env_ns > 0) ns = std::min(env_ns, nk);
     if (sizeof(T) == 2 && ns > 8) ns = ns / 8 * 8;  // split-major XCD mapping: one K slice per XCD
     const long long slab1 = (long long)n * Mq * g.cout * 4;
     while (ns > 1 && ns * slab1 > ws_bytes) --ns;

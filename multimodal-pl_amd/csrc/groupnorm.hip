@@ -133,23 +133,22 @@ __device__ __forceinline__ void combine_channels(const float* __restrict__ ws, c
       const int nn = p / g.c, c = p % g.c;
       // partials of other blocks (rows of nv x C per block; this pass reads rows k0, k0 + 1): sc1 loads only
       const float* q = ws + (long long)nn * g.nblk * nv * g.c + k0 * g.c + c;
-      int b = sl;
-      for (; b + 31 * spl < g.nblk; b += 32 * spl) {  // 64 loads in flight: the combine is one latency round
-        float a[32], bb[32];
+      // 16 predicated loads in flight per round, then the adds in block order (the same order as a serial walk):
+      // the combine costs ceil(nblk / (8 spl)) latency rounds instead of one per block
+      for (int b0 = sl; b0 < g.nblk; b0 += 8 * spl) {
+        float a[8], bb[8];
 #pragma unroll
-        for (int u = 0; u < 32; ++u) {
-          a[u] = ld_sc1(q + (long long)(b + u * spl) * nv * g.c);
-          bb[u] = ld_sc1(q + (long long)(b + u * spl) * nv * g.c + g.c);
+        for (int u = 0; u < 8; ++u) {
+          const int b = min(b0 + u * spl, g.nblk - 1);  // clamped address: straight-line loads, no branches
+          a[u] = ld_sc1(q + (long long)b * nv * g.c);
+          bb[u] = ld_sc1(q + (long long)b * nv * g.c + g.c);
         }
 #pragma unroll
-        for (int u = 0; u < 32; ++u) {
-          s1 += a[u];
-          s2 += bb[u];
+        for (int u = 0; u < 8; ++u) {
+          const bool ok = b0 + u * spl < g.nblk;
+          s1 += ok ? a[u] : 0.f;
+          s2 += ok ? bb[u] : 0.f;
         }
-      }
-      for (; b < g.nblk; b += spl) {
-        s1 += ld_sc1(q + (long long)b * nv * g.c);
-        s2 += ld_sc1(q + (long long)b * nv * g.c + g.c);
       }
     }
     part[tid][0] = s1;
@@ -182,35 +181,28 @@ __global__ __launch_bounds__(GT) void gn_stats_kernel(const T* __restrict__ x, R
     float shift[VEC];
     for (int e = 0; e < VEC; ++e) shift[e] = to_f(xn[((j * VEC + e) / g.cpg) * g.cpg]);  // x[n, voxel 0, first ch of group]
     const long long v0 = (long long)blk * g.vpb, v1 = std::min<long long>(g.v, v0 + g.vpb);
-    long long v = v0 + vl;
-    for (; v + 7 * g.vlanes < v1; v += 8 * g.vlanes) {  // 8 loads (64 KB per CU) in flight: HBM latency hidden
+    // rounds of 8 predicated loads (64 KB per CU in flight): a small tensor costs one latency round, not one per
+    // voxel; voxels past the range read as the shift (d = 0), so the sums are those of the serial walk
+    for (long long v = v0 + vl; v < v1; v += 8 * g.vlanes) {
       float xv[8][VEC];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) load16<T>(xn + (v + u * g.vlanes) * g.c + j * VEC, xv[u]);
+      for (int u = 0; u < 8; ++u) load16<T>(xn + std::min(v + u * g.vlanes, v1 - 1) * g.c + j * VEC, xv[u]);
 #pragma unroll
       for (int u = 0; u < 8; ++u)
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
-          const float d = xv[u][e] - shift[e];
+          const float d = v + u * g.vlanes < v1 ? xv[u][e] - shift[e] : 0.f;
           acc[0][e] += d;
           acc[1][e] = fmaf(d, d, acc[1][e]);
         }
-    }
-    for (; v < v1; v += g.vlanes) {
-      float xv[VEC];
-      load16<T>(xn + v * g.c + j * VEC, xv);
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        const float d = xv[e] - shift[e];
-        acc[0][e] += d;
-        acc[1][e] = fmaf(d, d, acc[1][e]);
-      }
     }
   }
   block_channel_reduce<VEC, 2>(acc, lds, g, ws + ((long long)n * g.nblk + blk) * 2 * g.c);
   if (!block_is_last(cnt, (unsigned)(g.n * g.nblk))) return;
   // combine: per (n, c) sums over the blocks, then per (n, group) over its channels, fixed order, fp64
   __shared__ double cs[GN_PAIRS_MAX][2];
+  // the first group's shift is loaded before the combine (its latency overlaps the partial loads)
+  const float sh0 = tid < g.n * g.groups ? to_f(x[(long long)(tid / g.groups) * g.v * g.c + (tid % g.groups) * g.cpg]) : 0.f;
   combine_channels(ws, g, cs);
   for (int p = tid; p < g.n * g.groups; p += GT) {
     const int nn = p / g.groups, gr = p % g.groups;
@@ -220,7 +212,7 @@ __global__ __launch_bounds__(GT) void gn_stats_kernel(const T* __restrict__ x, R
       s2 += cs[nn * g.c + gr * g.cpg + k][1];
     }
     const double M = (double)g.v * g.cpg;
-    const double shift = to_f(x[(long long)nn * g.v * g.c + gr * g.cpg]);
+    const double shift = p == tid ? sh0 : to_f(x[(long long)nn * g.v * g.c + gr * g.cpg]);
     const double dm = s1 / M;
     double var = s2 / M - dm * dm;
     if (var < 0) var = 0;
@@ -268,22 +260,22 @@ __global__ __launch_bounds__(GT) void gn_bwd_partial(const T* __restrict__ da, c
         acc[1][e] = fmaf(gd, xh, acc[1][e]);
       }
     };
-    long long v = v0 + vl;
-    for (; v + 3 * g.vlanes < v1; v += 4 * g.vlanes) {  // 8 loads (64 KB per CU) in flight per thread
+    // rounds of 4 predicated voxel pairs (8 loads in flight); past the range dA = 0 contributes nothing
+    for (long long v = v0 + vl; v < v1; v += 4 * g.vlanes) {
       float xv[4][VEC], dv[4][VEC];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        load16<T>(x + base + (v + u * g.vlanes) * g.c + j * VEC, xv[u]);
-        load16<T>(da + base + (v + u * g.vlanes) * g.c + j * VEC, dv[u]);
+        const long long vv = std::min(v + u * g.vlanes, v1 - 1);
+        load16<T>(x + base + vv * g.c + j * VEC, xv[u]);
+        load16<T>(da + base + vv * g.c + j * VEC, dv[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) step(xv[u], dv[u]);
-    }
-    for (; v < v1; v += g.vlanes) {
-      float xv[VEC], dv[VEC];
-      load16<T>(x + base + v * g.c + j * VEC, xv);
-      load16<T>(da + base + v * g.c + j * VEC, dv);
-      step(xv, dv);
+      for (int u = 0; u < 4; ++u) {
+        if (v + u * g.vlanes >= v1)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) dv[u][e] = 0.f;
+        step(xv[u], dv[u]);
+      }
     }
   }
   block_channel_reduce<VEC, 2>(acc, lds, g, ws + ((long long)n * g.nblk + blk) * 2 * g.c);
@@ -404,26 +396,22 @@ __global__ __launch_bounds__(GT) void gn_bwd2_partial(const T* __restrict__ da1,
         acc[3][e] = fmaf(g2, xh, acc[3][e]);
       }
     };
-    long long v = v0 + vl;
-    for (; v + 1 * g.vlanes < v1; v += 2 * g.vlanes) {  // 6 loads in flight per thread
+    for (long long v = v0 + vl; v < v1; v += 2 * g.vlanes) {  // rounds of 6 predicated loads
       float xv[2][VEC], d1[2][VEC], d2[2][VEC];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const long long off = base + (v + u * g.vlanes) * g.c + j * VEC;
+        const long long off = base + std::min(v + u * g.vlanes, v1 - 1) * g.c + j * VEC;
         load16<T>(x + off, xv[u]);
         load16<T>(da1 + off, d1[u]);
         load16<T>(da2 + off, d2[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) step(xv[u], d1[u], d2[u]);
-    }
-    for (; v < v1; v += g.vlanes) {
-      float xv[VEC], d1[VEC], d2[VEC];
-      const long long off = base + v * g.c + j * VEC;
-      load16<T>(x + off, xv);
-      load16<T>(da1 + off, d1);
-      load16<T>(da2 + off, d2);
-      step(xv, d1, d2);
+      for (int u = 0; u < 2; ++u) {
+        if (v + u * g.vlanes >= v1)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) d1[u][e] = d2[u][e] = 0.f;
+        step(xv[u], d1[u], d2[u]);
+      }
     }
   }
   block_channel_reduce<VEC, 4>(acc, lds, g, ws + ((long long)n * g.nblk + blk) * 4 * g.c);

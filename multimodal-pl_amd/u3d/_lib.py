@@ -4,7 +4,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libu3d.so")
+LIB_PATH = os.environ.get("U3D_LIB") or os.path.join(_HERE, "libu3d.so")  # U3D_LIB: A/B builds (tools/ab_lib)
 
 F32, BF16 = 0, 1
 

@@ -130,10 +130,35 @@ def _stem(stats, n=2, s=96):
     return t_(fn), 2.0 * n * s ** 3 * 27 * 32
 
 
-CASES_EXTRA = {"up96_stats": lambda: _up(True), "up96_plain_then_stats": lambda: _up(False),
+CASES_EXTRA = {"fwd_s2_96": lambda: _fwd(2, 32, 64, 96, 3, 2, True, False),
+               "fwd_s2_48": lambda: _fwd(2, 64, 128, 48, 3, 2, True, False),
+               "fwd_s2_12": lambda: _fwd(2, 256, 256, 12, 3, 2, True, False),
+               "fwd48_plain": lambda: _fwd(2, 64, 64, 48, 3, 1, False, False),
+               "fwd48_gn": lambda: _fwd(2, 64, 64, 48, 3, 1, True, False),
+               "fwd48_res": lambda: _fwd(2, 64, 64, 48, 3, 1, False, True),
+               "fwd24_plain": lambda: _fwd(2, 128, 128, 24, 3, 1, False, False),"up96_stats": lambda: _up(True), "up96_plain_then_stats": lambda: _up(False),
                "up24_stats": lambda: _up(True, 2, 12, 128), "up24_plain_then_stats": lambda: _up(False, 2, 12, 128),
                "stem96_stats": lambda: _stem(True), "stem96_plain_then_stats": lambda: _stem(False)}
 CASES.update(CASES_EXTRA)
+
+
+def _gn(kind, s, c, n=2, G=16):
+    x = torch.randn((n, s, s, s, c), device=dev).to(bf)
+    da = torch.randn_like(x)
+    da2 = torch.randn_like(x)
+    ga, be = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.1
+    st = ops.gn_stats(x, G)
+    dx = torch.empty_like(x)
+    fns = {"stats": lambda: ops.gn_stats(x, G),
+           "apply": lambda: ops.gn_apply(x, st, ga, be, G),
+           "bwd": lambda: ops.gn_bwd(da, x, st, ga, be, G, dx=dx, accumulate=True),
+           "bwd2": lambda: ops.gn_bwd2(da, da2, x, st, (ga, be), (ga, be), G, dx=dx, accumulate=True)}
+    return t_(fns[kind]), 0.0
+
+
+for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 256), ("6", 6, 256)]:
+    for kind in ("stats", "apply", "bwd", "bwd2"):
+        CASES[f"gn{kind}{lvl}"] = (lambda kind=kind, s=s, c=c: _gn(kind, s, c))
 
 
 if __name__ == "__main__":
