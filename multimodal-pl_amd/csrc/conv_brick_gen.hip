@@ -293,8 +293,13 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
   g.gn_groups = gn_groups;
   const int nb = n * g.nbd * g.nbh * g.nbw;
   hipStream_t s = (hipStream_t)stream;
-  const bool co64 = g.cout_p >= 64;
-  g.nct = co64 ? cdiv(cout, 64) : 1;
+  // 64-channel co tiles. 32-channel tiles when 64 would leave CUs idle (U3D_CONVG_CO32 = -1) or always (= 1) were
+  // measured slower (24^3 x 128 ch fwd 63.5 -> 78.7 us with 288 instead of 144 workgroups): off by default.
+  static const int env_co32 = [] { const char* e = getenv("U3D_CONVG_CO32"); return e ? atoi(e) : 0; }();
+  bool co64 = g.cout_p >= 64;
+  if (co64 && env_co32 == 1) co64 = false;
+  if (co64 && env_co32 < 0 && (long long)nb * cdiv(cout, 64) < 256) co64 = false;
+  g.nct = cdiv(cout, co64 ? 64 : 32);
   dim3 grid(nb * g.nct);
   if (co64) {
     if (flip)

@@ -27,7 +27,7 @@ class Engine(object):
             assert isinstance(custom_parser, argparse.ArgumentParser)
             self.parser = custom_parser
         self.inject_default_parser()
-        self.args, _ = self.parser.parse_known_args()
+        self.args = self.parser.parse_args()  # as the reference (engine.py:22): unknown flags are an error
         self.continue_state_object = self.args.continue_fpath
 
         self.world_size = int(os.environ.get("WORLD_SIZE", "1"))

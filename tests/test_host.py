@@ -116,6 +116,9 @@ def test_engine_flags_and_single_process():
             m = torch.nn.Linear(2, 2)
             w = e.data_parallel(m)
             assert w.module is m
+        sys.argv = ["x", "--no-such-flag"]
+        with pytest.raises(SystemExit):  # parse_args, as the reference: unknown flags are rejected
+            engine.Engine(custom_parser=argparse.ArgumentParser())
     finally:
         sys.argv = old
 
