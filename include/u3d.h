@@ -111,6 +111,15 @@ int u3d_conv_wgrad(int dtype, const void* dy, const void* x, int n, int cin, int
 int u3d_conv_dgrad_s2(const void* dy, int n, int cout, const void* wpk_dgrad, int cin, int d, int h, int w, void* dx,
                       u3d_stream_t stream);
 
+/* bf16 1^3 convolution, stride 1 or 2 (pad 0): y [n][od][oh][ow][cy] = W . relu(gn(x)) at the input voxel
+ * (s*od, s*oh, s*ow); x [n][d][h][w][cx], W = packed [round_up(cy, 32)][wpitch] bf16 (the forward pack of a 1^3
+ * weight, wpitch = round_up(cx, 32); or the data-gradient pack [cin_p][cout_p] of a stride-1 1^3 conv, which makes
+ * this its data gradient). gn_stats = NULL: no prologue. cx, cy multiples of 8, <= 256. Replaces F.conv3d for the
+ * 1^3 downsample / channel-change convs (reference unet3D.py:27 via NoBottleneck :56-73, _make_layer :1666-1686). */
+int u3d_conv1x1(const void* x, int n, int cx, int d, int h, int w, const void* wpk, int wpitch, int cy, int stride,
+                const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups, void* y,
+                u3d_stream_t stream);
+
 /* bf16 3^3 stride-1 conv for the small deep-level volumes (24^3 and below): one workgroup = a brick of <= 256
  * output voxels x 32 output channels with the whole contraction (no split-K slabs), GN+ReLU prologue applied
  * once per staged element, residual epilogue. flip/wpk/cin/cout as u3d_convg_brick. When there are too few

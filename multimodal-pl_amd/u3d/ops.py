@@ -166,6 +166,16 @@ def wstd_bwd(partials, nsplit, w, wstats, standardize, dw=None, accumulate=False
 
 
 # ------------------------------------------------------------------------------------------ convs
+# bf16 1^3 convs (stride 1 / 2, GN prologue in registers) and stride-1 1^3 data gradients: streaming kernel
+# (conv1x1.hip) instead of the implicit GEMM (+ GN materialisation). U3D_CONV1X1=0: the implicit GEMM.
+USE_CONV1X1 = os.environ.get("U3D_CONV1X1", "1") != "0"
+
+
+def _use_conv1x1(dtype, cx, cy, k, n):
+    return USE_CONV1X1 and k == 1 and dtype == torch.bfloat16 and cx % 8 == 0 and cy % 8 == 0 and max(cx, cy) <= 256 \
+        and n <= 65535
+
+
 def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32=False):
     """x: [n,d,h,w,cin] -> [n,od,oh,ow,cout]. gn = (stats, gamma, beta, groups) fuses GroupNorm+ReLU."""
     require_device(x)
@@ -173,6 +183,10 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
     od, oh, ow = out_dim(d, k, stride), out_dim(h, k, stride), out_dim(w_, k, stride)
     y = torch.empty((n, od, oh, ow, cout), dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
     st, ga, be, G = gn if gn is not None else (None, None, None, 0)
+    if _use_conv1x1(x.dtype, cin, cout, k, n) and residual is None and bias is None and not out_f32:
+        call("u3d_conv1x1", x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), wpk.shape[-1], cout, stride, _ptr(st),
+             _ptr(ga), _ptr(be), G, y.data_ptr(), _stream())
+        return y
     if _use_conv32(x.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(x) and not out_f32 and bias is None:
         probe = PROBE is not None
         if probe:  # bench.py: HIP events around the dominant kernel, on the stream it runs on
@@ -307,6 +321,10 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     n, d, h, w_ = in_shape
     cout = dy.shape[-1]
     dx = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
+    if stride == 1 and _use_conv1x1(dy.dtype, cout, cin, k, n):  # dx = dy . W^T: the dgrad pack is [cin_p][cout_p]
+        call("u3d_conv1x1", dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), wpk_dgrad.shape[-1], cin, 1, None,
+             None, None, 0, dx.data_ptr(), _stream())
+        return dx
     if _use_conv32(dy.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(dy):
         if _ring_queue(dgrad=True):
             call("u3d_conv32_ring_q", 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,

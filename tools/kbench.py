@@ -142,6 +142,14 @@ CASES_EXTRA = {"fwd_s2_96": lambda: _fwd(2, 32, 64, 96, 3, 2, True, False),
 CASES.update(CASES_EXTRA)
 
 
+for (nm, cx, cy, s_, st_) in [("c1_s2_96", 32, 64, 96, 2), ("c1_s2_48", 64, 128, 48, 2), ("c1_s2_24", 128, 256, 24, 2),
+                             ("c1_s2_12", 256, 256, 12, 2), ("c1_48", 64, 32, 48, 1), ("c1_24", 128, 64, 24, 1),
+                             ("c1_12", 256, 128, 12, 1), ("c1_6", 256, 256, 6, 1)]:
+    CASES[nm] = (lambda cx=cx, cy=cy, s_=s_, st_=st_: _fwd(2, cx, cy, s_, 1, st_, True, False))
+    if st_ == 1:
+        CASES["d" + nm] = (lambda cx=cx, cy=cy, s_=s_: _dgrad(2, cx, cy, s_, 1, 1))
+
+
 def _gn(kind, s, c, n=2, G=16):
     x = torch.randn((n, s, s, s, c), device=dev).to(bf)
     da = torch.randn_like(x)
