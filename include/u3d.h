@@ -266,6 +266,15 @@ int u3d_gn_bwd2(int dtype, const void* da1, const void* da2, const void* x, int 
                 void* dx, int accumulate, float* dgamma1, float* dbeta1, float* dgamma2, float* dbeta2,
                 int accumulate_params, float* ws, u3d_stream_t stream);
 
+/* u3d_gn_bwd2 where da2 is the data gradient of a stride-2 1^3 conv (the stage's downsample branch) given at that
+ * conv's OUTPUT resolution, da2c [n][(d-1)/2+1][(h-1)/2+1][(w-1)/2+1][c]: it is nonzero only at the x voxels with all
+ * coordinates even, so it is neither scattered to the full grid nor zero-filled. x [n][d][h][w][c]. Same semantics
+ * as u3d_gn_bwd2 otherwise (backward of gn1 + downsample GN of NoBottleneck, reference unet3D.py:44-73). */
+int u3d_gn_bwd2_s2(int dtype, const void* da1, const void* da2c, const void* x, int n, int c, int d, int h, int w,
+                   int groups, const float* stats, const float* gamma1, const float* beta1, const float* gamma2,
+                   const float* beta2, void* dx, int accumulate, float* dgamma1, float* dbeta1, float* dgamma2,
+                   float* dbeta2, int accumulate_params, float* ws, u3d_stream_t stream);
+
 /* ---------------------------------------------------------------- trilinear x2 upsample + skip (A6)
  * nn.Upsample(scale_factor=2, mode='trilinear') (align_corners=False) then `+ skip`
  * (unet3D.py:1646, 1764-1783). x [n][d][h][w][c] -> y [n][2d][2h][2w][c]; skip nullable. */

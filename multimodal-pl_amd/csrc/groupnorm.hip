@@ -23,7 +23,32 @@ constexpr int GN_PAIRS_MAX = 2048;  // n * c of the backward's last-block combin
 struct RedGeom {
   int n, c, groups, cpg, nblk, vpb, chn, vlanes;  // chn = 16-B chunks per voxel, vlanes = voxels per pass
   long long v;
+  int fh, fw, ch, cw;  // u3d_gn_bwd2_s2: fine h, w (x) and compact h, w (da2 = a stride-2 1^3 data gradient)
+  long long cv;        // compact voxels per sample
 };
+
+// da2 of u3d_gn_bwd2_s2 is the stride-2 1^3 conv's data gradient at the conv's OUTPUT resolution: nonzero only at
+// fine voxels with all coordinates even. Returns its compact index, or -1 (odd voxel: dA2 = 0).
+__device__ __forceinline__ long long s2_index(long long vv, const RedGeom& g) {
+  const int vi = (int)vv, hw = g.fh * g.fw;
+  const int a = vi / hw, rem = vi - a * hw, b = rem / g.fw, c = rem - b * g.fw;
+  return ((a | b | c) & 1) ? -1 : ((long long)(a >> 1) * g.ch + (b >> 1)) * g.cw + (c >> 1);
+}
+
+template <typename T, bool S2>
+__device__ __forceinline__ void load_da2(const T* __restrict__ da2, const RedGeom& g, int n, long long vv, int j,
+                                         long long off, float (&d2)[16 / sizeof(T)]) {
+  constexpr int VEC = 16 / sizeof(T);
+  if constexpr (S2) {
+    const long long ci = s2_index(vv, g);
+    load16<T>(da2 + ((long long)n * g.cv + (ci < 0 ? 0 : ci)) * g.c + j * VEC, d2);  // clamped: straight-line load
+    if (ci < 0)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) d2[e] = 0.f;
+  } else {
+    load16<T>(da2 + off, d2);
+  }
+}
 
 // reduction blocks over all samples (U3D_GN_MAXBLK overrides, for experiments)
 static long long gn_max_blocks() {
@@ -355,7 +380,7 @@ __global__ __launch_bounds__(GT) void gn_bwd_apply(const T* __restrict__ da, con
 // (per set k: s1_k = sum m_k dA_k, s2_k = sum m_k dA_k xhat) and one apply writing
 //   dx (+)= alpha1 m1 dA1 + alpha2 m2 dA2 + (bx1 + bx2) x + (d1 + d2)
 // instead of two full backward passes (x read 4 times, dx written twice). coef2 [2][n][5][C].
-template <typename T>
+template <typename T, bool S2>
 __global__ __launch_bounds__(GT) void gn_bwd2_partial(const T* __restrict__ da1, const T* __restrict__ da2,
                                                      const T* __restrict__ x, RedGeom g, const float* __restrict__ stats,
                                                      const float* __restrict__ gamma1, const float* __restrict__ beta1,
@@ -400,10 +425,11 @@ __global__ __launch_bounds__(GT) void gn_bwd2_partial(const T* __restrict__ da1,
       float xv[2][VEC], d1[2][VEC], d2[2][VEC];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const long long off = base + std::min(v + u * g.vlanes, v1 - 1) * g.c + j * VEC;
+        const long long vv = std::min(v + u * g.vlanes, v1 - 1);
+        const long long off = base + vv * g.c + j * VEC;
         load16<T>(x + off, xv[u]);
         load16<T>(da1 + off, d1[u]);
-        load16<T>(da2 + off, d2[u]);
+        load_da2<T, S2>(da2, g, n, vv, j, off, d2[u]);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -455,7 +481,7 @@ __global__ __launch_bounds__(GT) void gn_bwd2_partial(const T* __restrict__ da1,
   }
 }
 
-template <typename T>
+template <typename T, bool S2>
 __global__ __launch_bounds__(GT) void gn_bwd2_apply(const T* __restrict__ da1, const T* __restrict__ da2,
                                                    const T* __restrict__ x, RedGeom g, const float* __restrict__ coef,
                                                    T* __restrict__ dx, int accum) {
@@ -483,10 +509,11 @@ __global__ __launch_bounds__(GT) void gn_bwd2_apply(const T* __restrict__ da1, c
     float xv[2][VEC], d1[2][VEC], d2[2][VEC], o[2][VEC];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const long long off = nb + std::min(vox + (long long)u * vstep, g.v - 1) * g.c;
+      const long long vv = std::min(vox + (long long)u * vstep, g.v - 1);
+      const long long off = nb + vv * g.c;
       load16<T>(x + off, xv[u]);
       load16<T>(da1 + off, d1[u]);
-      load16<T>(da2 + off, d2[u]);
+      load_da2<T, S2>(da2, g, n, vv, j, off, d2[u]);
       if (accum) load16<T>(dx + off, o[u]);
     }
 #pragma unroll
@@ -616,11 +643,12 @@ extern "C" int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v,
   return check_launch("gn_apply_kernel");
 }
 
-extern "C" int u3d_gn_bwd2(int dtype, const void* da1, const void* da2, const void* x, int n, int c, long long v,
-                           int groups, const float* stats, const float* gamma1, const float* beta1,
-                           const float* gamma2, const float* beta2, void* dx, int accumulate, float* dgamma1,
-                           float* dbeta1, float* dgamma2, float* dbeta2, int accumulate_params, float* ws,
-                           u3d_stream_t stream) {
+template <bool S2>
+static int gn_bwd2_launch(int dtype, const void* da1, const void* da2, const void* x, int n, int c, long long v,
+                          int fh, int fw, int groups, const float* stats, const float* gamma1, const float* beta1,
+                          const float* gamma2, const float* beta2, void* dx, int accumulate, float* dgamma1,
+                          float* dbeta1, float* dgamma2, float* dbeta2, int accumulate_params, float* ws,
+                          u3d_stream_t stream) {
   U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "gn_bwd2: bad dtype");
   U3D_REQUIRE(da1 && da2 && x && stats && gamma1 && beta1 && gamma2 && beta2 && dx && ws && groups > 0 &&
               c % groups == 0, "gn_bwd2: bad args");
@@ -628,6 +656,13 @@ extern "C" int u3d_gn_bwd2(int dtype, const void* da1, const void* da2, const vo
   U3D_REQUIRE(c % vec == 0 && c <= 256, "gn_bwd2: channels %d unsupported", c);
   U3D_REQUIRE(n * c <= GN_PAIRS_MAX, "gn_bwd2: n * c must be <= %d", GN_PAIRS_MAX);
   RedGeom g = make_geom(n, c, v, groups, vec);
+  if (S2) {
+    U3D_REQUIRE(v < (1LL << 31) && fh > 0 && fw > 0 && v % ((long long)fh * fw) == 0, "gn_bwd2_s2: bad dims");
+    const int fd = (int)(v / ((long long)fh * fw));
+    g.fh = fh; g.fw = fw;
+    g.ch = (fh - 1) / 2 + 1; g.cw = (fw - 1) / 2 + 1;
+    g.cv = (long long)((fd - 1) / 2 + 1) * g.ch * g.cw;
+  }
   hipStream_t s = (hipStream_t)stream;
   unsigned* cnt = reinterpret_cast<unsigned*>(ws) + 2;
   float* coef = gn_coef_ptr(ws, g);
@@ -635,19 +670,38 @@ extern "C" int u3d_gn_bwd2(int dtype, const void* da1, const void* da2, const vo
   const int athr = GT / g.chn * g.chn;
   const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + 4LL * athr - 1) / (4LL * athr));
   if (dtype == U3D_BF16) {
-    hipLaunchKernelGGL(gn_bwd2_partial<bf16>, dim3(g.nblk, n), dim3(GT), 0, s, (const bf16*)da1, (const bf16*)da2,
-                       (const bf16*)x, g, stats, gamma1, beta1, gamma2, beta2, gn_part_ptr(ws), cnt, coef, dgamma1,
-                       dbeta1, dgamma2, dbeta2, accumulate_params);
-    hipLaunchKernelGGL(gn_bwd2_apply<bf16>, dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da1, (const bf16*)da2,
-                       (const bf16*)x, g, coef, (bf16*)dx, accumulate);
+    hipLaunchKernelGGL((gn_bwd2_partial<bf16, S2>), dim3(g.nblk, n), dim3(GT), 0, s, (const bf16*)da1,
+                       (const bf16*)da2, (const bf16*)x, g, stats, gamma1, beta1, gamma2, beta2, gn_part_ptr(ws), cnt,
+                       coef, dgamma1, dbeta1, dgamma2, dbeta2, accumulate_params);
+    hipLaunchKernelGGL((gn_bwd2_apply<bf16, S2>), dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da1,
+                       (const bf16*)da2, (const bf16*)x, g, coef, (bf16*)dx, accumulate);
   } else {
-    hipLaunchKernelGGL(gn_bwd2_partial<float>, dim3(g.nblk, n), dim3(GT), 0, s, (const float*)da1,
+    hipLaunchKernelGGL((gn_bwd2_partial<float, S2>), dim3(g.nblk, n), dim3(GT), 0, s, (const float*)da1,
                        (const float*)da2, (const float*)x, g, stats, gamma1, beta1, gamma2, beta2, gn_part_ptr(ws),
                        cnt, coef, dgamma1, dbeta1, dgamma2, dbeta2, accumulate_params);
-    hipLaunchKernelGGL(gn_bwd2_apply<float>, dim3(ablk, n), dim3(athr), 0, s, (const float*)da1, (const float*)da2,
-                       (const float*)x, g, coef, (float*)dx, accumulate);
+    hipLaunchKernelGGL((gn_bwd2_apply<float, S2>), dim3(ablk, n), dim3(athr), 0, s, (const float*)da1,
+                       (const float*)da2, (const float*)x, g, coef, (float*)dx, accumulate);
   }
   return check_launch("gn_bwd2");
+}
+
+extern "C" int u3d_gn_bwd2(int dtype, const void* da1, const void* da2, const void* x, int n, int c, long long v,
+                           int groups, const float* stats, const float* gamma1, const float* beta1,
+                           const float* gamma2, const float* beta2, void* dx, int accumulate, float* dgamma1,
+                           float* dbeta1, float* dgamma2, float* dbeta2, int accumulate_params, float* ws,
+                           u3d_stream_t stream) {
+  return gn_bwd2_launch<false>(dtype, da1, da2, x, n, c, v, 0, 0, groups, stats, gamma1, beta1, gamma2, beta2, dx,
+                               accumulate, dgamma1, dbeta1, dgamma2, dbeta2, accumulate_params, ws, stream);
+}
+
+extern "C" int u3d_gn_bwd2_s2(int dtype, const void* da1, const void* da2c, const void* x, int n, int c, int d, int h,
+                              int w, int groups, const float* stats, const float* gamma1, const float* beta1,
+                              const float* gamma2, const float* beta2, void* dx, int accumulate, float* dgamma1,
+                              float* dbeta1, float* dgamma2, float* dbeta2, int accumulate_params, float* ws,
+                              u3d_stream_t stream) {
+  return gn_bwd2_launch<true>(dtype, da1, da2c, x, n, c, (long long)d * h * w, h, w, groups, stats, gamma1, beta1,
+                              gamma2, beta2, dx, accumulate, dgamma1, dbeta1, dgamma2, dbeta2, accumulate_params, ws,
+                              stream);
 }
 
 extern "C" int u3d_gn_bwd_apply_coef(int dtype, const void* da, const void* x, int n, int c, long long v,

@@ -68,6 +68,7 @@ _SIGS = {
     "u3d_gn_apply": [I, P, I, I, L, I, P, P, P, P, P],
     "u3d_gn_bwd": [I, P, P, I, I, L, I, P, P, P, P, I, P, P, I, P, P],
     "u3d_gn_bwd2": [I, P, P, P, I, I, L, I, P, P, P, P, P, P, I, P, P, P, P, I, P, P],
+    "u3d_gn_bwd2_s2": [I, P, P, P, I, I, I, I, I, I, P, P, P, P, P, P, I, P, P, P, P, I, P, P],
     "u3d_upsample2x_add": [I, P, I, I, I, I, I, P, P, P],
     "u3d_upsample2x_bwd": [I, P, I, I, I, I, I, P, I, P],
     "u3d_add_inplace": [I, P, P, L, P],

@@ -352,6 +352,29 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     return dx
 
 
+# the downsample branch's stride-2 1^3 data gradient kept at the conv's output resolution when its GroupNorm backward
+# runs paired with gn1 (gn_bwd2(..., da2_s2=True)): no zero-filled full-resolution tensor (U3D_S2_COMPACT=0: off)
+S2_COMPACT = os.environ.get("U3D_S2_COMPACT", "1") != "0"
+
+
+def conv_dgrad_1x1s2_compact(dy, wpk_dgrad, cin):
+    """dx of a stride-2 1^3 conv at the conv's OUTPUT resolution (the values at the even input voxels; every
+    other input voxel's gradient is zero)."""
+    n, od, oh, ow, cout = dy.shape
+    dxc = torch.empty((n, od, oh, ow, cin), dtype=dy.dtype, device=dy.device)
+    call("u3d_conv1x1", dy.data_ptr(), n, cout, od, oh, ow, wpk_dgrad.data_ptr(), wpk_dgrad.shape[-1], cin, 1, None,
+         None, None, 0, dxc.data_ptr(), _stream())
+    return dxc
+
+
+def expand_s2(dxc, in_shape):
+    """Full-resolution tensor of a compact stride-2 1^3 data gradient (zeros at the odd voxels)."""
+    n, d, h, w_ = in_shape
+    full = torch.zeros((n, d, h, w_, dxc.shape[-1]), dtype=dxc.dtype, device=dxc.device)
+    full[:, ::2, ::2, ::2] = dxc
+    return full
+
+
 DGRAD_GN = os.environ.get("U3D_DGRAD_GN", "0") != "0"  # GN-bwd partials in the ring dgrad epilogue (measured: -0.3%, off)
 
 
@@ -537,13 +560,22 @@ def gn_bwd(da, x, stats, gamma, beta, groups, dx=None, accumulate=False, dgamma=
 
 
 def gn_bwd2(da1, da2, x, stats, gn1, gn2, groups, dx=None, accumulate=False, dparams1=(None, None),
-            dparams2=(None, None)):
-    """Two GroupNorm+ReLU consumers of x (same statistics): gn_k = (gamma_k, beta_k); one fused backward."""
+            dparams2=(None, None), da2_s2=False):
+    """Two GroupNorm+ReLU consumers of x (same statistics): gn_k = (gamma_k, beta_k); one fused backward.
+    da2_s2: da2 is a stride-2 1^3 conv's data gradient at that conv's output resolution (conv_dgrad_1x1s2_compact)."""
     n, c = x.shape[0], x.shape[-1]
     v = x.numel() // (n * c)
     if dx is None:
         dx = torch.empty_like(x)
         accumulate = False
+    if da2_s2:
+        d, h, w_ = x.shape[1:4]
+        assert tuple(da2.shape) == (n, out_dim(d, 1, 2), out_dim(h, 1, 2), out_dim(w_, 1, 2), c), da2.shape
+        call("u3d_gn_bwd2_s2", dt_code(x.dtype), da1.data_ptr(), da2.data_ptr(), x.data_ptr(), n, c, d, h, w_, groups,
+             stats.data_ptr(), gn1[0].data_ptr(), gn1[1].data_ptr(), gn2[0].data_ptr(), gn2[1].data_ptr(),
+             dx.data_ptr(), int(accumulate), _ptr(dparams1[0]), _ptr(dparams1[1]), _ptr(dparams2[0]),
+             _ptr(dparams2[1]), 0, _gn_ws(n, c, v, x.device).data_ptr(), _stream())
+        return dx
     call("u3d_gn_bwd2", dt_code(x.dtype), da1.data_ptr(), da2.data_ptr(), x.data_ptr(), n, c, v, groups,
          stats.data_ptr(), gn1[0].data_ptr(), gn1[1].data_ptr(), gn2[0].data_ptr(), gn2[1].data_ptr(), dx.data_ptr(),
          int(accumulate), _ptr(dparams1[0]), _ptr(dparams1[1]), _ptr(dparams2[0]), _ptr(dparams2[1]), 0,

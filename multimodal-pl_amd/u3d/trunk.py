@@ -54,7 +54,7 @@ class Act:
         self.t = t
         self.stats = {}
         self.grad = None
-        self.gn_pend = None  # the parked (dA, gn, key) of a block's downsample GN until gn1's backward fuses both
+        self.gn_pend = None  # the parked (dA, gn, key, compact) of a block's downsample GN until gn1's backward fuses both
 
 
 class Tape:
@@ -230,8 +230,8 @@ class Tape:
                 dy = out.grad
                 if dy is None:
                     if pair == "finish" and x.gn_pend:  # the parked partner still owes its GN backward
-                        dA2, gn2, key2 = x.gn_pend.pop()
-                        self.gn_bwd_one(x, dA2, gn2, key2, G)
+                        dA2, gn2, key2, s2c = x.gn_pend.pop()
+                        self.gn_bwd_one(x, ops.expand_s2(dA2, x.t.shape[:4]) if s2c else dA2, gn2, key2, G)
                     return
                 if head:  # dA, bf16 dy and the bias gradient in one pass over the fp32 dlogits
                     db = self.grad_out(key + ".bias", b) if bias else None
@@ -259,18 +259,23 @@ class Tape:
                     self.grad_done(gn_key + ".weight")
                     self.grad_done(gn_key + ".bias")
                     return
-                if not head:
+                s2c = (gn is not None and pair == "park" and k == 1 and stride == 2 and ops.S2_COMPACT
+                       and ops._use_conv1x1(dyT.dtype, dyT.shape[-1], cin, 1, dyT.shape[0]))
+                if s2c:  # kept at the conv's output resolution: the paired GN backward reads it in place
+                    dA = ops.conv_dgrad_1x1s2_compact(dyT, pd, cin)
+                elif not head:
                     dA = ops.conv_dgrad(dyT, pd, cin, x.t.shape[:4], k, stride)
                 if gn is not None and pair == "park":
-                    x.gn_pend = [(dA, gn, gn_key)]  # the block's gn1 backward (runs next) finishes the pair
+                    x.gn_pend = [(dA, gn, gn_key, s2c)]  # the block's gn1 backward (runs next) finishes the pair
                 elif gn is not None and pair == "finish" and x.gn_pend:
-                    dA2, gn2, key2 = x.gn_pend.pop()
+                    dA2, gn2, key2, s2c2 = x.gn_pend.pop()
                     dps = []
                     for key_, g_ in ((gn_key, gn), (key2, gn2)):
                         dps.append((self.grad_out(key_ + ".weight", g_[1]), self.grad_out(key_ + ".bias", g_[2])))
                     self.before_write(x.grad)
                     x.grad = ops.gn_bwd2(dA, dA2, x.t, gn[0], (gn[1], gn[2]), (gn2[1], gn2[2]), G, dx=x.grad,
-                                         accumulate=x.grad is not None, dparams1=dps[0], dparams2=dps[1])
+                                         accumulate=x.grad is not None, dparams1=dps[0], dparams2=dps[1],
+                                         da2_s2=s2c2)
                     for key_ in (gn_key, key2):
                         self.grad_done(key_ + ".weight")
                         self.grad_done(key_ + ".bias")

@@ -90,3 +90,32 @@ def test_conv1x1_bench_shapes(gpu):
                 ref = torch.einsum("hwc,oc->hwo", a[::s, ::s], wq)
                 err = (y[n, pd_].double().cpu() - ref).abs().max().item()
                 assert err < 1e-2 * ref.abs().max().item(), (cx, cy, n, pd_, err)
+
+
+@pytest.mark.parametrize("n,c,dims", [(2, 32, (12, 10, 16)), (2, 64, (8, 8, 8)), (3, 128, (5, 7, 9)), (1, 256, (4, 6, 3))])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_gn_bwd2_compact_stride2_da2(gpu, n, c, dims, dt):
+    """gn_bwd2 with the downsample branch's data gradient kept at the stride-2 conv's output resolution equals
+    gn_bwd2 on the zero-filled full-resolution tensor, bitwise (same arithmetic on the same values), including dx
+    accumulation and the GN parameter gradients."""
+    from u3d import ops
+    torch.manual_seed(c)
+    x = (torch.randn((n,) + dims + (c,), device=gpu) * 1.3 + 0.2).to(dt)
+    da1 = torch.randn_like(x)
+    od = tuple(ops.out_dim(d, 1, 2) for d in dims)
+    da2c = torch.randn((n,) + od + (c,), device=gpu).to(dt)
+    st = ops.gn_stats(x, 16)
+    g1 = (1 + 0.1 * torch.randn(c, device=gpu), 0.1 * torch.randn(c, device=gpu))
+    g2 = (1 + 0.1 * torch.randn(c, device=gpu), 0.1 * torch.randn(c, device=gpu))
+    base = torch.randn_like(x)
+    outs = []
+    for compact in (True, False):
+        dx = base.clone()
+        dps = [(torch.zeros(c, device=gpu), torch.zeros(c, device=gpu)) for _ in range(2)]
+        da2 = da2c if compact else ops.expand_s2(da2c, x.shape[:4])
+        ops.gn_bwd2(da1, da2, x, st, g1, g2, 16, dx=dx, accumulate=True, dparams1=dps[0], dparams2=dps[1],
+                    da2_s2=compact)
+        outs.append((dx, dps))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
