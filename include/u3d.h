@@ -111,6 +111,14 @@ int u3d_conv_wgrad(int dtype, const void* dy, const void* x, int n, int cin, int
 int u3d_conv_dgrad_s2(const void* dy, int n, int cout, const void* wpk_dgrad, int cin, int d, int h, int w, void* dx,
                       u3d_stream_t stream);
 
+/* bf16 3^3 stride-2 convolution forward (pad 1) with the GroupNorm+ReLU prologue (gn_stats NULL: none):
+ * x [n][d][h][w][cin] -> y [n][(d-1)/2+1][(h-1)/2+1][(w-1)/2+1][cout], wpk = forward pack [27][cout_p][cin_p].
+ * Halo-brick kernel (2x4x16 output voxels x 32 co per unit, persistent workgroups). Replaces F.conv3d(stride=2,
+ * padding=1) of the encoder's down-sampling convs (reference unet3D.py:27, _make_layer :1666-1686). */
+int u3d_conv_fwd_s2(const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                    const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups, void* y,
+                    u3d_stream_t stream);
+
 /* bf16 1^3 convolution, stride 1 or 2 (pad 0): y [n][od][oh][ow][cy] = W . relu(gn(x)) at the input voxel
  * (s*od, s*oh, s*ow); x [n][d][h][w][cx], W = packed [round_up(cy, 32)][wpitch] bf16 (the forward pack of a 1^3
  * weight, wpitch = round_up(cx, 32); or the data-gradient pack [cin_p][cout_p] of a stride-1 1^3 conv, which makes

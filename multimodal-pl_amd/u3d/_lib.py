@@ -34,6 +34,7 @@ _SIGS = {
     "u3d_sgd_step": [P, I, P, F, F, F, I, I, I, P],
     "u3d_conv_dgrad_s2": [P, I, I, P, I, I, I, I, P, P],
     "u3d_conv1x1": [P, I, I, I, I, I, P, I, I, I, P, P, P, I, P, P],
+    "u3d_conv_fwd_s2": [P, I, I, I, I, I, P, I, P, P, P, I, P, P],
     "u3d_conv_small": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P],
     "u3d_conv32_brick": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],

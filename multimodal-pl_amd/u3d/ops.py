@@ -171,6 +171,14 @@ def wstd_bwd(partials, nsplit, w, wstats, standardize, dw=None, accumulate=False
 USE_CONV1X1 = os.environ.get("U3D_CONV1X1", "1") != "0"
 
 
+# bf16 stride-2 3^3 forward convs: halo-brick kernel (conv_s2.hip) when the output is at least S2_FWD_MIN_W wide.
+# Parity-tested but measured no faster than the implicit GEMM (96^3 -> 48^3: 94.8 vs 96.6 us; 48^3: 68 vs 65;
+# 24^3: 51 vs 51): each 2x4x16-voxel unit stages a 95 KB halo for 7 MFLOP, so the walk is bound by halo traffic
+# (~3.5 TB/s). Off by default (U3D_S2_FWD=1 enables it).
+USE_S2_FWD = os.environ.get("U3D_S2_FWD", "0") != "0"
+S2_FWD_MIN_W = int(os.environ.get("U3D_S2_FWD_MIN_W", "12"))
+
+
 def _use_conv1x1(dtype, cx, cy, k, n):
     return USE_CONV1X1 and k == 1 and dtype == torch.bfloat16 and cx % 8 == 0 and cy % 8 == 0 and max(cx, cy) <= 256 \
         and n <= 65535
@@ -183,6 +191,11 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
     od, oh, ow = out_dim(d, k, stride), out_dim(h, k, stride), out_dim(w_, k, stride)
     y = torch.empty((n, od, oh, ow, cout), dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
     st, ga, be, G = gn if gn is not None else (None, None, None, 0)
+    if (USE_S2_FWD and k == 3 and stride == 2 and x.dtype == torch.bfloat16 and residual is None and bias is None
+            and not out_f32 and cin % 8 == 0 and cout % 8 == 0 and ow >= S2_FWD_MIN_W):
+        call("u3d_conv_fwd_s2", x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be), G,
+             y.data_ptr(), _stream())
+        return y
     if _use_conv1x1(x.dtype, cin, cout, k, n) and residual is None and bias is None and not out_f32:
         call("u3d_conv1x1", x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), wpk.shape[-1], cout, stride, _ptr(st),
              _ptr(ga), _ptr(be), G, y.data_ptr(), _stream())
@@ -211,7 +224,8 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
         call("u3d_convg_brick", 0, x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be),
              G, _ptr(residual), y.data_ptr(), _stream())
         return y
-    if st is not None and x.dtype == torch.bfloat16 and cin >= 64 and x.numel() * 2 <= GN_MATERIALIZE_BYTES:
+    if (st is not None and x.dtype == torch.bfloat16 and cin >= GN_MATERIALIZE_MIN_C
+            and x.numel() * 2 <= GN_MATERIALIZE_BYTES):
         # small deep-layer activation: materialise relu(gn(x)) once so the GEMM K loop has no GN arithmetic
         x = gn_apply(x, st, ga, be, G)
         st = ga = be = None
@@ -535,6 +549,7 @@ def gn_stats(x, groups):
 
 
 GN_MATERIALIZE_BYTES = 32 << 20
+GN_MATERIALIZE_MIN_C = 64
 
 
 def gn_apply(x, stats, gamma, beta, groups):
