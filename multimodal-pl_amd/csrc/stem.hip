@@ -444,6 +444,101 @@ extern "C" int u3d_stem_fwd_stats(const float* x, int n, int d, int h, int w, co
   return check_launch("stem1_fwd_kernel (statistics)");
 }
 
+// bf16 conv1 (cin 1 -> 32, stride 1) on the matrix cores: the 27 taps are the K dimension (padded to 32 = two k16
+// steps). One wave computes 32 consecutive w voxels of one output row: the MFMA is issued transposed (A = the 32 x 32
+// weight matrix [co][tap], loaded once into registers; B = the voxels' tap vectors, gathered from the fp32 input in
+// L1/L2 and rounded to bf16, as torch.autocast rounds conv inputs), so a lane's accumulators are 16 channels of one
+// voxel and every lane stores two 16-B chunks after one v_permlane32_swap per pair. The VALU form above spends
+// 27 x 32 fp32 FMAs per voxel; this one is bound by the 64 B/voxel output stores.
+__global__ __launch_bounds__(256) void stem1_mfma_fwd_kernel(const float* __restrict__ x, const bf16* __restrict__ wpk,
+                                                             bf16* __restrict__ y, int d, int h, int w, int cin_p,
+                                                             long long tiles, int tpr) {
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  // A fragments: weight [tap t][co r] at k = 16 s + 8 hh + e (taps >= 27 are zero)
+  s16x8 wa[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    uint32_t pk[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int t0 = 16 * st + 8 * hh + 2 * e, t1 = t0 + 1;
+      const uint32_t lo = t0 < 27 ? wpk[((long long)t0 * 32 + r) * cin_p] : 0;
+      const uint32_t hi = t1 < 27 ? wpk[((long long)t1 * 32 + r) * cin_p] : 0;
+      pk[e] = lo | (hi << 16);
+    }
+    wa[st] = __builtin_bit_cast(s16x8, (u32x4){pk[0], pk[1], pk[2], pk[3]});
+  }
+  __shared__ __attribute__((aligned(16))) char otile[4][32 * 64];
+  char* const ot = otile[threadIdx.x >> 6];
+  const long long wave0 = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6, nwave = (long long)gridDim.x * 4;
+  // 32-bit index math, one division chain per output row (64-bit divisions per tile cost more than the MFMAs; hoisting
+  // the 16 tap offsets into registers measured slower: 78 vs 59 us)
+  const int rows = (int)(tiles / tpr);
+  for (int row = (int)wave0; row < rows; row += (int)nwave) {
+  for (int x0 = 0; x0 < w; x0 += 32) {
+    const int yy = row % h, nz = row / h, z = nz % d;
+    const float* xb = x + (long long)(nz / d) * d * h * w;
+    const int xv = x0 + r;
+    s16x8 bfr[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int tap = 16 * st + 8 * hh + e;
+        const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
+        const int zd = z + kd - 1, zh = yy + kh - 1, zw = xv + kw - 1;
+        const bool ok = tap < 27 && (unsigned)zd < (unsigned)d && (unsigned)zh < (unsigned)h && (unsigned)zw < (unsigned)w;
+        const float a = xb[ok ? ((long long)zd * h + zh) * w + zw : 0];  // clamped address: straight-line loads
+        v[e] = ok ? a : 0.f;
+      }
+      bfr[st] = __builtin_bit_cast(s16x8, (u32x4){pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                  pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7])});
+    }
+    f32x16 acc = (f32x16){};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[0], bfr[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[1], bfr[1], acc, 0, 0, 0);
+    uint32_t pk[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) pk[q][e] = pack_bf16x2(acc[4 * q + 2 * e], acc[4 * q + 2 * e + 1]);
+#pragma unroll
+    for (int q = 0; q < 4; q += 2)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(pk[q][e], pk[q + 1][e], false, false);
+        pk[q][e] = sw[0];
+        pk[q + 1][e] = sw[1];
+      }
+    // through LDS so that each store instruction writes 1 KB contiguous (the tile is 32 voxels x 64 B)
+#pragma unroll
+    for (int u2 = 0; u2 < 2; ++u2)
+      *reinterpret_cast<u32x4*>(ot + r * 64 + 32 * u2 + 16 * hh) =
+          (u32x4){pk[2 * u2][0], pk[2 * u2][1], pk[2 * u2 + 1][0], pk[2 * u2 + 1][1]};
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const int nv = min(32, w - x0);
+#pragma unroll
+    for (int u2 = 0; u2 < 2; ++u2) {
+      const int q = lane + 64 * u2;  // 16-B chunk of the tile
+      const u32x4 v = *reinterpret_cast<const u32x4*>(ot + q * 16);
+      if ((q >> 2) < nv) *reinterpret_cast<u32x4*>(y + ((long long)row * w + x0) * 32 + q * 8) = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+  }
+}
+
+static bool stem1_mfma_on() {
+  static const bool on = [] {
+    const char* e = getenv("U3D_STEM_MFMA");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
 extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                             int stride, void* y, u3d_stream_t stream) {
   U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "stem_fwd: bad dtype");
@@ -451,6 +546,15 @@ extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, in
   hipStream_t s = (hipStream_t)stream;
   const int od = sdim(d, stride), oh = sdim(h, stride), ow = sdim(w, stride);
   const long long total = (long long)n * od * oh * ow;
+  if (dtype == U3D_BF16 && cin == 1 && stride == 1 && cout == 32 && stem1_mfma_on()) {
+    const int tpr = cdiv(w, 32);
+    const long long tiles = (long long)n * d * h * tpr;
+    U3D_REQUIRE((long long)n * d * h < (1LL << 31), "stem_fwd: too many rows");
+    const unsigned grid = (unsigned)std::min<long long>(8192, ((long long)n * d * h + 3) / 4);
+    hipLaunchKernelGGL(stem1_mfma_fwd_kernel, dim3(grid), dim3(256), 0, s, x, (const bf16*)wpk, (bf16*)y, d, h, w,
+                       round_up(cin, 32), tiles, tpr);
+    return check_launch("stem1_mfma_fwd_kernel");
+  }
   if (cin == 1 && stride == 1 && cout == 32 && w % 4 == 0 && (long long)n * d * h < 2147483647LL && stem1_on()) {
     const long long rows = (long long)n * d * h, items = rows * (w / 4);
     const dim3 grid((unsigned)((items + ST - 1) / ST));

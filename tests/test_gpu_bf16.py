@@ -228,9 +228,10 @@ def test_head_fwd_bwd(gpu, cin, cout, dims):
 
 
 @pytest.mark.parametrize("cin,cout,dims,s", [(1, 32, (8, 10, 12), 1), (2, 24, (8, 6, 10), 2), (1, 8, (5, 7, 9), 1),
-                                             (2, 32, (4, 4, 6), 1)])
+                                             (2, 32, (4, 4, 6), 1), (1, 32, (6, 9, 70), 1), (1, 32, (3, 4, 33), 1)])
 def test_bf16_stem_fwd(gpu, cin, cout, dims, s):
-    """Stem conv (fp32 input, bf16 packed weights, fp32 math, bf16 output) against fp64."""
+    """Stem conv (fp32 input, bf16 packed weights, bf16 output; conv1 1 -> 32 on the MFMA kernel with the input rounded
+    to bf16, the others fp32 VALU math) against fp64 on the fp32 input."""
     from u3d import ops
     torch.manual_seed(3)
     x = torch.randn((2, cin) + dims, device=gpu)
@@ -341,3 +342,22 @@ def test_gn_apply_materialised(gpu, dt, n, c, dims):
     else:
         ref = _act_ref(x, st, ga, be, 16)
         assert (y.double().cpu() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+
+
+def test_bf16_stem_mfma_bench_size(gpu):
+    """conv1 (1 -> 32, 2 x 96^3) on the MFMA stem kernel: sampled output planes (first, middle, last of each sample)
+    against fp64 on the bf16-rounded input (the kernel's operand), 1e-2 of the plane's max |y|."""
+    from u3d import ops
+    torch.manual_seed(5)
+    x = torch.rand((2, 1, 96, 96, 96), device=gpu) * 2 - 1
+    w = torch.randn(32, 1, 3, 3, 3, device=gpu)
+    pf, _, _ = ops.wstd_fwd(w, torch.bfloat16, True, need_dgrad=False)
+    y = ops.stem_fwd(x, pf, 32, 1, torch.bfloat16)
+    wq = pf.float().cpu()[:, :32, :1].permute(1, 2, 0).reshape(32, 1, 3, 3, 3).double()
+    xb = x.to(torch.bfloat16).double().cpu()
+    for n in range(2):
+        for z in (0, 47, 95):
+            lo, hi = max(0, z - 1), min(96, z + 2)
+            ref = F.conv3d(xb[n:n + 1, :, lo:hi], wq, padding=1)[0, :, z - lo].permute(1, 2, 0)
+            err = (y[n, z].double().cpu() - ref).abs().max().item()
+            assert err < 1e-2 * ref.abs().max().item(), (n, z, err)

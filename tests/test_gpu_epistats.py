@@ -52,7 +52,10 @@ def test_stem_epilogue_stats(gpu, n, dims, monkeypatch):
         return
     y, st = ops.stem_fwd_stats(x, pf, 32, 1, torch.bfloat16)
     assert st is not None
-    assert torch.equal(y, ops.stem_fwd(x, pf, 32, 1, torch.bfloat16))
+    # the plain bf16 conv1 runs on the MFMA kernel (bf16-rounded input), the statistics variant on the fp32-input VALU
+    # kernel: same output within bf16 rounding
+    yp = ops.stem_fwd(x, pf, 32, 1, torch.bfloat16)
+    assert (y.float() - yp.float()).abs().max().item() <= 1e-2 * yp.float().abs().max().item()
     _check_stats(st, ops.gn_stats(y, 16))
     _, st2 = ops.stem_fwd_stats(x, pf, 32, 1, torch.bfloat16)
     assert torch.equal(st, st2)

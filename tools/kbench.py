@@ -130,6 +130,13 @@ def _stem(stats, n=2, s=96):
     return t_(fn), 2.0 * n * s ** 3 * 27 * 32
 
 
+def _stem_plain(n=2, s=96):
+    x = torch.rand((n, 1, s, s, s), device=dev)
+    w = torch.randn(32, 1, 3, 3, 3, device=dev)
+    pf, _, _ = ops.wstd_fwd(w, bf, True, need_dgrad=False)
+    return t_(lambda: ops.stem_fwd(x, pf, 32, 1, bf)), 2.0 * n * s ** 3 * 27 * 32
+
+
 CASES_EXTRA = {"fwd_s2_96": lambda: _fwd(2, 32, 64, 96, 3, 2, True, False),
                "fwd_s2_48": lambda: _fwd(2, 64, 128, 48, 3, 2, True, False),
                "fwd_s2_12": lambda: _fwd(2, 256, 256, 12, 3, 2, True, False),
@@ -138,7 +145,8 @@ CASES_EXTRA = {"fwd_s2_96": lambda: _fwd(2, 32, 64, 96, 3, 2, True, False),
                "fwd48_res": lambda: _fwd(2, 64, 64, 48, 3, 1, False, True),
                "fwd24_plain": lambda: _fwd(2, 128, 128, 24, 3, 1, False, False),"up96_stats": lambda: _up(True), "up96_plain_then_stats": lambda: _up(False),
                "up24_stats": lambda: _up(True, 2, 12, 128), "up24_plain_then_stats": lambda: _up(False, 2, 12, 128),
-               "stem96_stats": lambda: _stem(True), "stem96_plain_then_stats": lambda: _stem(False)}
+               "stem96_stats": lambda: _stem(True), "stem96_plain_then_stats": lambda: _stem(False),
+               "stem96": lambda: _stem_plain()}
 CASES.update(CASES_EXTRA)
 
 
