@@ -4,7 +4,7 @@ import csv
 import sys
 
 d = sys.argv[1]
-marker = sys.argv[2] if len(sys.argv) > 2 else "stem1_fwd_kernel"
+marker = sys.argv[2] if len(sys.argv) > 2 else "stem1_"
 rows = sorted(csv.DictReader(open(f"{d}/run_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
 ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], r["Kernel_Name"]) for r in rows]
 starts = [k[0] for k in ks if marker in k[3]]
