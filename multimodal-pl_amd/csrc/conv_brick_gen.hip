@@ -293,12 +293,15 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
   g.gn_groups = gn_groups;
   const int nb = n * g.nbd * g.nbh * g.nbw;
   hipStream_t s = (hipStream_t)stream;
-  // 64-channel co tiles. 32-channel tiles when 64 would leave CUs idle (U3D_CONVG_CO32 = -1) or always (= 1) were
-  // measured slower (24^3 x 128 ch fwd 63.5 -> 78.7 us with 288 instead of 144 workgroups): off by default.
-  static const int env_co32 = [] { const char* e = getenv("U3D_CONVG_CO32"); return e ? atoi(e) : 0; }();
+  // 64-channel co tiles, unless they give fewer than 128 workgroups and 32-channel tiles give at least 128 (the 24^3 x
+  // 64-channel decoder convs: 72 -> 144 workgroups, fwd 49 -> 25 us, dgrad 40 -> 20 us). Not below that: at 24^3 x 128
+  // channels (144 workgroups with 64-channel tiles) 32-channel tiles measured slower (63.5 -> 78.7 us).
+  // U3D_CONVG_CO32 = 0 / 1 forces the choice (experiments).
+  static const int env_co32 = [] { const char* e = getenv("U3D_CONVG_CO32"); return e ? atoi(e) : -1; }();
   bool co64 = g.cout_p >= 64;
   if (co64 && env_co32 == 1) co64 = false;
-  if (co64 && env_co32 < 0 && (long long)nb * cdiv(cout, 64) < 256) co64 = false;
+  if (co64 && env_co32 < 0 && (long long)nb * cdiv(cout, 64) < 128 && (long long)nb * cdiv(cout, 32) >= 128)
+    co64 = false;
   g.nct = cdiv(cout, co64 ? 64 : 32);
   dim3 grid(nb * g.nct);
   if (co64) {

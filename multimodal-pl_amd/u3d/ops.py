@@ -328,7 +328,8 @@ def _use_gen_brick(dtype, cin, cout, k, stride, shape):
     if n > 16:
         return False
     nb = n * -(-d // 4) * -(-h // 8) * -(-w_ // 16)
-    return nb * max(1, -(-cout // 64)) >= BRICK_MIN_WG
+    # workgroups with 64-channel co tiles, or with 32-channel ones (the launcher picks those when 64 give too few)
+    return max(nb * max(1, -(-cout // 64)), nb * max(1, -(-cout // 32))) >= BRICK_MIN_WG
 
 
 def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):

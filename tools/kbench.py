@@ -158,6 +158,16 @@ for (nm, cx, cy, s_, st_) in [("c1_s2_96", 32, 64, 96, 2), ("c1_s2_48", 64, 128,
         CASES["d" + nm] = (lambda cx=cx, cy=cy, s_=s_: _dgrad(2, cx, cy, s_, 1, 1))
 
 
+CASES["dec24_c1"] = lambda: _fwd(2, 128, 64, 24, 3, 1, True, False)
+CASES["dec24_c2"] = lambda: _fwd(2, 64, 64, 24, 3, 1, True, True)
+CASES["ddec24_c1"] = lambda: _dgrad(2, 128, 64, 24, 3, 1)
+CASES["ddec24_c2"] = lambda: _dgrad(2, 64, 64, 24, 3, 1)
+CASES["dec48_c1"] = lambda: _fwd(2, 64, 32, 48, 3, 1, True, False)
+CASES["ddec48_c1"] = lambda: _dgrad(2, 64, 32, 48, 3, 1)
+CASES["dec12_c1"] = lambda: _fwd(2, 256, 128, 12, 3, 1, True, False)
+CASES["dec12_c2"] = lambda: _fwd(2, 128, 128, 12, 3, 1, True, True)
+
+
 def _gn(kind, s, c, n=2, G=16):
     x = torch.randn((n, s, s, s, c), device=dev).to(bf)
     da = torch.randn_like(x)
