@@ -433,8 +433,9 @@ def conv_wgrad(dy, x, k, stride, gn=None, brick=None):
     st, ga, be, G = gn if gn is not None else (None, None, None, 0)
     if brick is None:
         brick = USE_BRICK_WGRAD and x.dtype == torch.bfloat16
-        if brick and k == 3 and stride == 1 and USE_RING_WGRAD and min(h, w_) >= RING_WGRAD_MIN_HW:
-            brick = "ring"
+        if (brick and k == 3 and stride == 1 and USE_RING_WGRAD and min(h, w_) >= RING_WGRAD_MIN_HW
+                and max(x.numel() * x.element_size(), dy.numel() * dy.element_size()) < (1 << 31)):
+            brick = "ring"  # (the ring addresses its operands with 32-bit buffer offsets; larger ones: bricks)
     if brick == "ring":
         assert k == 3 and stride == 1 and x.dtype == torch.bfloat16
         ns = query("u3d_conv_wgrad_ring_splits", n, cin, d, h, w_, cout)

@@ -322,3 +322,28 @@ def test_ring_work_queue_matches_static_schedule(gpu, n, dims):
             assert ((a - b).abs() <= 1e-5 * a.abs() + 1e-7).all()
         else:
             assert torch.equal(a, b)
+
+
+def test_conv32_beyond_2gib_routes_off_the_ring(gpu):
+    """A 32 -> 32 activation larger than 2 GiB (the ring's 32-bit buffer offsets) — e.g. a whole-volume forward —
+    routes to the brick kernel instead of failing: sampled output planes against fp64 (as the bench-size tests), and
+    the weight gradient takes the brick path too. Reference: Conv3d.forward (unet3D.py:27)."""
+    from u3d import ops
+    torch.manual_seed(11)
+    n, d, h, w = 1, 136, 512, 512  # 2.28 GB of bf16 at 32 channels
+    x = (torch.randn((n, d, h, w, 32), device=gpu, dtype=torch.bfloat16) * 0.8 + 0.1)
+    assert x.numel() * 2 >= (1 << 31)
+    wt = torch.randn(32, 32, 3, 3, 3, device=gpu)
+    pf, pd, _ = ops.wstd_fwd(wt, torch.bfloat16, True)
+    y = ops.conv_fwd(x, pf, 32, 3, 1)
+    wq = pf.float().cpu()[:, :32, :32].permute(1, 2, 0).reshape(32, 32, 3, 3, 3).double()
+    for z in (0, d // 2, d - 1):
+        lo, hi = max(0, z - 1), min(d, z + 2)
+        xs = x[0, lo:hi, :64, :64].double().cpu().permute(3, 0, 1, 2)[None]
+        ref = F.conv3d(xs, wq, padding=1)[0, :, z - lo].permute(1, 2, 0)[:63, :63]
+        got = y[0, z, :63, :63].double().cpu()
+        assert (got - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    del y
+    dy = torch.randn_like(x)
+    part, ns = ops.conv_wgrad(dy[:, :, :, :, :32], x, 3, 1)
+    assert part.shape[1:] == (27, 32, 32) and torch.isfinite(part).all()
