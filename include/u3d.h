@@ -233,8 +233,8 @@ int u3d_conv_wgrad1(const void* dy, const void* x, int n, int cin, int d, int h,
                     float* partials, int nsplit, u3d_stream_t stream);
 
 /* Stem conv with cin <= 4 (conv1 1->32, unet3D.py:1632; conv0 2->f stride 2, :1514): fp32 NCDHW input, NDHWC
- * output. bf16 conv1 (cin 1 -> 32, stride 1): MFMA with the 27 taps as K (input rounded to bf16, as autocast does;
- * U3D_STEM_MFMA=0 selects the fp32-input VALU kernel); otherwise a direct VALU conv. */
+ * output, direct VALU conv with fp32 input. U3D_STEM_MFMA=1: bf16 conv1 (cin 1 -> 32, stride 1) on MFMA with the 27
+ * taps as K (input rounded to bf16, as autocast does; faster alone, step-neutral). */
 /* bf16 stem conv (cin 1 -> 32, 3^3, stride 1, w % 4 == 0) that also returns the GroupNorm(16) statistics (mean,
  * rstd) [n][16][2] of its stored output (layer0's gn1, unet3D.py:56-73) from the epilogue (fp64 across blocks,
  * fixed order). ws = u3d_stem_fwd_stats_ws_bytes(n, d, h, w) bytes, zero on first use (left reusable). */

@@ -531,10 +531,12 @@ __global__ __launch_bounds__(256) void stem1_mfma_fwd_kernel(const float* __rest
   }
 }
 
+// Off by default: 83 -> 59 us per launch in isolation but step-neutral (same-box A/B 6.961 vs 6.957 ms: in the step the
+// stem is bound by its 113 MB of output stores), and the VALU kernel keeps the fp32 input. U3D_STEM_MFMA=1 enables it.
 static bool stem1_mfma_on() {
   static const bool on = [] {
     const char* e = getenv("U3D_STEM_MFMA");
-    return !e || atoi(e) != 0;
+    return e && atoi(e) != 0;
   }();
   return on;
 }

@@ -344,9 +344,10 @@ def test_gn_apply_materialised(gpu, dt, n, c, dims):
         assert (y.double().cpu() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
 
 
-def test_bf16_stem_mfma_bench_size(gpu):
-    """conv1 (1 -> 32, 2 x 96^3) on the MFMA stem kernel: sampled output planes (first, middle, last of each sample)
-    against fp64 on the bf16-rounded input (the kernel's operand), 1e-2 of the plane's max |y|."""
+def test_bf16_stem_bench_size(gpu):
+    """conv1 (1 -> 32, 2 x 96^3) as the bench runs it: sampled output planes (first, middle, last of each sample)
+    against fp64 on the bf16-rounded input, 1e-2 of the plane's max |y| (covers both stem kernels: the MFMA one
+    rounds its input to bf16, the VALU one keeps fp32; tools/r02al.sh runs this with U3D_STEM_MFMA=1)."""
     from u3d import ops
     torch.manual_seed(5)
     x = torch.rand((2, 1, 96, 96, 96), device=gpu) * 2 - 1

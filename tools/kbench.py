@@ -158,6 +158,17 @@ for (nm, cx, cy, s_, st_) in [("c1_s2_96", 32, 64, 96, 2), ("c1_s2_48", 64, 128,
         CASES["d" + nm] = (lambda cx=cx, cy=cy, s_=s_: _dgrad(2, cx, cy, s_, 1, 1))
 
 
+def _upp(bwd, n=2, s=48, c=32):
+    x = torch.randn((n, s, s, s, c), device=dev).to(bf)
+    sk = torch.randn((n, 2 * s, 2 * s, 2 * s, c), device=dev).to(bf)
+    fn = (lambda: ops.upsample2x_bwd(sk, tuple(x.shape))) if bwd else (lambda: ops.upsample2x_add(x, sk))
+    return t_(fn), 0.0
+
+
+CASES["upf96"] = lambda: _upp(False)
+CASES["upf48"] = lambda: _upp(False, 2, 24, 64)
+CASES["upb96"] = lambda: _upp(True)
+CASES["upb48"] = lambda: _upp(True, 2, 24, 64)
 CASES["dec24_c1"] = lambda: _fwd(2, 128, 64, 24, 3, 1, True, False)
 CASES["dec24_c2"] = lambda: _fwd(2, 64, 64, 24, 3, 1, True, True)
 CASES["ddec24_c1"] = lambda: _dgrad(2, 128, 64, 24, 3, 1)

@@ -8,4 +8,5 @@ for cfg in "U3D_STEM_MFMA=0" "U3D_STEM_MFMA=1"; do
   echo "== $cfg" | tee -a $O/k.txt
   env $cfg timeout -k 10 100 python tools/kbench.py stem96 2>&1 | grep -v amdgpu.ids | tee -a $O/k.txt || exit 1
 done
+U3D_STEM_MFMA=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_bf16.py -k stem > $O/pytest_mfma.log 2>&1 || exit 1
 bash tools/ab.sh r02al "U3D_STEM_MFMA=0" "U3D_STEM_MFMA=1" 4
