@@ -276,9 +276,265 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
     }
 }
 
+// Persistent form of the same brick schedule (round 2): grid = one workgroup per CU (balanced), each walks a
+// contiguous run of (brick, co tile) units and treats the concatenated (unit, chunk, tap plane) steps as ONE
+// pipeline — the next unit's first halo chunk, its GroupNorm coefficients and its first weight plane are loaded
+// during the last tap plane of the current unit, so a unit costs no cold prologue (the one-shot kernel exposes a
+// full HBM round trip + the halo/weight staging per workgroup, ~1/3 of its time at 48^3). The MFMA is issued
+// transposed (A = weights, B = halo rows): a lane's accumulators are 16 output channels of one voxel, so the
+// epilogue is register-only (permlane32 swap, residual add, two 16-B stores per lane and co block) and never
+// touches the LDS the next unit's halo is being written into. Same operands, same fp32 accumulation order per
+// output (chunk, tap plane, tap, k-half) as convg_brick_kernel: bitwise-equal results.
+template <int CO, bool FLIP>
+__global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
+                                                               bf16* __restrict__ y, const bf16* __restrict__ res,
+                                                               const float* __restrict__ gstat,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, GBGeom g, int per,
+                                                               int nunits) {
+  constexpr int TN = CO / 32;
+  constexpr int WROWS = 9 * CO;
+  constexpr int WLD = (WROWS * 4 + GB_NT - 1) / GB_NT;
+  __shared__ __attribute__((aligned(16))) char hal[4 * GB_PS];
+  __shared__ __attribute__((aligned(16))) char wbuf[2][4 * WROWS * 16];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  int bid;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int u_begin = bid * per, u_end = min(nunits, u_begin + per);
+  const int nct = g.nct;
+  const bool has_gn = gstat != nullptr;
+  const int nchunk = g.cin_p / 32;
+  const int nsteps = nchunk * 3;
+
+  struct Unit {
+    int nn, d0, h0, w0, co0;
+  };
+  auto unit_geo = [&](int u) {
+    Unit q;
+    int b = u / nct;
+    q.co0 = (u - b * nct) * CO;
+    const int bw_ = b % g.nbw; b /= g.nbw;
+    const int bh_ = b % g.nbh; b /= g.nbh;
+    const int bd_ = b % g.nbd;
+    q.nn = b / g.nbd;
+    q.d0 = bd_ * GB_BD; q.h0 = bh_ * GB_BH; q.w0 = bw_ * GB_BW;
+    return q;
+  };
+
+  u32x4 hpre[GB_HLD];
+  unsigned hmask = 0;  // bit i: staged piece i is inside the volume (GroupNorm'd; padding stays zero)
+  u32x4 wpre[WLD];
+  const int sch = tid & 3, srow0 = tid >> 2;
+  f32x2 sc[4], sh[4];
+  auto halo_load = [&](const Unit& q, int c) {
+    hmask = 0;
+#pragma unroll
+    for (int i = 0; i < GB_HLD; ++i) {
+      const int row = srow0 + i * (GB_NT / 4);
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (row < GB_NH) {
+        const int hw = row % GB_HW, hr = (row / GB_HW) % GB_HH, hd = row / (GB_HW * GB_HH);
+        const int zd = q.d0 - 1 + hd, zh = q.h0 - 1 + hr, zw = q.w0 - 1 + hw;
+        const int cc = c * 32 + sch * 8;
+        if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w) {
+          hmask |= 1u << i;
+          if (cc < g.cin)
+            v = *reinterpret_cast<const u32x4*>(x + ((((long long)q.nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc);
+        }
+      }
+      hpre[i] = v;
+    }
+    if (has_gn) gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, q.nn, c * 32 + sch * 8, sc, sh);
+  };
+  auto halo_commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < GB_HLD; ++i) {
+      const int row = srow0 + i * (GB_NT / 4);
+      if (row < GB_NH) {
+        u32x4 v = hpre[i];
+        if (has_gn && ((hmask >> i) & 1u)) v = gn_relu8(v, sc, sh);
+        *reinterpret_cast<u32x4*>(hal + sch * GB_PS + row * 16) = v;
+      }
+    }
+  };
+  auto w_load = [&](int co0, int s) {
+    const int c = s / 3, td = s % 3;
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) {
+      const int ci = tid + i * GB_NT;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (ci < WROWS * 4) {
+        const int ch = ci / WROWS, row = ci % WROWS;
+        const int j = row / CO, co = co0 + row % CO;
+        const int t = td * 9 + j;
+        if (co < g.cout_p)
+          v = *reinterpret_cast<const u32x4*>(wpk + ((long long)t * g.cout_p + co) * g.cin_p + c * 32 + ch * 8);
+      }
+      wpre[i] = v;
+    }
+  };
+  auto w_commit = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) {
+      const int ci = tid + i * GB_NT;
+      if (ci < WROWS * 4) {
+        const int ch = ci / WROWS, row = ci % WROWS;
+        *reinterpret_cast<u32x4*>(wbuf[buf] + (ch * WROWS + row) * 16) = wpre[i];
+      }
+    }
+  };
+
+  // per-lane A row of tap (0,0,0) for row tile tm (rt = 2*wave + tm -> (d = rt >> 2, h-pair = rt & 3)) and the
+  // output voxel of MFMA column r
+  int arow[2];
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+    const int rt = 2 * wave + tm, vd = rt >> 2, vh = 2 * (rt & 3) + gb_seg(r);
+    arow[tm] = (vd * GB_HH + vh) * GB_HW + gb_pos(r);
+  }
+
+  Unit cu = unit_geo(u_begin);
+  halo_load(cu, 0);
+  w_load(cu.co0, 0);
+  halo_commit();
+  w_commit(0);
+  __syncthreads();
+  int par = 0;
+
+  for (int u = u_begin; u < u_end; ++u) {
+    const bool more = u + 1 < u_end;
+    const Unit nu = more ? unit_geo(u + 1) : cu;
+    f32x16 acc[2][TN];
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.f;
+    for (int s = 0; s < nsteps; ++s) {
+      const int td = s % 3;
+      const bool last = s + 1 == nsteps;
+      const bool next = !last || more;
+      if (next) {  // one call site each (the next step is (u, s + 1) or (u + 1, 0))
+        const Unit& lq = last ? nu : cu;
+        w_load(lq.co0, last ? 0 : s + 1);
+        if (td == 2) halo_load(lq, last ? 0 : s / 3 + 1);
+      }
+      const char* wb = wbuf[par];
+      const int od = FLIP ? 2 - td : td;
+#pragma unroll 3
+      for (int j = 0; j < 9; ++j) {
+        const int th = j / 3, tw = j % 3;
+        const int oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
+        const int toff = (od * GB_HH + oh) * GB_HW + ow;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int plane = 2 * k + hh;
+          bf16x8 a[2], bb[TN];
+#pragma unroll
+          for (int tm = 0; tm < 2; ++tm)
+            a[tm] = *reinterpret_cast<const bf16x8*>(hal + plane * GB_PS + (arow[tm] + toff) * 16);
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            bb[tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
+#pragma unroll
+          for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+              acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb[tn], a[tm], acc[tm][tn], 0, 0, 0);
+        }
+      }
+      if (next) {
+        w_commit(par ^ 1);  // the other buffer: its readers finished before the previous barrier
+        if (td == 2) {
+          __syncthreads();  // everyone done with this chunk's halo
+          halo_commit();
+        }
+      }
+      __syncthreads();
+      par ^= 1;
+    }
+
+    // epilogue from registers: lane (r, hh) holds channels tn*32 + 8q + 4hh + e (acc[tm][tn][4q + e]) of voxel
+    // ovox[tm]; after the swap it holds channels tn*32 + 8hh .. +7 and tn*32 + 16 + 8hh .. +7
+    // this lane's output voxels (MFMA column r of row tiles 0, 1)
+    long long ovox[2];
+    bool ook[2];
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+      const int rt = 2 * wave + tm;
+      const int zd = cu.d0 + (rt >> 2), zh = cu.h0 + 2 * (rt & 3) + gb_seg(r), zw = cu.w0 + gb_pos(r);
+      ook[tm] = zd < g.d && zh < g.h && zw < g.w;
+      ovox[tm] = (((long long)cu.nn * g.d + zd) * g.h + zh) * g.w + zw;
+    }
+    u32x4 rv[2][TN][2];
+    if (res) {
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+          for (int v = 0; v < 2; ++v) {
+            const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
+            rv[tm][tn][v] = (ook[tm] && co < g.cout) ? *reinterpret_cast<const u32x4*>(res + ovox[tm] * g.cout + co)
+                                                     : u32x4{0u, 0u, 0u, 0u};
+          }
+    }
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        uint32_t pk[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            pk[q][e] = pack_bf16x2(acc[tm][tn][4 * q + 2 * e], acc[tm][tn][4 * q + 2 * e + 1]);
+#pragma unroll
+        for (int q = 0; q < 4; q += 2)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(pk[q][e], pk[q + 1][e], false, false);
+            pk[q][e] = sw[0];
+            pk[q + 1][e] = sw[1];
+          }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
+          u32x4 o = {pk[2 * v][0], pk[2 * v][1], pk[2 * v + 1][0], pk[2 * v + 1][1]};
+          if (res) {
+            float a8[8], c8[8];
+            load16<bf16>(reinterpret_cast<const bf16*>(&o), a8);
+            load16<bf16>(reinterpret_cast<const bf16*>(&rv[tm][tn][v]), c8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a8[e] += c8[e];
+            store16<bf16>(reinterpret_cast<bf16*>(&o), a8);
+          }
+          if (ook[tm] && co < g.cout) *reinterpret_cast<u32x4*>(y + ovox[tm] * g.cout + co) = o;
+        }
+      }
+    cu = nu;
+  }
+}
+
 }  // namespace u3d
 
 using namespace u3d;
+
+static int convg_num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
 
 extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                                const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
@@ -304,6 +560,21 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
     co64 = false;
   g.nct = cdiv(cout, co64 ? 64 : 32);
   dim3 grid(nb * g.nct);
+  // persistent form (U3D_CONVG_PERSIST=0: the one-shot kernel; read per call so a test can compare both in-process)
+  const char* env_pers = getenv("U3D_CONVG_PERSIST");
+  if (!env_pers || atoi(env_pers) != 0) {
+    const int nunits = nb * g.nct, per = cdiv(nunits, convg_num_cus()), nwg = cdiv(nunits, per);
+#define U3D_PB(C, F)                                                                                              \
+  hipLaunchKernelGGL((convg_pbrick_kernel<C, F>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x, (const bf16*)wpk, \
+                     (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g, per, nunits)
+    if (co64) {
+      if (flip) U3D_PB(64, true); else U3D_PB(64, false);
+    } else {
+      if (flip) U3D_PB(32, true); else U3D_PB(32, false);
+    }
+#undef U3D_PB
+    return check_launch("convg_pbrick_kernel");
+  }
   if (co64) {
     if (flip)
       hipLaunchKernelGGL((convg_brick_kernel<64, true>), grid, dim3(GB_NT), 0, s, (const bf16*)x, (const bf16*)wpk,

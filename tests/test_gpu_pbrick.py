@@ -1,0 +1,60 @@
+"""Persistent generic brick conv (convg_pbrick_kernel, the default behind u3d_convg_brick) against the one-shot
+brick kernel (U3D_CONVG_PERSIST=0, the round-1 schedule, itself checked against fp64 in test_gpu_bf16.py and
+test_gpu_fullsize.py). Same operands, same per-output fp32 accumulation order: the results must be bitwise equal.
+Cases cover several units per workgroup (48^3-class grids), one unit per workgroup (24^3 x 128), 32-channel co
+tiles (the launcher's choice at 24^3 x 64), partial co tiles (cout 96), ragged volumes, GN prologue, residual, and
+the data gradient (flip). Reference: F.conv3d in Conv3d.forward (unet3D.py:27) through NoBottleneck (:56-73)."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # n, cin, cout, (d, h, w), gn, res, flip
+    (2, 64, 64, (48, 48, 48), True, True, False),
+    (2, 64, 64, (48, 48, 48), False, False, True),
+    (2, 128, 128, (24, 24, 24), True, True, False),
+    (2, 128, 128, (24, 24, 24), False, False, True),
+    (2, 64, 64, (24, 24, 24), True, False, False),
+    (1, 64, 96, (13, 17, 35), True, True, False),
+    (3, 96, 64, (9, 20, 19), False, True, True),
+    (1, 40, 48, (10, 30, 33), True, False, False),
+]
+
+
+def _run(gpu, n, cin, cout, dims, gn, res, flip, persist):
+    from u3d import _lib
+    torch.manual_seed(7)
+    x = (torch.randn((n,) + dims + (cin,), device=gpu) * 1.3 + 0.2).to(torch.bfloat16)
+    cin_p, cout_p = -(-cin // 32) * 32, -(-cout // 32) * 32
+    # packed weights [27][cout_p][cin_p] (forward) / [27][cin_p][cout_p]: random bf16, zero padding
+    wpk = torch.zeros((27, cout_p, cin_p), device=gpu, dtype=torch.bfloat16)
+    wpk[:, :cout, :cin] = (torch.randn((27, cout, cin), device=gpu) * 0.05).to(torch.bfloat16)
+    G = 16 if cin % 16 == 0 else 8
+    st = torch.stack([torch.randn(n, G, device=gpu) * 0.1, 0.5 + torch.rand(n, G, device=gpu)], -1).contiguous()
+    ga = 1 + 0.1 * torch.randn(cin, device=gpu)
+    be = 0.1 * torch.randn(cin, device=gpu)
+    r = torch.randn((n,) + dims + (cout,), device=gpu).to(torch.bfloat16) if res else None
+    y = torch.full((n,) + dims + (cout,), 7.0, device=gpu, dtype=torch.bfloat16)
+    os.environ["U3D_CONVG_PERSIST"] = "1" if persist else "0"
+    try:
+        p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        rc = _lib.lib().u3d_convg_brick(int(flip), p(x), n, cin, *dims, p(wpk), cout, p(st) if gn else None,
+                                        p(ga) if gn else None, p(be) if gn else None, G if gn else 0, p(r), p(y),
+                                        torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, _lib.lib().u3d_last_error()
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("U3D_CONVG_PERSIST", None)
+    return y
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"n{c[0]}_{c[1]}to{c[2]}_{'x'.join(map(str, c[3]))}"
+                         f"{'_gn' if c[4] else ''}{'_res' if c[5] else ''}{'_flip' if c[6] else ''}")
+def test_persistent_brick_bitwise_equal_one_shot(gpu, case):
+    a = _run(gpu, *case, persist=True)
+    b = _run(gpu, *case, persist=False)
+    assert torch.isfinite(a.float()).all()
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16)), \
+        f"max diff {(a.float() - b.float()).abs().max().item()}"
