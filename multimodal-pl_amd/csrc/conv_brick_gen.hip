@@ -25,6 +25,7 @@ constexpr int GB_NT = 512;
 constexpr int GB_HLD = (GB_NH + GB_NT / 4 - 1) / (GB_NT / 4);  // 9 halo loads per thread
 constexpr int GB_PS = GB_NH * 16 + 64;  // LDS plane stride (+64 B: conflict-free staging writes)
 constexpr int GB_MAXN = 16;
+constexpr int GB_MAXC = 256;  // persistent kernel with a GN prologue: cin_p <= GB_MAXC
 
 struct GBGeom {
   int n, d, h, w;
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
 // epilogue is register-only (permlane32 swap, residual add, two 16-B stores per lane and co block) and never
 // touches the LDS the next unit's halo is being written into. Same operands, same fp32 accumulation order per
 // output (chunk, tap plane, tap, k-half) as convg_brick_kernel: bitwise-equal results.
-template <int CO, bool FLIP>
+template <int CO, bool FLIP, int abl = 0>
 __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                                bf16* __restrict__ y, const bf16* __restrict__ res,
                                                                const float* __restrict__ gstat,
@@ -297,6 +298,9 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   constexpr int WLD = (WROWS * 4 + GB_NT - 1) / GB_NT;
   __shared__ __attribute__((aligned(16))) char hal[4 * GB_PS];
   __shared__ __attribute__((aligned(16))) char wbuf[2][4 * WROWS * 16];
+  // GroupNorm (scale, shift) per input channel of the samples in flight, slot = sample & 1: filled once per sample
+  // (the staging reads it from LDS — no global loads whose wait would drain the halo/weight prefetch)
+  __shared__ __attribute__((aligned(16))) f32x2 gtab[2][GB_MAXC];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -330,9 +334,20 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   unsigned hmask = 0;  // bit i: staged piece i is inside the volume (GroupNorm'd; padding stays zero)
   u32x4 wpre[WLD];
   const int sch = tid & 3, srow0 = tid >> 2;
-  f32x2 sc[4], sh[4];
+  int stg_nn = 0, stg_c = 0;  // sample and chunk of the staged halo (GN table lookup at commit)
+  auto gtab_fill = [&](int nn) {
+    if (has_gn && tid < g.cin_p) {
+      const int c = min(tid, g.cin - 1), gg = c / (g.cin / g.gn_groups);
+      const float mean = gstat[(nn * g.gn_groups + gg) * 2], rstd = gstat[(nn * g.gn_groups + gg) * 2 + 1];
+      const float sc_ = rstd * gamma[c];
+      gtab[nn & 1][tid] = f32x2{sc_, beta[c] - mean * sc_};
+    }
+  };
   auto halo_load = [&](const Unit& q, int c) {
     hmask = 0;
+    stg_nn = q.nn;
+    stg_c = c;
+    if constexpr ((abl & 4) != 0) return;
 #pragma unroll
     for (int i = 0; i < GB_HLD; ++i) {
       const int row = srow0 + i * (GB_NT / 4);
@@ -349,9 +364,19 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       }
       hpre[i] = v;
     }
-    if (has_gn) gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, q.nn, c * 32 + sch * 8, sc, sh);
   };
   auto halo_commit = [&]() {
+    if constexpr ((abl & 8) != 0) return;
+    f32x2 sc[4], sh[4];
+    if (has_gn) {
+      const f32x2* t = &gtab[stg_nn & 1][stg_c * 32 + sch * 8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f32x2 a0 = t[2 * e], a1 = t[2 * e + 1];
+        sc[e] = f32x2{a0[0], a1[0]};
+        sh[e] = f32x2{a0[1], a1[1]};
+      }
+    }
 #pragma unroll
     for (int i = 0; i < GB_HLD; ++i) {
       const int row = srow0 + i * (GB_NT / 4);
@@ -363,6 +388,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     }
   };
   auto w_load = [&](int co0, int s) {
+    if constexpr ((abl & 2) != 0) return;
     const int c = s / 3, td = s % 3;
 #pragma unroll
     for (int i = 0; i < WLD; ++i) {
@@ -379,6 +405,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     }
   };
   auto w_commit = [&](int buf) {
+    if constexpr ((abl & 8) != 0) return;
 #pragma unroll
     for (int i = 0; i < WLD; ++i) {
       const int ci = tid + i * GB_NT;
@@ -399,6 +426,8 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   }
 
   Unit cu = unit_geo(u_begin);
+  gtab_fill(cu.nn);
+  __syncthreads();
   halo_load(cu, 0);
   w_load(cu.co0, 0);
   halo_commit();
@@ -409,6 +438,9 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   for (int u = u_begin; u < u_end; ++u) {
     const bool more = u + 1 < u_end;
     const Unit nu = more ? unit_geo(u + 1) : cu;
+    // the next unit's sample table: its slot was last read before this unit's first barrier, and is first read at
+    // the commit in this unit's last step (>= 1 barrier later)
+    if (more && nu.nn != cu.nn) gtab_fill(nu.nn);
     f32x16 acc[2][TN];
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm)
@@ -436,17 +468,31 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
         for (int k = 0; k < 2; ++k) {
           const int plane = 2 * k + hh;
           bf16x8 a[2], bb[TN];
+          if constexpr (!(abl & 16)) {
 #pragma unroll
-          for (int tm = 0; tm < 2; ++tm)
-            a[tm] = *reinterpret_cast<const bf16x8*>(hal + plane * GB_PS + (arow[tm] + toff) * 16);
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn)
-            bb[tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
-#pragma unroll
-          for (int tm = 0; tm < 2; ++tm)
+            for (int tm = 0; tm < 2; ++tm)
+              a[tm] = *reinterpret_cast<const bf16x8*>(hal + plane * GB_PS + (arow[tm] + toff) * 16);
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
-              acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb[tn], a[tm], acc[tm][tn], 0, 0, 0);
+              bb[tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
+          } else {
+#pragma unroll
+            for (int tm = 0; tm < 2; ++tm) a[tm] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)(j + k), 1u, 2u, 3u});
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) bb[tn] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)tn, 1u, 2u, 3u});
+          }
+          if constexpr (!(abl & 1)) {
+#pragma unroll
+            for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+              for (int tn = 0; tn < TN; ++tn)
+                acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb[tn], a[tm], acc[tm][tn], 0, 0, 0);
+          } else {
+#pragma unroll
+            for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+              for (int tn = 0; tn < TN; ++tn) acc[tm][tn][0] += (float)a[tm][0] * 0.f + 0.f * (float)bb[tn][1];
+          }
         }
       }
       if (next) {
@@ -562,11 +608,31 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
   dim3 grid(nb * g.nct);
   // persistent form (U3D_CONVG_PERSIST=0: the one-shot kernel; read per call so a test can compare both in-process)
   const char* env_pers = getenv("U3D_CONVG_PERSIST");
-  if (!env_pers || atoi(env_pers) != 0) {
+  if ((!env_pers || atoi(env_pers) != 0) && (!gn_stats || g.cin_p <= GB_MAXC)) {
+    const char* env_abl = getenv("U3D_PB_ABL");  // timing ablations (wrong results): see convg_pbrick_kernel
+    const int abl = env_abl ? atoi(env_abl) : 0;
     const int nunits = nb * g.nct, per = cdiv(nunits, convg_num_cus()), nwg = cdiv(nunits, per);
 #define U3D_PB(C, F)                                                                                              \
   hipLaunchKernelGGL((convg_pbrick_kernel<C, F>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x, (const bf16*)wpk, \
                      (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g, per, nunits)
+#define U3D_PBA(A)                                                                                                \
+  hipLaunchKernelGGL((convg_pbrick_kernel<64, false, A>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,           \
+                     (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g, per, nunits)
+    if (abl && co64 && !flip) {
+      switch (abl) {
+        case 1: U3D_PBA(1); break;
+        case 2: U3D_PBA(2); break;
+        case 4: U3D_PBA(4); break;
+        case 6: U3D_PBA(6); break;
+        case 14: U3D_PBA(14); break;
+        case 16: U3D_PBA(16); break;
+        case 17: U3D_PBA(17); break;
+        case 31: U3D_PBA(31); break;
+        default: return fail(U3D_EINVAL, "U3D_PB_ABL: unknown ablation %d", abl);
+      }
+      return check_launch("convg_pbrick_kernel");
+    }
+#undef U3D_PBA
     if (co64) {
       if (flip) U3D_PB(64, true); else U3D_PB(64, false);
     } else {
