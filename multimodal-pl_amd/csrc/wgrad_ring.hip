@@ -42,18 +42,27 @@ __device__ __forceinline__ void sfor(F&& f) {
   }
 }
 
-constexpr int WR_PH = 16, WR_PW = 16, WR_HH = WR_PH + 2, WR_HW = WR_PW + 2;
-constexpr int WR_NR = WR_HH * WR_HW;  // 324 halo rows per input plane
-constexpr int WR_NV = WR_PH * WR_PW;  // 256 voxels per output plane = 16 k16 steps
 constexpr int WR_ROWB = 64;
-constexpr int WR_SLOT = WR_NR * WR_ROWB;
-constexpr int WR_DSLOT = WR_NV * WR_ROWB;
 constexpr int WR_NT = 512;
-constexpr int WR_LX = (WR_NR * 4 + WR_NT - 1) / WR_NT;  // 3 input pieces per thread and plane
-constexpr int WR_LY = WR_NV * 4 / WR_NT;                // 2 dy pieces
+// plane tile PH x PW (16 x 16; 12 x 24 for 24-wide planes and 12 x 12 for 12-wide ones, so that no k step is
+// spent on voxels past the volume): the k index of an output plane runs over its PH*PW voxels flattened (h, w), 16
+// per MFMA; each lane addresses its own voxel's (shifted) halo row, so any tile shape works.
+template <int PH, int PW>
+struct WRT {
+  static constexpr int HH = PH + 2, HW = PW + 2;
+  static constexpr int NR = HH * HW;                 // halo rows per input plane (324 at 16 x 16)
+  static constexpr int NV = PH * PW;                 // voxels per output plane (256 = 16 k16 steps)
+  static constexpr int KS = NV / 16;
+  static constexpr int SLOT = NR * WR_ROWB;
+  static constexpr int DSLOT = NV * WR_ROWB;
+  static constexpr int LX = (NR * 4 + WR_NT - 1) / WR_NT;  // input pieces per thread and plane
+  static constexpr int LY = (NV * 4 + WR_NT - 1) / WR_NT;  // dy pieces
+  static_assert(NV % 16 == 0, "k steps of 16 voxels");
+};
 
 struct WRGeom {
   int n, d, h, w, cin, cout, cin_p, cout_p;
+  int ph, pw;  // plane tile
   int nbh, nbw;
   long long planes;  // output planes per channel tile = n * nbh * nbw * d
   int per;           // output planes per split
@@ -86,8 +95,8 @@ struct WRWalk {
     const int bw_ = c % g.nbw; c /= g.nbw;
     const int bh_ = c % g.nbh;
     p.n = c / g.nbh;
-    p.h0 = bh_ * WR_PH;
-    p.w0 = bw_ * WR_PW;
+    p.h0 = bh_ * g.ph;
+    p.w0 = bw_ * g.pw;
     p.zin = zin;
     p.valid = true;
     p.out = zin >= zfirst + 1;
@@ -98,12 +107,15 @@ struct WRWalk {
 
 }  // namespace
 
-template <bool GN>
+template <bool GN, int PH = 16, int PW = 16>
 __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                              const float* __restrict__ gstat,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, float* __restrict__ part,
                                                              WRGeom g) {
+  using T = WRT<PH, PW>;
+  constexpr int WR_HW = T::HW, WR_NR = T::NR, WR_NV = T::NV, WR_SLOT = T::SLOT, WR_DSLOT = T::DSLOT, WR_LX = T::LX,
+                WR_LY = T::LY, WR_PW = PW;
   __shared__ __attribute__((aligned(16))) char lds[4 * WR_SLOT + 2 * WR_DSLOT + 1024];
   char* const ring = lds;
   char* const dyr = lds + 4 * WR_SLOT;
@@ -147,7 +159,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     for (int i = 0; i < WR_LY; ++i) {
       const int v = (tid >> 2) + i * (WR_NT / 4);
       const int zh = p.h0 + v / WR_PW, zw = p.w0 + v % WR_PW, zo = p.zin - 1;
-      const bool ok = p.valid && p.out && dok && zh < g.h && zw < g.w;
+      const bool ok = p.valid && p.out && dok && v < WR_NV && zh < g.h && zw < g.w;
       const unsigned off =
           ok ? (unsigned)(((((p.n * g.d + zo) * g.h + zh) * g.w + zw) * g.cout + co0 + ch * 8) * 2) : 0xFFFFFFF0u;
       vy[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0));
@@ -174,7 +186,8 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
 #pragma unroll
       for (int i = 0; i < WR_LY; ++i) {
         const int v = (tid >> 2) + i * (WR_NT / 4);
-        *reinterpret_cast<u32x4*>(dyr + dslot * WR_DSLOT + v * WR_ROWB + ch * 16) = vy[i];
+        if (WR_NV % (WR_NT / 4) == 0 || v < WR_NV)
+          *reinterpret_cast<u32x4*>(dyr + dslot * WR_DSLOT + v * WR_ROWB + ch * 16) = vy[i];
       }
     }
   };
@@ -198,7 +211,15 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
   const int colb = (16 * (gq & 1) + 4 * pp) * 2;
   int lrow[2];
 #pragma unroll
-  for (int m = 0; m < 2; ++m) lrow[m] = (8 * hh + 4 * m + q) * WR_ROWB + colb;  // voxel k of a 16-voxel row
+  for (int m = 0; m < 2; ++m) lrow[m] = 8 * hh + 4 * m + q;  // this lane's voxel k within a 16-voxel k step
+  // k step ks, half m: byte offsets of the lane's voxel f = 16 ks + lrow[m] in the dy plane (flattened) and of its
+  // halo row (f + 2 (f / PW): the halo rows are PW + 2 wide) in an input slot
+  auto dyoff = [&](int ks, int m) { return (16 * ks + lrow[m]) * WR_ROWB + colb; };
+  // (16 ks = a PW + b at compile time, so f / PW = a + [lrow >= PW - b]: one compare per fragment, no division)
+  auto xoff = [&](int ks, int m) {
+    const int a = 16 * ks / WR_PW, b = 16 * ks % WR_PW;
+    return (a * WR_HW + b + lrow[m] + (lrow[m] >= WR_PW - b ? 2 : 0)) * WR_ROWB + colb;
+  };
 
   auto compute = [&](int dslot, int s0, int s1, int s2, auto ntc) {
     constexpr int NTP = decltype(ntc)::value;
@@ -207,21 +228,20 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
 #pragma unroll
     for (int j = 0; j < NTP; ++j) tb[j] = sl[tap_d[j]] * WR_SLOT + tap_row[j];
     const char* dbase = dyr + dslot * WR_DSLOT;
-    constexpr int LA = GN ? 1 : 2;  // fragment lookahead (k16 steps); the GN variant's registers allow one
+    constexpr int LA = GN ? (PW == 16 ? 1 : 0) : 2;  // fragment lookahead (k16 steps): what the registers allow
     bf16x8 fa[LA + 1], fb[LA + 1][NTP];
     auto rd = [&](int ks, int k) {
-      fa[k] = frag2(trd(dbase, ks * WR_PW * WR_ROWB + lrow[0]), trd(dbase, ks * WR_PW * WR_ROWB + lrow[1]));
+      fa[k] = frag2(trd(dbase, dyoff(ks, 0)), trd(dbase, dyoff(ks, 1)));
+      const int x0 = xoff(ks, 0), x1 = xoff(ks, 1);
 #pragma unroll
-      for (int j = 0; j < NTP; ++j)
-        fb[k][j] = frag2(trd(ring, tb[j] + ks * WR_HW * WR_ROWB + lrow[0]),
-                         trd(ring, tb[j] + ks * WR_HW * WR_ROWB + lrow[1]));
+      for (int j = 0; j < NTP; ++j) fb[k][j] = frag2(trd(ring, tb[j] + x0), trd(ring, tb[j] + x1));
     };
 #pragma unroll
     for (int k = 0; k < LA; ++k) rd(k, k);
     __builtin_amdgcn_sched_barrier(0);
-    sfor<0, WR_PH>([&](auto kc) {
+    sfor<0, T::KS>([&](auto kc) {
       constexpr int ks = decltype(kc)::value;
-      if constexpr (ks + LA < WR_PH) rd(ks + LA, (ks + LA) % (LA + 1));
+      if constexpr (ks + LA < T::KS) rd(ks + LA, (ks + LA) % (LA + 1));
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NTP; ++j)
@@ -281,7 +301,15 @@ static void wr_geom(int n, int cin, int d, int h, int w, int cout, WRGeom& g) {
   g = WRGeom{};
   g.n = n; g.d = d; g.h = h; g.w = w; g.cin = cin; g.cout = cout;
   g.cin_p = round_up(cin, 32); g.cout_p = round_up(cout, 32);
-  g.nbh = cdiv(h, WR_PH); g.nbw = cdiv(w, WR_PW);
+  // plane tile: 16 x 16 unless the plane is 12- or 24-wide (and not a multiple of 16), where 16-wide tiles would spend
+  // 1/3 (24) or 1/4 (12) of every k step on voxels past the volume
+  g.ph = g.pw = 16;
+  const char* e16 = getenv("U3D_WR_TILE16");  // 1: 16 x 16 tiles everywhere (A/B)
+  if (!(e16 && atoi(e16)) && w % 16 != 0 && w % 12 == 0 && h % 12 == 0) {
+    g.ph = 12;
+    g.pw = w % 24 == 0 ? 24 : 12;
+  }
+  g.nbh = cdiv(h, g.ph); g.nbw = cdiv(w, g.pw);
   g.planes = (long long)n * g.nbh * g.nbw * d;
   g.xbytes = (long long)n * d * h * w * cin * 2;
   g.ybytes = (long long)n * d * h * w * cout * 2;
@@ -313,11 +341,17 @@ extern "C" int u3d_conv_wgrad_ring(const void* dy, const void* x, int n, int cin
     U3D_HIP(hipMemsetAsync(partials + (long long)ns_eff * 27 * g.cout_p * g.cin_p, 0,
                            (size_t)(nsplit - ns_eff) * 27 * g.cout_p * g.cin_p * 4, s));
   dim3 grid(g.cin_p / 32, g.cout_p / 32, ns_eff);
-  if (gn_stats)
-    hipLaunchKernelGGL(wgrad_ring_kernel<true>, grid, dim3(WR_NT), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats,
-                       gn_gamma, gn_beta, partials, g);
-  else
-    hipLaunchKernelGGL(wgrad_ring_kernel<false>, grid, dim3(WR_NT), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats,
-                       gn_gamma, gn_beta, partials, g);
+#define U3D_WR(GN_, PH_, PW_)                                                                                       \
+  hipLaunchKernelGGL((wgrad_ring_kernel<GN_, PH_, PW_>), grid, dim3(WR_NT), 0, s, (const bf16*)dy, (const bf16*)x, \
+                     gn_stats, gn_gamma, gn_beta, partials, g)
+  const bool gn = gn_stats != nullptr;
+  if (g.pw == 24) {
+    if (gn) U3D_WR(true, 12, 24); else U3D_WR(false, 12, 24);
+  } else if (g.pw == 12) {
+    if (gn) U3D_WR(true, 12, 12); else U3D_WR(false, 12, 12);
+  } else {
+    if (gn) U3D_WR(true, 16, 16); else U3D_WR(false, 16, 16);
+  }
+#undef U3D_WR
   return check_launch("wgrad_ring_kernel");
 }

@@ -347,3 +347,24 @@ def test_conv32_beyond_2gib_routes_off_the_ring(gpu):
     dy = torch.randn_like(x)
     part, ns = ops.conv_wgrad(dy[:, :, :, :, :32], x, 3, 1)
     assert part.shape[1:] == (27, 32, 32) and torch.isfinite(part).all()
+
+
+# wgrad ring plane tiles 12 x 24 (24-wide planes) and 12 x 12 (12-wide): flattened k over the tile's voxels, partial
+# h tiles (h % 12 != 0 is not routed there, so ragged depth / sample counts instead), several channel tiles, GN on/off
+WTILE = [(2, 32, 32, (24, 24, 24), True), (1, 64, 32, (7, 36, 24), True), (3, 32, 64, (5, 12, 36), False),
+         (2, 64, 64, (12, 12, 12), True), (1, 32, 32, (9, 24, 48), False)]
+
+
+@pytest.mark.parametrize("n,cin,cout,dims,use_gn", WTILE, ids=lambda v: str(v))
+def test_ring_wgrad_tiles_12(gpu, n, cin, cout, dims, use_gn):
+    from u3d import ops
+    x, _, gn = _operands(gpu, n, cin, cout, dims, 29)
+    gn = gn if use_gn else None
+    dy = torch.randn((n,) + dims + (cout,), device=gpu).to(torch.bfloat16)
+    part, ns = ops.conv_wgrad(dy, x, 3, 1, gn)
+    dw = part.sum(0).cpu().double()[:, :cout, :cin]
+    a = _act(x, gn, torch.float64) if gn is not None else _bf(x.cpu()).permute(0, 4, 1, 2, 3)
+    ref = torch.nn.grad.conv3d_weight(a, (cout, cin, 3, 3, 3), _bf(dy.cpu()).permute(0, 4, 1, 2, 3), padding=1)
+    ref = ref.reshape(cout, cin, 27).permute(2, 0, 1)
+    assert (dw - ref).abs().max().item() <= 2e-3 * ref.abs().max().item()
+    assert ((dw - ref).norm() / ref.norm()).item() <= 1e-3
