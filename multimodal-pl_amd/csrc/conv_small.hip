@@ -30,6 +30,7 @@ constexpr int SC_WPS = SC_NWR * 16 + 64;         // weight plane stride
 constexpr int SC_HLD = SC_HMAX * 4 / SC_NT;      // 5 halo loads per thread
 constexpr int SC_WLD = (SC_NWR * 4 + SC_NT - 1) / SC_NT;  // 7 weight loads per thread
 constexpr int SC_LDS = 4 * SC_PS + 4 * SC_WPS;
+constexpr int SC_MAXC = 1024;                    // GN prologue: cin_p <= SC_MAXC (per-channel table after SC_LDS)
 
 struct SCGeom {
   int n, d, h, w;
@@ -49,7 +50,7 @@ __global__ __launch_bounds__(SC_NT, 1) void conv_small_kernel(const bf16* __rest
                                                              const float* __restrict__ gstat,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, SCGeom g) {
-  __shared__ __attribute__((aligned(16))) char smem[SC_LDS];
+  __shared__ __attribute__((aligned(16))) char smem[SC_LDS + SC_MAXC * 8];
   char* const hal = smem;
   char* const wts = smem + 4 * SC_PS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -111,11 +112,22 @@ __global__ __launch_bounds__(SC_NT, 1) void conv_small_kernel(const bf16* __rest
       wpre[i] = val;
     }
   };
-  f32x2 sc[4], sh[4];  // GN scale/shift of the chunk being staged (computed with its prefetch)
-  auto gn_load = [&](int c) {
-    if (has_gn) gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, nn, c * 32 + sch * 8, sc, sh);
-  };
+  // GN scale/shift of this workgroup's sample per input channel, in LDS (filled once): the staging reads its 8
+  // channels there at commit time. (Computing them from global loads next to the chunk prefetch made the wait for
+  // those loads drain the halo/weight prefetch before the MFMAs.)
+  f32x2* const gtab = reinterpret_cast<f32x2*>(smem + SC_LDS);
+  int stg_c = 0;  // chunk of the staged prefetch
   auto commit = [&]() {
+    f32x2 sc[4], sh[4];
+    if (has_gn) {
+      const f32x2* t = gtab + stg_c * 32 + sch * 8;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f32x2 a0 = t[2 * e], a1 = t[2 * e + 1];
+        sc[e] = f32x2{a0[0], a1[0]};
+        sh[e] = f32x2{a0[1], a1[1]};
+      }
+    }
 #pragma unroll
     for (int i = 0; i < SC_HLD; ++i) {
       const int row = srow0 + i * (SC_NT / 4);
@@ -139,7 +151,16 @@ __global__ __launch_bounds__(SC_NT, 1) void conv_small_kernel(const bf16* __rest
   const int c0 = ks * g.cpk, c1 = min(g.cin_p / 32, c0 + g.cpk);
   halo_load(c0);
   w_load(c0);
-  gn_load(c0);
+  stg_c = c0;
+  if (has_gn) {
+    for (int i = tid; i < min(g.cin_p, SC_MAXC); i += SC_NT) {
+      const int c = min(i, g.cin - 1), gg = c / (g.cin / g.gn_groups);
+      const float mean = gstat[(nn * g.gn_groups + gg) * 2], rstd = gstat[(nn * g.gn_groups + gg) * 2 + 1];
+      const float sc_ = rstd * gamma[c];
+      gtab[i] = f32x2{sc_, beta[c] - mean * sc_};
+    }
+    __syncthreads();
+  }
   commit();
   __syncthreads();
   for (int c = c0; c < c1; ++c) {
@@ -147,7 +168,7 @@ __global__ __launch_bounds__(SC_NT, 1) void conv_small_kernel(const bf16* __rest
     if (more) {
       halo_load(c + 1);
       w_load(c + 1);
-      gn_load(c + 1);
+      stg_c = c + 1;
     }
     if (active) {
 #pragma unroll
@@ -261,6 +282,7 @@ extern "C" int u3d_conv_small(int flip, const void* x, int n, int cin, int d, in
   U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "conv_small: channels must be multiples of 8");
   U3D_REQUIRE(!gn_stats || (!flip && gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0),
               "conv_small: bad GN prologue");
+  U3D_REQUIRE(!gn_stats || round_up(cin, 32) <= SC_MAXC, "conv_small: GN prologue supports cin <= %d", SC_MAXC);
   SCGeom g{};
   g.n = n; g.d = d; g.h = h; g.w = w;
   g.cin = cin; g.cin_p = round_up(cin, 32); g.cout = cout; g.cout_p = round_up(cout, 32);
