@@ -149,6 +149,23 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// (channel tile x, channel tile y, work split) of a 3-D grid whose x / y enumerate channel tiles and z the splits of
+// the work. Workgroups are dispatched round-robin over the 8 XCDs in linear order (x fastest); this remaps so that
+// XCD k runs a contiguous range of (split, tile) indices, tile fastest: all channel tiles of a few consecutive splits
+// run on one XCD at the same time and read their shared operand rows (the same input rows for every output-channel
+// tile, the same dy rows for every input-channel tile) through that XCD's L2 instead of once per XCD from HBM.
+struct TileSplit {
+  int tx, ty, split;
+};
+__device__ __forceinline__ TileSplit xcd_tile_split() {
+  const int nt = gridDim.x * gridDim.y, total = nt * gridDim.z;
+  const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int q = total >> 3, rr = total & 7, xcd = L & 7, loc = L >> 3;
+  const int N = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  const int tile = N % nt;
+  return TileSplit{tile % (int)gridDim.x, tile / (int)gridDim.x, N / nt};
+}
+
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 __host__ __device__ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 

@@ -61,8 +61,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = tid & 3, row0 = tid >> 2;  // fixed channel chunk per thread
-  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * 32;
-  const long long b0 = (long long)blockIdx.z * g.per_split;
+  const TileSplit ts = xcd_tile_split();  // XCD-aware: the channel tiles of neighbouring brick ranges share an L2
+  const int ci0 = ts.tx * 32, co0 = ts.ty * 32;
+  const long long b0 = (long long)ts.split * g.per_split;
   const long long b1 = min(g.nbricks, b0 + g.per_split);
   const bool has_gn = gstat != nullptr;
 
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
   for (int j = 0; j < MAXT; ++j) {
     if (j < ntap) {
       const int tt = wave + 8 * j;
-      float* pp = part + ((long long)blockIdx.z * 27 + tt) * g.cout_p * g.cin_p;
+      float* pp = part + ((long long)ts.split * 27 + tt) * g.cout_p * g.cin_p;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int co = co0 + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -249,8 +250,9 @@ __global__ __launch_bounds__(512, 1) void wgrad1_kernel(const bf16* __restrict__
   char* at = lds + W1_NV * ROWB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = tid & 3, row0 = tid >> 2;
-  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * 32;
-  const long long v0 = (long long)blockIdx.z * g.per_split;
+  const TileSplit ts = xcd_tile_split();
+  const int ci0 = ts.tx * 32, co0 = ts.ty * 32;
+  const long long v0 = (long long)ts.split * g.per_split;
   const long long v1 = min(g.nvox, v0 + g.per_split);
   const bool has_gn = gstat != nullptr;
   const int h = lane >> 5, gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(512, 1) void wgrad1_kernel(const bf16* __restrict__
 #pragma unroll
   for (int i = 0; i < 16; ++i) red[(wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[i];
   __syncthreads();
-  float* pp = part + (long long)blockIdx.z * g.cout_p * g.cin_p;
+  float* pp = part + (long long)ts.split * g.cout_p * g.cin_p;
   for (int e = tid; e < 1024; e += NT) {
     float s = 0.f;
 #pragma unroll

@@ -122,12 +122,8 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
   char* const junk = dyr + 2 * WR_DSLOT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = tid & 3;
-  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * 32;
-  int split = blockIdx.z;
-  if (gridDim.x * gridDim.y == 1) {  // XCD-aware: XCD x runs a contiguous eighth of the plane ranges
-    const int nwg = gridDim.z, q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.z & 7, loc = blockIdx.z >> 3;
-    split = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
-  }
+  const TileSplit ts = xcd_tile_split();  // XCD-aware: the channel tiles of neighbouring plane ranges share an L2
+  const int ci0 = ts.tx * 32, co0 = ts.ty * 32, split = ts.split;
   WRWalk walk{};
   walk.o_next = (long long)split * g.per;
   walk.o_end = min(g.planes, walk.o_next + g.per);
@@ -283,7 +279,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
   for (int j = 0; j < MAXT; ++j) {
     if (j < ntap) {
       const int tt = wave + 8 * j;
-      float* pq = part + ((long long)blockIdx.z * 27 + tt) * g.cout_p * g.cin_p;
+      float* pq = part + ((long long)split * 27 + tt) * g.cout_p * g.cin_p;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int co = co0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
