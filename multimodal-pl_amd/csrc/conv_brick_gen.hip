@@ -495,12 +495,11 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
           }
         }
       }
-      if (next) {
-        w_commit(par ^ 1);  // the other buffer: its readers finished before the previous barrier
-        if (td == 2) {
-          __syncthreads();  // everyone done with this chunk's halo
-          halo_commit();
-        }
+      if (last) break;  // the last step's staging commit runs after the residual loads are issued (below)
+      w_commit(par ^ 1);  // the other buffer: its readers finished before the previous barrier
+      if (td == 2) {
+        __syncthreads();  // everyone done with this chunk's halo
+        halo_commit();
       }
       __syncthreads();
       par ^= 1;
@@ -531,6 +530,14 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
                                                      : u32x4{0u, 0u, 0u, 0u};
           }
     }
+    // the last step's staging commit (the next unit's first weights and halo) while the residual loads fly
+    if (more) {
+      w_commit(par ^ 1);
+      __syncthreads();
+      halo_commit();
+    }
+    __syncthreads();
+    par ^= 1;
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
