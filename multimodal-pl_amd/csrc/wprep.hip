@@ -64,13 +64,45 @@ __device__ __forceinline__ T block_sum(T v, T* red) {  // WB_T threads, fixed or
   return t;
 }
 
-// (1) mean / unbiased std of one row, as Conv3d.forward computes them
+// (1) mean / unbiased std of one row, as Conv3d.forward computes them. Rows up to WS_RV * 4 * WB_T floats (every trunk
+// conv: cin * 27 <= 6912) are read once, as 16-B vectors held in registers for both sums (K = cin * k3 is a multiple
+// of 8 and rows start 16-B aligned); longer rows take the two-pass scalar walk.
+constexpr int WS_RV = 7;
 __global__ __launch_bounds__(WB_T) void wstd_stats_kernel(WBatch<WRow> bt) {
   __shared__ double red[WB_T / 64];
   const WRow& D = bt.d[find_desc(bt, blockIdx.x)];
   const int co = blockIdx.x - D.b0;
   const int K = D.cin * D.k3;
   const float* wr = D.w + (long long)co * K;
+  if (K <= WS_RV * 4 * WB_T && K % 4 == 0) {
+    f32x4 r[WS_RV];
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < WS_RV; ++j) {
+      const int i = (threadIdx.x + j * WB_T) * 4;
+      r[j] = i < K ? *reinterpret_cast<const f32x4*>(wr + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < WS_RV; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += r[j][e];
+    const float mean = (float)(block_sum(s, red) / K);
+    double v = 0.0;
+#pragma unroll
+    for (int j = 0; j < WS_RV; ++j)
+      if ((threadIdx.x + j * WB_T) * 4 < K)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float c = r[j][e] - mean;
+          v += (double)c * c;
+        }
+    const float var = (float)(block_sum(v, red) / (K > 1 ? K - 1 : 1));  // torch.var: unbiased
+    if (threadIdx.x == 0) {
+      D.st[co * 2] = mean;
+      D.st[co * 2 + 1] = sqrtf(var + 1e-12f);
+    }
+    return;
+  }
   double s = 0.0;
   for (int i = threadIdx.x; i < K; i += WB_T) s += wr[i];
   const float mean = (float)(block_sum(s, red) / K);
@@ -112,14 +144,34 @@ __device__ __forceinline__ void pack_tile(const WPack& D, float* ws, const float
     const float v = ws[r * RS + c * K3 + t];
     return (co0 + r < D.cout && ci0 + c < D.cin) ? (v - mu[r]) / sg[r] : 0.f;
   };
-  for (int e = threadIdx.x; e < K3 * WB_CO * WB_CI; e += WB_TT) {  // (t, r, c), c fastest
-    const int c = e % WB_CI, r = (e / WB_CI) % WB_CO, t = e / (WB_CI * WB_CO);
-    pf[((long long)t * cout_p + co0 + r) * cin_p + ci0 + c] = from_f<T>(val(r, c, t));
-  }
-  if (pd) {
-    for (int e = threadIdx.x; e < K3 * WB_CO * WB_CI; e += WB_TT) {  // (t, c, r), r fastest
-      const int r = e % WB_CO, c = (e / WB_CO) % WB_CI, t = e / (WB_CI * WB_CO);
-      pd[((long long)t * cin_p + ci0 + c) * cout_p + co0 + r] = from_f<T>(val(r, c, t));
+  if constexpr (sizeof(T) == 2) {
+    // bf16: 8 consecutive outputs per thread, one 16-B store (v_cvt_pk_bf16_f32 = the RNE of from_f<bf16>)
+    for (int e = threadIdx.x; e < K3 * WB_CO * (WB_CI / 8); e += WB_TT) {  // (t, r, c8), c8 fastest
+      const int c8 = e % (WB_CI / 8), r = (e / (WB_CI / 8)) % WB_CO, t = e / (WB_CI / 8 * WB_CO);
+      u32x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = pack_bf16x2(val(r, c8 * 8 + 2 * q, t), val(r, c8 * 8 + 2 * q + 1, t));
+      *reinterpret_cast<u32x4*>(pf + ((long long)t * cout_p + co0 + r) * cin_p + ci0 + c8 * 8) = o;
+    }
+    if (pd) {
+      for (int e = threadIdx.x; e < K3 * WB_CI * (WB_CO / 8); e += WB_TT) {  // (t, c, r8), r8 fastest
+        const int r8 = e % (WB_CO / 8), c = (e / (WB_CO / 8)) % WB_CI, t = e / (WB_CO / 8 * WB_CI);
+        u32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = pack_bf16x2(val(r8 * 8 + 2 * q, c, t), val(r8 * 8 + 2 * q + 1, c, t));
+        *reinterpret_cast<u32x4*>(pd + ((long long)t * cin_p + ci0 + c) * cout_p + co0 + r8 * 8) = o;
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < K3 * WB_CO * WB_CI; e += WB_TT) {  // (t, r, c), c fastest
+      const int c = e % WB_CI, r = (e / WB_CI) % WB_CO, t = e / (WB_CI * WB_CO);
+      pf[((long long)t * cout_p + co0 + r) * cin_p + ci0 + c] = from_f<T>(val(r, c, t));
+    }
+    if (pd) {
+      for (int e = threadIdx.x; e < K3 * WB_CO * WB_CI; e += WB_TT) {  // (t, c, r), r fastest
+        const int r = e % WB_CO, c = (e / WB_CO) % WB_CI, t = e / (WB_CI * WB_CO);
+        pd[((long long)t * cin_p + ci0 + c) * cout_p + co0 + r] = from_f<T>(val(r, c, t));
+      }
     }
   }
 }
