@@ -119,11 +119,30 @@ __global__ __launch_bounds__(WB_T) void wstd_stats_kernel(WBatch<WRow> bt) {
 }
 
 // stage rows co0..co0+15, columns [ci0*K3, (ci0+32)*K3) of a [cout][cin*K3] fp32 matrix into LDS (zero padded)
+// (16-B loads, all issued before the LDS stores, when the rows are 16-B aligned: K3 = 27 with cin % 4 == 0, or
+// K3 = 1 with cin % 4 == 0 — every trunk conv; scalar otherwise, e.g. the 1-channel stem)
 template <int K3>
 __device__ __forceinline__ void stage_rows(float* s, const float* __restrict__ src, int cout, int cin, int co0,
                                            int ci0) {
-  constexpr int SEG = WB_CI * K3, RS = SEG + 1;
+  constexpr int SEG = WB_CI * K3, RS = SEG + 1, NQ = WB_CO * SEG / 4, QL = (NQ + WB_TT - 1) / WB_TT;
   const int K = cin * K3, valid = min(WB_CI, cin - ci0) * K3;
+  if (cin % 4 == 0 && (((uintptr_t)src) & 15) == 0) {
+    f32x4 v[QL];
+#pragma unroll
+    for (int i = 0; i < QL; ++i) {
+      const int q = threadIdx.x + i * WB_TT, r = q / (SEG / 4), c = (q - r * (SEG / 4)) * 4, co = co0 + r;
+      v[i] = (q < NQ && co < cout && c < valid) ? *reinterpret_cast<const f32x4*>(src + (long long)co * K + ci0 * K3 + c)
+                                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < QL; ++i) {
+      const int q = threadIdx.x + i * WB_TT, r = q / (SEG / 4), c = (q - r * (SEG / 4)) * 4;
+      if (q < NQ)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[r * RS + c + e] = v[i][e];
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < WB_CO * SEG; e += WB_TT) {
     const int r = e / SEG, c = e - r * SEG, co = co0 + r;
     s[r * RS + c] = (co < cout && c < valid) ? src[(long long)co * K + ci0 * K3 + c] : 0.f;
@@ -244,8 +263,9 @@ __global__ __launch_bounds__(WB_T) void wstd_sum_slabs_kernel(WBatch<WSum> bt) {
 // (4+5) dW of 8 output channels: pass 1 accumulates the row sums of g and g*W_hat over 32-channel chunks
 // staged through LDS (w rows [co][ci][t] contiguous, g [t][co][ci] rows contiguous), pass 2 re-stages the
 // chunks and writes dW = (g - mean(g) - W_hat * sum(g W_hat)/(K-1)) / std in parameter order (contiguous rows).
-// 32 threads per row, fixed-order reductions (deterministic).
-constexpr int WG_R = 8, WG_T = 256;
+// WG_T / WG_R threads per row, fixed-order reductions (deterministic). 4 rows per block: twice the blocks of 8 and
+// half the LDS, so more blocks stream per CU (the kernel is latency-bound on its chunk stage / barrier chain).
+constexpr int WG_R = 4, WG_T = 256, WG_TPR = WG_T / WG_R;
 
 template <int K3>
 __device__ __forceinline__ void wgrad_stage(const WPack& D, float* ws, float* gs, int co0, int ci0) {
@@ -300,7 +320,7 @@ __device__ __forceinline__ void wgrad_rows(const WPack& D, int co0) {
   __shared__ float ws[WG_R * (SEG + 1)];
   __shared__ float gs[K3 * WG_R * (WB_CI + 1)];
   __shared__ float f1s[WG_R], f2s[WG_R];
-  const int tid = threadIdx.x, r = tid >> 5, l = tid & 31, co = co0 + r;
+  const int tid = threadIdx.x, r = tid / WG_TPR, l = tid % WG_TPR, co = co0 + r;
   const bool std_ = D.st != nullptr, rok = co < D.cout;
   const float mu = std_ && rok ? D.st[co * 2] : 0.f;
   const float rsg = std_ && rok ? 1.f / D.st[co * 2 + 1] : 1.f;
@@ -312,7 +332,7 @@ __device__ __forceinline__ void wgrad_rows(const WPack& D, int co0) {
       wgrad_stage<K3>(D, ws, gs, co0, ci0);
       __syncthreads();
       const int valid = min(WB_CI, D.cin - ci0) * K3;
-      for (int e = l; e < valid; e += 32) {
+      for (int e = l; e < valid; e += WG_TPR) {
         const int c = e / K3, t = e - c * K3;
         const float gv = gs[(t * WG_R + r) * (WB_CI + 1) + c];
         m1 += gv;
@@ -320,9 +340,9 @@ __device__ __forceinline__ void wgrad_rows(const WPack& D, int co0) {
       }
     }
     double d1 = m1, d2 = m2;
-    for (int o = 16; o > 0; o >>= 1) {
-      d1 += __shfl_xor(d1, o, 32);
-      d2 += __shfl_xor(d2, o, 32);
+    for (int o = WG_TPR / 2; o > 0; o >>= 1) {
+      d1 += __shfl_xor(d1, o, WG_TPR);
+      d2 += __shfl_xor(d2, o, WG_TPR);
     }
     if (l == 0) {
       f1s[r] = (float)(d1 / K);
@@ -341,7 +361,7 @@ __device__ __forceinline__ void wgrad_rows(const WPack& D, int co0) {
     if (!rok) continue;
     const int valid = min(WB_CI, D.cin - ci0) * K3;
     float* o = D.dw + (long long)co * K + ci0 * K3;
-    for (int e = l; e < valid; e += 32) {
+    for (int e = l; e < valid; e += WG_TPR) {
       const int c = e / K3, t = e - c * K3;
       const float gv = gs[(t * WG_R + r) * (WB_CI + 1) + c];
       const float v = std_ ? (gv - f1 - (ws[r * (SEG + 1) + e] - mu) * rsg * f2) * rsg : gv;
