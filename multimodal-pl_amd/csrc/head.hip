@@ -15,11 +15,16 @@ namespace u3d {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
 constexpr int HD_T = 256;  // 4 waves
+constexpr int HD_GMAX = 2048;  // TR forward with GN: n * cin <= HD_GMAX (per-block LDS coefficient table)
 
 __device__ __forceinline__ bf16x8 as_frag(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
 
 // KS = cin / 16 k-steps (cin in {16, 32, 48, 64})
-template <int KS>
+// TR (cout % 8 == 0): the MFMA is issued transposed (A = weights, B = voxel rows), so after one permlane32 swap a
+// lane holds 8 consecutive channels x 2 of ONE voxel and writes them as 16-B stores (the untransposed form writes
+// 16 scalar 4-B stores per lane, half the lanes idle at cout = 16); the next tile's rows are loaded before the
+// current tile's MFMA and stores.
+template <int KS, bool TR>
 __global__ __launch_bounds__(HD_T) void head_fwd_kernel(const bf16* __restrict__ x, long long v, int cin,
                                                        const bf16* __restrict__ wpk, int cout, int cin_p,
                                                        const float* __restrict__ bias, const float* __restrict__ st,
@@ -31,12 +36,94 @@ __global__ __launch_bounds__(HD_T) void head_fwd_kernel(const bf16* __restrict__
 #pragma unroll
   for (int s = 0; s < KS; ++s)
     bw[s] = as_frag(*reinterpret_cast<const u32x4*>(wpk + (long long)r * cin_p + 16 * s + 8 * h));
-  const float bv = r < cout && bias ? bias[r] : 0.f;
   const long long tiles = (n * v + 31) / 32;
   const long long wid = (long long)blockIdx.x * (HD_T / 64) + (threadIdx.x >> 6);
   const long long nw = (long long)gridDim.x * (HD_T / 64);
   int gn_n = -1;
   f32x2 sc[KS][4], sh[KS][4];
+  if constexpr (TR) {
+    // GroupNorm scale / shift of every (sample, channel) in LDS, filled once per block (the per-sample coefficient
+    // loads inline in the loop held ~80 registers live and cut the occupancy of this streaming kernel to 2 waves)
+    __shared__ f32x2 gtab[HD_GMAX];
+    if (st) {
+      for (int i = threadIdx.x; i < n * cin; i += HD_T) {
+        const int nn = i / cin, c = i - nn * cin, gg = c / (cin / groups);
+        const float mean = st[(nn * groups + gg) * 2], rstd = st[(nn * groups + gg) * 2 + 1];
+        const float sc_ = rstd * ga[c];
+        gtab[i] = f32x2{sc_, be[c] - mean * sc_};
+      }
+      __syncthreads();
+    }
+    // bias of this lane's two 8-channel runs (8h .. 8h+7 and 16+8h .. 16+8h+7) after the swap
+    float b0[8], b1[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      b0[e] = bias && 8 * h + e < cout ? bias[8 * h + e] : 0.f;
+      b1[e] = bias && 16 + 8 * h + e < cout ? bias[16 + 8 * h + e] : 0.f;
+    }
+    auto load = [&](long long tile, u32x4 (&a)[KS]) {
+      const long long row = tile * 32 + r;
+      const bool ok = tile < tiles && row < n * v;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        a[s] = ok ? *reinterpret_cast<const u32x4*>(x + row * cin + 16 * s + 8 * h) : u32x4{0u, 0u, 0u, 0u};
+    };
+    u32x4 a[KS], an[KS];
+    load(wid, a);
+    for (long long tile = wid; tile < tiles; tile += nw) {
+      load(tile + nw, an);  // next tile's rows in flight under this tile's MFMAs and stores
+      const long long row = tile * 32 + r;
+      const bool ok = row < n * v;
+      const int nn = ok ? (int)((unsigned)row / (unsigned)v) : 0;  // n * v < 2^31 (host check): 32-bit division
+      if (st && ok) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          f32x2 sc_[4], sh_[4];
+          const f32x2* t = gtab + nn * cin + 16 * s + 8 * h;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f32x2 p0 = t[2 * e], p1 = t[2 * e + 1];
+            sc_[e] = f32x2{p0[0], p1[0]};
+            sh_[e] = f32x2{p0[1], p1[1]};
+          }
+          a[s] = gn_relu8(a[s], sc_, sh_);
+        }
+      }
+      f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[s], as_frag(a[s]), acc, 0, 0, 0);
+      // acc[4q + e] = channel 8q + 4h + e of voxel row; swap so lane h holds 8h..8h+7 and 16+8h..16+8h+7
+#pragma unroll
+      for (int q = 0; q < 4; q += 2)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[4 * q + e]),
+                                                           __float_as_uint(acc[4 * q + 4 + e]), false, false);
+          acc[4 * q + e] = __uint_as_float(sw[0]);
+          acc[4 * q + 4 + e] = __uint_as_float(sw[1]);
+        }
+      if (ok) {
+        float* yr = y + row * cout;
+        if (8 * h < cout) {
+          *reinterpret_cast<f32x4*>(yr + 8 * h) = f32x4{acc[0] + b0[0], acc[1] + b0[1], acc[2] + b0[2], acc[3] + b0[3]};
+          *reinterpret_cast<f32x4*>(yr + 8 * h + 4) =
+              f32x4{acc[4] + b0[4], acc[5] + b0[5], acc[6] + b0[6], acc[7] + b0[7]};
+        }
+        if (16 + 8 * h < cout) {
+          *reinterpret_cast<f32x4*>(yr + 16 + 8 * h) =
+              f32x4{acc[8] + b1[0], acc[9] + b1[1], acc[10] + b1[2], acc[11] + b1[3]};
+          *reinterpret_cast<f32x4*>(yr + 20 + 8 * h) =
+              f32x4{acc[12] + b1[4], acc[13] + b1[5], acc[14] + b1[6], acc[15] + b1[7]};
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s] = an[s];
+    }
+    return;
+  }
+  const float bv = r < cout && bias ? bias[r] : 0.f;
   for (long long tile = wid; tile < tiles; tile += nw) {
     const long long row = tile * 32 + r;  // this lane's A row (voxel over all samples)
     const bool ok = row < n * v;
@@ -73,7 +160,7 @@ __global__ __launch_bounds__(HD_T) void head_fwd_kernel(const bf16* __restrict__
 __global__ __launch_bounds__(HD_T) void head_bwd_kernel(const float* __restrict__ dy, long long rows, int cout,
                                                        const bf16* __restrict__ wpd, int cout_p, int cin,
                                                        bf16* __restrict__ dA, bf16* __restrict__ dyb, int cout8,
-                                                       float* __restrict__ dbp) {
+                                                       float* __restrict__ dbp, int tr) {
   __shared__ float red[HD_T / 64][32];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
   bf16x8 bw[2][2];  // [k-step][n-tile of 32 ci]
@@ -123,6 +210,33 @@ __global__ __launch_bounds__(HD_T) void head_bwd_kernel(const float* __restrict_
       f32x16 acc;
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      if (tr) {  // transposed: D[ci][voxel], a lane ends with 8 consecutive ci x 2 of its voxel -> 16-B stores
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[0][tn], as_frag(a[0]), acc, 0, 0, 0);
+        if (cout_p > 16) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[1][tn], as_frag(a[1]), acc, 0, 0, 0);
+        uint32_t pk[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) pk[q][e] = pack_bf16x2(acc[4 * q + 2 * e], acc[4 * q + 2 * e + 1]);
+#pragma unroll
+        for (int q = 0; q < 4; q += 2)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(pk[q][e], pk[q + 1][e], false, false);
+            pk[q][e] = sw[0];
+            pk[q + 1][e] = sw[1];
+          }
+        if (ok) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int ci = tn * 32 + 16 * u + 8 * h;
+            if (ci < cin)
+              *reinterpret_cast<u32x4*>(dA + row * cin + ci) =
+                  u32x4{pk[2 * u][0], pk[2 * u][1], pk[2 * u + 1][0], pk[2 * u + 1][1]};
+          }
+        }
+        continue;
+      }
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(a[0]), bw[0][tn], acc, 0, 0, 0);
       if (cout_p > 16) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_frag(a[1]), bw[1][tn], acc, 0, 0, 0);
       const int ci = tn * 32 + r;
@@ -172,17 +286,28 @@ extern "C" int u3d_head_fwd(const void* x, int n, long long v, int cin, const vo
   U3D_REQUIRE(cin % 16 == 0 && cin >= 16 && cin <= 64 && cout >= 1 && cout <= 32, "head_fwd: cin %d / cout %d", cin,
               cout);
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "head_fwd: bad GN");
+  U3D_REQUIRE((long long)n * v < (1LL << 31), "head_fwd: n * v must be < 2^31");
   const int cin_p = round_up(cin, 32);
   const int nb = head_blocks(n * v);
   hipStream_t s = (hipStream_t)stream;
-#define HF(KS)                                                                                                       \
-  hipLaunchKernelGGL(head_fwd_kernel<KS>, dim3(nb), dim3(HD_T), 0, s, (const bf16*)x, v, cin, (const bf16*)wpk, cout, \
-                     cin_p, bias, gn_stats, gn_gamma, gn_beta, gn_groups, n, y)
-  switch (cin / 16) {
-    case 1: HF(1); break;
-    case 2: HF(2); break;
-    case 3: HF(3); break;
-    default: HF(4); break;
+#define HF(KS, TR)                                                                                                   \
+  hipLaunchKernelGGL((head_fwd_kernel<KS, TR>), dim3(nb), dim3(HD_T), 0, s, (const bf16*)x, v, cin, (const bf16*)wpk, \
+                     cout, cin_p, bias, gn_stats, gn_gamma, gn_beta, gn_groups, n, y)
+  const char* etr = getenv("U3D_HEAD_TR");  // 0: the untransposed store path (A/B)
+  if (cout % 8 == 0 && !(etr && atoi(etr) == 0) && (!gn_stats || (long long)n * cin <= HD_GMAX)) {
+    switch (cin / 16) {
+      case 1: HF(1, true); break;
+      case 2: HF(2, true); break;
+      case 3: HF(3, true); break;
+      default: HF(4, true); break;
+    }
+  } else {
+    switch (cin / 16) {
+      case 1: HF(1, false); break;
+      case 2: HF(2, false); break;
+      case 3: HF(3, false); break;
+      default: HF(4, false); break;
+    }
   }
 #undef HF
   return check_launch("head_fwd_kernel");
@@ -195,7 +320,9 @@ extern "C" int u3d_head_bwd(const float* dy, long long rows, int cout, const voi
   U3D_REQUIRE(dy && wpk_dgrad && dA && dy_bf16 && dbias_partials && rows >= 1, "head_bwd: bad args");
   U3D_REQUIRE(cout >= 1 && cout <= 32 && cin % 8 == 0 && cin <= 64, "head_bwd: cout %d / cin %d", cout, cin);
   const int cout_p = round_up(cout, 32), cout8 = round_up(cout, 8);
+  const char* etr = getenv("U3D_HEAD_TR");  // 0: untransposed scalar dA stores (A/B)
+  const int tr = (etr && atoi(etr) == 0) ? 0 : 1;
   hipLaunchKernelGGL(head_bwd_kernel, dim3(head_blocks(rows)), dim3(HD_T), 0, (hipStream_t)stream, dy, rows, cout,
-                     (const bf16*)wpk_dgrad, cout_p, cin, (bf16*)dA, (bf16*)dy_bf16, cout8, dbias_partials);
+                     (const bf16*)wpk_dgrad, cout_p, cin, (bf16*)dA, (bf16*)dy_bf16, cout8, dbias_partials, tr);
   return check_launch("head_bwd_kernel");
 }

@@ -362,3 +362,30 @@ def test_bf16_stem_bench_size(gpu):
             ref = F.conv3d(xb[n:n + 1, :, lo:hi], wq, padding=1)[0, :, z - lo].permute(1, 2, 0)
             err = (y[n, z].double().cpu() - ref).abs().max().item()
             assert err < 1e-2 * ref.abs().max().item(), (n, z, err)
+
+
+@pytest.mark.parametrize("cin,cout,dims", [(32, 16, (48, 48, 48)), (64, 8, (5, 7, 9)), (16, 32, (3, 11, 13))])
+def test_head_transposed_bitwise_equal(gpu, cin, cout, dims):
+    """The transposed-MFMA head (16-B stores; default for cout % 8 == 0) against the untransposed form
+    (U3D_HEAD_TR=0): the same products summed in the same order, the same bf16 rounding -> bitwise equal."""
+    import os
+    from u3d import ops
+    n = 2
+    x, _, st, ga, be, G = _case(gpu, n, cin, cout, dims, True, 9)
+    w = torch.randn(cout, cin, 1, 1, 1, device=gpu)
+    pf, pd, _ = ops.wstd_fwd(w, torch.bfloat16, False)
+    b = torch.randn(cout, device=gpu)
+    dy = torch.randn(x.shape[:-1] + (cout,), device=gpu)
+    out = []
+    for tr in ("1", "0"):
+        os.environ["U3D_HEAD_TR"] = tr
+        try:
+            y = ops.head_fwd(x, pf, cout, b, (st, ga, be, G))
+            dA, dyb = ops.head_bwd(dy, pd, cin)
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("U3D_HEAD_TR", None)
+        out.append((y, dA, dyb))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1].view(torch.int16), out[1][1].view(torch.int16))
+    assert torch.equal(out[0][2].view(torch.int16), out[1][2].view(torch.int16))
