@@ -96,7 +96,60 @@ __global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restric
   for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int c = 0; c < NC; ++c) acc[k][c] = 0.f;
-  for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < nvox; v += (long long)gridDim.x * LT) {
+  const long long stride = (long long)gridDim.x * LT;
+  if constexpr (NC % 4 == 0 && NC <= 16) {
+    if (softmax == 1 && uce != 2 && C == NC) {
+      // software-pipelined softmax path: the next voxel's logits and label are loaded before this voxel's math
+      // (one voxel per thread in flight otherwise: the pass waited on every load at 3 waves per SIMD)
+      long long v = blockIdx.x * (long long)LT + threadIdx.x;
+      f32x4 cur[NC / 4], nxt[NC / 4];
+      float tcur = 0.f, tnxt = 0.f;
+      auto load = [&](long long vv, f32x4 (&q)[NC / 4], float& t) {
+        if (vv < nvox) {
+#pragma unroll
+          for (int k = 0; k < NC / 4; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + vv * NC + 4 * k);
+          t = lab[vv];
+        }
+      };
+      load(v, cur, tcur);
+      for (; v < nvox; v += stride) {
+        load(v + stride, nxt, tnxt);
+        float x[NC], e[NC];
+#pragma unroll
+        for (int k = 0; k < NC / 4; ++k)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[4 * k + j] = cur[k][j];
+        float m = x[0];
+#pragma unroll
+        for (int c = 1; c < NC; ++c) m = fmaxf(m, x[c]);
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          x[c] -= m;
+          e[c] = __builtin_amdgcn_exp2f(x[c] * LOG2E);
+          s += e[c];
+        }
+        const float inv = __builtin_amdgcn_rcpf(s), ls = __builtin_amdgcn_logf(s) * LN2;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const bool hit = tcur == (float)c;
+          const float tc = hit ? 1.f : 0.f, p = e[c] * inv;
+          acc[0][c] = fmaf(p, tc, acc[0][c]);
+          acc[1][c] = fmaf(p, p, acc[1][c]);
+          acc[2][c] += tc;
+          if (uce == 1) {
+            const float lq = hit ? x[c] - ls : __builtin_amdgcn_logf(s - e[c]) * LN2 - ls;
+            acc[3][c] -= fmaxf(lq, -100.f);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < NC / 4; ++k) cur[k] = nxt[k];
+        tcur = tnxt;
+      }
+      goto reduce;
+    }
+  }
+  for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < nvox; v += stride) {
     const float t = lab[v];
     if (softmax == 1) {
       float x[NC], e[NC], s, inv;
@@ -131,6 +184,7 @@ __global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restric
         }
     }
   }
+reduce:
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < 4; ++k)
