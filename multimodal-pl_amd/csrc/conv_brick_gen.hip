@@ -286,7 +286,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
 // epilogue is register-only (permlane32 swap, residual add, two 16-B stores per lane and co block) and never
 // touches the LDS the next unit's halo is being written into. Same operands, same fp32 accumulation order per
 // output (chunk, tap plane, tap, k-half) as convg_brick_kernel: bitwise-equal results.
-template <int CO, bool FLIP, int abl = 0>
+template <int CO, bool FLIP, int abl = 0, int BWX = 16>
 __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                                bf16* __restrict__ y, const bf16* __restrict__ res,
                                                                const float* __restrict__ gstat,
@@ -296,7 +296,20 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   constexpr int TN = CO / 32;
   constexpr int WROWS = 9 * CO;
   constexpr int WLD = (WROWS * 4 + GB_NT - 1) / GB_NT;
-  __shared__ __attribute__((aligned(16))) char hal[4 * GB_PS];
+  // brick 4 x 8 x BWX: BWX = 16 -> 16 row tiles of (2 h-rows x 16 w), TM = 2 per wave; BWX = 8 (8- but not 16-multiple
+  // planes, e.g. 24^3: no half-empty bricks) -> 8 row tiles of (4 h-rows x 8 w), TM = 1 per wave
+  constexpr int BW = BWX, HH = GB_BH + 2, HW = BW + 2, NH = (GB_BD + 2) * HH * HW;
+  constexpr int HLD = (NH + GB_NT / 4 - 1) / (GB_NT / 4), PS = NH * 16 + 64, TM = BW / 8;
+  static_assert(BW == 16 || BW == 8, "brick width");
+  // MFMA row r of row tile rt -> (d, h, w) inside the brick
+  auto tile_vox = [](int rt, int r, int& vd, int& vh, int& vw) {
+    if constexpr (BW == 16) {
+      vd = rt >> 2; vh = 2 * (rt & 3) + gb_seg(r); vw = gb_pos(r);
+    } else {
+      vd = rt >> 1; vh = 4 * (rt & 1) + (r >> 3); vw = r & 7;
+    }
+  };
+  __shared__ __attribute__((aligned(16))) char hal[4 * PS];
   __shared__ __attribute__((aligned(16))) char wbuf[2][4 * WROWS * 16];
   // GroupNorm (scale, shift) per input channel of the samples in flight, slot = sample & 1: filled once per sample
   // (the staging reads it from LDS — no global loads whose wait would drain the halo/weight prefetch)
@@ -326,11 +339,11 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     const int bh_ = b % g.nbh; b /= g.nbh;
     const int bd_ = b % g.nbd;
     q.nn = b / g.nbd;
-    q.d0 = bd_ * GB_BD; q.h0 = bh_ * GB_BH; q.w0 = bw_ * GB_BW;
+    q.d0 = bd_ * GB_BD; q.h0 = bh_ * GB_BH; q.w0 = bw_ * BW;
     return q;
   };
 
-  u32x4 hpre[GB_HLD];
+  u32x4 hpre[HLD];
   unsigned hmask = 0;  // bit i: staged piece i is inside the volume (GroupNorm'd; padding stays zero)
   u32x4 wpre[WLD];
   const int sch = tid & 3, srow0 = tid >> 2;
@@ -349,11 +362,11 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     stg_c = c;
     if constexpr ((abl & 4) != 0) return;
 #pragma unroll
-    for (int i = 0; i < GB_HLD; ++i) {
+    for (int i = 0; i < HLD; ++i) {
       const int row = srow0 + i * (GB_NT / 4);
       u32x4 v = {0u, 0u, 0u, 0u};
-      if (row < GB_NH) {
-        const int hw = row % GB_HW, hr = (row / GB_HW) % GB_HH, hd = row / (GB_HW * GB_HH);
+      if (row < NH) {
+        const int hw = row % HW, hr = (row / HW) % HH, hd = row / (HW * HH);
         const int zd = q.d0 - 1 + hd, zh = q.h0 - 1 + hr, zw = q.w0 - 1 + hw;
         const int cc = c * 32 + sch * 8;
         if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w) {
@@ -378,12 +391,12 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       }
     }
 #pragma unroll
-    for (int i = 0; i < GB_HLD; ++i) {
+    for (int i = 0; i < HLD; ++i) {
       const int row = srow0 + i * (GB_NT / 4);
-      if (row < GB_NH) {
+      if (row < NH) {
         u32x4 v = hpre[i];
         if (has_gn && ((hmask >> i) & 1u)) v = gn_relu8(v, sc, sh);
-        *reinterpret_cast<u32x4*>(hal + sch * GB_PS + row * 16) = v;
+        *reinterpret_cast<u32x4*>(hal + sch * PS + row * 16) = v;
       }
     }
   };
@@ -418,11 +431,12 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
 
   // per-lane A row of tap (0,0,0) for row tile tm (rt = 2*wave + tm -> (d = rt >> 2, h-pair = rt & 3)) and the
   // output voxel of MFMA column r
-  int arow[2];
+  int arow[TM];
 #pragma unroll
-  for (int tm = 0; tm < 2; ++tm) {
-    const int rt = 2 * wave + tm, vd = rt >> 2, vh = 2 * (rt & 3) + gb_seg(r);
-    arow[tm] = (vd * GB_HH + vh) * GB_HW + gb_pos(r);
+  for (int tm = 0; tm < TM; ++tm) {
+    int vd, vh, vw;
+    tile_vox(TM * wave + tm, r, vd, vh, vw);
+    arow[tm] = (vd * HH + vh) * HW + vw;
   }
 
   Unit cu = unit_geo(u_begin);
@@ -441,9 +455,9 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     // the next unit's sample table: its slot was last read before this unit's first barrier, and is first read at
     // the commit in this unit's last step (>= 1 barrier later)
     if (more && nu.nn != cu.nn) gtab_fill(nu.nn);
-    f32x16 acc[2][TN];
+    f32x16 acc[TM][TN];
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
@@ -463,33 +477,33 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       for (int j = 0; j < 9; ++j) {
         const int th = j / 3, tw = j % 3;
         const int oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
-        const int toff = (od * GB_HH + oh) * GB_HW + ow;
+        const int toff = (od * HH + oh) * HW + ow;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           const int plane = 2 * k + hh;
-          bf16x8 a[2], bb[TN];
+          bf16x8 a[TM], bb[TN];
           if constexpr (!(abl & 16)) {
 #pragma unroll
-            for (int tm = 0; tm < 2; ++tm)
-              a[tm] = *reinterpret_cast<const bf16x8*>(hal + plane * GB_PS + (arow[tm] + toff) * 16);
+            for (int tm = 0; tm < TM; ++tm)
+              a[tm] = *reinterpret_cast<const bf16x8*>(hal + plane * PS + (arow[tm] + toff) * 16);
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
               bb[tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
           } else {
 #pragma unroll
-            for (int tm = 0; tm < 2; ++tm) a[tm] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)(j + k), 1u, 2u, 3u});
+            for (int tm = 0; tm < TM; ++tm) a[tm] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)(j + k), 1u, 2u, 3u});
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) bb[tn] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)tn, 1u, 2u, 3u});
           }
           if constexpr (!(abl & 1)) {
 #pragma unroll
-            for (int tm = 0; tm < 2; ++tm)
+            for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
               for (int tn = 0; tn < TN; ++tn)
                 acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb[tn], a[tm], acc[tm][tn], 0, 0, 0);
           } else {
 #pragma unroll
-            for (int tm = 0; tm < 2; ++tm)
+            for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
               for (int tn = 0; tn < TN; ++tn) acc[tm][tn][0] += (float)a[tm][0] * 0.f + 0.f * (float)bb[tn][1];
           }
@@ -508,19 +522,20 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     // epilogue from registers: lane (r, hh) holds channels tn*32 + 8q + 4hh + e (acc[tm][tn][4q + e]) of voxel
     // ovox[tm]; after the swap it holds channels tn*32 + 8hh .. +7 and tn*32 + 16 + 8hh .. +7
     // this lane's output voxels (MFMA column r of row tiles 0, 1)
-    long long ovox[2];
-    bool ook[2];
+    long long ovox[TM];
+    bool ook[TM];
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm) {
-      const int rt = 2 * wave + tm;
-      const int zd = cu.d0 + (rt >> 2), zh = cu.h0 + 2 * (rt & 3) + gb_seg(r), zw = cu.w0 + gb_pos(r);
+    for (int tm = 0; tm < TM; ++tm) {
+      int vd, vh, vw;
+      tile_vox(TM * wave + tm, r, vd, vh, vw);
+      const int zd = cu.d0 + vd, zh = cu.h0 + vh, zw = cu.w0 + vw;
       ook[tm] = zd < g.d && zh < g.h && zw < g.w;
       ovox[tm] = (((long long)cu.nn * g.d + zd) * g.h + zh) * g.w + zw;
     }
-    u32x4 rv[2][TN][2];
+    u32x4 rv[TM][TN][2];
     if (res) {
 #pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
+      for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
@@ -539,7 +554,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     __syncthreads();
     par ^= 1;
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         uint32_t pk[4][2];
@@ -618,13 +633,36 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
   if ((!env_pers || atoi(env_pers) != 0) && (!gn_stats || g.cin_p <= GB_MAXC)) {
     const char* env_abl = getenv("U3D_PB_ABL");  // timing ablations (wrong results): see convg_pbrick_kernel
     const int abl = env_abl ? atoi(env_abl) : 0;
-    const int nunits = nb * g.nct, per = cdiv(nunits, convg_num_cus()), nwg = cdiv(nunits, per);
-#define U3D_PB(C, F)                                                                                              \
-  hipLaunchKernelGGL((convg_pbrick_kernel<C, F>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x, (const bf16*)wpk, \
-                     (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g, per, nunits)
+    // 8-wide bricks where the plane width is a multiple of 8 but not of 16 (24^3: the 16-wide bricks' second
+    // column is half empty); U3D_CONVG_BW8=0 / 1 forces the choice (A/B)
+    const char* e8 = getenv("U3D_CONVG_BW8");
+    const bool bw8 = abl == 0 && (e8 ? atoi(e8) != 0 : (w % 16 != 0 && w % 8 == 0));
+    GBGeom gp = g;
+    if (bw8) {
+      gp.nbw = cdiv(w, 8);
+      const long long nb8 = (long long)n * gp.nbd * gp.nbh * gp.nbw;
+      bool c64 = gp.cout_p >= 64;
+      if (c64 && env_co32 == 1) c64 = false;
+      if (c64 && env_co32 < 0 && nb8 * cdiv(cout, 64) < 128 && nb8 * cdiv(cout, 32) >= 128) c64 = false;
+      co64 = c64;
+      gp.nct = cdiv(cout, co64 ? 64 : 32);
+    }
+    const int nunits = n * gp.nbd * gp.nbh * gp.nbw * gp.nct, per = cdiv(nunits, convg_num_cus()),
+              nwg = cdiv(nunits, per);
+#define U3D_PB(C, F)                                                                                               \
+  do {                                                                                                             \
+    if (bw8)                                                                                                       \
+      hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 0, 8>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,          \
+                         (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
+                         nunits);                                                                                  \
+    else                                                                                                           \
+      hipLaunchKernelGGL((convg_pbrick_kernel<C, F>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,                \
+                         (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
+                         nunits);                                                                                  \
+  } while (0)
 #define U3D_PBA(A)                                                                                                \
   hipLaunchKernelGGL((convg_pbrick_kernel<64, false, A>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,           \
-                     (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g, per, nunits)
+                     (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per, nunits)
     if (abl && co64 && !flip) {
       switch (abl) {
         case 1: U3D_PBA(1); break;

@@ -1,9 +1,9 @@
 """Persistent generic brick conv (convg_pbrick_kernel, the default behind u3d_convg_brick) against the one-shot
 brick kernel (U3D_CONVG_PERSIST=0, the round-1 schedule, itself checked against fp64 in test_gpu_bf16.py and
 test_gpu_fullsize.py). Same operands, same per-output fp32 accumulation order: the results must be bitwise equal.
-Cases cover several units per workgroup (48^3-class grids), one unit per workgroup (24^3 x 128), 32-channel co
-tiles (the launcher's choice at 24^3 x 64), partial co tiles (cout 96), ragged volumes, GN prologue, residual, and
-the data gradient (flip). Reference: F.conv3d in Conv3d.forward (unet3D.py:27) through NoBottleneck (:56-73)."""
+Cases cover several units per workgroup (48^3-class grids), the 8-wide bricks of 8- but not 16-multiple planes
+(24^3), 32-channel co tiles (the launcher's choice at 24^3 x 64), partial co tiles (cout 96), ragged volumes, GN
+prologue, residual, and the data gradient (flip). Reference: F.conv3d in Conv3d.forward (unet3D.py:27) through NoBottleneck (:56-73)."""
 import os
 
 import pytest
@@ -20,6 +20,10 @@ CASES = [  # n, cin, cout, (d, h, w), gn, res, flip
     (1, 64, 96, (13, 17, 35), True, True, False),
     (3, 96, 64, (9, 20, 19), False, True, True),
     (1, 40, 48, (10, 30, 33), True, False, False),
+    # 8-wide bricks (plane width a multiple of 8, not of 16): ragged d / h, partial co tile, flip
+    (1, 64, 96, (13, 17, 40), True, True, False),
+    (3, 32, 64, (5, 9, 24), False, True, True),
+    (2, 128, 64, (24, 24, 24), False, False, True),
 ]
 
 
