@@ -218,6 +218,17 @@ int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, int h, int w
                     const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                     const void* residual, void* y, u3d_stream_t stream);
 
+/* u3d_convg_brick forward (flip = 0) that also returns the GroupNorm(16) statistics [n][16][2] (mean, rstd) of its
+ * output (after the residual add, of the stored bf16 values) — the input of the next GroupNorm in NoBottleneck
+ * (unet3D.py:44-53) — from per-unit channel-pair partials accumulated in the persistent kernel's epilogue
+ * (stats_ws, >= u3d_convg_brick_stats_ws_floats floats) and a fixed-order fp64 finalize. Replaces the separate
+ * statistics pass over y. Requires cout % 32 == 0 and cin <= 256 with a GN prologue. */
+long long u3d_convg_brick_stats_ws_floats(int n, int d, int h, int w, int cout);
+int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                          const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                          const void* residual, void* y, float* stats_ws, long long ws_floats, float* stats_out,
+                          u3d_stream_t stream);
+
 /* bf16 3^3 weight gradient in halo-brick form (ds_read_b64_tr_b16 operands, all 27 taps per workgroup);
  * same partial-slab output as u3d_conv_wgrad (nsplit from u3d_conv_wgrad_brick_splits). */
 int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, int cout, int stride);

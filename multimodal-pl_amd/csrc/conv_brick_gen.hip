@@ -292,7 +292,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
                                                                const float* __restrict__ gstat,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta, GBGeom g, int per,
-                                                               int nunits) {
+                                                               int nunits, float* __restrict__ spart = nullptr) {
   constexpr int TN = CO / 32;
   constexpr int WROWS = 9 * CO;
   constexpr int WLD = (WROWS * 4 + GB_NT - 1) / GB_NT;
@@ -314,6 +314,8 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   // GroupNorm (scale, shift) per input channel of the samples in flight, slot = sample & 1: filled once per sample
   // (the staging reads it from LDS — no global loads whose wait would drain the halo/weight prefetch)
   __shared__ __attribute__((aligned(16))) f32x2 gtab[2][GB_MAXC];
+  // output GroupNorm statistics (spart != nullptr): per (wave, lane half, tn, run v, channel pair q) (sum, sum sq)
+  __shared__ f32x2 sst[8][2][TN * 2 * 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -553,6 +555,11 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     }
     __syncthreads();
     par ^= 1;
+    // (statistics of the stored bf16 outputs, per channel pair: the GN(16) groups of every cout % 32 == 0 hold
+    // whole pairs; fp32 per lane and unit, fixed-order reductions, fp64 across units in the finalize)
+    f32x2 ps[TN * 2 * 4];
+#pragma unroll
+    for (int i = 0; i < TN * 2 * 4; ++i) ps[i] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -584,9 +591,70 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
             store16<bf16>(reinterpret_cast<bf16*>(&o), a8);
           }
           if (ook[tm] && co < g.cout) *reinterpret_cast<u32x4*>(y + ovox[tm] * g.cout + co) = o;
+          if (spart != nullptr) {
+            float f8[8];
+            load16<bf16>(reinterpret_cast<const bf16*>(&o), f8);
+            const bool on = ook[tm] && co < g.cout;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float a0 = on ? f8[2 * q] : 0.f, a1 = on ? f8[2 * q + 1] : 0.f;
+              f32x2& t = ps[(tn * 2 + v) * 4 + q];
+              t[0] += a0 + a1;
+              t[1] = fmaf(a0, a0, fmaf(a1, a1, t[1]));
+            }
+          }
         }
       }
+    if (spart != nullptr) {  // reduce over the 32 voxels of each lane half, then the 8 waves in order
+#pragma unroll
+      for (int i = 0; i < TN * 2 * 4; ++i)
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          ps[i][0] += __shfl_xor(ps[i][0], o);
+          ps[i][1] += __shfl_xor(ps[i][1], o);
+        }
+      if (r == 0)
+#pragma unroll
+        for (int i = 0; i < TN * 2 * 4; ++i) sst[wave][hh][i] = ps[i];
+      __syncthreads();
+      if (tid < CO / 2) {  // channel pair tid of the tile: c = 2 tid -> (tn, v, hh, q)
+        const int c = 2 * tid, tn = c >> 5, w32 = c & 31, v = w32 >> 4, h_ = (w32 >> 3) & 1, q = (w32 & 7) >> 1;
+        f32x2 t = {0.f, 0.f};
+        for (int w = 0; w < 8; ++w) t += sst[w][h_][(tn * 2 + v) * 4 + q];
+        *reinterpret_cast<f32x2*>(spart + ((long long)u * CO + c)) = t;
+      }
+    }
     cu = nu;
+  }
+}
+
+// GroupNorm(16) (mean, rstd) of the persistent brick conv's output from its per-unit channel-pair partials
+// spart[unit][CO / 2][2] (unit = brick * nct + co tile): one wave per (sample, group), lanes strided over the
+// sample's bricks, pairs summed in order, fp64 butterfly in fixed order (deterministic)
+__global__ __launch_bounds__(64) void pbrick_gn_finalize_kernel(const float* __restrict__ spart, int co_tile, int nct,
+                                                               int bricks_per_sample, int cout, double m,
+                                                               float* __restrict__ stats) {
+  const int p = blockIdx.x, nn = p / 16, gr = p % 16, cpg = cout / 16;
+  double s1 = 0, s2 = 0;
+  for (int b = threadIdx.x; b < bricks_per_sample; b += 64) {
+    const long long brick = (long long)nn * bricks_per_sample + b;
+    for (int c = gr * cpg; c < (gr + 1) * cpg; c += 2) {
+      const int ct = c / co_tile, cl = c - ct * co_tile;
+      const float* q = spart + ((brick * nct + ct) * co_tile + cl);
+      s1 += q[0];
+      s2 += q[1];
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  if (threadIdx.x == 0) {
+    const double mean = s1 / m;
+    double var = s2 / m - mean * mean;
+    if (var < 0) var = 0;
+    stats[p * 2] = (float)mean;
+    stats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
   }
 }
 
@@ -604,9 +672,9 @@ static int convg_num_cus() {
   return n;
 }
 
-extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
-                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                               const void* residual, void* y, u3d_stream_t stream) {
+static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                      const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                      const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && n <= GB_MAXN, "convg_brick: bad args");
   U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "convg_brick: channels must be multiples of 8");
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "convg_brick: bad GN");
@@ -630,7 +698,9 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
   dim3 grid(nb * g.nct);
   // persistent form (U3D_CONVG_PERSIST=0: the one-shot kernel; read per call so a test can compare both in-process)
   const char* env_pers = getenv("U3D_CONVG_PERSIST");
-  if ((!env_pers || atoi(env_pers) != 0) && (!gn_stats || g.cin_p <= GB_MAXC)) {
+  const bool pers = (!env_pers || atoi(env_pers) != 0) && (!gn_stats || g.cin_p <= GB_MAXC);
+  U3D_REQUIRE(!spart || (pers && !flip && cout % 32 == 0), "convg_brick_stats: needs the persistent forward, cout %% 32 == 0");
+  if (pers) {
     const char* env_abl = getenv("U3D_PB_ABL");  // timing ablations (wrong results): see convg_pbrick_kernel
     const int abl = env_abl ? atoi(env_abl) : 0;
     // 8-wide bricks where the plane width is a multiple of 8 but not of 16 (24^3: the 16-wide bricks' second
@@ -654,16 +724,16 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
     if (bw8)                                                                                                       \
       hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 0, 8>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,          \
                          (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
-                         nunits);                                                                                  \
+                         nunits, spart);                                                                           \
     else                                                                                                           \
       hipLaunchKernelGGL((convg_pbrick_kernel<C, F>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,                \
                          (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
-                         nunits);                                                                                  \
+                         nunits, spart);                                                                           \
   } while (0)
 #define U3D_PBA(A)                                                                                                \
   hipLaunchKernelGGL((convg_pbrick_kernel<64, false, A>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,           \
                      (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per, nunits)
-    if (abl && co64 && !flip) {
+    if (abl && co64 && !flip && !spart) {
       switch (abl) {
         case 1: U3D_PBA(1); break;
         case 2: U3D_PBA(2); break;
@@ -684,7 +754,11 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
       if (flip) U3D_PB(32, true); else U3D_PB(32, false);
     }
 #undef U3D_PB
-    return check_launch("convg_pbrick_kernel");
+    int rc = check_launch("convg_pbrick_kernel");
+    if (rc || !spart) return rc;
+    hipLaunchKernelGGL(pbrick_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, spart, co64 ? 64 : 32, gp.nct,
+                       gp.nbd * gp.nbh * gp.nbw, cout, (double)(cout / 16) * d * h * w, stats_out);
+    return check_launch("pbrick_gn_finalize_kernel");
   }
   if (co64) {
     if (flip)
@@ -702,4 +776,26 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
                          (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
   }
   return check_launch("convg_brick_kernel");
+}
+
+extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                               const void* residual, void* y, u3d_stream_t stream) {
+  return convg_impl(flip, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, nullptr,
+                    nullptr, stream);
+}
+
+extern "C" long long u3d_convg_brick_stats_ws_floats(int n, int d, int h, int w, int cout) {
+  // upper bound over both brick widths and co tiles: units x 64 floats
+  return (long long)n * cdiv(d, GB_BD) * cdiv(h, GB_BH) * cdiv(w, 8) * cdiv(cout, 32) * 64;
+}
+
+extern "C" int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                                     const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                                     const void* residual, void* y, float* stats_ws, long long ws_floats,
+                                     float* stats_out, u3d_stream_t stream) {
+  U3D_REQUIRE(stats_ws && stats_out, "convg_brick_stats: null statistics buffers");
+  U3D_REQUIRE(ws_floats >= u3d_convg_brick_stats_ws_floats(n, d, h, w, cout), "convg_brick_stats: workspace too small");
+  return convg_impl(0, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
+                    stats_out, stream);
 }

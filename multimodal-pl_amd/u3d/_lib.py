@@ -52,6 +52,8 @@ _SIGS = {
     "u3d_conv_wgrad_ring_splits": [I, I, I, I, I, I],
     "u3d_conv_wgrad_ring": [P, P, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_convg_brick": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P],
+    "u3d_convg_brick_stats_ws_floats": [I, I, I, I, I],
+    "u3d_convg_brick_stats": [P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P, P],
     "u3d_conv_wgrad_brick_splits": [I, I, I, I, I, I, I],
     "u3d_conv_wgrad_brick": [P, P, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_conv_wgrad1_splits": [I, I, I, I, I, I, I],
@@ -113,7 +115,7 @@ _SIGS = {
 }
 _RESTYPE = {"u3d_upsample2x_stats_ws_bytes": L, "u3d_stem_fwd_stats_ws_bytes": L, "u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
             "u3d_eam_attn_bwd_part_floats": L, "u3d_upsample_trilinear_bwd_ws_floats": L, "u3d_renew_token_ws_bytes": L,
-            "u3d_consistency_ws_bytes": L, "u3d_volume_stats_ws_bytes": L}
+            "u3d_consistency_ws_bytes": L, "u3d_volume_stats_ws_bytes": L, "u3d_convg_brick_stats_ws_floats": L}
 
 _lib = None
 

@@ -265,6 +265,20 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
         fin = "u3d_conv32_ring_q_stats_finalize" if q else "u3d_conv32_ring_stats_finalize"
         call(fin, ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
         return y, stats
+    if (BRICK_STATS and cout % 32 == 0 and cin <= 256 and k == 3 and stride == 1
+            and _use_gen_brick(x.dtype, cin, cout, k, stride, (n, d, h, w_))
+            and not _use_conv1x1(x.dtype, cin, cout, k, n) and not _use_conv32(x.dtype, cin, cout, k, stride, n, w_)
+            and not _use_small(x.dtype, cin, cout, k, stride, (n, d, h, w_))
+            and os.environ.get("U3D_CONVG_PERSIST", "1") != "0"):
+        # persistent brick conv with the output's GroupNorm(16) statistics from its epilogue (no statistics pass)
+        st, ga, be, G = gn if gn is not None else (None, None, None, 0)
+        y = torch.empty((n, d, h, w_, cout), dtype=x.dtype, device=x.device)
+        stats = torch.empty((n, 16, 2), dtype=torch.float32, device=x.device)
+        nws = query("u3d_convg_brick_stats_ws_floats", n, d, h, w_, cout)
+        ws = WS.get(4 * nws, x.device, slot=9)
+        call("u3d_convg_brick_stats", x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga),
+             _ptr(be), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), nws, stats.data_ptr(), _stream())
+        return y, stats
     return conv_fwd(x, wpk, cout, k, stride, gn, residual), None
 
 
@@ -290,6 +304,7 @@ def _queue(device, shape):
     return WS.get(query("u3d_conv32_ring_q_queue_bytes", *shape), device, slot=QUEUE_SLOT).data_ptr()
 
 
+BRICK_STATS = os.environ.get("U3D_BRICK_STATS", "1") != "0"  # GN statistics from the persistent brick's epilogue
 RING_STATS = os.environ.get("U3D_RING_STATS", "1") != "0"  # GroupNorm statistics from the ring conv epilogue (False: separate u3d_gn_stats pass)
 SPLITK_WS_BYTES = 64 << 20
 PROBE = None  # list -> conv32_brick forward launches record (start, end, voxels) HIP events (bench.py roofline)

@@ -218,7 +218,7 @@ class Tape:
         st16 = None
         if head:  # precls_conv: streaming MFMA head (head.hip)
             y = ops.head_fwd(x.t, pf, cout, b, gn)
-        elif gn is not None and b is None and not out_f32 and cout == 32:
+        elif gn is not None and b is None and not out_f32 and (cout == 32 or (ops.BRICK_STATS and cout % 32 == 0)):
             y, st16 = ops.conv_fwd_stats(x.t, pf, cout, k, stride, gn, residual.t if residual is not None else None)
         else:
             y = ops.conv_fwd(x.t, pf, cout, k, stride, gn, residual.t if residual is not None else None, b, out_f32)
