@@ -85,6 +85,9 @@ for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 
     CASES[f"dgrad{lvl}"] = (lambda s=s, c=c: _dgrad(2, c, c, s, 3, 1))
     CASES[f"wgrad{lvl}"] = (lambda s=s, c=c: _wgrad(2, c, c, s, 3, 1))
 CASES["fwd12nogn"] = lambda: _fwd(2, 256, 256, 12, 3, 1, False, False)
+CASES["wgrad_s2_96"] = lambda: _wgrad(2, 32, 64, 96, 3, 2)
+CASES["wgrad_s2_48"] = lambda: _wgrad(2, 64, 128, 48, 3, 2)
+CASES["wgrad_s2_24"] = lambda: _wgrad(2, 128, 256, 24, 3, 2)
 CASES["fwd_s2_24"] = lambda: _fwd(2, 128, 256, 24, 3, 2, True, False)
 CASES["dgrad_s2_24"] = lambda: _dgrad(2, 128, 256, 24, 3, 2)
 CASES["dgrad_s2_96"] = lambda: _dgrad(2, 32, 64, 96, 3, 2)
