@@ -258,6 +258,61 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
     kb[c] = e;
   }
   __syncthreads();
+  if constexpr (NC == 16 && sizeof(TO) == 4) {
+    if (softmax == 1 && uce == 1 && C == NC) {
+      // software-pipelined softmax + BCE path (the bench's loss): the next voxel's logits and label are loaded
+      // before this voxel's math; same arithmetic as the generic loop below
+      const long long stride = (long long)gridDim.x * LT;
+      long long v = blockIdx.x * (long long)LT + threadIdx.x;
+      f32x4 cur[4], nxt[4];
+      float tcur = 0.f, tnxt = 0.f;
+      auto load = [&](long long vv, f32x4 (&q)[4], float& t) {
+        if (vv < nvox) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + vv * 16 + 4 * k);
+          t = lab[vv];
+        }
+      };
+      load(v, cur, tcur);
+      for (; v < nvox; v += stride) {
+        load(v + stride, nxt, tnxt);
+        float x[16], p[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[4 * k + j] = cur[k][j];
+        float m = x[0];
+#pragma unroll
+        for (int c = 1; c < 16; ++c) m = fmaxf(m, x[c]);
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          p[c] = __builtin_amdgcn_exp2f((x[c] - m) * LOG2E);
+          s += p[c];
+        }
+        const float inv = __builtin_amdgcn_rcpf(s);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) p[c] *= inv;
+        float g[16], dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const float tc = (tcur == (float)c) ? 1.f : 0.f;
+          float gc = fmaf(tc, kd_a[c], p[c] * kd_b[c]);
+          gc += kb[c] * (p[c] - tc) * __builtin_amdgcn_rcpf(fmaxf((1.f - p[c]) * p[c], 1e-12f));
+          g[c] = gc;
+          dot = fmaf(gc, p[c], dot);
+        }
+#pragma unroll
+        for (int c = 0; c < 16; c += 4)
+          *reinterpret_cast<f32x4*>(dl + v * 16 + c) = f32x4{p[c] * (g[c] - dot), p[c + 1] * (g[c + 1] - dot),
+                                                             p[c + 2] * (g[c + 2] - dot), p[c + 3] * (g[c + 3] - dot)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+        tcur = tnxt;
+      }
+      return;
+    }
+  }
   for (long long v = blockIdx.x * (long long)LT + threadIdx.x; v < nvox; v += (long long)gridDim.x * LT) {
     float p[NC], g[NC];
     if (softmax == 1) {
