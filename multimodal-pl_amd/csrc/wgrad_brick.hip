@@ -370,7 +370,11 @@ extern "C" int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, 
   const int od = (d - 1) / stride + 1, oh = (h - 1) / stride + 1, ow = (w - 1) / stride + 1;
   const long long nb = (long long)n * cdiv(od, bd) * cdiv(oh, bh) * cdiv(ow, bw);
   const long long tiles = (long long)cdiv(cin, 32) * cdiv(cout, 32);
-  long long want = std::max(1LL, 256 / tiles);
+  static const long long target = [] {  // workgroups aimed at (U3D_WB_WGS: experiments)
+    const char* e = getenv("U3D_WB_WGS");
+    return e ? std::max(1LL, atoll(e)) : 256LL;
+  }();
+  long long want = std::max(1LL, target / tiles);
   const long long ns = std::max(1LL, std::min(want, nb));
   const long long per = (nb + ns - 1) / ns;
   return (int)((nb + per - 1) / per);  // splits that all receive bricks: no zero-filled slabs

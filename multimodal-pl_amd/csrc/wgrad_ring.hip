@@ -315,7 +315,11 @@ extern "C" int u3d_conv_wgrad_ring_splits(int n, int cin, int d, int h, int w, i
   WRGeom g;
   wr_geom(n, cin, d, h, w, cout, g);
   const long long tiles = (long long)(g.cin_p / 32) * (g.cout_p / 32);
-  const long long want = std::max(1LL, std::min(g.planes, 256 / tiles));
+  static const long long target = [] {  // workgroups aimed at (U3D_WR_WGS: experiments)
+    const char* e = getenv("U3D_WR_WGS");
+    return e ? std::max(1LL, atoll(e)) : 256LL;
+  }();
+  const long long want = std::max(1LL, std::min(g.planes, target / tiles));
   const long long per = (g.planes + want - 1) / want;
   return (int)((g.planes + per - 1) / per);  // every split receives planes: no zero-filled slabs
 }
