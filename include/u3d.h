@@ -224,6 +224,15 @@ int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, int h, int w
  * (stats_ws, >= u3d_convg_brick_stats_ws_floats floats) and a fixed-order fp64 finalize. Replaces the separate
  * statistics pass over y. Requires cout % 32 == 0 and cin <= 256 with a GN prologue. */
 long long u3d_convg_brick_stats_ws_floats(int n, int d, int h, int w, int cout);
+/* u3d_convg_brick data gradient (dy [n][d][h][w][cout] -> dA [..][cin], wpk = data-grad pack) of a conv whose forward
+ * had the GroupNorm + ReLU prologue gn(x) (x = the GN input, gn_* = that GroupNorm): also forms, from per-channel
+ * partial sums (sum m dA, sum m dA x) taken in the epilogue, the GN-backward apply coefficients coef[n][5][cin] and
+ * dgamma / dbeta (accumulated when accumulate_params) for u3d_gn_bwd_apply_coef — no partial pass over dA and x.
+ * part_ws >= u3d_convg_brick_stats_ws_floats(n, d, h, w, 2 * cin) floats; cin <= 256, n <= 16. */
+int u3d_convg_brick_dgrad_gn(const void* dy, int n, int cout, int d, int h, int w, const void* wpk_dgrad, int cin,
+                             const void* x, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
+                             int gn_groups, void* dA, float* part_ws, long long ws_floats, float* coef, float* dgamma,
+                             float* dbeta, int accumulate_params, u3d_stream_t stream);
 int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                           const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                           const void* residual, void* y, float* stats_ws, long long ws_floats, float* stats_out,

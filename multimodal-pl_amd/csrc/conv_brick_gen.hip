@@ -286,18 +286,21 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
 // epilogue is register-only (permlane32 swap, residual add, two 16-B stores per lane and co block) and never
 // touches the LDS the next unit's halo is being written into. Same operands, same fp32 accumulation order per
 // output (chunk, tap plane, tap, k-half) as convg_brick_kernel: bitwise-equal results.
-template <int CO, bool FLIP, int abl = 0, int BWX = 16>
+template <int CO, bool FLIP, int abl = 0, int BWX = 16, bool BGT = false>
 __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                                bf16* __restrict__ y, const bf16* __restrict__ res,
                                                                const float* __restrict__ gstat,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta, GBGeom g, int per,
-                                                               int nunits, float* __restrict__ spart = nullptr) {
+                                                               int nunits, float* __restrict__ spart = nullptr,
+                                                               float* __restrict__ bgpart = nullptr) {
   constexpr int TN = CO / 32;
   constexpr int WROWS = 9 * CO;
   constexpr int WLD = (WROWS * 4 + GB_NT - 1) / GB_NT;
   // brick 4 x 8 x BWX: BWX = 16 -> 16 row tiles of (2 h-rows x 16 w), TM = 2 per wave; BWX = 8 (8- but not 16-multiple
   // planes, e.g. 24^3: no half-empty bricks) -> 8 row tiles of (4 h-rows x 8 w), TM = 1 per wave
+  // GN-backward partials in the data-gradient epilogue (compile time: the plain data gradient keeps its registers)
+  constexpr bool BGC = FLIP && BGT;
   constexpr int BW = BWX, HH = GB_BH + 2, HW = BW + 2, NH = (GB_BD + 2) * HH * HW;
   constexpr int HLD = (NH + GB_NT / 4 - 1) / (GB_NT / 4), PS = NH * 16 + 64, TM = BW / 8;
   static_assert(BW == 16 || BW == 8, "brick width");
@@ -316,6 +319,9 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   __shared__ __attribute__((aligned(16))) f32x2 gtab[2][GB_MAXC];
   // output GroupNorm statistics (spart != nullptr): per (wave, lane half, tn, run v, channel pair q) (sum, sum sq)
   __shared__ f32x2 sst[8][2][TN * 2 * 4];
+  // data gradient with the GN-backward partials (bgpart, FLIP): per (wave, lane half, tn, run v, channel e)
+  // (sum m dA, sum m dA x) of the GroupNorm + ReLU in front of the forward conv; res = that GN's input x
+  __shared__ f32x2 bst[BGC ? 8 : 1][2][BGC ? TN * 2 * 8 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -327,6 +333,8 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   const int u_begin = bid * per, u_end = min(nunits, u_begin + per);
   const int nct = g.nct;
   const bool has_gn = gstat != nullptr;
+  const bool pro_gn = !FLIP && has_gn;             // GN + ReLU prologue on the staged input (forward only)
+  const int gtc = FLIP ? g.cout : g.cin, gtc_p = FLIP ? g.cout_p : g.cin_p;  // channels of the LDS GN table
   const int nchunk = g.cin_p / 32;
   const int nsteps = nchunk * 3;
 
@@ -351,8 +359,8 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   const int sch = tid & 3, srow0 = tid >> 2;
   int stg_nn = 0, stg_c = 0;  // sample and chunk of the staged halo (GN table lookup at commit)
   auto gtab_fill = [&](int nn) {
-    if (has_gn && tid < g.cin_p) {
-      const int c = min(tid, g.cin - 1), gg = c / (g.cin / g.gn_groups);
+    if (has_gn && tid < gtc_p) {
+      const int c = min(tid, gtc - 1), gg = c / (gtc / g.gn_groups);
       const float mean = gstat[(nn * g.gn_groups + gg) * 2], rstd = gstat[(nn * g.gn_groups + gg) * 2 + 1];
       const float sc_ = rstd * gamma[c];
       gtab[nn & 1][tid] = f32x2{sc_, beta[c] - mean * sc_};
@@ -383,7 +391,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   auto halo_commit = [&]() {
     if constexpr ((abl & 8) != 0) return;
     f32x2 sc[4], sh[4];
-    if (has_gn) {
+    if (pro_gn) {
       const f32x2* t = &gtab[stg_nn & 1][stg_c * 32 + sch * 8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -397,7 +405,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       const int row = srow0 + i * (GB_NT / 4);
       if (row < NH) {
         u32x4 v = hpre[i];
-        if (has_gn && ((hmask >> i) & 1u)) v = gn_relu8(v, sc, sh);
+        if (pro_gn && ((hmask >> i) & 1u)) v = gn_relu8(v, sc, sh);
         *reinterpret_cast<u32x4*>(hal + sch * PS + row * 16) = v;
       }
     }
@@ -560,10 +568,15 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     f32x2 ps[TN * 2 * 4];
 #pragma unroll
     for (int i = 0; i < TN * 2 * 4; ++i) ps[i] = f32x2{0.f, 0.f};
+    f32x2 bs[BGC ? 2 * 8 : 1];  // BG: this tn's (v, e) channel sums (one co block at a time: fewer live registers)
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
+    for (int tn = 0; tn < TN; ++tn) {
+      if constexpr (BGC) {
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
+        for (int i = 0; i < 2 * 8; ++i) bs[i] = f32x2{0.f, 0.f};
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
         uint32_t pk[4][2];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -582,7 +595,24 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
         for (int v = 0; v < 2; ++v) {
           const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
           u32x4 o = {pk[2 * v][0], pk[2 * v][1], pk[2 * v + 1][0], pk[2 * v + 1][1]};
-          if (res) {
+          if constexpr (BGC) {
+            {  // m = relu mask of the forward GN prologue on x; gd = m dA (the stored bf16 dA)
+              float a8[8], x8[8];
+              load16<bf16>(reinterpret_cast<const bf16*>(&o), a8);
+              load16<bf16>(reinterpret_cast<const bf16*>(&rv[tm][tn][v]), x8);
+              const f32x2* gt = &gtab[cu.nn & 1][min(co, gtc_p - 8)];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const f32x2 cf = gt[e];
+                const bool on = ook[tm] && co + e < g.cout && fmaf(x8[e], cf[0], cf[1]) > 0.f;
+                const float gd = on ? a8[e] : 0.f;
+                f32x2& t = bs[v * 8 + e];
+                t[0] += gd;
+                t[1] = fmaf(gd, on ? x8[e] : 0.f, t[1]);
+              }
+            }
+          }
+          if (res && !BGC) {
             float a8[8], c8[8];
             load16<bf16>(reinterpret_cast<const bf16*>(&o), a8);
             load16<bf16>(reinterpret_cast<const bf16*>(&rv[tm][tn][v]), c8);
@@ -605,6 +635,28 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
           }
         }
       }
+      if constexpr (BGC) {  // this tn's channel sums: reduce over the 32 voxels of each lane half into the LDS
+#pragma unroll
+        for (int i = 0; i < 2 * 8; ++i)
+#pragma unroll
+          for (int o = 1; o < 32; o <<= 1) {
+            bs[i][0] += __shfl_xor(bs[i][0], o);
+            bs[i][1] += __shfl_xor(bs[i][1], o);
+          }
+        if (r == 0)
+#pragma unroll
+          for (int i = 0; i < 2 * 8; ++i) bst[wave][hh][tn * 16 + i] = bs[i];
+      }
+    }
+    if constexpr (BGC) {  // the 8 waves in order, per channel of the tile
+      __syncthreads();
+      if (tid < CO) {  // channel tid -> (tn, v, hh, e)
+        const int c = tid, tn = c >> 5, w32 = c & 31, v = w32 >> 4, h_ = (w32 >> 3) & 1, e = w32 & 7;
+        f32x2 t = {0.f, 0.f};
+        for (int w = 0; w < 8; ++w) t += bst[w][h_][tn * 16 + v * 8 + e];
+        *reinterpret_cast<f32x2*>(bgpart + ((long long)u * CO + c) * 2) = t;
+      }
+    }
     if (spart != nullptr) {  // reduce over the 32 voxels of each lane half, then the 8 waves in order
 #pragma unroll
       for (int i = 0; i < TN * 2 * 4; ++i)
@@ -658,6 +710,68 @@ __global__ __launch_bounds__(64) void pbrick_gn_finalize_kernel(const float* __r
   }
 }
 
+// GroupNorm backward coefficients from the data-gradient epilogue partials bgpart[unit][CO][2] = (sum m dA,
+// sum m dA x) per channel (unit = brick * nct + co tile), as ring_gn_bwd_coef_kernel for C <= 256 channels:
+//   s2 = sum m dA xhat = rstd (s3 - mean s1) per channel, then per group a = sum gamma s1 / M, b = sum gamma s2 / M,
+//   coef[n][5][C] = (sc, sh, rstd gamma, -rstd^2 b, -rstd a + rstd^2 b mean); dgamma = sum_n s2, dbeta = sum_n s1.
+// One block: one wave per (sample, channel) with lanes over the sample's bricks, fp64, fixed order.
+__global__ __launch_bounds__(1024) void pbrick_gn_bwd_coef_kernel(const float* __restrict__ part, int n, int C, int co_tile,
+                                                                 int nct, int bps, int groups, double m,
+                                                                 const float* __restrict__ stats,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, float* __restrict__ coef,
+                                                                 float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                                 int accp) {
+  __shared__ double cs[16][GB_MAXC][2];
+  const int cpg = C / groups, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int p = wave; p < n * C; p += 16) {
+    const int nn = p / C, c = p % C, gr = c / cpg, ct = c / co_tile, cl = c - ct * co_tile;
+    double s1 = 0, s3 = 0;
+    for (int b = lane; b < bps; b += 64) {
+      const float* q = part + ((((long long)nn * bps + b) * nct + ct) * co_tile + cl) * 2;
+      s1 += q[0];
+      s3 += q[1];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o);
+      s3 += __shfl_xor(s3, o);
+    }
+    if (lane == 0) {
+      const double mu = stats[(nn * groups + gr) * 2], rs = stats[(nn * groups + gr) * 2 + 1];
+      cs[nn][c][0] = s1;
+      cs[nn][c][1] = rs * (s3 - mu * s1);
+    }
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < n * C; p += 1024) {
+    const int nn = p / C, c = p % C, gr = c / cpg;
+    double a = 0, bb = 0;
+    for (int q = 0; q < cpg; ++q) {
+      const int cc = gr * cpg + q;
+      a += (double)gamma[cc] * cs[nn][cc][0];
+      bb += (double)gamma[cc] * cs[nn][cc][1];
+    }
+    const float ca = (float)(a / m), cb = (float)(bb / m);
+    const float mu = stats[(nn * groups + gr) * 2], rs = stats[(nn * groups + gr) * 2 + 1];
+    const float scv = rs * gamma[c];
+    float* o = coef + (long long)nn * 5 * C;
+    o[c] = scv;
+    o[C + c] = beta[c] - mu * scv;
+    o[2 * C + c] = rs * gamma[c];
+    o[3 * C + c] = -rs * rs * cb;
+    o[4 * C + c] = -rs * ca + rs * rs * cb * mu;
+  }
+  for (int c = threadIdx.x; c < C; c += 1024) {
+    double tg = 0, tb = 0;
+    for (int nn = 0; nn < n; ++nn) {
+      tb += cs[nn][c][0];
+      tg += cs[nn][c][1];
+    }
+    if (dgamma) dgamma[c] = (accp ? dgamma[c] : 0.f) + (float)tg;
+    if (dbeta) dbeta[c] = (accp ? dbeta[c] : 0.f) + (float)tb;
+  }
+}
+
 }  // namespace u3d
 
 using namespace u3d;
@@ -674,7 +788,9 @@ static int convg_num_cus() {
 
 static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                       const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                      const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream) {
+                      const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream,
+                      float* bgpart = nullptr, float* bg_coef = nullptr, float* dgamma = nullptr, float* dbeta = nullptr,
+                      int accp = 0) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && n <= GB_MAXN, "convg_brick: bad args");
   U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "convg_brick: channels must be multiples of 8");
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "convg_brick: bad GN");
@@ -700,7 +816,11 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
   const char* env_pers = getenv("U3D_CONVG_PERSIST");
   const bool pers = (!env_pers || atoi(env_pers) != 0) && (!gn_stats || g.cin_p <= GB_MAXC);
   U3D_REQUIRE(!spart || (pers && !flip && cout % 32 == 0), "convg_brick_stats: needs the persistent forward, cout %% 32 == 0");
-  if (pers) {
+  U3D_REQUIRE(!bgpart || (flip && (!env_pers || atoi(env_pers) != 0) && gn_stats && g.cout_p <= GB_MAXC && n <= 16 &&
+                          cout % gn_groups == 0 && bg_coef),
+              "convg_brick_dgrad_gn: needs the persistent data gradient, cout <= %d, n <= 16", GB_MAXC);
+  const bool pers_any = pers || bgpart;
+  if (pers_any) {
     const char* env_abl = getenv("U3D_PB_ABL");  // timing ablations (wrong results): see convg_pbrick_kernel
     const int abl = env_abl ? atoi(env_abl) : 0;
     // 8-wide bricks where the plane width is a multiple of 8 but not of 16 (24^3: the 16-wide bricks' second
@@ -721,7 +841,16 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
               nwg = cdiv(nunits, per);
 #define U3D_PB(C, F)                                                                                               \
   do {                                                                                                             \
-    if (bw8)                                                                                                       \
+    if (F && bgpart) {                                                                                             \
+      if (bw8)                                                                                                     \
+        hipLaunchKernelGGL((convg_pbrick_kernel<C, true, 0, 8, true>), dim3(nwg), dim3(GB_NT), 0, s,               \
+                           (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma,  \
+                           gn_beta, gp, per, nunits, nullptr, bgpart);                                             \
+      else                                                                                                         \
+        hipLaunchKernelGGL((convg_pbrick_kernel<C, true, 0, 16, true>), dim3(nwg), dim3(GB_NT), 0, s,              \
+                           (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma,  \
+                           gn_beta, gp, per, nunits, nullptr, bgpart);                                             \
+    } else if (bw8)                                                                                                \
       hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 0, 8>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,          \
                          (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
                          nunits, spart);                                                                           \
@@ -755,7 +884,14 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
     }
 #undef U3D_PB
     int rc = check_launch("convg_pbrick_kernel");
-    if (rc || !spart) return rc;
+    if (rc) return rc;
+    if (bgpart) {
+      hipLaunchKernelGGL(pbrick_gn_bwd_coef_kernel, dim3(1), dim3(1024), 0, s, bgpart, n, cout, co64 ? 64 : 32, gp.nct,
+                         gp.nbd * gp.nbh * gp.nbw, gn_groups, (double)(cout / gn_groups) * d * h * w, gn_stats, gn_gamma,
+                         gn_beta, bg_coef, dgamma, dbeta, accp);
+      return check_launch("pbrick_gn_bwd_coef_kernel");
+    }
+    if (!spart) return rc;
     hipLaunchKernelGGL(pbrick_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, spart, co64 ? 64 : 32, gp.nct,
                        gp.nbd * gp.nbh * gp.nbw, cout, (double)(cout / 16) * d * h * w, stats_out);
     return check_launch("pbrick_gn_finalize_kernel");
@@ -798,4 +934,21 @@ extern "C" int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h
   U3D_REQUIRE(ws_floats >= u3d_convg_brick_stats_ws_floats(n, d, h, w, cout), "convg_brick_stats: workspace too small");
   return convg_impl(0, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
                     stats_out, stream);
+}
+
+// u3d_convg_brick data gradient (flip = 1) of a conv whose forward had the GroupNorm + ReLU prologue gn(x) (x = the
+// GN input [n][d][h][w][cin]; gn_* = that GroupNorm): writes dA and, from partial sums taken in the epilogue, the
+// GN-backward apply coefficients coef[n][5][cin] (+ dgamma / dbeta, accumulated when accumulate_params) for
+// u3d_gn_bwd_apply_coef — no separate partial pass over dA and x (unet3D.py:44-53 autograd). part_ws: >=
+// u3d_convg_brick_stats_ws_floats(n, d, h, w, 2 * cin) floats.
+extern "C" int u3d_convg_brick_dgrad_gn(const void* dy, int n, int cout, int d, int h, int w, const void* wpk_dgrad,
+                                        int cin, const void* x, const float* gn_stats, const float* gn_gamma,
+                                        const float* gn_beta, int gn_groups, void* dA, float* part_ws,
+                                        long long ws_floats, float* coef, float* dgamma, float* dbeta,
+                                        int accumulate_params, u3d_stream_t stream) {
+  U3D_REQUIRE(dy && x && dA && part_ws && coef && gn_stats && gn_gamma && gn_beta && gn_groups > 0,
+              "convg_brick_dgrad_gn: bad args");
+  U3D_REQUIRE(ws_floats >= u3d_convg_brick_stats_ws_floats(n, d, h, w, 2 * cin), "convg_brick_dgrad_gn: workspace too small");
+  return convg_impl(1, dy, n, cout, d, h, w, wpk_dgrad, cin, gn_stats, gn_gamma, gn_beta, gn_groups, x, dA, nullptr,
+                    nullptr, stream, part_ws, coef, dgamma, dbeta, accumulate_params);
 }
