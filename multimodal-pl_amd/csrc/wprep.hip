@@ -226,22 +226,20 @@ __global__ __launch_bounds__(WB_T) void wstd_sum_slabs_kernel(WBatch<WSum> bt) {
   const bool in = i < D.per4;
   const f32x4* p = reinterpret_cast<const f32x4*>(D.p);
   double a[4] = {0, 0, 0, 0};
-  if (in) {
-    const int step = D.sg;
-    int s = q;
-    for (; s + 7 * step < D.ns; s += 8 * step) {
+  if (in && q < D.ns) {
+    const int step = D.sg, last = q + (D.ns - 1 - q) / step * step;  // this group's last slab
+    // rounds of 8 loads in flight, the partial last round with clamped addresses (straight-line loads; a slab
+    // count below 8 per group, e.g. the 4-16 slabs of the 12^3 / 6^3 weights, is not a chain of dependent loads);
+    // the adds run in slab order, so the sum is that of the serial walk
+    for (int s = q; s < D.ns; s += 8 * step) {
       f32x4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[(long long)(s + u * step) * D.per4 + i];
+      for (int u = 0; u < 8; ++u) v[u] = p[(long long)min(s + u * step, last) * D.per4 + i];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
+        if (s + u * step < D.ns)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) a[e] += v[u][e];
-    }
-    for (; s < D.ns; s += step) {
-      const f32x4 v = p[(long long)s * D.per4 + i];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) a[e] += v[e];
+          for (int e = 0; e < 4; ++e) a[e] += v[u][e];
     }
   }
   if (D.sg == 1) {

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Final-tree check: the whole GPU suite, then smoke().
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r02_final_gpu
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
