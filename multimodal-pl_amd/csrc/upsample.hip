@@ -3,6 +3,8 @@
 // `x = x + skip{3,2,1,0}` (unet3D.py:1764-1783); also the logit upsample of unet3D_g (:1621).
 // Source index per dim (PyTorch area_pixel_compute_source_index, scale 1/2):
 //   src = max(0, (o + 0.5) * 0.5 - 0.5); i0 = floor(src); i1 = i0 + (i0 < n-1); l1 = src - i0; l0 = 1 - l1.
+#include <cstdlib>
+
 #include "common.h"
 #include "gnpart.h"
 
@@ -121,6 +123,82 @@ __global__ __launch_bounds__(256) void up_bwd_kernel(const T* __restrict__ dy, T
     for (int e = 0; e < VEC; ++e) acc[e] += o[e];
   }
   storev<T, VEC>(dx + off, acc);
+}
+
+// The same gather for a 2 x 2 block of input rows (id0, id0 + 1) x (ih0, ih0 + 1) per thread: the w-partial sum of an
+// output row (od, oh) is computed once and added to every input row that reads it (6 x 6 output rows for 4 input
+// rows instead of 4 x 16). Each accumulator sees the same taps, weights and add order as up_bwd_kernel (od ascending,
+// then oh ascending, zero-weight taps skipped), so the results are bitwise equal.
+// grid: x = (iw, chunk) pairs of one input row, y = ih pair, z = n * ceil(d / 2) + id pair
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void up_bwd_blk_kernel(const T* __restrict__ dy, T* __restrict__ dx, int n, int c,
+                                                        int d, int h, int w, int accum) {
+  const int chn = c / VEC, D = 2 * d, H = 2 * h, W = 2 * w, dp = (d + 1) / 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w * chn) return;
+  const int j = i % chn, iw = i / chn, ih0 = 2 * blockIdx.y, id0 = 2 * (blockIdx.z % dp), nn = blockIdx.z / dp;
+  int ow_[4];
+  float ww[4];
+  const int cw = taps_of(iw, w, ow_, ww);
+  float acc[2][2][VEC];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[p][r][e] = 0.f;
+  const bool v1d = id0 + 1 < d, v1h = ih0 + 1 < h;
+  const T* yb = dy + (long long)nn * D * H * W * c + j * VEC;
+  for (int od = 2 * id0 - 1; od <= 2 * id0 + 4; ++od) {
+    if (od < 0 || od >= D) continue;
+    const float wd0 = wt_of(od, id0, d), wd1 = v1d ? wt_of(od, id0 + 1, d) : 0.f;
+    if (wd0 == 0.f && wd1 == 0.f) continue;
+    for (int oh = 2 * ih0 - 1; oh <= 2 * ih0 + 4; ++oh) {
+      if (oh < 0 || oh >= H) continue;
+      const float wh0 = wt_of(oh, ih0, h), wh1 = v1h ? wt_of(oh, ih0 + 1, h) : 0.f;
+      if (wh0 == 0.f && wh1 == 0.f) continue;
+      const T* yr = yb + ((long long)od * H + oh) * W * c;
+      float part[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) part[e] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q < cw) {
+          float v[VEC];
+          loadv<T, VEC>(yr + ow_[q] * c, v);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) part[e] = fmaf(ww[q], v[e], part[e]);
+        }
+      }
+      const float wdp[2] = {wd0, wd1}, whr[2] = {wh0, wh1};
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          if (wdp[p] != 0.f && whr[r] != 0.f) {
+            const float wdh = wdp[p] * whr[r];
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) acc[p][r][e] = fmaf(wdh, part[e], acc[p][r][e]);
+          }
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if ((p && !v1d) || (r && !v1h)) continue;
+      const long long off = ((((long long)nn * d + id0 + p) * h + ih0 + r) * w + iw) * c + j * VEC;
+      float o[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) o[e] = acc[p][r][e];
+      if (accum) {
+        float pv[VEC];
+        loadv<T, VEC>(dx + off, pv);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) o[e] += pv[e];
+      }
+      storev<T, VEC>(dx + off, o);
+    }
 }
 
 // Forward with the GroupNorm(16) statistics of the stored (bf16-rounded) output accumulated in the epilogue
@@ -245,6 +323,16 @@ extern "C" int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d
   const int row = w * (vect ? c / vec : c);
   U3D_REQUIRE((long long)n * d < 65536 && h < 65536, "upsample_bwd: volume too large for the row grid");
   const dim3 gr(cdiv(row, 256), h, n * d), bl(256);
+  // 2 x 2 input rows per thread with U3D_UP_BWD_BLK=1 (read per call; off by default until measured)
+  const char* eb = getenv("U3D_UP_BWD_BLK");
+  if (vect && eb && atoi(eb) != 0) {
+    const dim3 g2(cdiv(row, 256), cdiv(h, 2), n * cdiv(d, 2));
+    if (dtype == U3D_BF16)
+      hipLaunchKernelGGL((up_bwd_blk_kernel<bf16, 8>), g2, bl, 0, s, (const bf16*)dy, (bf16*)dx, n, c, d, h, w, accumulate);
+    else
+      hipLaunchKernelGGL((up_bwd_blk_kernel<float, 4>), g2, bl, 0, s, (const float*)dy, (float*)dx, n, c, d, h, w, accumulate);
+    return check_launch("up_bwd_blk_kernel");
+  }
   if (dtype == U3D_BF16) {
     if (vect) hipLaunchKernelGGL((up_bwd_kernel<bf16, 8>), gr, bl, 0, s, (const bf16*)dy, (bf16*)dx, n, c, d, h, w, accumulate);
     else hipLaunchKernelGGL((up_bwd_kernel<bf16, 1>), gr, bl, 0, s, (const bf16*)dy, (bf16*)dx, n, c, d, h, w, accumulate);
