@@ -1,4 +1,4 @@
-"""Trilinear x2 backward with 2 x 2 input rows per thread (up_bwd_blk_kernel behind u3d_upsample2x_bwd with U3D_UP_BWD_BLK=1)
+"""Trilinear x2 backward with 2 x 2 input rows per thread (up_bwd_blk_kernel, u3d_upsample2x_bwd's choice for grids of >= 1024 workgroups)
 against the one-row gather (U3D_UP_BWD_BLK=0, itself checked against torch autograd in test_gpu_parity.py). Same taps,
 weights and add order per output: bitwise equal. Odd d / h (a half-empty row pair), size-1 dims, accumulate, fp32 and
 bf16. Reference: nn.Upsample(scale_factor=2, mode='trilinear') (unet3D.py:1646)."""
