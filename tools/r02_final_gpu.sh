@@ -1,7 +1,7 @@
 #!/bin/bash
 # Final-tree check: the whole GPU suite, then smoke().
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r02_final_gpu
+O=$R/gpurun_out/r02_final_gpu2
 mkdir -p $O
 cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
