@@ -100,28 +100,41 @@ def dominant_kernel_roofline(device, batch, patch, live=None, reps=20):
             "peak_measured": measured_peak(achieved)}
 
 
+def newest_profile(suffix):
+    """The committed profile of the newest round: profiles/rNN_<suffix> with the highest NN; a plain `rNN_` file (the
+    final tree of that round) wins over the round's intermediate `rNN<tag>_` files, whatever their names sort as."""
+    import glob
+    import re
+    best = None
+    for f in glob.glob(os.path.join(REPO, "profiles", "r*_" + suffix)):
+        m = re.match(r"r(\d+)([a-z0-9]*)_" + re.escape(suffix) + "$", os.path.basename(f))
+        if m:
+            key = (int(m.group(1)), m.group(2) == "", m.group(2))
+            if best is None or key > best[0]:
+                best = (key, f)
+    return None if best is None else best[1]
+
+
 def pmc_traffic(batch, patch):
     """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
     (profiles/rNN_pmc_conv32_fwd.json, made by tools/pmc_traffic.py: 2*FETCH_SIZE + WRITE_SIZE, gfx950
     FETCH_SIZE correction). Only valid for the configuration it was measured on (2x96^3)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_conv32_fwd.json")))
-    if not files or (batch, patch) != (2, 96):
+    f = newest_profile("pmc_conv32_fwd.json")
+    if f is None or (batch, patch) != (2, 96):
         return None, None
-    with open(files[-1]) as f:
-        return int(json.load(f)["traffic_bytes"]), os.path.relpath(files[-1], REPO)
+    with open(f) as fh:
+        return int(json.load(fh)["traffic_bytes"]), os.path.relpath(f, REPO)
 
 
 def measured_peak(achieved):
     """The newest committed on-box calibration (profiles/rNN_peaks.json, tools/peak.hip: back-to-back bf16 MFMA on
     every CU at the clock held under load; HBM read/copy). `peak` stays the guide's dense figure; this is beside it."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_peaks.json")))
-    if not files:
+    f = newest_profile("peaks.json")
+    if f is None:
         return None
-    with open(files[-1]) as f:
-        c = json.load(f)
-    return {"file": os.path.relpath(files[-1], REPO), "mfma_bf16_tflops": c["mfma_bf16_dense_tflops"],
+    with open(f) as fh:
+        c = json.load(fh)
+    return {"file": os.path.relpath(f, REPO), "mfma_bf16_tflops": c["mfma_bf16_dense_tflops"],
             "hbm_read_gbs": c["hbm_read_gbs"], "frac_of_measured": round(achieved / c["mfma_bf16_dense_tflops"], 4)}
 
 
@@ -129,13 +142,12 @@ def timing_check(batch, patch, flops):
     """The newest committed cross-check of the live event timing against the rocprofv3 kernel trace of the same
     run (profiles/rNN_conv32_timing_check.json, tools/timing_check.py): reported beside `achieved`, with the
     roofline fraction the trace's in-step average gives. Only valid for the configuration it was measured on."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_conv32_timing_check.json")))
-    if not files or (batch, patch) != (2, 96):
+    f = newest_profile("conv32_timing_check.json")
+    if f is None or (batch, patch) != (2, 96):
         return None
-    with open(files[-1]) as f:
-        c = json.load(f)
-    return {"file": os.path.relpath(files[-1], REPO), "in_step_events_us": c["in_step_events_us"],
+    with open(f) as fh:
+        c = json.load(fh)
+    return {"file": os.path.relpath(f, REPO), "in_step_events_us": c["in_step_events_us"],
             "in_step_trace_us": c["in_step_trace_us"], "standalone_events_us": c["standalone_events_us"],
             "standalone_trace_us": c["standalone_trace_us"],
             "frac_at_trace_in_step": round(flops / (c["in_step_trace_us"] * 1e-6) / 1e12 / PEAK_BF16_TFLOPS, 4)}

@@ -38,6 +38,11 @@ typedef void* u3d_stream_t; /* hipStream_t */
 
 const char* u3d_last_error(void);
 int u3d_abi_version(void);
+/* Host-side tuning options (csrc/common.h enum Opt; names without the U3D_ prefix, e.g. "CONVG_PERSIST"). The defaults
+ * are the measured product routing; the environment (U3D_<NAME>) is read once at the first query, for A/B scripts;
+ * these two calls change / read a value in-process (tests comparing two routings). No reference counterpart. */
+int u3d_set_option(const char* name, int value);
+int u3d_get_option(const char* name, int* value);
 
 /* ---------------------------------------------------------------- weight standardisation (A1)
  * Replaces Conv3d.forward's weight.mean(...)/torch.var/div, unet3D.py:21-26, and packs the weight for

@@ -767,11 +767,9 @@ static int launch_igemm(Geom g, int n, const T* x, const T* wpk, TO* y, const T*
                         hipStream_t s) {
   const int Mq = g.qd * g.qh * g.qw;
   if (Mq <= 0) return U3D_OK;
-  static const int env_bn = [] { const char* e = getenv("U3D_IGEMM_BN"); return e ? atoi(e) : 0; }();
-  static const int env_ns = [] { const char* e = getenv("U3D_IGEMM_NS"); return e ? atoi(e) : 0; }();
-  static const int env_target = [] { const char* e = getenv("U3D_IGEMM_TARGET"); return e ? atoi(e) : 512; }();
+  const int env_bn = opt(OPT_IGEMM_BN), env_ns = opt(OPT_IGEMM_NS), env_target = opt(OPT_IGEMM_TARGET);
   int BN = g.cout_p <= 32 ? 32 : (sizeof(T) == 2 && g.cout_p >= 128) ? 128 : 64;
-  static const bool auto_bn = [] { const char* e = getenv("U3D_IGEMM_AUTO"); return !e || atoi(e) != 0; }();
+  const bool auto_bn = opt(OPT_IGEMM_AUTO) != 0;
   if (sizeof(T) == 2 && auto_bn) {
     // too few output tiles to fill the CUs: narrower N tiles before splitting K (measured, tools/igemm_sweep.sh:
     // 48^3 64->128 s2 91 -> 66 us at BN 64, 12^3 256->256 s2 50 -> 37 us at BN 32)

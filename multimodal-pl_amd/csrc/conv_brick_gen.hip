@@ -286,7 +286,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
 // epilogue is register-only (permlane32 swap, residual add, two 16-B stores per lane and co block) and never
 // touches the LDS the next unit's halo is being written into. Same operands, same fp32 accumulation order per
 // output (chunk, tap plane, tap, k-half) as convg_brick_kernel: bitwise-equal results.
-template <int CO, bool FLIP, int abl = 0, int BWX = 16, bool BGT = false>
+template <int CO, bool FLIP, int BWX = 16, bool BGT = false>
 __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                                bf16* __restrict__ y, const bf16* __restrict__ res,
                                                                const float* __restrict__ gstat,
@@ -370,7 +370,6 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     hmask = 0;
     stg_nn = q.nn;
     stg_c = c;
-    if constexpr ((abl & 4) != 0) return;
 #pragma unroll
     for (int i = 0; i < HLD; ++i) {
       const int row = srow0 + i * (GB_NT / 4);
@@ -389,7 +388,6 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     }
   };
   auto halo_commit = [&]() {
-    if constexpr ((abl & 8) != 0) return;
     f32x2 sc[4], sh[4];
     if (pro_gn) {
       const f32x2* t = &gtab[stg_nn & 1][stg_c * 32 + sch * 8];
@@ -411,7 +409,6 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     }
   };
   auto w_load = [&](int co0, int s) {
-    if constexpr ((abl & 2) != 0) return;
     const int c = s / 3, td = s % 3;
 #pragma unroll
     for (int i = 0; i < WLD; ++i) {
@@ -428,7 +425,6 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     }
   };
   auto w_commit = [&](int buf) {
-    if constexpr ((abl & 8) != 0) return;
 #pragma unroll
     for (int i = 0; i < WLD; ++i) {
       const int ci = tid + i * GB_NT;
@@ -492,31 +488,17 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
         for (int k = 0; k < 2; ++k) {
           const int plane = 2 * k + hh;
           bf16x8 a[TM], bb[TN];
-          if constexpr (!(abl & 16)) {
 #pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-              a[tm] = *reinterpret_cast<const bf16x8*>(hal + plane * PS + (arow[tm] + toff) * 16);
+          for (int tm = 0; tm < TM; ++tm)
+            a[tm] = *reinterpret_cast<const bf16x8*>(hal + plane * PS + (arow[tm] + toff) * 16);
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            bb[tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
-              bb[tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
-          } else {
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) a[tm] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)(j + k), 1u, 2u, 3u});
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) bb[tn] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)tn, 1u, 2u, 3u});
-          }
-          if constexpr (!(abl & 1)) {
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-              for (int tn = 0; tn < TN; ++tn)
-                acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb[tn], a[tm], acc[tm][tn], 0, 0, 0);
-          } else {
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-              for (int tn = 0; tn < TN; ++tn) acc[tm][tn][0] += (float)a[tm][0] * 0.f + 0.f * (float)bb[tn][1];
-          }
+              acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb[tn], a[tm], acc[tm][tn], 0, 0, 0);
         }
       }
       if (last) break;  // the last step's staging commit runs after the residual loads are issued (below)
@@ -805,28 +787,26 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
   // 64-channel decoder convs: 72 -> 144 workgroups, fwd 49 -> 25 us, dgrad 40 -> 20 us). Not below that: at 24^3 x 128
   // channels (144 workgroups with 64-channel tiles) 32-channel tiles measured slower (63.5 -> 78.7 us).
   // U3D_CONVG_CO32 = 0 / 1 forces the choice (experiments).
-  static const int env_co32 = [] { const char* e = getenv("U3D_CONVG_CO32"); return e ? atoi(e) : -1; }();
+  const int env_co32 = opt(OPT_CONVG_CO32);
   bool co64 = g.cout_p >= 64;
   if (co64 && env_co32 == 1) co64 = false;
   if (co64 && env_co32 < 0 && (long long)nb * cdiv(cout, 64) < 128 && (long long)nb * cdiv(cout, 32) >= 128)
     co64 = false;
   g.nct = cdiv(cout, co64 ? 64 : 32);
   dim3 grid(nb * g.nct);
-  // persistent form (U3D_CONVG_PERSIST=0: the one-shot kernel; read per call so a test can compare both in-process)
-  const char* env_pers = getenv("U3D_CONVG_PERSIST");
-  const bool pers = (!env_pers || atoi(env_pers) != 0) && (!gn_stats || g.cin_p <= GB_MAXC);
+  // persistent form (CONVG_PERSIST = 0: the one-shot kernel; u3d_set_option lets a test compare both in-process)
+  const bool pers_on = opt(OPT_CONVG_PERSIST) != 0;
+  const bool pers = pers_on && (!gn_stats || g.cin_p <= GB_MAXC);
   U3D_REQUIRE(!spart || (pers && !flip && cout % 32 == 0), "convg_brick_stats: needs the persistent forward, cout %% 32 == 0");
-  U3D_REQUIRE(!bgpart || (flip && (!env_pers || atoi(env_pers) != 0) && gn_stats && g.cout_p <= GB_MAXC && n <= 16 &&
+  U3D_REQUIRE(!bgpart || (flip && pers_on && gn_stats && g.cout_p <= GB_MAXC && n <= 16 &&
                           cout % gn_groups == 0 && bg_coef),
               "convg_brick_dgrad_gn: needs the persistent data gradient, cout <= %d, n <= 16", GB_MAXC);
   const bool pers_any = pers || bgpart;
   if (pers_any) {
-    const char* env_abl = getenv("U3D_PB_ABL");  // timing ablations (wrong results): see convg_pbrick_kernel
-    const int abl = env_abl ? atoi(env_abl) : 0;
     // 8-wide bricks where the plane width is a multiple of 8 but not of 16 (24^3: the 16-wide bricks' second
-    // column is half empty); U3D_CONVG_BW8=0 / 1 forces the choice (A/B)
-    const char* e8 = getenv("U3D_CONVG_BW8");
-    const bool bw8 = abl == 0 && (e8 ? atoi(e8) != 0 : (w % 16 != 0 && w % 8 == 0));
+    // column is half empty); CONVG_BW8 = 0 / 1 forces the choice (A/B)
+    const int e8 = opt(OPT_CONVG_BW8);
+    const bool bw8 = e8 >= 0 ? e8 != 0 : (w % 16 != 0 && w % 8 == 0);
     GBGeom gp = g;
     if (bw8) {
       gp.nbw = cdiv(w, 8);
@@ -843,15 +823,15 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
   do {                                                                                                             \
     if (F && bgpart) {                                                                                             \
       if (bw8)                                                                                                     \
-        hipLaunchKernelGGL((convg_pbrick_kernel<C, true, 0, 8, true>), dim3(nwg), dim3(GB_NT), 0, s,               \
+        hipLaunchKernelGGL((convg_pbrick_kernel<C, true, 8, true>), dim3(nwg), dim3(GB_NT), 0, s,               \
                            (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma,  \
                            gn_beta, gp, per, nunits, nullptr, bgpart);                                             \
       else                                                                                                         \
-        hipLaunchKernelGGL((convg_pbrick_kernel<C, true, 0, 16, true>), dim3(nwg), dim3(GB_NT), 0, s,              \
+        hipLaunchKernelGGL((convg_pbrick_kernel<C, true, 16, true>), dim3(nwg), dim3(GB_NT), 0, s,              \
                            (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma,  \
                            gn_beta, gp, per, nunits, nullptr, bgpart);                                             \
     } else if (bw8)                                                                                                \
-      hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 0, 8>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,          \
+      hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 8>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,          \
                          (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
                          nunits, spart);                                                                           \
     else                                                                                                           \
@@ -859,24 +839,6 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
                          (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
                          nunits, spart);                                                                           \
   } while (0)
-#define U3D_PBA(A)                                                                                                \
-  hipLaunchKernelGGL((convg_pbrick_kernel<64, false, A>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,           \
-                     (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per, nunits)
-    if (abl && co64 && !flip && !spart) {
-      switch (abl) {
-        case 1: U3D_PBA(1); break;
-        case 2: U3D_PBA(2); break;
-        case 4: U3D_PBA(4); break;
-        case 6: U3D_PBA(6); break;
-        case 14: U3D_PBA(14); break;
-        case 16: U3D_PBA(16); break;
-        case 17: U3D_PBA(17); break;
-        case 31: U3D_PBA(31); break;
-        default: return fail(U3D_EINVAL, "U3D_PB_ABL: unknown ablation %d", abl);
-      }
-      return check_launch("convg_pbrick_kernel");
-    }
-#undef U3D_PBA
     if (co64) {
       if (flip) U3D_PB(64, true); else U3D_PB(64, false);
     } else {

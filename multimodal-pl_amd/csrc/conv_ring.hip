@@ -964,21 +964,12 @@ __global__ __launch_bounds__(R2_NT, 1) void conv32_ring2_kernel(const bf16* __re
 
 using namespace u3d;
 
-static int ring_kr(int dflt) {  // U3D_RING_KR=0: no weight steps in registers (experiments)
-  static const int kr = [] {
-    const char* e = getenv("U3D_RING_KR");
-    return e ? atoi(e) : -1;
-  }();
+static int ring_kr(int dflt) {  // RING_KR = 0: no weight steps in registers (experiments)
+  const int kr = opt(OPT_RING_KR);
   return kr < 0 ? dflt : kr;
 }
 
-static int ring_wgs() {  // persistent grid size target (U3D_RING_WGS; default one workgroup per CU)
-  static const int v = [] {
-    const char* e = getenv("U3D_RING_WGS");
-    return e ? atoi(e) : 256;
-  }();
-  return v;
-}
+static int ring_wgs() { return std::max(1, opt(OPT_RING_WGS)); }  // persistent grid target: one workgroup per CU
 static bool ring_v2() {  // U3D_RING_V2=1: the register-blocked schedule (measured equal or slower: off)
   static const bool on = [] {
     const char* e = getenv("U3D_RING_V2");
@@ -1052,13 +1043,7 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
 }
 
 // ------------------------------------------------------------------------------------------- work-stealing mode
-static int ring_sc_env() {  // U3D_RING_SC: output planes per sub-chunk (experiments; 0 = default)
-  static const int v = [] {
-    const char* e = getenv("U3D_RING_SC");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+static int ring_sc_env() { return opt(OPT_RING_SC); }  // output planes per sub-chunk (0 = default)
 
 // the static split of conv32_ring_impl (~256 workgroups, ranges of `per` planes never straddling samples), each
 // range cut into sub-chunks of about a ninth of it (>= 3 planes); a third when the launch accumulates GroupNorm

@@ -303,10 +303,7 @@ extern "C" int u3d_conv_small(int flip, const void* x, int n, int cin, int d, in
   // split the contraction over workgroups until ~2 workgroups per CU: the per-CU operand stream (55 KB of
   // weights + the halo per 32-channel chunk), not the MFMAs, bounds these small layers
   const int nchunk = g.cin_p / 32;
-  static const long long target = [] {  // workgroups aimed at (U3D_SMALL_WGS: experiments)
-    const char* e = getenv("U3D_SMALL_WGS");
-    return e ? std::max(1LL, atoll(e)) : 256LL;
-  }();
+  const long long target = std::max(1, opt(OPT_SMALL_WGS));  // workgroups aimed at
   int nks = (int)std::min<long long>(nchunk, std::max<long long>(1, (target + tiles - 1) / tiles));
   const long long slab1 = (long long)n * d * h * w * cout * 4;
   if (cout % 4) nks = 1;

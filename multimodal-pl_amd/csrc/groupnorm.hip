@@ -50,14 +50,8 @@ __device__ __forceinline__ void load_da2(const T* __restrict__ da2, const RedGeo
   }
 }
 
-// reduction blocks over all samples (U3D_GN_MAXBLK overrides, for experiments)
-static long long gn_max_blocks() {
-  static const long long m = [] {
-    const char* e = getenv("U3D_GN_MAXBLK");
-    return e ? atoll(e) : 256LL;
-  }();
-  return m;
-}
+// reduction blocks over all samples
+static long long gn_max_blocks() { return std::max(1, opt(OPT_GN_MAXBLK)); }
 
 static RedGeom make_geom(int n, int c, long long v, int groups, int vec) {
   RedGeom g{};

@@ -293,8 +293,7 @@ extern "C" int u3d_head_fwd(const void* x, int n, long long v, int cin, const vo
 #define HF(KS, TR)                                                                                                   \
   hipLaunchKernelGGL((head_fwd_kernel<KS, TR>), dim3(nb), dim3(HD_T), 0, s, (const bf16*)x, v, cin, (const bf16*)wpk, \
                      cout, cin_p, bias, gn_stats, gn_gamma, gn_beta, gn_groups, n, y)
-  const char* etr = getenv("U3D_HEAD_TR");  // 0: the untransposed store path (A/B)
-  if (cout % 8 == 0 && !(etr && atoi(etr) == 0) && (!gn_stats || (long long)n * cin <= HD_GMAX)) {
+  if (cout % 8 == 0 && opt(OPT_HEAD_TR) != 0 && (!gn_stats || (long long)n * cin <= HD_GMAX)) {
     switch (cin / 16) {
       case 1: HF(1, true); break;
       case 2: HF(2, true); break;
@@ -320,8 +319,7 @@ extern "C" int u3d_head_bwd(const float* dy, long long rows, int cout, const voi
   U3D_REQUIRE(dy && wpk_dgrad && dA && dy_bf16 && dbias_partials && rows >= 1, "head_bwd: bad args");
   U3D_REQUIRE(cout >= 1 && cout <= 32 && cin % 8 == 0 && cin <= 64, "head_bwd: cout %d / cin %d", cout, cin);
   const int cout_p = round_up(cout, 32), cout8 = round_up(cout, 8);
-  const char* etr = getenv("U3D_HEAD_TR");  // 0: untransposed scalar dA stores (A/B)
-  const int tr = (etr && atoi(etr) == 0) ? 0 : 1;
+  const int tr = opt(OPT_HEAD_TR) != 0 ? 1 : 0;  // 0: untransposed scalar dA stores
   hipLaunchKernelGGL(head_bwd_kernel, dim3(head_blocks(rows)), dim3(HD_T), 0, (hipStream_t)stream, dy, rows, cout,
                      (const bf16*)wpk_dgrad, cout_p, cin, (bf16*)dA, (bf16*)dy_bf16, cout8, dbias_partials, tr);
   return check_launch("head_bwd_kernel");

@@ -416,13 +416,7 @@ using namespace u3d;
 
 static int sdim(int d, int s) { return (d - 1) / s + 1; }  // k3 pad1: (d + 2 - 3)/s + 1
 
-static bool stem1_on() {  // U3D_STEM1=0: the generic one-voxel kernel (A/B experiments)
-  static const bool on = [] {
-    const char* e = getenv("U3D_STEM1");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+static bool stem1_on() { return opt(OPT_STEM1) != 0; }  // 0: the generic one-voxel kernel
 
 extern "C" long long u3d_stem_fwd_stats_ws_bytes(int n, int d, int h, int w) {
   const long long items = (long long)n * d * h * (w / 4);

@@ -325,10 +325,10 @@ extern "C" int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d
   const dim3 gr(cdiv(row, 256), h, n * d), bl(256);
   // 2 x 2 input rows per thread where that still leaves >= 1024 workgroups (2x48^3 -> 96^3: 83.5 -> 61.3 us; at
   // 2x24^3 x 64 its 288 workgroups measured 30.0 -> 49.8 us, so the one-row gather stays there).
-  // U3D_UP_BWD_BLK=1 / 0 forces the choice (A/B, tests; read per call).
+  // UP_BWD_BLK = 1 / 0 forces the choice (A/B, tests).
   const dim3 g2(cdiv(row, 256), cdiv(h, 2), n * cdiv(d, 2));
-  const char* eb = getenv("U3D_UP_BWD_BLK");
-  const bool blk = eb ? atoi(eb) != 0 : (long long)g2.x * g2.y * g2.z >= 1024;
+  const int eb = opt(OPT_UP_BWD_BLK);
+  const bool blk = eb >= 0 ? eb != 0 : (long long)g2.x * g2.y * g2.z >= 1024;
   if (vect && blk) {
     if (dtype == U3D_BF16)
       hipLaunchKernelGGL((up_bwd_blk_kernel<bf16, 8>), g2, bl, 0, s, (const bf16*)dy, (bf16*)dx, n, c, d, h, w, accumulate);

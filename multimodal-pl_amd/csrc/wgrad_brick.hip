@@ -351,13 +351,7 @@ __global__ __launch_bounds__(512, 1) void wgrad1_kernel(const bf16* __restrict__
 
 using namespace u3d;
 
-static int wgrad_bd() {  // brick depth of the stride-1 kernel (3; U3D_WGRAD_BD=2 selects the 2x8x16 brick)
-  static const int bd = [] {
-    const char* e = getenv("U3D_WGRAD_BD");
-    return (e && atoi(e) == 2) ? 2 : 3;
-  }();
-  return bd;
-}
+static int wgrad_bd() { return opt(OPT_WGRAD_BD) == 2 ? 2 : 3; }  // brick depth of the stride-1 kernel
 
 static void brick_dims(int stride, int* bd, int* bh, int* bw) {
   if (stride == 1) { *bd = wgrad_bd(); *bh = 8; *bw = 16; }
@@ -370,10 +364,7 @@ extern "C" int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, 
   const int od = (d - 1) / stride + 1, oh = (h - 1) / stride + 1, ow = (w - 1) / stride + 1;
   const long long nb = (long long)n * cdiv(od, bd) * cdiv(oh, bh) * cdiv(ow, bw);
   const long long tiles = (long long)cdiv(cin, 32) * cdiv(cout, 32);
-  static const long long target = [] {  // workgroups aimed at (U3D_WB_WGS: experiments)
-    const char* e = getenv("U3D_WB_WGS");
-    return e ? std::max(1LL, atoll(e)) : 256LL;
-  }();
+  const long long target = std::max(1, opt(OPT_WB_WGS));  // workgroups aimed at
   long long want = std::max(1LL, target / tiles);
   const long long ns = std::max(1LL, std::min(want, nb));
   const long long per = (nb + ns - 1) / ns;

@@ -300,8 +300,7 @@ static void wr_geom(int n, int cin, int d, int h, int w, int cout, WRGeom& g) {
   // plane tile: 16 x 16 unless the plane is 12- or 24-wide (and not a multiple of 16), where 16-wide tiles would spend
   // 1/3 (24) or 1/4 (12) of every k step on voxels past the volume
   g.ph = g.pw = 16;
-  const char* e16 = getenv("U3D_WR_TILE16");  // 1: 16 x 16 tiles everywhere (A/B)
-  if (!(e16 && atoi(e16)) && w % 16 != 0 && w % 12 == 0 && h % 12 == 0) {
+  if (opt(OPT_WR_TILE16) == 0 && w % 16 != 0 && w % 12 == 0 && h % 12 == 0) {
     g.ph = 12;
     g.pw = w % 24 == 0 ? 24 : 12;
   }
@@ -315,10 +314,7 @@ extern "C" int u3d_conv_wgrad_ring_splits(int n, int cin, int d, int h, int w, i
   WRGeom g;
   wr_geom(n, cin, d, h, w, cout, g);
   const long long tiles = (long long)(g.cin_p / 32) * (g.cout_p / 32);
-  static const long long target = [] {  // workgroups aimed at (U3D_WR_WGS: experiments)
-    const char* e = getenv("U3D_WR_WGS");
-    return e ? std::max(1LL, atoll(e)) : 256LL;
-  }();
+  const long long target = std::max(1, opt(OPT_WR_WGS));  // workgroups aimed at
   const long long want = std::max(1LL, std::min(g.planes, target / tiles));
   const long long per = (g.planes + want - 1) / want;
   return (int)((g.planes + per - 1) / per);  // every split receives planes: no zero-filled slabs

@@ -16,6 +16,8 @@ F = ctypes.c_float
 # name -> argtypes (restype int unless noted)
 _SIGS = {
     "u3d_abi_version": [],
+    "u3d_set_option": [ctypes.c_char_p, I],
+    "u3d_get_option": [ctypes.c_char_p, P],
     "u3d_wstd_fwd": [I, P, I, I, I, I, P, P, P, P],
     "u3d_wstd_bwd": [P, I, P, P, I, I, I, I, P, I, P],
     "u3d_wstd_fwd_batch": [I, P, I, P],

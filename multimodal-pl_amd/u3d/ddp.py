@@ -9,6 +9,7 @@ bucket is averaged in place; the trunk's autograd Function returns the bucket vi
 """
 import contextlib
 import threading
+import zlib
 
 import torch
 import torch.distributed as dist
@@ -56,6 +57,7 @@ class GradBucketer:
         self.synced = set()
 
     def begin(self):
+        ops.COLLECTIVE_IN_FLIGHT[0] = False  # a backward that raised before finish() must not leave it set
         self.bufs = [torch.empty(nel, dtype=torch.float32, device=self.device) for _, nel in self.buckets]
         self.left = [len(names) for names, _ in self.buckets]
         self.done_names = set()
@@ -119,12 +121,23 @@ class GradBucketer:
         ops.COLLECTIVE_IN_FLIGHT[0] = False
 
     def average(self, t):
-        """Synchronous mean over ranks of one gradient the native backward did not produce."""
+        """Mean over ranks of one flat tensor, in place (stream-ordered)."""
         if self.avg_native:
             dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group)
         else:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
             t.div_(self.world)
+
+    def check_same(self, names):
+        """Every rank must average the same fallback gradients in the same order: a rank whose backward reached a
+        different set would otherwise block in (or mis-pair) the collective. One all-gather of (count, crc32)."""
+        key = torch.tensor([len(names), zlib.crc32("\0".join(names).encode())], dtype=torch.int64,
+                           device=self.device if self.avg_native else "cpu")
+        got = [torch.empty_like(key) for _ in range(self.world)]
+        dist.all_gather(got, key, group=self.group)
+        if any(not torch.equal(g, key) for g in got):
+            raise RuntimeError(f"U3DDataParallel: ranks reached different sets of non-native parameter gradients "
+                               f"({[tuple(g.tolist()) for g in got]} as (count, crc32)); this rank: {names}")
 
 
 class U3DDataParallel(torch.nn.Module):
@@ -132,8 +145,9 @@ class U3DDataParallel(torch.nn.Module):
 
     Gradients written by the native tapes (trunk, dynamic head, feam heads) are averaged in buckets from inside
     the backward. Any other parameter gradient (plain torch autograd, a subgraph the tapes do not cover) is caught
-    by a post-accumulate hook and averaged there, synchronously, so no rank is ever left with an unsynchronised
-    gradient."""
+    by a post-accumulate hook and collected; at the end of the backward (an autograd engine callback) the collected
+    gradients are checked to be the same set on every rank (fail loudly otherwise), flattened into ONE buffer,
+    averaged by one all-reduce and copied back, so no rank is ever left with an unsynchronised gradient."""
 
     def __init__(self, module, group=None, bucket_mb=25.0):
         super().__init__()
@@ -141,6 +155,7 @@ class U3DDataParallel(torch.nn.Module):
         self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
         self.bucketer = GradBucketer(module.named_parameters(), bucket_mb, group) if self.distributed else None
         self.fallback_names = []  # parameters averaged by the hook in the last backward (tests / diagnostics)
+        self._pending = []        # (name, param) collected by the hooks of the running backward
         if self.distributed:
             with torch.no_grad():  # start from identical weights on every rank (DDP's init broadcast)
                 for p in module.parameters():
@@ -155,13 +170,29 @@ class U3DDataParallel(torch.nn.Module):
             if name in self.bucketer.synced:  # averaged in its bucket: exempt this one accumulation
                 self.bucketer.synced.discard(name)
                 return
-            self.bucketer.average(p.grad)
-            self.fallback_names.append(name)
+            if not self._pending:
+                torch.autograd.Variable._execution_engine.queue_callback(self._flush_fallback)
+            self._pending.append((name, p))
         return fn
+
+    def _flush_fallback(self):
+        """End of the backward: one all-reduce over every gradient the hooks collected (fixed hook order)."""
+        pend, self._pending = self._pending, []
+        names = [n for n, _ in pend]
+        self.bucketer.check_same(names)
+        grads = [p.grad for _, p in pend]
+        flat = torch.cat([g.reshape(-1).float() for g in grads])
+        self.bucketer.average(flat)
+        off = 0
+        for g in grads:
+            g.copy_(flat[off:off + g.numel()].view_as(g))
+            off += g.numel()
+        self.fallback_names.extend(names)
 
     def forward(self, *args, **kwargs):
         if self.bucketer is None or not torch.is_grad_enabled():
             return self.module(*args, **kwargs)
         self.fallback_names = []
+        self.bucketer.synced = set()  # exemptions of a previous step whose accumulation never fired do not carry over
         with use_sink(self.bucketer):
             return self.module(*args, **kwargs)

@@ -1,5 +1,6 @@
 """Tensor-level wrappers over the libu3d C ABI. Torch is only the allocator / stream provider here: every
 value is computed by a HIP kernel. All activations are NDHWC tensors of shape [n, d, h, w, c]."""
+import contextlib
 import ctypes
 import os
 
@@ -8,6 +9,21 @@ import torch
 from . import _lib
 from ._lib import BF16, F32, call, query
 
+
+
+@contextlib.contextmanager
+def option(name, value):
+    """Temporarily set a library tuning option (csrc/common.h ``Opt``; e.g. ``option("CONVG_PERSIST", 0)``) for a test
+    that compares two routings in one process; restores the previous value."""
+    h = _lib.lib()
+    old = ctypes.c_int(0)
+    if h.u3d_get_option(name.encode(), ctypes.byref(old)) != 0:
+        raise _lib.U3DError(h.u3d_last_error().decode())
+    h.u3d_set_option(name.encode(), int(value))
+    try:
+        yield
+    finally:
+        h.u3d_set_option(name.encode(), old.value)
 
 def _ptr(t):
     return None if t is None else t.data_ptr()

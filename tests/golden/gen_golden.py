@@ -533,7 +533,54 @@ def g13():
     save("g13_predict_sliding.npz", **out)
 
 
+def _driver_lines(first, last):
+    """Source lines first..last (1-based, inclusive) of the reference driver, dedented: the driver is not importable
+    here (batchgenerators / SimpleITK / torchvision absent), so its own lines are run instead of a restatement."""
+    import textwrap
+    with open(os.path.join(REF, "train_amos_atlas_final.py")) as f:
+        lines = f.read().splitlines()[first - 1:last]
+    return textwrap.dedent("\n".join(lines))
+
+
+def g14():
+    """A12: the partial-label target of the driver on the reference's own supervision table. Runs the driver's
+    mask_dict construction (train_amos_atlas_final.py:177-183; the cluster path of :178 replaced by the local
+    /root/reference/supervise_mask.csv) and its 13 masked writes (:252-255) on seeded synthetic labels 0..15, for
+    EVERY row of the table (241 volumes: CT rows with one labelled organ, the 40 all-zero MRI rows). The batch holds
+    two samples, as the driver masks the whole batch with the first volume's row."""
+    import csv
+    import re
+    src_dict = _driver_lines(177, 183)
+    src_mask = _driver_lines(252, 255)
+    assert "mask_file = " in src_dict and "cmask[cmask == l] = 0" in src_mask, "driver lines moved"
+    import tempfile
+    with open(os.path.join(REF, "supervise_mask.csv")) as f:  # the driver eval()s each cell: plain int lists only
+        rows = list(csv.reader(f))
+    assert rows[0] == ["name", "mask"] and all(re.fullmatch(r"\[[0-9, ]*\]", m) for _, m in rows[1:])
+    # the driver's loop has no header skip (eval("mask") of the header row fails), so the cluster file had none: the
+    # local copy is handed over without its header line
+    tmp = tempfile.NamedTemporaryFile("w", suffix=".csv", delete=False)
+    csv.writer(tmp).writerows(rows[1:])
+    tmp.close()
+    src_dict = re.sub(r'mask_file = "[^"]*"', f"mask_file = {tmp.name!r}", src_dict)
+    ns = {"csv": csv, "np": np, "torch": torch}
+    exec(compile(src_dict, "train_amos_atlas_final.py:177-183", "exec"), ns)
+    mask_dict = ns["mask_dict"]
+    rng = np.random.default_rng([14, 14])
+    labels = torch.from_numpy(rng.integers(0, 16, (2, 1, 6, 7, 5)).astype(np.float32))
+    names = [n for n, _ in rows[1:]]
+    outs, masks = [], []
+    for name in names:
+        ns_m = {"labels": labels, "mask_dict": mask_dict, "volumeName": name}
+        exec(compile(src_mask, "train_amos_atlas_final.py:252-255", "exec"), ns_m)
+        outs.append(ns_m["cmask"].numpy().astype(np.uint8))
+        masks.append(mask_dict[name].numpy().astype(np.int8))
+    save("g14_partial_target.npz", names=np.array(names), masks=np.stack(masks), labels=labels.numpy(),
+         cmask=np.stack(outs))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12", "g13"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12", "g13",
+                             "g14"]
     for w in which:
         globals()[w]()

@@ -367,8 +367,7 @@ def test_bf16_stem_bench_size(gpu):
 @pytest.mark.parametrize("cin,cout,dims", [(32, 16, (48, 48, 48)), (64, 8, (5, 7, 9)), (16, 32, (3, 11, 13))])
 def test_head_transposed_bitwise_equal(gpu, cin, cout, dims):
     """The transposed-MFMA head (16-B stores; default for cout % 8 == 0) against the untransposed form
-    (U3D_HEAD_TR=0): the same products summed in the same order, the same bf16 rounding -> bitwise equal."""
-    import os
+    (option HEAD_TR=0): the same products summed in the same order, the same bf16 rounding -> bitwise equal."""
     from u3d import ops
     n = 2
     x, _, st, ga, be, G = _case(gpu, n, cin, cout, dims, True, 9)
@@ -377,14 +376,11 @@ def test_head_transposed_bitwise_equal(gpu, cin, cout, dims):
     b = torch.randn(cout, device=gpu)
     dy = torch.randn(x.shape[:-1] + (cout,), device=gpu)
     out = []
-    for tr in ("1", "0"):
-        os.environ["U3D_HEAD_TR"] = tr
-        try:
+    for tr in (1, 0):
+        with ops.option("HEAD_TR", tr):
             y = ops.head_fwd(x, pf, cout, b, (st, ga, be, G))
             dA, dyb = ops.head_bwd(dy, pd, cin)
             torch.cuda.synchronize()
-        finally:
-            os.environ.pop("U3D_HEAD_TR", None)
         out.append((y, dA, dyb))
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1].view(torch.int16), out[1][1].view(torch.int16))

@@ -327,6 +327,18 @@ def test_partial_target_vs_oracle(gpu):
     np.testing.assert_array_equal(got.reshape(ref.shape), ref)
 
 
+
+def test_partial_target_every_supervise_mask_row(gpu):
+    """A12 on the reference's own table (G14: the driver's lines run on all 240 rows of supervise_mask.csv, batch of
+    two masked with one row as the driver does): the device pass is bit-exact for every row."""
+    from loss_functions import losses
+    g = golden("g14_partial_target.npz")
+    lab = torch.from_numpy(g["labels"]).to(gpu)
+    for i in range(len(g["names"])):
+        got = losses.make_partial_target(lab, torch.from_numpy(g["masks"][i].astype(np.int64))).cpu().numpy()
+        np.testing.assert_array_equal(got.astype(np.uint8), g["cmask"][i])
+        assert got.dtype == np.float32 and got.shape == g["labels"].shape
+
 # ------------------------------------------------------------- f2/f3: consistency branch of get_loss (G9)
 @pytest.mark.parametrize("tag", ["mix", "none", "all"])
 def test_g9_get_loss_consistency(gpu, tag):

@@ -1,10 +1,9 @@
 """Persistent generic brick conv (convg_pbrick_kernel, the default behind u3d_convg_brick) against the one-shot
-brick kernel (U3D_CONVG_PERSIST=0, the round-1 schedule, itself checked against fp64 in test_gpu_bf16.py and
+brick kernel (option CONVG_PERSIST=0, the round-1 schedule, itself checked against fp64 in test_gpu_bf16.py and
 test_gpu_fullsize.py). Same operands, same per-output fp32 accumulation order: the results must be bitwise equal.
 Cases cover several units per workgroup (48^3-class grids), the 8-wide bricks of 8- but not 16-multiple planes
 (24^3), 32-channel co tiles (the launcher's choice at 24^3 x 64), partial co tiles (cout 96), ragged volumes, GN
 prologue, residual, and the data gradient (flip). Reference: F.conv3d in Conv3d.forward (unet3D.py:27) through NoBottleneck (:56-73)."""
-import os
 
 import pytest
 import torch
@@ -41,16 +40,14 @@ def _run(gpu, n, cin, cout, dims, gn, res, flip, persist):
     be = 0.1 * torch.randn(cin, device=gpu)
     r = torch.randn((n,) + dims + (cout,), device=gpu).to(torch.bfloat16) if res else None
     y = torch.full((n,) + dims + (cout,), 7.0, device=gpu, dtype=torch.bfloat16)
-    os.environ["U3D_CONVG_PERSIST"] = "1" if persist else "0"
-    try:
+    from u3d import ops
+    with ops.option("CONVG_PERSIST", 1 if persist else 0):
         p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         rc = _lib.lib().u3d_convg_brick(int(flip), p(x), n, cin, *dims, p(wpk), cout, p(st) if gn else None,
                                         p(ga) if gn else None, p(be) if gn else None, G if gn else 0, p(r), p(y),
                                         torch.cuda.current_stream().cuda_stream)
         assert rc == 0, _lib.lib().u3d_last_error()
         torch.cuda.synchronize()
-    finally:
-        os.environ.pop("U3D_CONVG_PERSIST", None)
     return y
 
 

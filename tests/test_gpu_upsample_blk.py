@@ -1,8 +1,7 @@
 """Trilinear x2 backward with 2 x 2 input rows per thread (up_bwd_blk_kernel, u3d_upsample2x_bwd's choice for grids of >= 1024 workgroups)
-against the one-row gather (U3D_UP_BWD_BLK=0, itself checked against torch autograd in test_gpu_parity.py). Same taps,
+against the one-row gather (option UP_BWD_BLK=0, itself checked against torch autograd in test_gpu_parity.py). Same taps,
 weights and add order per output: bitwise equal. Odd d / h (a half-empty row pair), size-1 dims, accumulate, fp32 and
 bf16. Reference: nn.Upsample(scale_factor=2, mode='trilinear') (unet3D.py:1646)."""
-import os
 
 import pytest
 import torch
@@ -15,12 +14,9 @@ SHAPES = [(2, 48, 48, 48, 32), (2, 24, 24, 24, 64), (1, 5, 7, 9, 16), (2, 3, 4, 
 
 def _bwd(dy, shape, prev, blk):
     from u3d import ops
-    os.environ["U3D_UP_BWD_BLK"] = "1" if blk else "0"
-    try:
+    with ops.option("UP_BWD_BLK", 1 if blk else 0):
         dx = ops.upsample2x_bwd(dy, shape, dx=None if prev is None else prev.clone(), accumulate=prev is not None)
         torch.cuda.synchronize()
-    finally:
-        os.environ.pop("U3D_UP_BWD_BLK", None)
     return dx
 
 

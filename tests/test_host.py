@@ -229,6 +229,39 @@ def test_ddp_fallback_hook_averages_non_native_grads_gloo_world2():
             assert np.allclose(grads[k], p.grad.numpy(), rtol=1e-6, atol=1e-7), (rank, k)
 
 
+
+def _fallback_mismatch_worker(rank, world, port, q):
+    """Rank 1's backward reaches a parameter rank 0's does not: both ranks must raise, not hang or mis-pair."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    from u3d.ddp import U3DDataParallel
+    torch.manual_seed(0)
+    m = torch.nn.ModuleList([torch.nn.Linear(4, 4), torch.nn.Linear(4, 4)])
+    net = U3DDataParallel(m)
+    x = torch.randn(2, 4)
+    y = net.module[0](x) if rank == 0 else net.module[1](net.module[0](x))
+    try:
+        y.sum().backward()
+        q.put((rank, "no error"))
+    except RuntimeError as e:
+        q.put((rank, "raised" if "different sets" in str(e) else repr(e)))
+    dist.destroy_process_group()
+
+
+def test_ddp_fallback_mismatch_fails_loudly_gloo_world2():
+    """ranks whose backward reaches different non-native parameters raise instead of hanging."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fallback_mismatch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=60) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert out == [(0, "raised"), (1, "raised")], out
+
 def test_bench_gpus_flag_launches_ranks():
     """`python bench.py --gpus N` (the driver's SCALE command shape, no torchrun) starts N ranks itself, each with
     its own RANK / LOCAL_RANK / WORLD_SIZE and a 127.0.0.1 rendezvous, before any GPU call."""

@@ -334,3 +334,12 @@ def test_g13_predict_sliding_oracle_vs_reference(tag):
     out = O.predict_sliding(pred_fn, g[f"{tag}_img"], tuple(int(v) for v in g[f"{tag}_tile"]), ref.shape[1],
                             tta=bool(g[f"{tag}_tta"]))
     assert np.abs(out - ref).max() <= 1e-6 * np.abs(ref).max()
+
+
+def test_g14_partial_target_every_supervise_mask_row():
+    """A12 pinned on reference-held data: the driver's own mask_dict + masked-write lines
+    (train_amos_atlas_final.py:177-183, 252-255) run on every row of supervise_mask.csv (G14)."""
+    g = golden("g14_partial_target.npz")
+    assert len(g["names"]) == 240 and int((g["masks"].sum(1) == 0).sum()) == 40  # the all-zero MRI rows
+    for i in range(len(g["names"])):
+        np.testing.assert_array_equal(O.partial_target(g["labels"], g["masks"][i]).astype(np.uint8), g["cmask"][i])
