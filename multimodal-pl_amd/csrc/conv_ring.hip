@@ -62,28 +62,33 @@ struct RGPlane {
 
 // Walks the workgroup's output range [o, o_end) as a sequence of input planes: each maximal run of outputs
 // z0..z1-1 inside one column stages zin = z0-1 .. z1.
+// The column coordinates (n, h0, w0) are decoded once per run (the divisions are off the per-plane path).
 struct RGWalk {
   long long o_next, o_end;
-  int col, zin, zfirst, zlast;
+  int zin, zfirst, zlast;
+  int cn, ch0, cw0;
   bool done;
   __device__ void start_run(const RGGeom& g) {
     if (o_next >= o_end) { done = true; return; }
-    col = (int)(o_next / g.d);
+    const int col = (int)(o_next / g.d);
     zfirst = (int)(o_next - (long long)col * g.d);
     zlast = (int)min<long long>(g.d, zfirst + (o_end - o_next));
     o_next += zlast - zfirst;
     zin = zfirst - 1;
+    int c = col;
+    const int bw_ = c % g.nbw; c /= g.nbw;
+    const int bh_ = c % g.nbh;
+    cn = c / g.nbh;
+    ch0 = bh_ * RG_BH;
+    cw0 = bw_ * RG_BW;
   }
   __device__ RGPlane next(const RGGeom& g) {
     RGPlane p{};
     if (!done && zin > zlast) start_run(g);
     if (done) return p;
-    int c = col;
-    const int bw_ = c % g.nbw; c /= g.nbw;
-    const int bh_ = c % g.nbh;
-    p.n = c / g.nbh;
-    p.h0 = bh_ * RG_BH;
-    p.w0 = bw_ * RG_BW;
+    p.n = cn;
+    p.h0 = ch0;
+    p.w0 = cw0;
     p.zin = zin;
     p.valid = true;
     p.out = zin >= zfirst + 1;
@@ -106,7 +111,10 @@ struct RGWalk {
 // tail is one sub-chunk instead of a whole range; uncontended, the walk is the static one. GroupNorm statistics go
 // to per-(sub-chunk, wave) slots (fixed-order finalize: deterministic whatever the assignment). The last workgroup
 // to exit resets the words and the exit counter to zero for the next launch.
-template <bool FLIP, bool GN, bool RES, int KR, bool BG = false, bool Q = false>
+// EXP (diagnostic builds only, -DU3D_RING_EXP; results are wrong when set): 1 no per-step barrier, 2 no x staging
+// loads, 4 no MFMAs (a dependent VALU op keeps the fragment reads live), 8 no LDS fragment reads after the first
+// steps, 16 no residual loads / y stores, 32 both SIMD partners use the same side-work schedule (no stagger).
+template <bool FLIP, bool GN, bool RES, int KR, bool BG = false, bool Q = false, int EXP = 0>
 __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                               bf16* __restrict__ y, const bf16* __restrict__ res,
                                                               const float* __restrict__ gstat,
@@ -218,19 +226,23 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   f32x2 sc[4], sh[4];
   int gn_n = -1;
   // branch-free staging: out-of-volume rows load a valid dummy address and are zeroed when written
-  auto load_plane = [&](const RGPlane& p, u32x4 (&v)[RG_LD], unsigned& m) {
-    m = 0;
-#pragma unroll
-    for (int i = 0; i < RG_LD; ++i) {
-      const int row = (tid >> 2) + i * (RG_NT / 4);
-      const int hw = row % RG_HW, hh = row / RG_HW;
-      const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
-      const bool ok = p.valid && row < RG_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
-                      (unsigned)zw < (unsigned)g.w;
-      const unsigned off = ok ? (unsigned)((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * 64 + ch * 16) : 0xFFFFFFF0u;
+  // staged piece i of plane p (16 B of one halo row) into v[i]; bit i of m = the row is inside the volume
+  auto load_piece = [&](const RGPlane& p, int i, u32x4 (&v)[RG_LD], unsigned& m) {
+    const int row = (tid >> 2) + i * (RG_NT / 4);
+    const int hw = row % RG_HW, hh = row / RG_HW;
+    const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
+    const bool ok = p.valid && row < RG_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
+                    (unsigned)zw < (unsigned)g.w;
+    const unsigned off = ok ? (unsigned)((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * 64 + ch * 16) : 0xFFFFFFF0u;
+    if constexpr ((EXP & 2) != 0)
+      v[i] = u32x4{off, off >> 3, off >> 5, 0x3f80u};
+    else
       v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-      m |= (ok ? 1u : 0u) << i;
-    }
+    m = (i == 0 ? 0u : m) | ((ok ? 1u : 0u) << i);
+  };
+  auto load_plane = [&](const RGPlane& p, u32x4 (&v)[RG_LD], unsigned& m) {
+#pragma unroll
+    for (int i = 0; i < RG_LD; ++i) load_piece(p, i, v, m);
   };
   auto gn_table = [&](const RGPlane& p) {
     if (GN && p.valid && p.n != gn_n) {
@@ -344,7 +356,11 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         }
         store16<bf16>(reinterpret_cast<bf16*>(&v), a);
       }
-      if (p.ok) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
+      if constexpr ((EXP & 16) != 0) {
+        if (p.ok && v[0] == 0x7fc17fc1u) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
+      } else {
+        if (p.ok) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
+      }
       if constexpr (BG) {
         float a[8], xv[8];
         load16<bf16>(reinterpret_cast<const bf16*>(&v), a);       // the stored (bf16) dA
@@ -361,9 +377,14 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
   };
 
-  // output plane from the three slots s0 (z-1), s1 (z), s2 (z+1); the staging writes of the next plane and
-  // the previous plane's epilogue are issued between the MFMAs
-  auto compute = [&](const RGPlane& pc, int s0, int s1, int s2) __attribute__((always_inline)) {
+  // output plane from the three slots s0 (z-1), s1 (z), s2 (z+1); the staging writes of the staged plane, the
+  // loads of the next one (side(st), at compile-time MFMA steps) and the previous plane's epilogue are issued between
+  // the MFMAs. H = 1 places them at later steps (15.., epilogue 44): staggering the two waves of a SIMD pair that way
+  // (waves >= 4 on H = 1, MI355X_MICROARCH.md two waves per SIMD, item 9) measured equal or 2-3% slower at 96^3
+  // (profiles/r03_ring_ablations.log), so every wave runs H = 0.
+  auto compute = [&](const RGPlane& pc, int s0, int s1, int s2, auto hc, auto&& side) __attribute__((always_inline)) {
+    constexpr int H = (EXP & 32) != 0 ? 0 : decltype(hc)::value;
+    constexpr int EPI = H ? 44 : 30;
     const int zo = pc.zin - 1;
     const int zh = pc.h0 + wave, zw = pc.w0 + r;
     Pending nw;
@@ -371,7 +392,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     nw.ok = zh < g.h && zw < g.w;
     nw.vox = (((long long)pc.n * g.d + zo) * g.h + zh) * g.w + zw;
     nw.rv[0] = nw.rv[1] = u32x4{0u, 0u, 0u, 0u};
-    if constexpr (RES || BG) {
+    if constexpr ((RES || BG) && (EXP & 16) == 0) {
       const unsigned ro = nw.ok ? (unsigned)(nw.vox * 64 + 16 * h) : 0xFFFFFFC0u;
       nw.rv[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
       nw.rv[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro + 32, 0, 0));
@@ -393,6 +414,9 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     constexpr int LA = 3;
     bf16x8 fa[LA + 1], fb[LA + 1];
     auto rd = [&](int st, int k) {
+      if constexpr ((EXP & 8) != 0) {
+        if (st >= LA + 1) return;
+      }
       fa[k] = *reinterpret_cast<const bf16x8*>(abase + aoff(st));
       if (st < KR)
         fb[k] = wreg[st < KR ? st : 0];
@@ -404,9 +428,13 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     auto mstep = [&](auto stc) {
       constexpr int st = decltype(stc)::value;
       if constexpr (st + LA < 54) rd(st + LA, (st + LA) % (LA + 1));
-      if constexpr (st == 30) epilogue(pend);
+      side(std::integral_constant<int, st - (H ? 15 : 1)>{});
+      if constexpr (st == EPI) epilogue(pend);
       __builtin_amdgcn_sched_barrier(0);
-      nw.acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[st % (LA + 1)], fa[st % (LA + 1)], nw.acc, 0, 0, 0);
+      if constexpr ((EXP & 4) != 0)
+        nw.acc[st & 15] += (float)fa[st % (LA + 1)][0] * (float)fb[st % (LA + 1)][1];
+      else
+        nw.acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[st % (LA + 1)], fa[st % (LA + 1)], nw.acc, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     };
     __builtin_amdgcn_sched_barrier(0);
@@ -528,14 +556,25 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
     gn_table(pw);
     const int slot = s & 3;
-    if (pw.valid) {
-#pragma unroll
-      for (int i = 0; i < RG_LD; ++i) write_piece(i, vcur[i], mcur, slot);
-    }
     const RGPlane pl = next_plane();  // plane s+1
-    load_plane(pl, vnxt, mnxt);
-    if (pc.valid && pc.out) compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3);
-    __syncthreads();
+    // side work of the step, k = 0 .. 2 RG_LD - 1: even k writes staged piece k/2 of plane s into slot s & 3 (its
+    // loads were issued a full step ago), odd k issues the load of piece k/2 of plane s + 1
+    auto side = [&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (k >= 0 && k < 2 * RG_LD) {
+        if constexpr ((k & 1) == 0) {
+          if (pw.valid) write_piece(k >> 1, vcur[k >> 1], mcur, slot);
+        } else {
+          load_piece(pl, k >> 1, vnxt, mnxt);
+        }
+      }
+    };
+    if (pc.valid && pc.out) {
+      compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 0>{}, side);
+    } else {
+      static_for<0, 2 * RG_LD>(side);
+    }
+    if constexpr ((EXP & 1) == 0) __syncthreads();
     pc = pw;
     pw = pl;
     ++s;
@@ -641,325 +680,6 @@ __global__ __launch_bounds__(64) void ring_gn_finalize_kernel(const float* __res
   }
 }
 
-// ---------------------------------------------------------------------------------------------------------------
-// Register-blocked ring (round 2). Same geometry, walk, staging, epilogue and statistics contract as
-// conv32_ring_kernel, but 4 waves (one per SIMD, the 512-register budget) each computing TWO output rows of the
-// 8 x 32 plane tile. Output rows 2w and 2w+1 read halo rows 2w .. 2w+3: per (kd, kw, k-half) group the wave reads
-// 4 input fragments from LDS and issues 6 MFMAs (row j, tap kh <- halo row j + kh), and the first KR weight
-// fragments of the 54 (tap, k-half) live in registers. LDS reads per MFMA fall from ~1.8 (one input + most weight
-// fragments per MFMA) to 0.67 input + the (54 - KR) / 108 weight fragments, well under the 256 B/clk the
-// one-fragment-per-MFMA schedule saturated at the MFMA rate.
-constexpr int R2_NT = 256;
-constexpr int R2_LD = (RG_NR * 4 + R2_NT - 1) / R2_NT;  // 6 staged 16-B pieces per thread and plane
-
-// ABL (timing ablations only, results are wrong when set): 1 no per-plane barrier, 2 no LDS fragment reads in the
-// MFMA chain, 4 no staging global loads, 8 no staging LDS writes, 16 no MFMAs, 32 no epilogue stores
-template <bool FLIP, bool GN, bool RES, int KR, int ABL = 0, int PF = 1, int LAG = 1>
-__global__ __launch_bounds__(R2_NT, 1) void conv32_ring2_kernel(const bf16* __restrict__ x,
-                                                               const bf16* __restrict__ wpk, bf16* __restrict__ y,
-                                                               const bf16* __restrict__ res,
-                                                               const float* __restrict__ gstat,
-                                                               const float* __restrict__ gamma,
-                                                               const float* __restrict__ beta,
-                                                               float* __restrict__ spart, RGGeom g) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024];
-  char* const ring = smem;
-  char* const wts = smem + 4 * RG_SS;
-  char* const junk = wts + 4 * RG_NWR * 16;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int ch = tid & 3;
-
-  int bid = blockIdx.x;
-  {
-    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
-    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
-  }
-  RGWalk walk{};
-  const int smp = bid / g.wps, jw = bid - smp * g.wps;
-  walk.o_next = (long long)smp * g.pps + (long long)jw * g.per;
-  walk.o_end = min((long long)(smp + 1) * g.pps, walk.o_next + g.per);
-  walk.done = false;
-  walk.zin = 1;
-  walk.zlast = 0;
-
-  for (int i = tid; i < RG_NWR * 4; i += R2_NT) {
-    const int c = i / RG_NWR, row = i % RG_NWR;
-    *reinterpret_cast<u32x4*>(wts + (c * RG_NWR + row) * 16) = *reinterpret_cast<const u32x4*>(wpk + row * 32 + c * 8);
-  }
-  // weight fragment f = 2 t + s (tap t, k-half s): this lane's W[t][r][16 s + 8 h .. +8]
-  bf16x8 wreg[KR > 0 ? KR : 1];
-#pragma unroll
-  for (int f = 0; f < KR; ++f)
-    wreg[f] = *reinterpret_cast<const bf16x8*>(wpk + ((f >> 1) * 32 + r) * 32 + (f & 1) * 16 + 8 * h);
-
-  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)g.xbytes, 0x00020000);
-  const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, RES ? (int)g.xbytes : 0, 0x00020000);
-  f32x2 sc[4], sh[4];
-  int gn_n = -1;
-  auto load_plane = [&](const RGPlane& p, u32x4 (&v)[R2_LD], unsigned& m) {
-    m = 0;
-#pragma unroll
-    for (int i = 0; i < R2_LD; ++i) {
-      const int row = (tid >> 2) + i * (R2_NT / 4);
-      const int hw = row % RG_HW, hh = row / RG_HW;
-      const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
-      const bool ok = p.valid && row < RG_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
-                      (unsigned)zw < (unsigned)g.w;
-      const unsigned off = ok ? (unsigned)((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * 64 + ch * 16) : 0xFFFFFFF0u;
-      if constexpr (ABL & 4)
-        v[i] = u32x4{off, off, off, off};
-      else
-        v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-      m |= (ok ? 1u : 0u) << i;
-    }
-  };
-  auto gn_table = [&](const RGPlane& p) {
-    if (GN && p.valid && p.n != gn_n) {
-      gn_n = p.n;
-      gn_coef8(gstat, gamma, beta, g.gn_groups, 32, p.n, ch * 8, sc, sh);
-    }
-  };
-  auto write_piece = [&](int i, const u32x4& v, unsigned m, int slot) {
-    if constexpr (ABL & 8) return;
-    const int row = (tid >> 2) + i * (R2_NT / 4);
-    u32x4 val = v;
-    if constexpr (GN) val = gn_relu8(v, sc, sh);
-    if constexpr (GN) if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};
-    char* dst = row < RG_NR ? ring + slot * RG_SS + ch * RG_PS + row * 16 : junk + lane * 16;
-    *reinterpret_cast<u32x4*>(dst) = val;
-  };
-
-  struct Pending {
-    f32x16 acc;
-    u32x4 rv[2];
-    long long vox;
-    bool ok;
-  };
-  Pending pend[2];
-  pend[0].ok = pend[1].ok = false;
-  pend[0].vox = pend[1].vox = 0;
-  float gs[8], gq[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) gs[j] = gq[j] = 0.f;
-  auto epilogue = [&](const Pending& p) {
-    if constexpr (GN && !RES) {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const float t = p.ok ? p.acc[k] : 0.f;
-        gs[2 * (k >> 2) + ((k & 3) >> 1)] += t;
-        gq[2 * (k >> 2) + ((k & 3) >> 1)] = fmaf(t, t, gq[2 * (k >> 2) + ((k & 3) >> 1)]);
-      }
-    }
-    uint32_t pk[4][2];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-        pk[q][e] = pack_bf16x2(p.acc[4 * q + 2 * e], p.acc[4 * q + 2 * e + 1]);
-#pragma unroll
-    for (int q = 0; q < 4; q += 2)
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(pk[q][e], pk[q + 1][e], false, false);
-        pk[q][e] = sw[0];
-        pk[q + 1][e] = sw[1];
-      }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      u32x4 v = {pk[2 * u][0], pk[2 * u][1], pk[2 * u + 1][0], pk[2 * u + 1][1]};
-      if constexpr (RES) {
-        float a[8], c[8];
-        load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
-        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[u]), c);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) a[e] += c[e];
-        if constexpr (GN) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float t = p.ok ? a[e] : 0.f;
-            gs[4 * u + (e >> 1)] += t;
-            gq[4 * u + (e >> 1)] = fmaf(t, t, gq[4 * u + (e >> 1)]);
-          }
-        }
-        store16<bf16>(reinterpret_cast<bf16*>(&v), a);
-      }
-      if constexpr (ABL & 32) {
-        if (p.ok && v[0] == 0x7fc17fc1u) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
-      } else {
-        if (p.ok) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
-      }
-    }
-  };
-
-  // output plane of the triple (s0, s1, s2) = slots of input planes z-1, z, z+1: rows 2 wave + j, j = 0, 1
-  auto compute = [&](const RGPlane& pc, int s0, int s1, int s2) {
-    const int zo = pc.zin - 1;
-    const int zw = pc.w0 + r;
-    Pending nw[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int zh = pc.h0 + 2 * wave + j;
-      nw[j].ok = zh < g.h && zw < g.w;
-      nw[j].vox = (((long long)pc.n * g.d + zo) * g.h + zh) * g.w + zw;
-      nw[j].rv[0] = nw[j].rv[1] = u32x4{0u, 0u, 0u, 0u};
-      if constexpr (RES) {
-        const unsigned ro = nw[j].ok ? (unsigned)(nw[j].vox * 64 + 16 * h) : 0xFFFFFFC0u;
-        nw[j].rv[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
-        nw[j].rv[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro + 32, 0, 0));
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) nw[j].acc[e] = 0.f;
-    }
-    const int sl[3] = {FLIP ? s2 : s0, s1, FLIP ? s0 : s2};
-    // group G = (td, tw, s), G = (td * 3 + tw) * 2 + s: 4 input fragments (halo rows 2 wave + q) and the weight
-    // fragments of taps (td, th, tw), th = 0..2, which are not held in registers
-    const char* abase = ring + h * RG_PS + (2 * wave * RG_HW + r) * 16;
-    const char* bbase = wts + (h * RG_NWR + r) * 16;
-    auto a_off = [&](int G, int q) {
-      const int td = G / 6, tw = (G / 2) % 3, s = G & 1;
-      const int ow = FLIP ? 2 - tw : tw;
-      return sl[td] * RG_SS + (q * RG_HW + ow) * 16 + 2 * s * RG_PS;
-    };
-    auto wfrag = [](int G, int th) {  // fragment index 2 t + s of tap (td, th, tw)
-      const int td = G / 6, tw = (G / 2) % 3, s = G & 1;
-      return ((td * 3 + th) * 3 + tw) * 2 + s;
-    };
-    constexpr int NB = LAG + 1;  // fragment buffers: group G's reads are issued during group G - LAG
-    bf16x8 fa[NB][4], fw[NB][3];
-    auto rd_a = [&](int G, int q) {
-      if constexpr (ABL & 2) {
-        if (G >= 2) return;
-      }
-      fa[G % NB][q] = *reinterpret_cast<const bf16x8*>(abase + a_off(G, q));
-    };
-    auto rd_w = [&](int G, int th) {
-      const int f = wfrag(G, th);
-      if constexpr (ABL & 2) {
-        if (G >= 2) return;
-      }
-      if (f >= KR) fw[G % NB][th] = *reinterpret_cast<const bf16x8*>(bbase + ((f & 1) * 2 * RG_NWR + (f >> 1) * 32) * 16);
-    };
-    auto wsel = [&](int G, int th) -> const bf16x8& {
-      const int f = wfrag(G, th);
-      return f < KR ? wreg[f < KR ? f : 0] : fw[G % NB][th];
-    };
-#pragma unroll
-    for (int G0 = 0; G0 < LAG; ++G0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) rd_a(G0, q);
-#pragma unroll
-      for (int th = 0; th < 3; ++th) rd_w(G0, th);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    auto group = [&](auto gc) {
-      constexpr int G = decltype(gc)::value;
-      // the 6 MFMAs of group G: (q, j) with kh = q - j in [0, 2]; th = FLIP ? 2 - kh : kh
-      constexpr int MQ[6] = {0, 1, 1, 2, 2, 3}, MJ[6] = {0, 0, 1, 0, 1, 1};
-      static_for<0, 6>([&](auto mc) {
-        constexpr int m = decltype(mc)::value;
-        if constexpr (G + LAG < 18) {  // group G + LAG's fragments, one or two reads per MFMA gap
-          if constexpr (m < 4) rd_a(G + LAG, m);
-          if constexpr (m >= 3) rd_w(G + LAG, m - 3);
-        }
-        if constexpr (G == 6 && m == 2) epilogue(pend[0]);
-        if constexpr (G == 12 && m == 2) epilogue(pend[1]);
-        __builtin_amdgcn_sched_barrier(0);
-        constexpr int q = MQ[m], j = MJ[m], kh = q - j, th = FLIP ? 2 - kh : kh;
-        if constexpr (!(ABL & 16))
-          nw[j].acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsel(G, th), fa[G % NB][q], nw[j].acc, 0, 0, 0);
-        else
-          nw[j].acc[q] += __builtin_bit_cast(float, (uint32_t)(uint16_t)wsel(G, th)[0]) * (float)fa[G % NB][q][1];
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    };
-    static_for<0, 18>(group);
-    pend[0] = nw[0];
-    pend[1] = nw[1];
-  };
-
-  u32x4 va[R2_LD], vb[R2_LD];
-  unsigned ma = 0, mb = 0;
-  RGPlane pc{};
-  int s = 0;
-  if constexpr (PF == 2) {
-    // staging loads two planes ahead: plane s is written from the register set it was loaded into two steps
-    // earlier, which then receives plane s + 2 (sets alternate; unrolled by two so the sets are static)
-    RGPlane pw = walk.next(g);
-    load_plane(pw, va, ma);
-    RGPlane pn = walk.next(g);
-    load_plane(pn, vb, mb);
-    __syncthreads();
-    auto step = [&](u32x4 (&cur)[R2_LD], unsigned& mcur) {
-      gn_table(pw);
-      if (pw.valid) {
-#pragma unroll
-        for (int i = 0; i < R2_LD; ++i) write_piece(i, cur[i], mcur, s & 3);
-      }
-      const RGPlane pl = walk.next(g);
-      load_plane(pl, cur, mcur);
-      if (pc.valid && pc.out) compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3);
-      if constexpr (!(ABL & 1)) __syncthreads();
-      pc = pw;
-      pw = pn;
-      pn = pl;
-      ++s;
-    };
-    while (pw.valid || (pc.valid && pc.out)) {
-      step(va, ma);
-      if (!(pw.valid || (pc.valid && pc.out))) break;
-      step(vb, mb);
-    }
-  } else {
-    RGPlane pw = walk.next(g);
-    load_plane(pw, va, ma);
-    __syncthreads();
-    while (pw.valid || (pc.valid && pc.out)) {
-      gn_table(pw);
-      const int slot = s & 3;
-      if (pw.valid) {
-#pragma unroll
-        for (int i = 0; i < R2_LD; ++i) write_piece(i, va[i], ma, slot);
-      }
-      const RGPlane pl = walk.next(g);
-      load_plane(pl, va, ma);
-      if (pc.valid && pc.out) compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3);
-      if constexpr (!(ABL & 1)) __syncthreads();
-      pc = pw;
-      pw = pl;
-      ++s;
-    }
-  }
-  epilogue(pend[0]);
-  epilogue(pend[1]);
-  if constexpr (GN) {
-    if (spart == nullptr) return;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        gs[j] += __shfl_xor(gs[j], o);
-        gq[j] += __shfl_xor(gq[j], o);
-      }
-    float* red = reinterpret_cast<float*>(ring);  // [wave][group 16][2]
-    if (r == 0) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int grp = RES ? 8 * (j >> 2) + 4 * h + (j & 3) : 4 * (j >> 1) + 2 * h + (j & 1);
-        red[(wave * 16 + grp) * 2] = gs[j];
-        red[(wave * 16 + grp) * 2 + 1] = gq[j];
-      }
-    }
-    __syncthreads();
-    if (tid < 32) {
-      float t = 0.f;
-#pragma unroll
-      for (int wv = 0; wv < R2_NT / 64; ++wv) t += red[wv * 32 + tid];
-      spart[(long long)bid * 32 + tid] = t;
-    }
-  }
-}
-
 }  // namespace u3d
 
 using namespace u3d;
@@ -970,14 +690,6 @@ static int ring_kr(int dflt) {  // RING_KR = 0: no weight steps in registers (ex
 }
 
 static int ring_wgs() { return std::max(1, opt(OPT_RING_WGS)); }  // persistent grid target: one workgroup per CU
-static bool ring_v2() {  // U3D_RING_V2=1: the register-blocked schedule (measured equal or slower: off)
-  static const bool on = [] {
-    const char* e = getenv("U3D_RING_V2");
-    return e && atoi(e) != 0;
-  }();
-  return on;
-}
-
 static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
                             const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                             const void* residual, void* y, float* stats_out, float* stats_ws, u3d_stream_t stream,
@@ -1017,19 +729,36 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
     return check_launch("conv32_ring_kernel (dgrad + GN backward partials)");
   }
   U3D_REQUIRE(!(flip && (gn_stats || residual)), "conv32_ring: the data gradient takes no prologue / residual");
-  if (ring_v2()) {  // register-blocked schedule: KR = 24 register weight fragments, staging two planes ahead
-#define R2_LAUNCH(F, G, R)                                                                                        \
-  hipLaunchKernelGGL((conv32_ring2_kernel<F, G, R, 24, 0, 2, 1>), dim3((unsigned)grid), dim3(R2_NT), 0, s,        \
-                     (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, \
+#ifdef U3D_RING_EXP
+  if (const int ex = opt(OPT_RING_EXP)) {  // diagnostic build: timing ablations of the static schedule
+#define RG_EX(F, G, R, K, E)                                                                                     \
+  hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K, false, false, E>), dim3((unsigned)grid), dim3(RG_NT), 0, s,  \
+                     (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta,  \
                      sp, g)
-    if (flip) R2_LAUNCH(true, false, false);
-    else if (gn_stats && residual) R2_LAUNCH(false, true, true);
-    else if (gn_stats) R2_LAUNCH(false, true, false);
-    else if (residual) R2_LAUNCH(false, false, true);
-    else R2_LAUNCH(false, false, false);
-#undef R2_LAUNCH
-    return check_launch("conv32_ring2_kernel");
+#define RG_EXS(E)                                                                   \
+  do {                                                                              \
+    if (flip) RG_EX(true, false, false, 27, E);                                     \
+    else if (gn_stats && residual) RG_EX(false, true, true, 12, E);                 \
+    else if (gn_stats) RG_EX(false, true, false, 16, E);                            \
+    else RG_EX(false, false, false, 27, E);                                         \
+  } while (0)
+    switch (ex) {
+      case 1: RG_EXS(1); break;
+      case 2: RG_EXS(2); break;
+      case 4: RG_EXS(4); break;
+      case 8: RG_EXS(8); break;
+      case 16: RG_EXS(16); break;
+      case 32: RG_EXS(32); break;
+      case 18: RG_EXS(18); break;
+      case 12: RG_EXS(12); break;
+      case 3: RG_EXS(3); break;
+      default: return fail(U3D_EINVAL, "RING_EXP: unknown ablation %d", ex);
+    }
+#undef RG_EXS
+#undef RG_EX
+    return check_launch("conv32_ring_kernel (ablation)");
   }
+#endif
   // register budget (2 waves per SIMD): GN + residual holds 12 weight steps, GN 16, the others 27
   const bool kr = ring_kr(1) != 0;
   if (flip) RG_KR(true, false, false, 27);

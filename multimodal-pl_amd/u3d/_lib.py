@@ -152,7 +152,10 @@ def lib():
             raise U3DError(f"libu3d.so not found at {LIB_PATH}: build it (python -c 'import __graft_entry__ as g; "
                            "g.build()'); the HIP path has no fallback")
         h = ctypes.CDLL(LIB_PATH)
+        ab = bool(os.environ.get("U3D_LIB"))  # an A/B build of an older tree may lack entry points added since
         for name, args in _SIGS.items():
+            if ab and not hasattr(h, name):
+                continue
             f = getattr(h, name)
             f.argtypes = args
             f.restype = _RESTYPE.get(name, I)

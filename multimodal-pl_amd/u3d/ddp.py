@@ -149,10 +149,13 @@ class U3DDataParallel(torch.nn.Module):
     gradients are checked to be the same set on every rank (fail loudly otherwise), flattened into ONE buffer,
     averaged by one all-reduce and copied back, so no rank is ever left with an unsynchronised gradient."""
 
-    def __init__(self, module, group=None, bucket_mb=25.0):
+    def __init__(self, module, group=None, bucket_mb=25.0, force_buckets=False):
+        """``force_buckets``: run the bucketed all-reduce machinery even at world size 1 (tests of the RCCL branch
+        on a one-GPU box; at world 1 the average is the identity)."""
         super().__init__()
         self.module = module
-        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.distributed = dist.is_available() and dist.is_initialized() and (
+            dist.get_world_size(group) > 1 or force_buckets)
         self.bucketer = GradBucketer(module.named_parameters(), bucket_mb, group) if self.distributed else None
         self.fallback_names = []  # parameters averaged by the hook in the last backward (tests / diagnostics)
         self._pending = []        # (name, param) collected by the hooks of the running backward

@@ -11,6 +11,15 @@ from ._lib import BF16, F32, call, query
 
 
 
+def get_option(name):
+    """Current value of a library tuning option (csrc/common.h ``Opt``)."""
+    h = _lib.lib()
+    v = ctypes.c_int(0)
+    if h.u3d_get_option(name.encode(), ctypes.byref(v)) != 0:
+        raise _lib.U3DError(h.u3d_last_error().decode())
+    return v.value
+
+
 @contextlib.contextmanager
 def option(name, value):
     """Temporarily set a library tuning option (csrc/common.h ``Opt``; e.g. ``option("CONVG_PERSIST", 0)``) for a test
@@ -285,7 +294,7 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
             and _use_gen_brick(x.dtype, cin, cout, k, stride, (n, d, h, w_))
             and not _use_conv1x1(x.dtype, cin, cout, k, n) and not _use_conv32(x.dtype, cin, cout, k, stride, n, w_)
             and not _use_small(x.dtype, cin, cout, k, stride, (n, d, h, w_))
-            and os.environ.get("U3D_CONVG_PERSIST", "1") != "0"):
+            and get_option("CONVG_PERSIST") != 0):
         # persistent brick conv with the output's GroupNorm(16) statistics from its epilogue (no statistics pass)
         st, ga, be, G = gn if gn is not None else (None, None, None, 0)
         y = torch.empty((n, d, h, w_, cout), dtype=x.dtype, device=x.device)
@@ -431,7 +440,7 @@ def _brick_dgrad_gn_ok(dy, cin, k, stride, x_shape, G):
     n, d, h, w_ = x_shape
     cout = dy.shape[-1]
     return (BRICK_DGRAD_GN and dy.dtype == torch.bfloat16 and k == 3 and stride == 1 and n <= 16 and cin <= 256
-            and cin % G == 0 and os.environ.get("U3D_CONVG_PERSIST", "1") != "0"
+            and cin % G == 0 and get_option("CONVG_PERSIST") != 0
             and not _use_conv1x1(dy.dtype, cout, cin, k, n) and not _use_conv32(dy.dtype, cin, cout, k, stride, n, w_)
             and not _use_small(dy.dtype, cout, cin, k, stride, (n, d, h, w_))
             and _use_gen_brick(dy.dtype, cout, cin, k, stride, (n, d, h, w_)))

@@ -120,3 +120,65 @@ def test_u3d_data_parallel_world2_equals_concatenated_batch(gpu, tmp_path):
         assert fallback == ["extra_scale"], fallback  # everything else went through the native buckets
     for p in procs:
         assert p.exitcode == 0
+
+
+
+def test_rccl_world1_bucketed_step_matches_plain_step(gpu, monkeypatch):
+    """The RCCL branch of the data-parallel path on the box's one GPU (never executed): torch.distributed
+    backend "nccl" (= RCCL) at world size 1, U3DDataParallel forced onto its bucket machinery (1 MB buckets: the
+    all-reduces are launched from inside the native backward), ReduceOp.AVG (avg_native), the async works waited on
+    the stream, the fallback path (one flat all-reduce after a rank-consistency all-gather) for the plain-autograd
+    parameter, and COLLECTIVE_IN_FLIGHT switching the 96^3-class data-gradient rings to the work-stealing kernel
+    (u3d_conv32_ring_q). bf16 step on 2 x 1 x 64^3 (the 32-channel convs run on the ring). Averaging over one rank is
+    exact and the work-stealing ring is bitwise equal to the static one, so gradients and post-SGD weights must
+    equal the plain single-process step (checked to <= 1e-6 relative; reference: train_amos_atlas_final.py:141-144,
+    375 and run_amos_atlas_final.sh:2)."""
+    import torch.distributed as dist
+    from loss_functions.loss_partial import EDiceLoss_partial
+    from oracle.weights_recipe import input_volume, label_volume
+    from u3d import _lib, ops
+    from u3d.ddp import U3DDataParallel
+    from u3d.optim import SGD
+
+    x = torch.from_numpy(input_volume((2, 1, 64, 64, 64), seed=61, kind="ct")).to(gpu)
+    lab = torch.from_numpy(label_volume((2, 64, 64, 64), 16, seed=62)).to(gpu)
+    mask = [torch.tensor(MASK)]
+
+    def step(m, net):
+        opt = SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            lg, _, _ = net(x)
+        loss = EDiceLoss_partial(16)(lg.float() * m.extra_scale, lab, mask=mask)
+        loss.backward()
+        g = {k: p.grad.detach().double().clone() for k, p in m.named_parameters()}
+        opt.step()
+        torch.cuda.synchronize()
+        return g, {k: p.detach().double().clone() for k, p in m.named_parameters()}
+
+    m = _build(gpu)
+    g_ref, w_ref = step(m, m)
+    del m
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        called = []
+        real_call = _lib.call
+        monkeypatch.setattr(ops, "call", lambda name, *a: (called.append((name, ops.COLLECTIVE_IN_FLIGHT[0])),
+                                                            real_call(name, *a))[1])
+        m = _build(gpu)
+        net = U3DDataParallel(m, bucket_mb=1.0, force_buckets=True)
+        assert net.bucketer is not None and net.bucketer.avg_native and len(net.bucketer.buckets) > 10
+        g, w = step(m, net)
+    finally:
+        dist.destroy_process_group()
+    assert not ops.COLLECTIVE_IN_FLIGHT[0]
+    assert ("u3d_conv32_ring_q", True) in called, "no work-stealing data-gradient ring while a bucket was in flight"
+    assert net.fallback_names == ["extra_scale"], net.fallback_names
+    for k in g_ref:
+        r = ((g[k] - g_ref[k]).norm() / g_ref[k].norm().clamp_min(1e-30)).item()
+        assert r <= 1e-6, f"{k}: gradient rel L2 {r:.3e} vs the plain step"
+        assert (w[k] - w_ref[k]).abs().max().item() <= 1e-6 * max(1.0, w_ref[k].abs().max().item()), k

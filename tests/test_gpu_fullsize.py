@@ -212,7 +212,8 @@ def test_trunk_conv_wgrad_bench_size(gpu, cin, cout, D, k, s):
 
 
 # ------------------------------------------------------------------------------------------ whole step
-def test_bf16_training_step_2x96_tracks_fp32(gpu):
+@pytest.mark.parametrize("modality", ["ct", "mixed"])
+def test_bf16_training_step_2x96_tracks_fp32(gpu, modality):
     """The bench step (BASELINE configs[1]: unet3D_baseline(16), 2 x 1 x 96^3, EDiceLoss_partial(16) with uce,
     backward) in bf16 against the same step in the fp32 parity mode, whose forward is pinned to the reference at
     96^3 by G5 and whose backward by G3 (32^3).
@@ -232,13 +233,19 @@ def test_bf16_training_step_2x96_tracks_fp32(gpu):
     GroupNorm — and its gradient error against the fp32 native step is the yardstick: per parameter the native
     bf16 error <= 1.5 x the autocast error + 1e-2 (measured: the two agree within 1.5x on every parameter, worst
     ratio layer0.0.gn2.weight 5.1e-2 vs 3.5e-2; largest 0.38 vs 0.38 on layer4.0.conv1), and the cosine of every
-    conv-weight gradient >= 0.9."""
+    conv-weight gradient >= 0.9.
+
+    modality "mixed" = BASELINE configs[3] on one GPU: one CT-normalised patch and one z-scored MRI-like patch
+    (N(0, 1); MOTSDataset.py:183-185) in the batch, the batch's mask[0] applied to both (loss_partial.py:87), the
+    same tolerances."""
     import unet3D
     from loss_functions.loss_partial import EDiceLoss_partial
     from oracle import ref_cpu as O
     from oracle.weights_recipe import apply_recipe, input_volume, label_volume
 
     x = torch.from_numpy(input_volume((2, 1, 96, 96, 96), seed=41, kind="ct")).to(gpu)
+    if modality == "mixed":  # sample 1: z-scored MRI
+        x[1:] = torch.from_numpy(input_volume((1, 1, 96, 96, 96), seed=43, kind="normal")).to(gpu)
     lab = torch.from_numpy(label_volume((2, 96, 96, 96), 16, seed=42)).to(gpu)
     mask = [torch.tensor([1, 1, 0, 1, 1, 0, 1, 1, 1, 0, 1, 1, 1, 1, 0, 1])]
     crit = EDiceLoss_partial(16)
