@@ -194,20 +194,6 @@ int u3d_conv32_ring_q(int flip, const void* x, int n, int d, int h, int w, const
                       float* stats_ws, int* queue, u3d_stream_t stream);
 int u3d_conv32_ring_q_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
                                      u3d_stream_t stream);
-/* Data gradient of the 32->32 conv (u3d_conv32_ring flip) that also accumulates the partial sums of the backward
- * of the GroupNorm + ReLU in front of the forward conv (x = that GroupNorm's input, gn_* its statistics and affine;
- * unet3D.py:44-53) into part_ws (u3d_conv32_ring_stats_ws_floats(n) floats); u3d_conv32_ring_gn_bwd_coef turns
- * them into the apply coefficients coef [n][5][32] + dgamma/dbeta (+= when accumulate_params), and
- * u3d_gn_bwd_apply_coef writes dx (+)= alpha m dA + bx x + d — the separate partial pass over dA and x is gone. */
-int u3d_conv32_ring_dgrad_gn(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad, const void* x,
-                             const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                             void* dx, float* part_ws, u3d_stream_t stream);
-int u3d_conv32_ring_gn_bwd_coef(const float* part_ws, int n, int d, int h, int w, int gn_groups,
-                                const float* gn_stats, const float* gn_gamma, const float* gn_beta, float* coef,
-                                float* dgamma, float* dbeta, int accumulate_params, u3d_stream_t stream);
-int u3d_gn_bwd_apply_coef(int dtype, const void* da, const void* x, int n, int c, long long v, const float* coef,
-                          void* dx, int accumulate, u3d_stream_t stream);
-
 /* Stride-1 3^3 weight gradient, depth-streaming ring schedule (wgrad_ring.hip): same partial-slab contract as
  * u3d_conv_wgrad_brick ([nsplit][27][cout_p][cin_p] fp32, summed by the caller in fixed order); a split is a
  * contiguous range of 16x16-voxel output planes walked down d. */
@@ -229,15 +215,6 @@ int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, int h, int w
  * (stats_ws, >= u3d_convg_brick_stats_ws_floats floats) and a fixed-order fp64 finalize. Replaces the separate
  * statistics pass over y. Requires cout % 32 == 0 and cin <= 256 with a GN prologue. */
 long long u3d_convg_brick_stats_ws_floats(int n, int d, int h, int w, int cout);
-/* u3d_convg_brick data gradient (dy [n][d][h][w][cout] -> dA [..][cin], wpk = data-grad pack) of a conv whose forward
- * had the GroupNorm + ReLU prologue gn(x) (x = the GN input, gn_* = that GroupNorm): also forms, from per-channel
- * partial sums (sum m dA, sum m dA x) taken in the epilogue, the GN-backward apply coefficients coef[n][5][cin] and
- * dgamma / dbeta (accumulated when accumulate_params) for u3d_gn_bwd_apply_coef — no partial pass over dA and x.
- * part_ws >= u3d_convg_brick_stats_ws_floats(n, d, h, w, 2 * cin) floats; cin <= 256, n <= 16. */
-int u3d_convg_brick_dgrad_gn(const void* dy, int n, int cout, int d, int h, int w, const void* wpk_dgrad, int cin,
-                             const void* x, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
-                             int gn_groups, void* dA, float* part_ws, long long ws_floats, float* coef, float* dgamma,
-                             float* dbeta, int accumulate_params, u3d_stream_t stream);
 int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                           const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                           const void* residual, void* y, float* stats_ws, long long ws_floats, float* stats_out,

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <algorithm>
 #include <string>
+#include <type_traits>
 
 #include "../../include/u3d.h"
 
@@ -53,6 +54,15 @@ int opt(Opt o);
     if (e_ != hipSuccess)                                                           \
       return ::u3d::fail(U3D_EHIP, "%s: %s", #expr, hipGetErrorString(e_));         \
   } while (0)
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
 
 // ------------------------------------------------------------------------------------- bf16 / f32
 typedef uint16_t bf16;  // bf16 stored as its bit pattern
@@ -153,17 +163,25 @@ __device__ __forceinline__ u32x4 gn_relu8(u32x4 v, const f32x2 (&sc)[4], const f
 }
 
 // per-thread scale/shift of channels c0 .. c0+7 (clamped) of sample n for gn_relu8
+// (buffer loads: 32-bit offsets from scalar bases, so a caller that refreshes the table inside a loop holds no
+// per-lane 64-bit addresses across it)
 __device__ __forceinline__ void gn_coef8(const float* __restrict__ st, const float* __restrict__ gamma,
                                          const float* __restrict__ beta, int groups, int cin, int n, int c0,
                                          f32x2 (&sc)[4], f32x2 (&sh)[4]) {
   const int cpg = cin / groups;
+  const auto srs = __builtin_amdgcn_make_buffer_rsrc((void*)st, 0, 0x7FFFFFFF, 0x00020000);
+  const auto grs = __builtin_amdgcn_make_buffer_rsrc((void*)gamma, 0, 0x7FFFFFFF, 0x00020000);
+  const auto brs = __builtin_amdgcn_make_buffer_rsrc((void*)beta, 0, 0x7FFFFFFF, 0x00020000);
+  asm volatile("" : "+v"(c0));  // the channel offsets are formed here, not hoisted into the caller's loop
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = min(c0 + e, cin - 1), gg = c / cpg;
-    const float mean = st[(n * groups + gg) * 2], rstd = st[(n * groups + gg) * 2 + 1];
-    const float s = rstd * gamma[c];
+    const int so = (n * groups + gg) * 8;
+    const float mean = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, so, 0, 0));
+    const float rstd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, so + 4, 0, 0));
+    const float s = rstd * __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, c * 4, 0, 0));
     sc[e >> 1][e & 1] = s;
-    sh[e >> 1][e & 1] = beta[c] - mean * s;
+    sh[e >> 1][e & 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, c * 4, 0, 0)) - mean * s;
   }
 }
 

@@ -286,21 +286,18 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
 // epilogue is register-only (permlane32 swap, residual add, two 16-B stores per lane and co block) and never
 // touches the LDS the next unit's halo is being written into. Same operands, same fp32 accumulation order per
 // output (chunk, tap plane, tap, k-half) as convg_brick_kernel: bitwise-equal results.
-template <int CO, bool FLIP, int BWX = 16, bool BGT = false>
+template <int CO, bool FLIP, int BWX = 16>
 __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                                bf16* __restrict__ y, const bf16* __restrict__ res,
                                                                const float* __restrict__ gstat,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta, GBGeom g, int per,
-                                                               int nunits, float* __restrict__ spart = nullptr,
-                                                               float* __restrict__ bgpart = nullptr) {
+                                                               int nunits, float* __restrict__ spart = nullptr) {
   constexpr int TN = CO / 32;
   constexpr int WROWS = 9 * CO;
   constexpr int WLD = (WROWS * 4 + GB_NT - 1) / GB_NT;
   // brick 4 x 8 x BWX: BWX = 16 -> 16 row tiles of (2 h-rows x 16 w), TM = 2 per wave; BWX = 8 (8- but not 16-multiple
   // planes, e.g. 24^3: no half-empty bricks) -> 8 row tiles of (4 h-rows x 8 w), TM = 1 per wave
-  // GN-backward partials in the data-gradient epilogue (compile time: the plain data gradient keeps its registers)
-  constexpr bool BGC = FLIP && BGT;
   constexpr int BW = BWX, HH = GB_BH + 2, HW = BW + 2, NH = (GB_BD + 2) * HH * HW;
   constexpr int HLD = (NH + GB_NT / 4 - 1) / (GB_NT / 4), PS = NH * 16 + 64, TM = BW / 8;
   static_assert(BW == 16 || BW == 8, "brick width");
@@ -319,10 +316,13 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   __shared__ __attribute__((aligned(16))) f32x2 gtab[2][GB_MAXC];
   // output GroupNorm statistics (spart != nullptr): per (wave, lane half, tn, run v, channel pair q) (sum, sum sq)
   __shared__ f32x2 sst[8][2][TN * 2 * 4];
-  // data gradient with the GN-backward partials (bgpart, FLIP): per (wave, lane half, tn, run v, channel e)
-  // (sum m dA, sum m dA x) of the GroupNorm + ReLU in front of the forward conv; res = that GN's input x
-  __shared__ f32x2 bst[BGC ? 8 : 1][2][BGC ? TN * 2 * 8 : 1];
 
+  // the data gradient never takes a residual or output statistics (convg_impl): dead at compile time, so its
+  // epilogue's registers are not reserved
+  if constexpr (FLIP) {
+    res = nullptr;
+    spart = nullptr;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int bid;
@@ -358,33 +358,46 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   u32x4 wpre[WLD];
   const int sch = tid & 3, srow0 = tid >> 2;
   int stg_nn = 0, stg_c = 0;  // sample and chunk of the staged halo (GN table lookup at commit)
+  // (buffer loads: 32-bit offsets from scalar bases, no per-lane 64-bit addresses held across the unit loop)
+  const auto srs = __builtin_amdgcn_make_buffer_rsrc((void*)gstat, 0, has_gn ? 0x7FFFFFFF : 0, 0x00020000);
+  const auto grs = __builtin_amdgcn_make_buffer_rsrc((void*)gamma, 0, has_gn ? 0x7FFFFFFF : 0, 0x00020000);
+  const auto brs = __builtin_amdgcn_make_buffer_rsrc((void*)beta, 0, has_gn ? 0x7FFFFFFF : 0, 0x00020000);
   auto gtab_fill = [&](int nn) {
     if (has_gn && tid < gtc_p) {
-      const int c = min(tid, gtc - 1), gg = c / (gtc / g.gn_groups);
-      const float mean = gstat[(nn * g.gn_groups + gg) * 2], rstd = gstat[(nn * g.gn_groups + gg) * 2 + 1];
-      const float sc_ = rstd * gamma[c];
-      gtab[nn & 1][tid] = f32x2{sc_, beta[c] - mean * sc_};
+      int t = tid;
+      asm volatile("" : "+v"(t));  // recompute channel and group here (once per sample), not held across the loop
+      const int c = min(t, gtc - 1), gg = c / (gtc / g.gn_groups);
+      const int so = (nn * g.gn_groups + gg) * 8;
+      const float mean = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, so, 0, 0));
+      const float rstd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, so + 4, 0, 0));
+      const float sc_ = rstd * __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, c * 4, 0, 0));
+      gtab[nn & 1][tid] = f32x2{sc_, __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, c * 4, 0, 0)) - mean * sc_};
     }
   };
+  // buffer loads with 32-bit offsets (the host guarantees x and the weight pack below 2 GiB): out-of-range offsets
+  // return zeros with no branch around the load, and an offset needs one register, not a 64-bit address
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, 0x7FFFFFFF, 0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)wpk, 0, 0x7FFFFFFF, 0x00020000);
+  const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, res ? 0x7FFFFFFF : 0, 0x00020000);
+  const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, 0x7FFFFFFF, 0x00020000);
+  const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)spart, 0, spart ? 0x7FFFFFFF : 0, 0x00020000);
+  typedef __attribute__((ext_vector_type(2))) uint32_t v2u32;
   auto halo_load = [&](const Unit& q, int c) {
     hmask = 0;
     stg_nn = q.nn;
     stg_c = c;
+    const int cc = c * 32 + sch * 8;
 #pragma unroll
     for (int i = 0; i < HLD; ++i) {
       const int row = srow0 + i * (GB_NT / 4);
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (row < NH) {
-        const int hw = row % HW, hr = (row / HW) % HH, hd = row / (HW * HH);
-        const int zd = q.d0 - 1 + hd, zh = q.h0 - 1 + hr, zw = q.w0 - 1 + hw;
-        const int cc = c * 32 + sch * 8;
-        if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w) {
-          hmask |= 1u << i;
-          if (cc < g.cin)
-            v = *reinterpret_cast<const u32x4*>(x + ((((long long)q.nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc);
-        }
-      }
-      hpre[i] = v;
+      const int hw = row % HW, hr = (row / HW) % HH, hd = row / (HW * HH);
+      const int zd = q.d0 - 1 + hd, zh = q.h0 - 1 + hr, zw = q.w0 - 1 + hw;
+      const bool in = row < NH && (unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
+                      (unsigned)zw < (unsigned)g.w;
+      hmask |= (in ? 1u : 0u) << i;
+      const unsigned off =
+          in && cc < g.cin ? (unsigned)(((((q.nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc) * 2) : 0x7FFFFFF0u;
+      hpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
   };
   auto halo_commit = [&]() {
@@ -413,15 +426,12 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
 #pragma unroll
     for (int i = 0; i < WLD; ++i) {
       const int ci = tid + i * GB_NT;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (ci < WROWS * 4) {
-        const int ch = ci / WROWS, row = ci % WROWS;
-        const int j = row / CO, co = co0 + row % CO;
-        const int t = td * 9 + j;
-        if (co < g.cout_p)
-          v = *reinterpret_cast<const u32x4*>(wpk + ((long long)t * g.cout_p + co) * g.cin_p + c * 32 + ch * 8);
-      }
-      wpre[i] = v;
+      const int ch = ci / WROWS, row = ci % WROWS;
+      const int j = row / CO, co = co0 + row % CO;
+      const int t = td * 9 + j;
+      const unsigned off = ci < WROWS * 4 && co < g.cout_p
+                               ? (unsigned)(((t * g.cout_p + co) * g.cin_p + c * 32 + ch * 8) * 2) : 0x7FFFFFF0u;
+      wpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
     }
   };
   auto w_commit = [&](int buf) {
@@ -479,27 +489,37 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       }
       const char* wb = wbuf[par];
       const int od = FLIP ? 2 - td : td;
-#pragma unroll 3
-      for (int j = 0; j < 9; ++j) {
+      // the tap plane's 18 k16 steps (tap j, k-half k), the fragments of step i + 1 read before the MFMAs of step
+      // i (one scheduling region per step): two fragment sets in flight, so the 64-channel variants keep the
+      // accumulators and the staging prefetch within 256 VGPRs
+      bf16x8 fa[2][TM], fb[2][TN];
+      auto rd = [&](int j, int k, int slot) {
         const int th = j / 3, tw = j % 3;
         const int oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
         const int toff = (od * HH + oh) * HW + ow;
+        const int plane = 2 * k + hh;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int plane = 2 * k + hh;
-          bf16x8 a[TM], bb[TN];
+        for (int tm = 0; tm < TM; ++tm)
+          fa[slot][tm] = *reinterpret_cast<const bf16x8*>(hal + plane * PS + (arow[tm] + toff) * 16);
 #pragma unroll
-          for (int tm = 0; tm < TM; ++tm)
-            a[tm] = *reinterpret_cast<const bf16x8*>(hal + plane * PS + (arow[tm] + toff) * 16);
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn)
-            bb[tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
+        for (int tn = 0; tn < TN; ++tn)
+          fb[slot][tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
+      };
+      rd(0, 0, 0);
+#pragma unroll 1
+      for (int j0 = 0; j0 < 9; j0 += 3) {
+        static_for<0, 6>([&](auto ic) {
+          constexpr int i = decltype(ic)::value, slot = i & 1;
+          const int j = j0 + (i >> 1);
+          if (i < 5 || j0 < 6) rd(i < 5 ? j + ((i & 1) ? 1 : 0) : j0 + 3, (i + 1) & 1, slot ^ 1);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
-              acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bb[tn], a[tm], acc[tm][tn], 0, 0, 0);
-        }
+              acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[slot][tn], fa[slot][tm], acc[tm][tn], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        });
       }
       if (last) break;  // the last step's staging commit runs after the residual loads are issued (below)
       w_commit(par ^ 1);  // the other buffer: its readers finished before the previous barrier
@@ -514,7 +534,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     // epilogue from registers: lane (r, hh) holds channels tn*32 + 8q + 4hh + e (acc[tm][tn][4q + e]) of voxel
     // ovox[tm]; after the swap it holds channels tn*32 + 8hh .. +7 and tn*32 + 16 + 8hh .. +7
     // this lane's output voxels (MFMA column r of row tiles 0, 1)
-    long long ovox[TM];
+    int ovox[TM];  // < 2^31 voxels x channels (host check): 32-bit buffer offsets
     bool ook[TM];
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
@@ -522,41 +542,42 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       tile_vox(TM * wave + tm, r, vd, vh, vw);
       const int zd = cu.d0 + vd, zh = cu.h0 + vh, zw = cu.w0 + vw;
       ook[tm] = zd < g.d && zh < g.h && zw < g.w;
-      ovox[tm] = (((long long)cu.nn * g.d + zd) * g.h + zh) * g.w + zw;
+      ovox[tm] = ((cu.nn * g.d + zd) * g.h + zh) * g.w + zw;
     }
     u32x4 rv[TM][TN][2];
-    if (res) {
+    auto res_load = [&](int tn) {  // the residual of co block tn (buffer loads: zeros where res is null)
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-          for (int v = 0; v < 2; ++v) {
-            const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
-            rv[tm][tn][v] = (ook[tm] && co < g.cout) ? *reinterpret_cast<const u32x4*>(res + ovox[tm] * g.cout + co)
-                                                     : u32x4{0u, 0u, 0u, 0u};
-          }
-    }
-    // the last step's staging commit (the next unit's first weights and halo) while the residual loads fly
+        for (int v = 0; v < 2; ++v) {
+          const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
+          const unsigned ro = (ook[tm] && co < g.cout) ? (unsigned)((ovox[tm] * g.cout + co) * 2) : 0x7FFFFFF0u;
+          rv[tm][tn][v] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
+        }
+    };
+    // the first co block's residual flies under the last step's staging commit (the next unit's first weights and
+    // halo); the other blocks' are issued after it, when the staging registers are free
+    if (res) res_load(0);
     if (more) {
       w_commit(par ^ 1);
       __syncthreads();
       halo_commit();
     }
+    if (res) {
+#pragma unroll
+      for (int tn = 1; tn < TN; ++tn) res_load(tn);
+    }
     __syncthreads();
     par ^= 1;
     // (statistics of the stored bf16 outputs, per channel pair: the GN(16) groups of every cout % 32 == 0 hold
     // whole pairs; fp32 per lane and unit, fixed-order reductions, fp64 across units in the finalize)
-    f32x2 ps[TN * 2 * 4];
-#pragma unroll
-    for (int i = 0; i < TN * 2 * 4; ++i) ps[i] = f32x2{0.f, 0.f};
-    f32x2 bs[BGC ? 2 * 8 : 1];  // BG: this tn's (v, e) channel sums (one co block at a time: fewer live registers)
+    // per co block tn: (sum, sum sq) of the 4 channel pairs q of each v half, over this lane's voxels; reduced over the
+    // lane half (32 voxels) and stored per wave into the LDS before the next co block (8 pairs live, not 16)
+    f32x2 ps[2 * 4];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      if constexpr (BGC) {
 #pragma unroll
-        for (int i = 0; i < 2 * 8; ++i) bs[i] = f32x2{0.f, 0.f};
-      }
+      for (int i = 0; i < 2 * 4; ++i) ps[i] = f32x2{0.f, 0.f};
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
         uint32_t pk[4][2];
@@ -577,24 +598,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
         for (int v = 0; v < 2; ++v) {
           const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
           u32x4 o = {pk[2 * v][0], pk[2 * v][1], pk[2 * v + 1][0], pk[2 * v + 1][1]};
-          if constexpr (BGC) {
-            {  // m = relu mask of the forward GN prologue on x; gd = m dA (the stored bf16 dA)
-              float a8[8], x8[8];
-              load16<bf16>(reinterpret_cast<const bf16*>(&o), a8);
-              load16<bf16>(reinterpret_cast<const bf16*>(&rv[tm][tn][v]), x8);
-              const f32x2* gt = &gtab[cu.nn & 1][min(co, gtc_p - 8)];
-#pragma unroll
-              for (int e = 0; e < 8; ++e) {
-                const f32x2 cf = gt[e];
-                const bool on = ook[tm] && co + e < g.cout && fmaf(x8[e], cf[0], cf[1]) > 0.f;
-                const float gd = on ? a8[e] : 0.f;
-                f32x2& t = bs[v * 8 + e];
-                t[0] += gd;
-                t[1] = fmaf(gd, on ? x8[e] : 0.f, t[1]);
-              }
-            }
-          }
-          if (res && !BGC) {
+          if (res) {
             float a8[8], c8[8];
             load16<bf16>(reinterpret_cast<const bf16*>(&o), a8);
             load16<bf16>(reinterpret_cast<const bf16*>(&rv[tm][tn][v]), c8);
@@ -602,7 +606,8 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
             for (int e = 0; e < 8; ++e) a8[e] += c8[e];
             store16<bf16>(reinterpret_cast<bf16*>(&o), a8);
           }
-          if (ook[tm] && co < g.cout) *reinterpret_cast<u32x4*>(y + ovox[tm] * g.cout + co) = o;
+          if (ook[tm] && co < g.cout)
+            __builtin_amdgcn_raw_buffer_store_b128(o, yrs, (unsigned)((ovox[tm] * g.cout + co) * 2), 0, 0);
           if (spart != nullptr) {
             float f8[8];
             load16<bf16>(reinterpret_cast<const bf16*>(&o), f8);
@@ -610,52 +615,33 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const float a0 = on ? f8[2 * q] : 0.f, a1 = on ? f8[2 * q + 1] : 0.f;
-              f32x2& t = ps[(tn * 2 + v) * 4 + q];
+              f32x2& t = ps[v * 4 + q];
               t[0] += a0 + a1;
               t[1] = fmaf(a0, a0, fmaf(a1, a1, t[1]));
             }
           }
         }
       }
-      if constexpr (BGC) {  // this tn's channel sums: reduce over the 32 voxels of each lane half into the LDS
+      if (spart != nullptr) {  // this tn's pairs: reduce over the 32 voxels of each lane half into the LDS
 #pragma unroll
-        for (int i = 0; i < 2 * 8; ++i)
+        for (int i = 0; i < 2 * 4; ++i)
 #pragma unroll
           for (int o = 1; o < 32; o <<= 1) {
-            bs[i][0] += __shfl_xor(bs[i][0], o);
-            bs[i][1] += __shfl_xor(bs[i][1], o);
+            ps[i][0] += __shfl_xor(ps[i][0], o);
+            ps[i][1] += __shfl_xor(ps[i][1], o);
           }
         if (r == 0)
 #pragma unroll
-          for (int i = 0; i < 2 * 8; ++i) bst[wave][hh][tn * 16 + i] = bs[i];
+          for (int i = 0; i < 2 * 4; ++i) sst[wave][hh][tn * 8 + i] = ps[i];
       }
     }
-    if constexpr (BGC) {  // the 8 waves in order, per channel of the tile
-      __syncthreads();
-      if (tid < CO) {  // channel tid -> (tn, v, hh, e)
-        const int c = tid, tn = c >> 5, w32 = c & 31, v = w32 >> 4, h_ = (w32 >> 3) & 1, e = w32 & 7;
-        f32x2 t = {0.f, 0.f};
-        for (int w = 0; w < 8; ++w) t += bst[w][h_][tn * 16 + v * 8 + e];
-        *reinterpret_cast<f32x2*>(bgpart + ((long long)u * CO + c) * 2) = t;
-      }
-    }
-    if (spart != nullptr) {  // reduce over the 32 voxels of each lane half, then the 8 waves in order
-#pragma unroll
-      for (int i = 0; i < TN * 2 * 4; ++i)
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          ps[i][0] += __shfl_xor(ps[i][0], o);
-          ps[i][1] += __shfl_xor(ps[i][1], o);
-        }
-      if (r == 0)
-#pragma unroll
-        for (int i = 0; i < TN * 2 * 4; ++i) sst[wave][hh][i] = ps[i];
+    if (spart != nullptr) {  // the 8 waves in order, per channel pair of the tile
       __syncthreads();
       if (tid < CO / 2) {  // channel pair tid of the tile: c = 2 tid -> (tn, v, hh, q)
         const int c = 2 * tid, tn = c >> 5, w32 = c & 31, v = w32 >> 4, h_ = (w32 >> 3) & 1, q = (w32 & 7) >> 1;
         f32x2 t = {0.f, 0.f};
         for (int w = 0; w < 8; ++w) t += sst[w][h_][(tn * 2 + v) * 4 + q];
-        *reinterpret_cast<f32x2*>(spart + ((long long)u * CO + c)) = t;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, t), prs, (u * CO + c) * 4, 0, 0);
       }
     }
     cu = nu;
@@ -692,67 +678,6 @@ __global__ __launch_bounds__(64) void pbrick_gn_finalize_kernel(const float* __r
   }
 }
 
-// GroupNorm backward coefficients from the data-gradient epilogue partials bgpart[unit][CO][2] = (sum m dA,
-// sum m dA x) per channel (unit = brick * nct + co tile), as ring_gn_bwd_coef_kernel for C <= 256 channels:
-//   s2 = sum m dA xhat = rstd (s3 - mean s1) per channel, then per group a = sum gamma s1 / M, b = sum gamma s2 / M,
-//   coef[n][5][C] = (sc, sh, rstd gamma, -rstd^2 b, -rstd a + rstd^2 b mean); dgamma = sum_n s2, dbeta = sum_n s1.
-// One block: one wave per (sample, channel) with lanes over the sample's bricks, fp64, fixed order.
-__global__ __launch_bounds__(1024) void pbrick_gn_bwd_coef_kernel(const float* __restrict__ part, int n, int C, int co_tile,
-                                                                 int nct, int bps, int groups, double m,
-                                                                 const float* __restrict__ stats,
-                                                                 const float* __restrict__ gamma,
-                                                                 const float* __restrict__ beta, float* __restrict__ coef,
-                                                                 float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                                 int accp) {
-  __shared__ double cs[16][GB_MAXC][2];
-  const int cpg = C / groups, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int p = wave; p < n * C; p += 16) {
-    const int nn = p / C, c = p % C, gr = c / cpg, ct = c / co_tile, cl = c - ct * co_tile;
-    double s1 = 0, s3 = 0;
-    for (int b = lane; b < bps; b += 64) {
-      const float* q = part + ((((long long)nn * bps + b) * nct + ct) * co_tile + cl) * 2;
-      s1 += q[0];
-      s3 += q[1];
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      s1 += __shfl_xor(s1, o);
-      s3 += __shfl_xor(s3, o);
-    }
-    if (lane == 0) {
-      const double mu = stats[(nn * groups + gr) * 2], rs = stats[(nn * groups + gr) * 2 + 1];
-      cs[nn][c][0] = s1;
-      cs[nn][c][1] = rs * (s3 - mu * s1);
-    }
-  }
-  __syncthreads();
-  for (int p = threadIdx.x; p < n * C; p += 1024) {
-    const int nn = p / C, c = p % C, gr = c / cpg;
-    double a = 0, bb = 0;
-    for (int q = 0; q < cpg; ++q) {
-      const int cc = gr * cpg + q;
-      a += (double)gamma[cc] * cs[nn][cc][0];
-      bb += (double)gamma[cc] * cs[nn][cc][1];
-    }
-    const float ca = (float)(a / m), cb = (float)(bb / m);
-    const float mu = stats[(nn * groups + gr) * 2], rs = stats[(nn * groups + gr) * 2 + 1];
-    const float scv = rs * gamma[c];
-    float* o = coef + (long long)nn * 5 * C;
-    o[c] = scv;
-    o[C + c] = beta[c] - mu * scv;
-    o[2 * C + c] = rs * gamma[c];
-    o[3 * C + c] = -rs * rs * cb;
-    o[4 * C + c] = -rs * ca + rs * rs * cb * mu;
-  }
-  for (int c = threadIdx.x; c < C; c += 1024) {
-    double tg = 0, tb = 0;
-    for (int nn = 0; nn < n; ++nn) {
-      tb += cs[nn][c][0];
-      tg += cs[nn][c][1];
-    }
-    if (dgamma) dgamma[c] = (accp ? dgamma[c] : 0.f) + (float)tg;
-    if (dbeta) dbeta[c] = (accp ? dbeta[c] : 0.f) + (float)tb;
-  }
-}
 
 }  // namespace u3d
 
@@ -770,9 +695,7 @@ static int convg_num_cus() {
 
 static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                       const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                      const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream,
-                      float* bgpart = nullptr, float* bg_coef = nullptr, float* dgamma = nullptr, float* dbeta = nullptr,
-                      int accp = 0) {
+                      const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && n <= GB_MAXN, "convg_brick: bad args");
   U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "convg_brick: channels must be multiples of 8");
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "convg_brick: bad GN");
@@ -796,13 +719,12 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
   dim3 grid(nb * g.nct);
   // persistent form (CONVG_PERSIST = 0: the one-shot kernel; u3d_set_option lets a test compare both in-process)
   const bool pers_on = opt(OPT_CONVG_PERSIST) != 0;
-  const bool pers = pers_on && (!gn_stats || g.cin_p <= GB_MAXC);
+  // the persistent kernel addresses x and the weight pack with 32-bit buffer offsets
+  const bool small = (long long)n * d * h * w * std::max(cin, cout) * 2 < (1LL << 31) - 64 &&
+                     27LL * g.cout_p * g.cin_p * 2 < (1LL << 31) - 64;
+  const bool pers = pers_on && small && (!gn_stats || g.cin_p <= GB_MAXC);
   U3D_REQUIRE(!spart || (pers && !flip && cout % 32 == 0), "convg_brick_stats: needs the persistent forward, cout %% 32 == 0");
-  U3D_REQUIRE(!bgpart || (flip && pers_on && gn_stats && g.cout_p <= GB_MAXC && n <= 16 &&
-                          cout % gn_groups == 0 && bg_coef),
-              "convg_brick_dgrad_gn: needs the persistent data gradient, cout <= %d, n <= 16", GB_MAXC);
-  const bool pers_any = pers || bgpart;
-  if (pers_any) {
+  if (pers) {
     // 8-wide bricks where the plane width is a multiple of 8 but not of 16 (24^3: the 16-wide bricks' second
     // column is half empty); CONVG_BW8 = 0 / 1 forces the choice (A/B)
     const int e8 = opt(OPT_CONVG_BW8);
@@ -821,16 +743,7 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
               nwg = cdiv(nunits, per);
 #define U3D_PB(C, F)                                                                                               \
   do {                                                                                                             \
-    if (F && bgpart) {                                                                                             \
-      if (bw8)                                                                                                     \
-        hipLaunchKernelGGL((convg_pbrick_kernel<C, true, 8, true>), dim3(nwg), dim3(GB_NT), 0, s,               \
-                           (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma,  \
-                           gn_beta, gp, per, nunits, nullptr, bgpart);                                             \
-      else                                                                                                         \
-        hipLaunchKernelGGL((convg_pbrick_kernel<C, true, 16, true>), dim3(nwg), dim3(GB_NT), 0, s,              \
-                           (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma,  \
-                           gn_beta, gp, per, nunits, nullptr, bgpart);                                             \
-    } else if (bw8)                                                                                                \
+    if (bw8)                                                                                                       \
       hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 8>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,          \
                          (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
                          nunits, spart);                                                                           \
@@ -847,12 +760,6 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
 #undef U3D_PB
     int rc = check_launch("convg_pbrick_kernel");
     if (rc) return rc;
-    if (bgpart) {
-      hipLaunchKernelGGL(pbrick_gn_bwd_coef_kernel, dim3(1), dim3(1024), 0, s, bgpart, n, cout, co64 ? 64 : 32, gp.nct,
-                         gp.nbd * gp.nbh * gp.nbw, gn_groups, (double)(cout / gn_groups) * d * h * w, gn_stats, gn_gamma,
-                         gn_beta, bg_coef, dgamma, dbeta, accp);
-      return check_launch("pbrick_gn_bwd_coef_kernel");
-    }
     if (!spart) return rc;
     hipLaunchKernelGGL(pbrick_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, spart, co64 ? 64 : 32, gp.nct,
                        gp.nbd * gp.nbh * gp.nbw, cout, (double)(cout / 16) * d * h * w, stats_out);
@@ -896,21 +803,4 @@ extern "C" int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h
   U3D_REQUIRE(ws_floats >= u3d_convg_brick_stats_ws_floats(n, d, h, w, cout), "convg_brick_stats: workspace too small");
   return convg_impl(0, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
                     stats_out, stream);
-}
-
-// u3d_convg_brick data gradient (flip = 1) of a conv whose forward had the GroupNorm + ReLU prologue gn(x) (x = the
-// GN input [n][d][h][w][cin]; gn_* = that GroupNorm): writes dA and, from partial sums taken in the epilogue, the
-// GN-backward apply coefficients coef[n][5][cin] (+ dgamma / dbeta, accumulated when accumulate_params) for
-// u3d_gn_bwd_apply_coef — no separate partial pass over dA and x (unet3D.py:44-53 autograd). part_ws: >=
-// u3d_convg_brick_stats_ws_floats(n, d, h, w, 2 * cin) floats.
-extern "C" int u3d_convg_brick_dgrad_gn(const void* dy, int n, int cout, int d, int h, int w, const void* wpk_dgrad,
-                                        int cin, const void* x, const float* gn_stats, const float* gn_gamma,
-                                        const float* gn_beta, int gn_groups, void* dA, float* part_ws,
-                                        long long ws_floats, float* coef, float* dgamma, float* dbeta,
-                                        int accumulate_params, u3d_stream_t stream) {
-  U3D_REQUIRE(dy && x && dA && part_ws && coef && gn_stats && gn_gamma && gn_beta && gn_groups > 0,
-              "convg_brick_dgrad_gn: bad args");
-  U3D_REQUIRE(ws_floats >= u3d_convg_brick_stats_ws_floats(n, d, h, w, 2 * cin), "convg_brick_dgrad_gn: workspace too small");
-  return convg_impl(1, dy, n, cout, d, h, w, wpk_dgrad, cin, gn_stats, gn_gamma, gn_beta, gn_groups, x, dA, nullptr,
-                    nullptr, stream, part_ws, coef, dgamma, dbeta, accumulate_params);
 }

@@ -21,15 +21,6 @@
 
 namespace u3d {
 
-// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
 constexpr int RG_BH = 8, RG_BW = 32, RG_HH = RG_BH + 2, RG_HW = RG_BW + 2;
@@ -97,12 +88,6 @@ struct RGWalk {
   }
 };
 
-// BG (data gradient only): the output dA feeds the backward of the GroupNorm + ReLU in front of the forward conv
-// (unet3D.py:44-53); the epilogue also accumulates that backward's per-channel partial sums s1 = sum m dA and
-// s3 = sum m dA x (m = the forward prologue's ReLU test on x, the GN input, read in the epilogue through the
-// residual slot; gstat/gamma/beta = that GroupNorm) into spart[wg][32][2]; s2 = sum m dA xhat = rstd (s3 - mean s1)
-// is formed per group in fp64 by the coefficient kernel. No separate partial pass over dA and x is needed
-// (u3d_gn_bwd_apply_coef finishes the backward).
 // Q (work-stealing mode): each workgroup still owns the static range of output planes, split into sub-chunks of g.sc
 // planes, and claims them front to back (one 64-bit compare-and-swap per sub-chunk on its range's word (front,
 // stolen), lane 0, vector atomics) while walking the range as before; a workgroup whose range is exhausted steals
@@ -114,7 +99,7 @@ struct RGWalk {
 // EXP (diagnostic builds only, -DU3D_RING_EXP; results are wrong when set): 1 no per-step barrier, 2 no x staging
 // loads, 4 no MFMAs (a dependent VALU op keeps the fragment reads live), 8 no LDS fragment reads after the first
 // steps, 16 no residual loads / y stores, 32 both SIMD partners use the same side-work schedule (no stagger).
-template <bool FLIP, bool GN, bool RES, int KR, bool BG = false, bool Q = false, int EXP = 0>
+template <bool FLIP, bool GN, bool RES, int KR, bool Q = false, int EXP = 0>
 __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                               bf16* __restrict__ y, const bf16* __restrict__ res,
                                                               const float* __restrict__ gstat,
@@ -210,19 +195,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   // buffer loads: out-of-range offsets return zeros with no branch around the load (no exec-masked paths whose
   // merge would make the wait-count insertion pessimistic)
   const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)g.xbytes, 0x00020000);
-  const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, (RES || BG) ? (int)g.xbytes : 0, 0x00020000);
-  // BG: per-channel (scale, shift, mean, rstd) of the GroupNorm in front of the forward conv, for this sample
-  float* const bgt = reinterpret_cast<float*>(smem + 4 * RG_SS + 4 * RG_NWR * 16 + 1024);
-  if constexpr (BG) {
-    const int smp_ = bid / g.wps;
-    if (tid < 32) {
-      const int cpg = 32 / g.gn_groups, gg = tid / cpg;
-      const float mean = gstat[(smp_ * g.gn_groups + gg) * 2], rstd = gstat[(smp_ * g.gn_groups + gg) * 2 + 1];
-      const float sc_ = rstd * gamma[tid];
-      bgt[tid] = sc_;
-      bgt[32 + tid] = beta[tid] - mean * sc_;
-    }
-  }
+  const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, RES ? (int)g.xbytes : 0, 0x00020000);
   f32x2 sc[4], sh[4];
   int gn_n = -1;
   // branch-free staging: out-of-volume rows load a valid dummy address and are zeroed when written
@@ -281,9 +254,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   float gs[8], gq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) gs[j] = gq[j] = 0.f;
-  float b1[BG ? 16 : 1], b2[BG ? 16 : 1];  // BG: channels 16u + 8h + e -> slot 8u + e
-#pragma unroll
-  for (int j = 0; j < (BG ? 16 : 1); ++j) b1[j] = b2[j] = 0.f;
   int acc_chunk = -1;
   // work-queue mode: the statistics of one chunk, per wave: reduce over the wave's voxels (xor within the 32-lane
   // halves) and write slot (chunk, wave); no barrier, so it can run inside the MFMA chain
@@ -361,19 +331,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       } else {
         if (p.ok) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
       }
-      if constexpr (BG) {
-        float a[8], xv[8];
-        load16<bf16>(reinterpret_cast<const bf16*>(&v), a);       // the stored (bf16) dA
-        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[u]), xv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int c = 16 * u + 8 * h + e;
-          const bool on = p.ok && fmaf(xv[e], bgt[c], bgt[32 + c]) > 0.f;
-          const float gd = on ? a[e] : 0.f;
-          b1[8 * u + e] += gd;
-          b2[8 * u + e] = fmaf(gd, on ? xv[e] : 0.f, b2[8 * u + e]);  // sum m dA x: xhat is formed per group later
-        }
-      }
     }
   };
 
@@ -392,7 +349,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     nw.ok = zh < g.h && zw < g.w;
     nw.vox = (((long long)pc.n * g.d + zo) * g.h + zh) * g.w + zw;
     nw.rv[0] = nw.rv[1] = u32x4{0u, 0u, 0u, 0u};
-    if constexpr ((RES || BG) && (EXP & 16) == 0) {
+    if constexpr (RES && (EXP & 16) == 0) {
       const unsigned ro = nw.ok ? (unsigned)(nw.vox * 64 + 16 * h) : 0xFFFFFFC0u;
       nw.rv[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
       nw.rv[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro + 32, 0, 0));
@@ -600,33 +557,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
     return;
   }
-  if constexpr (BG) {
-    if (spart == nullptr) return;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        b1[j] += __shfl_xor(b1[j], o);
-        b2[j] += __shfl_xor(b2[j], o);
-      }
-    float* red = reinterpret_cast<float*>(ring);  // [wave][channel 32][2]
-    if (r == 0) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int c = 16 * (j >> 3) + 8 * h + (j & 7);
-        red[(wave * 32 + c) * 2] = b1[j];
-        red[(wave * 32 + c) * 2 + 1] = b2[j];
-      }
-    }
-    __syncthreads();
-    if (tid < 64) {
-      float t = 0.f;
-#pragma unroll
-      for (int wv = 0; wv < RG_NT / 64; ++wv) t += red[wv * 64 + tid];
-      spart[(long long)bid * 64 + tid] = t;  // [sample][wps][channel][2]
-    }
-    return;
-  }
   if constexpr (GN) {
     if (spart == nullptr) return;
     // lanes with the same h hold the same groups: reduce over r (xor within 32-lane halves), then over the waves in
@@ -692,8 +622,7 @@ static int ring_kr(int dflt) {  // RING_KR = 0: no weight steps in registers (ex
 static int ring_wgs() { return std::max(1, opt(OPT_RING_WGS)); }  // persistent grid target: one workgroup per CU
 static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
                             const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                            const void* residual, void* y, float* stats_out, float* stats_ws, u3d_stream_t stream,
-                            const void* bg_x = nullptr) {
+                            const void* residual, void* y, float* stats_out, float* stats_ws, u3d_stream_t stream) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv32_ring: bad args");
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0), "conv32_ring: bad GN");
   U3D_REQUIRE(!stats_out || (gn_stats && stats_ws), "conv32_ring: output statistics need the GN prologue + ws");
@@ -721,18 +650,11 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
     if (kr) RG_LAUNCH(F, G, R, K);         \
     else RG_LAUNCH(F, G, R, 0);            \
   } while (0)
-  if (bg_x) {  // data gradient + the backward partial sums of the GroupNorm in front of the forward conv
-    U3D_REQUIRE(flip && gn_stats && stats_ws && !residual, "conv32_ring: bad GN-backward arguments");
-    hipLaunchKernelGGL((conv32_ring_kernel<true, false, false, 12, true>), dim3((unsigned)grid), dim3(RG_NT), 0, s,
-                       (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)bg_x, gn_stats, gn_gamma, gn_beta,
-                       stats_ws, g);
-    return check_launch("conv32_ring_kernel (dgrad + GN backward partials)");
-  }
   U3D_REQUIRE(!(flip && (gn_stats || residual)), "conv32_ring: the data gradient takes no prologue / residual");
 #ifdef U3D_RING_EXP
   if (const int ex = opt(OPT_RING_EXP)) {  // diagnostic build: timing ablations of the static schedule
 #define RG_EX(F, G, R, K, E)                                                                                     \
-  hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K, false, false, E>), dim3((unsigned)grid), dim3(RG_NT), 0, s,  \
+  hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K, false, E>), dim3((unsigned)grid), dim3(RG_NT), 0, s,  \
                      (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta,  \
                      sp, g)
 #define RG_EXS(E)                                                                   \
@@ -821,7 +743,7 @@ extern "C" int u3d_conv32_ring_q(int flip, const void* x, int n, int d, int h, i
   const unsigned grid = (unsigned)(n * g.wps);
   hipStream_t s = (hipStream_t)stream;
 #define RQ_LAUNCH(F, G, R, K)                                                                                     \
-  hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K, false, true>), dim3(grid), dim3(RG_NT), 0, s, (const bf16*)x, \
+  hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K, true>), dim3(grid), dim3(RG_NT), 0, s, (const bf16*)x, \
                      (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, stats_ws, g, queue)
   // register budget: the claim state costs the weight steps of the static variants a few registers
   if (flip) RQ_LAUNCH(true, false, false, 24);
@@ -901,93 +823,6 @@ extern "C" int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, 
   U3D_REQUIRE(stats_ws, "conv32_ring_stats: null statistics workspace");
   return conv32_ring_impl(0, x, n, d, h, w, wpk, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
                           stats_ws, stream);
-}
-
-extern "C" int u3d_conv32_ring_dgrad_gn(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad,
-                                         const void* x, const float* gn_stats, const float* gn_gamma,
-                                         const float* gn_beta, int gn_groups, void* dx, float* part_ws,
-                                         u3d_stream_t stream) {
-  U3D_REQUIRE(x && part_ws && gn_stats && gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0,
-              "conv32_ring_dgrad_gn: bad args");
-  return conv32_ring_impl(1, dy, n, d, h, w, wpk_dgrad, gn_stats, gn_gamma, gn_beta, gn_groups, nullptr, dx, nullptr,
-                          part_ws, stream, x);
-}
-
-// GroupNorm backward coefficients from the ring data-gradient partials (fixed-order fp64): per (n, c) s1, s2 over
-// the sample's workgroups, then per group a = sum gamma s1 / M, b = sum gamma s2 / M and coef[n][5][32] exactly as
-// gn_bwd_partial's last block (sc, sh, alpha, bx, d); dgamma = sum_n s2, dbeta = sum_n s1 (+= when accp).
-__global__ __launch_bounds__(1024) void ring_gn_bwd_coef_kernel(const float* __restrict__ part, int n, int wps,
-                                                               int groups, double m, const float* __restrict__ stats,
-                                                               const float* __restrict__ gamma,
-                                                               const float* __restrict__ beta,
-                                                               float* __restrict__ coef, float* __restrict__ dgamma,
-                                                               float* __restrict__ dbeta, int accp) {
-  __shared__ double cs[16][32][2];
-  const int cpg = 32 / groups;
-  // one wave per (sample, channel): lanes stride over the workgroups' partials, fp64 butterfly (fixed order)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int p = wave; p < n * 32; p += 16) {
-    const int nn = p / 32, c = p % 32, gr = c / cpg;
-    double s1 = 0, s3 = 0;
-    for (int w = lane; w < wps; w += 64) {
-      s1 += part[((long long)nn * wps + w) * 64 + c * 2];
-      s3 += part[((long long)nn * wps + w) * 64 + c * 2 + 1];
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      s1 += __shfl_xor(s1, o);
-      s3 += __shfl_xor(s3, o);
-    }
-    if (lane == 0) {
-      const double mu = stats[(nn * groups + gr) * 2], rs = stats[(nn * groups + gr) * 2 + 1];
-      cs[nn][c][0] = s1;
-      cs[nn][c][1] = rs * (s3 - mu * s1);  // sum m dA xhat
-    }
-  }
-  __syncthreads();
-  for (int p = threadIdx.x; p < n * 32; p += 1024) {
-    const int nn = p / 32, c = p % 32, gr = c / cpg;
-    double a = 0, bb = 0;
-    for (int q = 0; q < cpg; ++q) {
-      const int cc = gr * cpg + q;
-      a += (double)gamma[cc] * cs[nn][cc][0];
-      bb += (double)gamma[cc] * cs[nn][cc][1];
-    }
-    const float ca = (float)(a / m), cb = (float)(bb / m);
-    const float mu = stats[(nn * groups + gr) * 2], rs = stats[(nn * groups + gr) * 2 + 1];
-    const float scv = rs * gamma[c];
-    float* o = coef + (long long)nn * 5 * 32;
-    o[c] = scv;
-    o[32 + c] = beta[c] - mu * scv;
-    o[64 + c] = rs * gamma[c];
-    o[96 + c] = -rs * rs * cb;
-    o[128 + c] = -rs * ca + rs * rs * cb * mu;
-  }
-  if (threadIdx.x < 32) {
-    const int c = threadIdx.x;
-    double tg = 0, tb = 0;
-    for (int nn = 0; nn < n; ++nn) {
-      tb += cs[nn][c][0];
-      tg += cs[nn][c][1];
-    }
-    if (dgamma) dgamma[c] = (accp ? dgamma[c] : 0.f) + (float)tg;
-    if (dbeta) dbeta[c] = (accp ? dbeta[c] : 0.f) + (float)tb;
-  }
-}
-
-extern "C" int u3d_conv32_ring_gn_bwd_coef(const float* part_ws, int n, int d, int h, int w, int gn_groups,
-                                           const float* gn_stats, const float* gn_gamma, const float* gn_beta,
-                                           float* coef, float* dgamma, float* dbeta, int accumulate_params,
-                                           u3d_stream_t stream) {
-  U3D_REQUIRE(part_ws && gn_stats && gn_gamma && gn_beta && coef && n >= 1 && n <= 16 && gn_groups > 0 &&
-              32 % gn_groups == 0, "conv32_ring_gn_bwd_coef: bad args (n <= 16)");
-  const long long pps = (long long)cdiv(h, RG_BH) * cdiv(w, RG_BW) * d;  // same split as conv32_ring_impl
-  const long long wps0 = std::max<long long>(1, std::min<long long>(pps, ring_wgs() / n));
-  const long long per = (pps + wps0 - 1) / wps0;
-  const int wps = (int)((pps + per - 1) / per);
-  hipLaunchKernelGGL(ring_gn_bwd_coef_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, part_ws, n, wps, gn_groups,
-                     (double)d * h * w * (32 / gn_groups), gn_stats, gn_gamma, gn_beta, coef, dgamma, dbeta,
-                     accumulate_params);
-  return check_launch("ring_gn_bwd_coef_kernel");
 }
 
 extern "C" int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,

@@ -95,7 +95,11 @@ __global__ __launch_bounds__(256) void dynhead_bwd_kernel(const float* __restric
   float g[162];
 #pragma unroll
   for (int k = 0; k < 162; ++k) g[k] = 0.f;
+#pragma unroll 1
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < v; i += (long long)gridDim.x * 256) {
+    // the 162 parameters are re-read from the LDS each voxel (broadcast reads), not hoisted into registers next to
+    // the 162 gradient accumulators
+    asm volatile("" ::: "memory");
     const float* hv = h + ((long long)n * v + i) * 8;
     float x0[8], a1[8], r1[8], a2[8], r2[8];
 #pragma unroll
@@ -164,9 +168,10 @@ __global__ __launch_bounds__(256) void dynhead_bwd_kernel(const float* __restric
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < 162; ++k) {
+  for (int k = 0; k < 162; ++k) {  // one scheduling region per accumulator: the 162 reductions are not interleaved
     const float t = wave_sum(g[k]);
     if (lane == 0) red[wave][k] = t;
+    __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();
   for (int k = threadIdx.x; k < 162; k += 256)

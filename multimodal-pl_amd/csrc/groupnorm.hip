@@ -697,23 +697,3 @@ extern "C" int u3d_gn_bwd2_s2(int dtype, const void* da1, const void* da2c, cons
                               gamma2, beta2, dx, accumulate, dgamma1, dbeta1, dgamma2, dbeta2, accumulate_params, ws,
                               stream);
 }
-
-extern "C" int u3d_gn_bwd_apply_coef(int dtype, const void* da, const void* x, int n, int c, long long v,
-                                     const float* coef, void* dx, int accumulate, u3d_stream_t stream) {
-  U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "gn_bwd_apply_coef: bad dtype");
-  U3D_REQUIRE(da && x && coef && dx && n > 0 && v > 0, "gn_bwd_apply_coef: bad args");
-  const int vec = dtype == U3D_BF16 ? 8 : 4;
-  U3D_REQUIRE(c % vec == 0 && c <= 256, "gn_bwd_apply_coef: channels %d unsupported", c);
-  RedGeom g = make_geom(n, c, v, 1, vec);
-  const long long nvec = v * g.chn;
-  const int athr = GT / g.chn * g.chn;
-  const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + athr - 1) / athr);
-  hipStream_t s = (hipStream_t)stream;
-  if (dtype == U3D_BF16)
-    hipLaunchKernelGGL(gn_bwd_apply<bf16>, dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da, (const bf16*)x, g, coef,
-                       (bf16*)dx, accumulate);
-  else
-    hipLaunchKernelGGL(gn_bwd_apply<float>, dim3(ablk, n), dim3(athr), 0, s, (const float*)da, (const float*)x, g,
-                       coef, (float*)dx, accumulate);
-  return check_launch("gn_bwd_apply_coef");
-}

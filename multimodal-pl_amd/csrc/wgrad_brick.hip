@@ -203,18 +203,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
     if (more) commit(b + 1);
     __syncthreads();
   }
-  // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h
-  const int r = lane & 31;
+  // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h. Buffer stores with 32-bit
+  // offsets computed here (the host keeps the slabs below 2 GiB): no 64-bit addresses held across the brick loop.
+  int t0 = tid;
+  asm volatile("" : "+v"(t0));
+  const int r = t0 & 31, w8 = t0 >> 6, h8 = (t0 >> 5) & 1;
+  const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
     if (j < ntap) {
-      const int tt = wave + 8 * j;
-      float* pp = part + ((long long)ts.split * 27 + tt) * g.cout_p * g.cin_p;
+      const int tt = w8 + 8 * j;
+      const int base = ((ts.split * 27 + tt) * g.cout_p + co0 + 4 * h8) * g.cin_p + ci0 + r;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int co = co0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        pp[(long long)co * g.cin_p + ci0 + r] = acc[j][i];
-      }
+      for (int i = 0; i < 16; ++i)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[j][i]), prs,
+                                              (unsigned)((base + ((i & 3) + 8 * (i >> 2)) * g.cin_p) * 4), 0, 0);
     }
   }
 }
@@ -377,6 +380,8 @@ extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int ci
   U3D_REQUIRE(dy && x && partials && nsplit >= 1, "wgrad_brick: null pointer");
   U3D_REQUIRE(stride == 1 || stride == 2, "wgrad_brick: stride %d", stride);
   U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "wgrad_brick: channels must be multiples of 8");
+  U3D_REQUIRE((long long)nsplit * 27 * round_up(cin, 32) * round_up(cout, 32) * 4 < (1LL << 31),
+              "wgrad_brick: partial slabs beyond the 2 GiB offset range");
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0),
               "wgrad_brick: bad GroupNorm prologue");
   WBGeom g{};

@@ -219,10 +219,11 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
 
   auto compute = [&](int dslot, int s0, int s1, int s2, auto ntc) {
     constexpr int NTP = decltype(ntc)::value;
-    const int sl[3] = {s0, s1, s2};
-    int tb[NTP];
+    (void)s1;
+    (void)s2;
+    int tb[NTP];  // slot of tap depth td = (s0 + td) & 3 (the three slots are consecutive): no indexed array
 #pragma unroll
-    for (int j = 0; j < NTP; ++j) tb[j] = sl[tap_d[j]] * WR_SLOT + tap_row[j];
+    for (int j = 0; j < NTP; ++j) tb[j] = ((s0 + tap_d[j]) & 3) * WR_SLOT + tap_row[j];
     const char* dbase = dyr + dslot * WR_DSLOT;
     constexpr int LA = GN ? (PW == 16 ? 1 : 0) : 2;  // fragment lookahead (k16 steps): what the registers allow
     bf16x8 fa[LA + 1], fb[LA + 1][NTP];
@@ -273,18 +274,21 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     if (!(pw.valid || (pc.valid && pc.out))) break;
     step(xb, yb, mb, xa, ya, ma);
   }
-  // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h
-  const int r = lane & 31;
+  // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h. Buffer stores with 32-bit
+  // offsets computed here (the host keeps the slabs below 2 GiB): no 64-bit addresses held across the walk.
+  int t0 = tid;
+  asm volatile("" : "+v"(t0));
+  const int r = t0 & 31, w8 = t0 >> 6;
+  const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
     if (j < ntap) {
-      const int tt = wave + 8 * j;
-      float* pq = part + ((long long)split * 27 + tt) * g.cout_p * g.cin_p;
+      const int tt = w8 + 8 * j;
+      const int base = ((split * 27 + tt) * g.cout_p + co0 + 4 * hh) * g.cin_p + ci0 + r;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int co = co0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        pq[(long long)co * g.cin_p + ci0 + r] = acc[j][i];
-      }
+      for (int i = 0; i < 16; ++i)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[j][i]), prs,
+                                              (unsigned)((base + ((i & 3) + 8 * (i >> 2)) * g.cin_p) * 4), 0, 0);
     }
   }
 }
@@ -329,6 +333,7 @@ extern "C" int u3d_conv_wgrad_ring(const void* dy, const void* x, int n, int cin
   WRGeom g;
   wr_geom(n, cin, d, h, w, cout, g);
   U3D_REQUIRE(g.xbytes < (1LL << 31) && g.ybytes < (1LL << 31), "wgrad_ring: tensors beyond the 2 GiB offset range");
+  U3D_REQUIRE((long long)nsplit * 27 * g.cout_p * g.cin_p * 4 < (1LL << 31), "wgrad_ring: partial slabs beyond 2 GiB");
   g.per = (int)((g.planes + nsplit - 1) / nsplit);
   g.gn_groups = gn_groups;
   const int ns_eff = (int)((g.planes + g.per - 1) / g.per);

@@ -48,15 +48,11 @@ _SIGS = {
     "u3d_diag_occupy": [I, L, P, P],
     "u3d_conv32_ring_q": [I, P, I, I, I, I, P, P, P, P, I, P, P, P, P, P],
     "u3d_conv32_ring_q_stats_finalize": [P, I, I, I, I, P, P],
-    "u3d_conv32_ring_dgrad_gn": [P, I, I, I, I, P, P, P, P, P, I, P, P, P],
-    "u3d_conv32_ring_gn_bwd_coef": [P, I, I, I, I, I, P, P, P, P, P, P, I, P],
-    "u3d_gn_bwd_apply_coef": [I, P, P, I, I, L, P, P, I, P],
     "u3d_conv_wgrad_ring_splits": [I, I, I, I, I, I],
     "u3d_conv_wgrad_ring": [P, P, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_convg_brick": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P],
     "u3d_convg_brick_stats_ws_floats": [I, I, I, I, I],
     "u3d_convg_brick_stats": [P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P, P],
-    "u3d_convg_brick_dgrad_gn": [P, I, I, I, I, I, P, I, P, P, P, P, I, P, P, L, P, P, P, I, P],
     "u3d_conv_wgrad_brick_splits": [I, I, I, I, I, I, I],
     "u3d_conv_wgrad_brick": [P, P, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_conv_wgrad1_splits": [I, I, I, I, I, I, I],

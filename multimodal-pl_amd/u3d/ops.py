@@ -14,6 +14,8 @@ from ._lib import BF16, F32, call, query
 def get_option(name):
     """Current value of a library tuning option (csrc/common.h ``Opt``)."""
     h = _lib.lib()
+    if not hasattr(h, "u3d_get_option"):  # an A/B build of a tree older than the option table (U3D_LIB)
+        return int(os.environ.get("U3D_" + name, {"CONVG_PERSIST": 1}.get(name, 0)))
     v = ctypes.c_int(0)
     if h.u3d_get_option(name.encode(), ctypes.byref(v)) != 0:
         raise _lib.U3DError(h.u3d_last_error().decode())
@@ -428,63 +430,6 @@ def expand_s2(dxc, in_shape):
     full = torch.zeros((n, d, h, w_, dxc.shape[-1]), dtype=dxc.dtype, device=dxc.device)
     full[:, ::2, ::2, ::2] = dxc
     return full
-
-
-DGRAD_GN = os.environ.get("U3D_DGRAD_GN", "0") != "0"  # GN-bwd partials in the ring dgrad epilogue (measured: -0.3%, off)
-
-
-BRICK_DGRAD_GN = os.environ.get("U3D_BRICK_DGRAD_GN", "0") != "0"  # GN-bwd partials in the persistent brick dgrad
-
-
-def _brick_dgrad_gn_ok(dy, cin, k, stride, x_shape, G):
-    n, d, h, w_ = x_shape
-    cout = dy.shape[-1]
-    return (BRICK_DGRAD_GN and dy.dtype == torch.bfloat16 and k == 3 and stride == 1 and n <= 16 and cin <= 256
-            and cin % G == 0 and get_option("CONVG_PERSIST") != 0
-            and not _use_conv1x1(dy.dtype, cout, cin, k, n) and not _use_conv32(dy.dtype, cin, cout, k, stride, n, w_)
-            and not _use_small(dy.dtype, cout, cin, k, stride, (n, d, h, w_))
-            and _use_gen_brick(dy.dtype, cout, cin, k, stride, (n, d, h, w_)))
-
-
-def dgrad_gn_ok(dy, cin, k, stride, x_shape, G):
-    n, d, h, w_ = x_shape
-    return ((DGRAD_GN and CONV32_FN == "u3d_conv32_ring" and dy.dtype == torch.bfloat16 and n <= 16 and 32 % G == 0
-             and _use_conv32(dy.dtype, cin, dy.shape[-1], k, stride, n, w_) and _conv32_fits(dy))
-            or _brick_dgrad_gn_ok(dy, cin, k, stride, x_shape, G))
-
-
-def conv_dgrad_gn_bwd(dy, wpk_dgrad, x, gn, dx=None, accumulate=False, dgamma=None, dbeta=None):
-    """Ring data gradient of the 32->32 conv + the backward of the GroupNorm+ReLU in front of it, with the GN
-    partial sums taken in the dgrad epilogue: returns the gradient w.r.t. the GN input x (written into / added to
-    ``dx``)."""
-    st, ga, be, G = gn
-    n, d, h, w_, c = x.shape
-    dA = torch.empty_like(x)
-    if _brick_dgrad_gn_ok(dy, c, 3, 1, (n, d, h, w_), G):  # persistent brick data gradient (48^3 / 24^3 levels)
-        nws = query("u3d_convg_brick_stats_ws_floats", n, d, h, w_, 2 * c)
-        ws = WS.get(4 * nws, x.device, slot=10)
-        coef = torch.empty((n, 5, c), dtype=torch.float32, device=x.device)
-        call("u3d_convg_brick_dgrad_gn", dy.data_ptr(), n, dy.shape[-1], d, h, w_, wpk_dgrad.data_ptr(), c, x.data_ptr(),
-             st.data_ptr(), ga.data_ptr(), be.data_ptr(), G, dA.data_ptr(), ws.data_ptr(), nws, coef.data_ptr(),
-             _ptr(dgamma), _ptr(dbeta), 0, _stream())
-        if dx is None:
-            dx = torch.empty_like(x)
-            accumulate = False
-        call("u3d_gn_bwd_apply_coef", dt_code(x.dtype), dA.data_ptr(), x.data_ptr(), n, c, d * h * w_, coef.data_ptr(),
-             dx.data_ptr(), int(accumulate), _stream())
-        return dx
-    ws = WS.get(4 * query("u3d_conv32_ring_stats_ws_floats", n), x.device, slot=10)
-    call("u3d_conv32_ring_dgrad_gn", dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), x.data_ptr(), st.data_ptr(),
-         ga.data_ptr(), be.data_ptr(), G, dA.data_ptr(), ws.data_ptr(), _stream())
-    coef = torch.empty((n, 5, 32), dtype=torch.float32, device=x.device)
-    call("u3d_conv32_ring_gn_bwd_coef", ws.data_ptr(), n, d, h, w_, G, st.data_ptr(), ga.data_ptr(), be.data_ptr(),
-         coef.data_ptr(), _ptr(dgamma), _ptr(dbeta), 0, _stream())
-    if dx is None:
-        dx = torch.empty_like(x)
-        accumulate = False
-    call("u3d_gn_bwd_apply_coef", dt_code(x.dtype), dA.data_ptr(), x.data_ptr(), n, c, d * h * w_, coef.data_ptr(),
-         dx.data_ptr(), int(accumulate), _stream())
-    return dx
 
 
 USE_BRICK_WGRAD = True

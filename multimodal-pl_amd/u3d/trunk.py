@@ -248,17 +248,6 @@ class Tape:
                 part, ns = self.wgrad_async(lambda: ops.conv_wgrad(dyT, x.t, k, stride, gn), dyT, x.t,
                                             gn[0] if gn is not None else None)
                 self.pend_wgrad(part, ns, W, st, std, key + ".weight")
-                if (not head and gn is not None and pair is None
-                        and ops.dgrad_gn_ok(dyT, cin, k, stride, x.t.shape[:4], G)):
-                    # the GN backward's partial sums come from the dgrad epilogue: one apply pass remains
-                    dg = self.grad_out(gn_key + ".weight", gn[1])
-                    db = self.grad_out(gn_key + ".bias", gn[2])
-                    self.before_write(x.grad)
-                    x.grad = ops.conv_dgrad_gn_bwd(dyT, pd, x.t, gn, dx=x.grad, accumulate=x.grad is not None,
-                                                   dgamma=dg, dbeta=db)
-                    self.grad_done(gn_key + ".weight")
-                    self.grad_done(gn_key + ".bias")
-                    return
                 s2c = (gn is not None and pair == "park" and k == 1 and stride == 2 and ops.S2_COMPACT
                        and ops._use_conv1x1(dyT.dtype, dyT.shape[-1], cin, 1, dyT.shape[0]))
                 if s2c:  # kept at the conv's output resolution: the paired GN backward reads it in place

@@ -373,3 +373,21 @@ def test_driver_import_line_resolves():
                        (losses, ["get_loss_refine", "get_loss", "SmoothCrossEntropyLoss", "bce_loss"])):
         for n in names:
             assert hasattr(mod, n), (mod.__name__, n)
+
+
+def test_no_kernel_spills_to_scratch():
+    """no kernel of the shipped library spills VGPRs or uses a private (scratch) segment — read from
+    the AMDGPU metadata notes of the gfx950 code objects inside libu3d.so (tools/kernel_resources.py)."""
+    import shutil
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import kernel_resources as KR
+    lib = os.path.join(REPO, "multimodal-pl_amd", "u3d", "libu3d.so")
+    if not os.path.exists(lib) or not os.path.exists(os.path.join(KR.LLVM, "llvm-readelf")):
+        pytest.skip("library or llvm tools not present")
+    ks = KR.kernels(lib)
+    assert len(ks) > 100, len(ks)
+    bad = {k: v for k, v in ks.items() if v[".vgpr_spill_count"] or v[".private_segment_fixed_size"]}
+    assert not bad, "kernels with VGPR spills / scratch: " + ", ".join(
+        f"{n} ({v['.vgpr_spill_count']} spills, {v['.private_segment_fixed_size']} B)" for n, v in
+        zip(KR.demangle(list(bad)), bad.values()))
