@@ -374,12 +374,14 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       gtab[nn & 1][tid] = f32x2{sc_, __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, c * 4, 0, 0)) - mean * sc_};
     }
   };
-  // buffer loads with 32-bit offsets (the host guarantees x and the weight pack below 2 GiB): out-of-range offsets
-  // return zeros with no branch around the load, and an offset needs one register, not a 64-bit address
-  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, 0x7FFFFFFF, 0x00020000);
-  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)wpk, 0, 0x7FFFFFFF, 0x00020000);
-  const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, res ? 0x7FFFFFFF : 0, 0x00020000);
-  const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, 0x7FFFFFFF, 0x00020000);
+  // buffer loads with 32-bit offsets (the host guarantees x, y / the residual and the weight pack below 2 GiB): the
+  // records are the tensors' exact byte sizes, so the sentinel offset 0xFFFFFFF0 of a masked piece is out of range and
+  // returns zeros with no branch around the load; an offset needs one register, not a 64-bit address
+  const int xbytes = g.n * g.d * g.h * g.w * g.cin * 2, ybytes = g.n * g.d * g.h * g.w * g.cout * 2;
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, xbytes, 0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)wpk, 0, 27 * g.cout_p * g.cin_p * 2, 0x00020000);
+  const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, res ? ybytes : 0, 0x00020000);
+  const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, ybytes, 0x00020000);
   const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)spart, 0, spart ? 0x7FFFFFFF : 0, 0x00020000);
   typedef __attribute__((ext_vector_type(2))) uint32_t v2u32;
   auto halo_load = [&](const Unit& q, int c) {
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
                       (unsigned)zw < (unsigned)g.w;
       hmask |= (in ? 1u : 0u) << i;
       const unsigned off =
-          in && cc < g.cin ? (unsigned)(((((q.nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc) * 2) : 0x7FFFFFF0u;
+          in && cc < g.cin ? (unsigned)(((((q.nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc) * 2) : 0xFFFFFFF0u;
       hpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
   };
@@ -430,7 +432,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       const int j = row / CO, co = co0 + row % CO;
       const int t = td * 9 + j;
       const unsigned off = ci < WROWS * 4 && co < g.cout_p
-                               ? (unsigned)(((t * g.cout_p + co) * g.cin_p + c * 32 + ch * 8) * 2) : 0x7FFFFFF0u;
+                               ? (unsigned)(((t * g.cout_p + co) * g.cin_p + c * 32 + ch * 8) * 2) : 0xFFFFFFF0u;
       wpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
     }
   };
@@ -551,7 +553,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
           const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
-          const unsigned ro = (ook[tm] && co < g.cout) ? (unsigned)((ovox[tm] * g.cout + co) * 2) : 0x7FFFFFF0u;
+          const unsigned ro = (ook[tm] && co < g.cout) ? (unsigned)((ovox[tm] * g.cout + co) * 2) : 0xFFFFFFF0u;
           rv[tm][tn][v] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
         }
     };
