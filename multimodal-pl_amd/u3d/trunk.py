@@ -44,6 +44,7 @@ def side_stream(device):
 # ms/step — a concurrent kernel takes CUs from the persistent 256-workgroup ring convs, whose tail then doubles.
 SIDE_FLUSH = int(os.environ.get("U3D_SIDE_FLUSH", "0"))
 USE_SIDE_STREAM = os.environ.get("U3D_SIDE_STREAM", "0") != "0"  # measured slower (8.82 vs 9.23 ms)
+FLUSH_EACH = os.environ.get("U3D_FLUSH_EACH", "0") != "0"
 
 
 class Act:
@@ -359,6 +360,11 @@ class Tape:
                 self.flush_wgrads()
             elif self.sink is None and SIDE_FLUSH and len(self.pending) >= SIDE_FLUSH and self.dtype == torch.bfloat16:
                 self.flush_wgrads(on_side=True)
+            elif self.pending and FLUSH_EACH and not USE_SIDE_STREAM:
+                # slab sum + standardisation backward right behind each weight gradient, on the main stream: the
+                # partial slabs (~28 MB per conv) are summed while resident in the Infinity Cache, and their freed
+                # block is reused by the next conv's slabs (fewer HBM write-backs)
+                self.flush_wgrads()
         self.flush_wgrads()
         self.join_side()
         self.ops = []
