@@ -724,7 +724,9 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
   // the persistent kernel addresses x and the weight pack with 32-bit buffer offsets
   const bool small = (long long)n * d * h * w * std::max(cin, cout) * 2 < (1LL << 31) - 64 &&
                      27LL * g.cout_p * g.cin_p * 2 < (1LL << 31) - 64;
-  const bool pers = pers_on && small && (!gn_stats || g.cin_p <= GB_MAXC);
+  // (a data gradient with a residual add — not a trunk routing, kept for the ABI — runs the one-shot kernel: the
+  // persistent data gradient has no residual path, so its epilogue reserves no registers for one)
+  const bool pers = pers_on && small && (!gn_stats || g.cin_p <= GB_MAXC) && !(flip && residual);
   U3D_REQUIRE(!spart || (pers && !flip && cout % 32 == 0), "convg_brick_stats: needs the persistent forward, cout %% 32 == 0");
   if (pers) {
     // 8-wide bricks where the plane width is a multiple of 8 but not of 16 (24^3: the 16-wide bricks' second
