@@ -285,10 +285,14 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     if (j < ntap) {
       const int tt = w8 + 8 * j;
       const int base = ((split * 27 + tt) * g.cout_p + co0 + 4 * hh) * g.cin_p + ci0 + r;
+      // (the whole accumulator is bit-cast first: a bit_cast of a single element of the fp32 vector fed to
+      // raw_buffer_store_b32 is miscompiled by ROCm 7.2 clang into stores of element 0)
+      typedef __attribute__((ext_vector_type(16))) uint32_t u32x16;
+      const u32x16 ua = __builtin_bit_cast(u32x16, acc[j]);
 #pragma unroll
       for (int i = 0; i < 16; ++i)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[j][i]), prs,
-                                              (unsigned)((base + ((i & 3) + 8 * (i >> 2)) * g.cin_p) * 4), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(ua[i], prs, (unsigned)((base + ((i & 3) + 8 * (i >> 2)) * g.cin_p) * 4),
+                                              0, 0);
     }
   }
 }
