@@ -84,7 +84,6 @@ def eam_op(tape, f, key, token, up):
             dM = torch.empty((nt, c), dtype=torch.float32, device=dev)
             dg2 = tape.grad_out(key + ".norm2.weight", g2)
             db2 = tape.grad_out(key + ".norm2.bias", b2)
-            tape.before_write(f.grad)
             acc = f.grad is not None
             dx = f.grad if acc else torch.empty_like(x)
             s = ops._stream()

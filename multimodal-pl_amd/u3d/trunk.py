@@ -7,7 +7,6 @@ Graph (reference unet3D.forward :1734-1806 / unet3D_baseline.forward :663-718 / 
   stem conv1 (or conv0 s2 -> conv1) -> layer0..4 (NoBottleneck :40-73) -> fusionConv (GN,ReLU,1^3)
   -> 4 x [trilinear x2 + skip -> x{8,4,2,1}_resb] -> precls_conv (GN,ReLU,1^3+bias) [-> x2 upsample (unet3D_g)]
 """
-import os
 from dataclasses import dataclass
 
 import torch
@@ -24,27 +23,6 @@ class TrunkCfg:
     conv0: bool = False       # unet3D_g: stride-2 stem conv0 then a plain conv1
     final_up: bool = False    # unet3D_g: x2 trilinear upsample of the logits
     weight_std: bool = True
-
-
-_SIDE = {}
-
-
-def side_stream(device):
-    """Per-device side stream for the weight gradients: wgrad(dy, x) does not depend on dgrad(dy, W), so the
-    two run concurrently (the small deep levels leave most CUs idle when either runs alone)."""
-    key = torch.device(device)
-    st = _SIDE.get(key)
-    if st is None:
-        st = _SIDE[key] = torch.cuda.Stream(device=key)
-    return st
-
-
-# single-GPU backward: every SIDE_FLUSH pending weight gradients, their slab sum + standardisation backward run on the
-# side stream (0 = all at the end of backward, on the main stream). Off: measured 7.83 (0) vs 7.93 (4) / 7.90 (8)
-# ms/step — a concurrent kernel takes CUs from the persistent 256-workgroup ring convs, whose tail then doubles.
-SIDE_FLUSH = int(os.environ.get("U3D_SIDE_FLUSH", "0"))
-USE_SIDE_STREAM = os.environ.get("U3D_SIDE_STREAM", "0") != "0"  # measured slower (8.82 vs 9.23 ms)
-FLUSH_EACH = os.environ.get("U3D_FLUSH_EACH", "0") != "0"
 
 
 class Act:
@@ -69,8 +47,6 @@ class Tape:
         self.sink = None
         self.std = True
         self.pending = []   # weight grads waiting for the batched standardisation backward
-        self.side_used = False
-        self.side_reads = set()  # data_ptrs the side stream may still read
 
     def prepack(self, plan):
         """Standardise + pack every conv weight of ``plan`` [(key, standardize, need_dgrad)] in one launch."""
@@ -94,56 +70,13 @@ class Tape:
     def pend_wgrad(self, part, ns, W, st, std, name):
         self.pending.append((part, ns, W, st, std, self.grad_out(name, W), False, name))
 
-    def wgrad_async(self, fn, *tensors):
-        """Run fn() (a weight-gradient launch returning (partials, nsplit)) on the side stream after everything
-        queued so far on the main stream; the partials are consumed on the main stream after a join."""
-        if not USE_SIDE_STREAM:
-            return fn()
-        main = torch.cuda.current_stream()
-        side = side_stream(main.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            part, ns = fn()
-        for t in tensors:
-            if t is not None:
-                t.record_stream(side)
-                self.side_reads.add(t.data_ptr())
-        part.record_stream(main)
-        self.side_used = True
-        return part, ns
-
-    def join_side(self):
-        if self.side_used:
-            main = torch.cuda.current_stream()
-            main.wait_stream(side_stream(main.device))
-            self.side_used = False
-            self.side_reads.clear()
-
-    def before_write(self, t):
-        """An in-place update of ``t`` is about to be queued on the main stream: if a side-stream weight
-        gradient still reads it (an aliased residual gradient), wait for the side stream first."""
-        if t is not None and self.side_used and t.data_ptr() in self.side_reads:
-            self.join_side()
-
-    def flush_wgrads(self, on_side=False):
-        """Slab sum + standardisation backward of the pending weight gradients. ``on_side``: queue them on the side
-        stream behind everything issued so far, so this HBM-bound pass overlaps the MFMA-bound data-gradient convs
-        that follow on the main stream (the dW outputs are read only after the final join)."""
+    def flush_wgrads(self):
+        """Slab sum + standardisation backward of the pending weight gradients, in one batched launch pair.
+        Batched at the end of the backward (or at a DDP bucket boundary): flushing after every conv measured
+        7.33 vs 6.61 ms/step (r03, gpurun_out/r03i/flush), the per-conv launches cost more than the Infinity Cache
+        residency of the slabs saves; a side-stream flush measured 7.93 vs 7.83 (round 2)."""
         if not self.pending:
             return
-        if on_side:
-            main = torch.cuda.current_stream()
-            side = side_stream(main.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                ops.wstd_bwd_batch([p[:7] for p in self.pending])
-            for p in self.pending:
-                p[0].record_stream(side)  # partials: freed on the host now, still read by the side stream
-                p[5].record_stream(side)
-            self.side_used = True
-            self.pending = []
-            return
-        self.join_side()
         ops.wstd_bwd_batch([p[:7] for p in self.pending])
         names = [p[7] for p in self.pending]
         self.pending = []
@@ -166,7 +99,6 @@ class Tape:
         if act.grad is None:
             act.grad = g
         else:
-            self.before_write(act.grad)
             ops.add_(act.grad, g)
 
     def grad_out(self, name, like):
@@ -199,7 +131,7 @@ class Tape:
             def bwd():
                 if out.grad is None:
                     return
-                part, ns = self.wgrad_async(lambda: ops.stem_wgrad(out.grad, x, stride), out.grad, x)
+                part, ns = ops.stem_wgrad(out.grad, x, stride)
                 self.pend_wgrad(part, ns, W, st, self.std, key + ".weight")
             self.ops.append(bwd)
         return out
@@ -246,8 +178,7 @@ class Tape:
                     if residual is not None:
                         self.acc_grad(residual, dy)
                     dyT = ops.cast(dy, self.dtype, pad_to=8)  # GEMM operand: channels padded to 8 (2-class head)
-                part, ns = self.wgrad_async(lambda: ops.conv_wgrad(dyT, x.t, k, stride, gn), dyT, x.t,
-                                            gn[0] if gn is not None else None)
+                part, ns = ops.conv_wgrad(dyT, x.t, k, stride, gn)
                 self.pend_wgrad(part, ns, W, st, std, key + ".weight")
                 s2c = (gn is not None and pair == "park" and k == 1 and stride == 2 and ops.S2_COMPACT
                        and ops._use_conv1x1(dyT.dtype, dyT.shape[-1], cin, 1, dyT.shape[0]))
@@ -262,7 +193,6 @@ class Tape:
                     dps = []
                     for key_, g_ in ((gn_key, gn), (key2, gn2)):
                         dps.append((self.grad_out(key_ + ".weight", g_[1]), self.grad_out(key_ + ".bias", g_[2])))
-                    self.before_write(x.grad)
                     x.grad = ops.gn_bwd2(dA, dA2, x.t, gn[0], (gn[1], gn[2]), (gn2[1], gn2[2]), G, dx=x.grad,
                                          accumulate=x.grad is not None, dparams1=dps[0], dparams2=dps[1],
                                          da2_s2=s2c2)
@@ -279,7 +209,6 @@ class Tape:
     def gn_bwd_one(self, x, dA, gn, gn_key, G):
         dg = self.grad_out(gn_key + ".weight", gn[1])
         db = self.grad_out(gn_key + ".bias", gn[2])
-        self.before_write(x.grad)
         x.grad = ops.gn_bwd(dA, x.t, gn[0], gn[1], gn[2], G, dx=x.grad,
                             accumulate=x.grad is not None, dgamma=dg, dbeta=db)
         self.grad_done(gn_key + ".weight")
@@ -303,7 +232,6 @@ class Tape:
                     return
                 if skip is not None:
                     self.acc_grad(skip, dy)
-                self.before_write(x.grad)
                 x.grad = ops.upsample2x_bwd(dy, tuple(x.t.shape), dx=x.grad, accumulate=x.grad is not None)
             self.ops.append(bwd)
         return out
@@ -358,15 +286,7 @@ class Tape:
             fn()
             if self.pending and self.sink is not None and self.sink.needs_flush([p[7] for p in self.pending]):
                 self.flush_wgrads()
-            elif self.sink is None and SIDE_FLUSH and len(self.pending) >= SIDE_FLUSH and self.dtype == torch.bfloat16:
-                self.flush_wgrads(on_side=True)
-            elif self.pending and FLUSH_EACH and not USE_SIDE_STREAM:
-                # slab sum + standardisation backward right behind each weight gradient, on the main stream: the
-                # partial slabs (~28 MB per conv) are summed while resident in the Infinity Cache, and their freed
-                # block is reused by the next conv's slabs (fewer HBM write-backs)
-                self.flush_wgrads()
         self.flush_wgrads()
-        self.join_side()
         self.ops = []
 
 
