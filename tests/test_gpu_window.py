@@ -107,3 +107,44 @@ def test_predict_sliding_vs_reference_fixture(gpu, tag):
         out = predict_sliding(None, nets, g[f"{tag}_img"], tile, ref.shape[1], 0, tta=bool(g[f"{tag}_tta"]))
     err = np.abs(out.double().cpu().numpy() - ref).max()
     assert err <= WIN_TOL * np.abs(ref).max(), err
+
+
+def test_predict_sliding_full_tiles_bf16_vs_fp32(gpu):
+    """BASELINE configs[4] at its real tile size: two overlapping 64 x 192 x 192 tiles (1 x 1 x 64 x 192 x 240
+    volume, stride 144 along W) of unet3D_baseline(16) through predict_sliding, the bf16 native path (autocast, as
+    the bench's inference mode) against the fp32 native path (pinned to the reference forward by G5).
+
+    The reference's "fp16" for this config computes fp32: evaluate_amos.py:594-601 (--FP16 selects a checkpoint
+    branch identical to the other) and the forward is never autocast. Tolerance as for the bf16 training forward
+    (test_gpu_fullsize.py: ~40 rounded stages, sqrt(40) x 2^-8 = 2.5e-2): relative L2 of the accumulated
+    probabilities <= 5e-2, and the arg-max label agrees on >= 97% of the voxels where the fp32 top-2 margin
+    exceeds 5% of the logit scale."""
+    import time
+    import unet3D
+    import evaluate_amos as E
+    from oracle.weights_recipe import apply_recipe, input_volume
+    m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=16, weight_std=True)
+    apply_recipe(m, seed=0)
+    m = m.to(gpu).eval()
+    image = input_volume((1, 1, 64, 192, 240), seed=71, kind="ct")
+    tile = [64, 192, 192]
+    assert len(E.tile_plan(image.shape, tile)) == 2
+    outs, ms = {}, {}
+    for mode in ("fp32", "bf16"):
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode == "bf16"):
+            E.predict_sliding(None, [m], image, tile, 16, None)  # warm-up (weight packs, workspaces)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            outs[mode] = E.predict_sliding(None, [m], image, tile, 16, None)
+            torch.cuda.synchronize()
+            ms[mode] = (time.perf_counter() - t0) * 1e3
+    a, b = outs["fp32"].double(), outs["bf16"].double()
+    assert torch.isfinite(b).all()
+    rel = ((b - a).norm() / a.norm()).item()
+    top2 = a.topk(2, dim=1).values
+    sure = (top2[:, 0] - top2[:, 1]) > 0.05 * a.abs().max()
+    agree = (a.argmax(1) == b.argmax(1))[sure].double().mean().item()
+    print(f"2 x 64x192x192 tiles: fp32 {ms['fp32']:.1f} ms, bf16 {ms['bf16']:.1f} ms; rel L2 {rel:.3e}, "
+          f"arg-max agreement {agree:.4f} on {sure.double().mean().item():.3f} of the voxels")
+    assert rel <= 5e-2, rel
+    assert agree >= 0.97, agree
