@@ -116,14 +116,6 @@ int u3d_conv_wgrad(int dtype, const void* dy, const void* x, int n, int cin, int
 int u3d_conv_dgrad_s2(const void* dy, int n, int cout, const void* wpk_dgrad, int cin, int d, int h, int w, void* dx,
                       u3d_stream_t stream);
 
-/* bf16 3^3 stride-2 convolution forward (pad 1) with the GroupNorm+ReLU prologue (gn_stats NULL: none):
- * x [n][d][h][w][cin] -> y [n][(d-1)/2+1][(h-1)/2+1][(w-1)/2+1][cout], wpk = forward pack [27][cout_p][cin_p].
- * Halo-brick kernel (2x4x16 output voxels x 32 co per unit, persistent workgroups). Replaces F.conv3d(stride=2,
- * padding=1) of the encoder's down-sampling convs (reference unet3D.py:27, _make_layer :1666-1686). */
-int u3d_conv_fwd_s2(const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
-                    const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups, void* y,
-                    u3d_stream_t stream);
-
 /* bf16 1^3 convolution, stride 1 or 2 (pad 0): y [n][od][oh][ow][cy] = W . relu(gn(x)) at the input voxel
  * (s*od, s*oh, s*ow); x [n][d][h][w][cx], W = packed [round_up(cy, 32)][wpitch] bf16 (the forward pack of a 1^3
  * weight, wpitch = round_up(cx, 32); or the data-gradient pack [cin_p][cout_p] of a stride-1 1^3 conv, which makes
@@ -235,14 +227,7 @@ int u3d_conv_wgrad1(const void* dy, const void* x, int n, int cin, int d, int h,
                     float* partials, int nsplit, u3d_stream_t stream);
 
 /* Stem conv with cin <= 4 (conv1 1->32, unet3D.py:1632; conv0 2->f stride 2, :1514): fp32 NCDHW input, NDHWC
- * output, direct VALU conv with fp32 input. U3D_STEM_MFMA=1: bf16 conv1 (cin 1 -> 32, stride 1) on MFMA with the 27
- * taps as K (input rounded to bf16, as autocast does; faster alone, step-neutral). */
-/* bf16 stem conv (cin 1 -> 32, 3^3, stride 1, w % 4 == 0) that also returns the GroupNorm(16) statistics (mean,
- * rstd) [n][16][2] of its stored output (layer0's gn1, unet3D.py:56-73) from the epilogue (fp64 across blocks,
- * fixed order). ws = u3d_stem_fwd_stats_ws_bytes(n, d, h, w) bytes, zero on first use (left reusable). */
-long long u3d_stem_fwd_stats_ws_bytes(int n, int d, int h, int w);
-int u3d_stem_fwd_stats(const float* x, int n, int d, int h, int w, const void* wpk, void* y, float* stats, void* ws,
-                       u3d_stream_t stream);
+ * output, direct VALU conv with fp32 input (conv1 1 -> 32 stride 1: packed FMAs with wave-uniform weights). */
 int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                  int stride, void* y, u3d_stream_t stream);
 /* split count for u3d_stem_wgrad given its dtype/channels (the bf16 1->32 stride-1 stem runs on MFMA) */
@@ -291,13 +276,6 @@ int u3d_gn_bwd2_s2(int dtype, const void* da1, const void* da2c, const void* x, 
  * (unet3D.py:1646, 1764-1783). x [n][d][h][w][c] -> y [n][2d][2h][2w][c]; skip nullable. */
 int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
                        u3d_stream_t stream);
-/* u3d_upsample2x_add (bf16) that also returns the GroupNorm(16) statistics (mean, rstd) [n][16][2] of its stored
- * output — the decoder block's gn1 / downsample-GN input (unet3D.py:56-73) — accumulated in the epilogue (fp64
- * per-block partials, fixed-order last-block combine). c a power of two in [16, 256]. ws =
- * u3d_upsample2x_stats_ws_bytes(n, c, d) bytes, zero on first use (left reusable). */
-long long u3d_upsample2x_stats_ws_bytes(int n, int c, int d);
-int u3d_upsample2x_add_stats(const void* x, int n, int c, int d, int h, int w, const void* skip, void* y, float* stats,
-                             void* ws, u3d_stream_t stream);
 int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d, int h, int w, void* dx, int accumulate,
                        u3d_stream_t stream);
 

@@ -2,10 +2,7 @@
 // stride-2 conv0 of unet3D_g (in_channel -> init_filter, :1514). K = 27*cin is far below one MFMA
 // K-block, so this is a direct VALU conv: one thread per output voxel keeps all cout accumulators in
 // registers; the standardised weights sit in LDS as fp32. Input is the model's fp32 NCDHW volume.
-#include <cstdlib>
-
 #include "common.h"
-#include "gnpart.h"
 
 namespace u3d {
 
@@ -62,31 +59,28 @@ __global__ __launch_bounds__(ST) void stem_fwd_kernel(const float* __restrict__ 
 }
 
 // cin = 1, stride 1, cout = 32 (conv1 of every trunk, unet3D.py:1632): a thread computes FOUR consecutive w voxels
-// x 32 channels, so each tap's 32 weights (8 LDS vector reads) serve four voxels and the 3 x 6 input row window is
-// read once for them (the one-voxel form was LDS-bound: 216 vector reads per voxel). Same fp32 FMA chain per output
-// as stem_fwd_kernel (x fp32, weights from the packed bf16/f32 image), so results are bitwise those of the generic
-// kernel. One thread per (output row, group of four w voxels).
-// STATS: also the GroupNorm(16, 32) statistics of the stored output (layer0's gn1 input, unet3D.py:56-73):
-// per-thread fp32 sums of its 4 voxels x 2 channels per group, fp64 across the block (xor tree + waves in order)
-// and the blocks (gnpart.h last-block combine).
-template <typename T, bool STATS = false>
+// x 32 channels from the 3 x 6 input window of each (kd, kh) row. The weights are wave-uniform: they are read with
+// scalar loads (the 27 x 32 values sit in the scalar cache) and fed to v_pk_fma_f32 as an SGPR pair, the input
+// value broadcast to both halves, so the kernel is bound by packed FMAs (864 per voxel, two per lane-instruction)
+// and the 64 B/voxel output stores; no LDS. Same fp32 FMA chain per output (taps in order, fma(x, w, acc)) as
+// stem_fwd_kernel, so results are bitwise those of the generic kernel. One thread per (output row, 4-voxel group).
+template <typename T>
+__device__ __forceinline__ float stem_w(const T* __restrict__ wpk, int idx) {
+  if constexpr (sizeof(T) == 2) {  // bf16: the dword holding (ci 0, ci 1) of the packed image; ci 0 = low half
+    return __uint_as_float(reinterpret_cast<const uint32_t*>(wpk)[idx >> 1] << 16);
+  } else {
+    return wpk[idx];
+  }
+}
+
+template <typename T>
 __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__ x, const T* __restrict__ wpk,
                                                       T* __restrict__ y, int d, int h, int w, int cin_p,
-                                                      long long rows, double* __restrict__ part = nullptr,
-                                                      unsigned* __restrict__ cnt = nullptr,
-                                                      float* __restrict__ stats = nullptr, int n = 0) {
-  __shared__ f32x4 wl[27 * 8];  // [t][co/4]
-  for (int i = threadIdx.x; i < 27 * 32; i += ST) {
-    const int co = i % 32, t = i / 32;
-    reinterpret_cast<float*>(wl)[i] = to_f(wpk[((long long)t * 32 + co) * cin_p]);
-  }
-  __syncthreads();
+                                                      long long rows) {
   const int w4 = w >> 2;
   const long long item = (long long)blockIdx.x * ST + threadIdx.x;  // (output row, 4-voxel group)
-  const long long row0 = item / w4;
-  const bool live = row0 < rows;
-  if (!STATS && !live) return;
-  const long long row = live ? row0 : rows - 1;
+  const long long row = item / w4;
+  if (row >= rows) return;
   const int q = (int)(item - row * w4);
   const int yy = (int)(row % h);
   const long long nz = row / h;
@@ -94,11 +88,11 @@ __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__
   const long long nn = nz / d;
   const int x0 = 4 * q;
   const float* xb = x + nn * d * h * w;
-  float acc[4][32];
+  f32x2 acc[4][16];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int c = 0; c < 32; ++c) acc[j][c] = 0.f;
+    for (int c = 0; c < 16; ++c) acc[j][c] = (f32x2){0.f, 0.f};
 #pragma unroll 1
   for (int kd = 0; kd < 3; ++kd) {
     const int zd = z + kd - 1;
@@ -112,113 +106,33 @@ __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__
         const int zw = x0 + k - 1;
         in[k] = rowok && (unsigned)zw < (unsigned)w ? xb[((long long)zd * h + zh) * w + zw] : 0.f;
       }
+      const int t0 = (kd * 3 + kh) * 3;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const int t = (kd * 3 + kh) * 3 + kw;
+        const int wb = (t0 + kw) * 32 * cin_p;
 #pragma unroll
-        for (int c4 = 0; c4 < 8; ++c4) {
-          const f32x4 wv = wl[t * 8 + c4];
+        for (int c = 0; c < 16; ++c) {
+          const f32x2 wv = {stem_w(wpk, wb + (2 * c) * cin_p), stem_w(wpk, wb + (2 * c + 1) * cin_p)};
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[j][4 * c4 + e] = fmaf(in[j + kw], wv[e], acc[j][4 * c4 + e]);
+          for (int j = 0; j < 4; ++j) {
+            const f32x2 xv = {in[j + kw], in[j + kw]};
+            acc[j][c] = __builtin_elementwise_fma(xv, wv, acc[j][c]);
+          }
         }
       }
     }
   }
   T* yr = y + (row * w + x0) * 32;
   constexpr int VEC = 16 / sizeof(T);
-  if (live) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int c = 0; c < 32; c += VEC) {
-        float v[VEC];
+    for (int c = 0; c < 32; c += VEC) {
+      float v[VEC];
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) v[e] = acc[j][c + e];
-        store16<T>(yr + j * 32 + c, v);
-      }
-  }
-  if constexpr (STATS) {
-    // a block may straddle two samples: partials per (block, which sample); a thread's rows belong to sample
-    // nn = row / (d * h). fp32 within a wave (512 values), fp64 across waves and blocks.
-    __shared__ double red[ST / 64][2][32];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const long long nn = row / ((long long)d * h);
-    const long long nfirst = ((long long)blockIdx.x * ST / w4) / ((long long)d * h);
-    const int which = (int)(nn - nfirst);  // 0 or 1: a block spans at most two samples (d * h * w / 4 >= ST)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-#pragma unroll
-      for (int gq = 0; gq < 16; ++gq) {
-        float s1 = 0.f, s2 = 0.f;
-        if (live && which == q) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const float t = to_f(from_f<T>(acc[j][2 * gq + e]));  // the stored value
-              s1 += t;
-              s2 = fmaf(t, t, s2);
-            }
-        }
-        for (int o = 1; o < 64; o <<= 1) {
-          s1 += __shfl_xor(s1, o);
-          s2 += __shfl_xor(s2, o);
-        }
-        if (lane == 0) {
-          red[wave][q][2 * gq] = s1;
-          red[wave][q][2 * gq + 1] = s2;
-        }
-      }
+      for (int e = 0; e < VEC; ++e) v[e] = acc[j][(c + e) >> 1][(c + e) & 1];
+      store16<T>(yr + j * 32 + c, v);
     }
-    __syncthreads();
-    // part[block][which][16][2] (which = 0: the first sample the block touches, 1: the next one, zeros if none)
-    const int nblk = gridDim.x;
-    if (threadIdx.x < 64) {
-      const int q = threadIdx.x >> 5, k = threadIdx.x & 31;
-      double v = 0;
-      for (int wv = 0; wv < ST / 64; ++wv) v += red[wv][q][k];
-      __hip_atomic_store(part + ((long long)blockIdx.x * 2 + q) * 32 + k, v, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!gn_part_is_last(cnt, (unsigned)nblk)) return;
-    // sample s is touched by the contiguous blocks b_lo..b_hi; block b holds it in slot s - (first sample of b)
-    __shared__ double fin[ST][2];
-    const long long ips = (long long)d * h * w4;  // items per sample
-    const int npairs = n * 16, spl = npairs >= ST ? 1 : ST / npairs;
-    for (int p0 = 0; p0 < npairs; p0 += ST) {
-      const int p = p0 + threadIdx.x % min(npairs, ST), sl = threadIdx.x / min(npairs, ST);
-      double s1 = 0, s2 = 0;
-      if (p < npairs && sl < spl) {
-        const int smp = p / 16, gq = p % 16;
-        const int lo = (int)((smp * ips) / ST), hi = (int)(((smp + 1) * ips - 1) / ST);
-        const int b0 = lo + (int)((long long)(hi - lo + 1) * sl / spl), b1 = lo + (int)((long long)(hi - lo + 1) * (sl + 1) / spl);
-        for (int bb = b0; bb < b1; ++bb) {
-          const int which = smp - (int)(((long long)bb * ST / w4) / ((long long)d * h));
-          const double* q = part + ((long long)bb * 2 + which) * 32 + 2 * gq;
-          s1 += __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s2 += __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      fin[threadIdx.x][0] = s1;
-      fin[threadIdx.x][1] = s2;
-      __syncthreads();
-      if (threadIdx.x < min(npairs, ST) && p < npairs) {
-        double t1 = 0, t2 = 0;
-        for (int k = 0; k < spl; ++k) {
-          t1 += fin[k * min(npairs, ST) + threadIdx.x][0];
-          t2 += fin[k * min(npairs, ST) + threadIdx.x][1];
-        }
-        const double M = (double)d * h * w * 2, mean = t1 / M;
-        double var = t2 / M - mean * mean;
-        if (var < 0) var = 0;
-        stats[p * 2] = (float)mean;
-        stats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
-      }
-      __syncthreads();
-    }
-  }
 }
 
 // dW[t][co][ci] partial over a voxel split: thread per (t, ci, co) output, loop over the split's voxels.
@@ -418,123 +332,6 @@ static int sdim(int d, int s) { return (d - 1) / s + 1; }  // k3 pad1: (d + 2 - 
 
 static bool stem1_on() { return opt(OPT_STEM1) != 0; }  // 0: the generic one-voxel kernel
 
-extern "C" long long u3d_stem_fwd_stats_ws_bytes(int n, int d, int h, int w) {
-  const long long items = (long long)n * d * h * (w / 4);
-  return 256 + ((items + ST - 1) / ST) * 2 * 32 * 8;
-}
-
-extern "C" int u3d_stem_fwd_stats(const float* x, int n, int d, int h, int w, const void* wpk, void* y, float* stats,
-                                  void* ws, u3d_stream_t stream) {
-  U3D_REQUIRE(x && wpk && y && stats && ws && n >= 1 && d >= 1 && h >= 1 && w % 4 == 0 && w >= 4,
-              "stem_fwd_stats: bad args (cin 1 -> 32, stride 1, w %% 4 == 0)");
-  U3D_REQUIRE((long long)d * h * (w / 4) >= ST, "stem_fwd_stats: volume too small (a block must span <= 2 samples)");
-  const long long rows = (long long)n * d * h, items = rows * (w / 4);
-  U3D_REQUIRE(rows < 2147483647LL, "stem_fwd_stats: volume too large");
-  const dim3 grid((unsigned)((items + ST - 1) / ST));
-  unsigned* cnt = reinterpret_cast<unsigned*>(ws);
-  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
-  hipLaunchKernelGGL((stem1_fwd_kernel<bf16, true>), grid, dim3(ST), 0, (hipStream_t)stream, x, (const bf16*)wpk,
-                     (bf16*)y, d, h, w, 32, rows, part, cnt, stats, n);
-  return check_launch("stem1_fwd_kernel (statistics)");
-}
-
-// bf16 conv1 (cin 1 -> 32, stride 1) on the matrix cores: the 27 taps are the K dimension (padded to 32 = two k16
-// steps). One wave computes 32 consecutive w voxels of one output row: the MFMA is issued transposed (A = the 32 x 32
-// weight matrix [co][tap], loaded once into registers; B = the voxels' tap vectors, gathered from the fp32 input in
-// L1/L2 and rounded to bf16, as torch.autocast rounds conv inputs), so a lane's accumulators are 16 channels of one
-// voxel and every lane stores two 16-B chunks after one v_permlane32_swap per pair. The VALU form above spends
-// 27 x 32 fp32 FMAs per voxel; this one is bound by the 64 B/voxel output stores.
-__global__ __launch_bounds__(256) void stem1_mfma_fwd_kernel(const float* __restrict__ x, const bf16* __restrict__ wpk,
-                                                             bf16* __restrict__ y, int d, int h, int w, int cin_p,
-                                                             long long tiles, int tpr) {
-  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-  // A fragments: weight [tap t][co r] at k = 16 s + 8 hh + e (taps >= 27 are zero)
-  s16x8 wa[2];
-#pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    uint32_t pk[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int t0 = 16 * st + 8 * hh + 2 * e, t1 = t0 + 1;
-      const uint32_t lo = t0 < 27 ? wpk[((long long)t0 * 32 + r) * cin_p] : 0;
-      const uint32_t hi = t1 < 27 ? wpk[((long long)t1 * 32 + r) * cin_p] : 0;
-      pk[e] = lo | (hi << 16);
-    }
-    wa[st] = __builtin_bit_cast(s16x8, (u32x4){pk[0], pk[1], pk[2], pk[3]});
-  }
-  __shared__ __attribute__((aligned(16))) char otile[4][32 * 64];
-  char* const ot = otile[threadIdx.x >> 6];
-  const long long wave0 = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6, nwave = (long long)gridDim.x * 4;
-  // 32-bit index math, one division chain per output row (64-bit divisions per tile cost more than the MFMAs; hoisting
-  // the 16 tap offsets into registers measured slower: 78 vs 59 us)
-  const int rows = (int)(tiles / tpr);
-  for (int row = (int)wave0; row < rows; row += (int)nwave) {
-  for (int x0 = 0; x0 < w; x0 += 32) {
-    const int yy = row % h, nz = row / h, z = nz % d;
-    const float* xb = x + (long long)(nz / d) * d * h * w;
-    const int xv = x0 + r;
-    s16x8 bfr[2];
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int tap = 16 * st + 8 * hh + e;
-        const int kd = tap / 9, kh = (tap / 3) % 3, kw = tap % 3;
-        const int zd = z + kd - 1, zh = yy + kh - 1, zw = xv + kw - 1;
-        const bool ok = tap < 27 && (unsigned)zd < (unsigned)d && (unsigned)zh < (unsigned)h && (unsigned)zw < (unsigned)w;
-        const float a = xb[ok ? ((long long)zd * h + zh) * w + zw : 0];  // clamped address: straight-line loads
-        v[e] = ok ? a : 0.f;
-      }
-      bfr[st] = __builtin_bit_cast(s16x8, (u32x4){pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
-                                                  pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7])});
-    }
-    f32x16 acc = (f32x16){};
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[0], bfr[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[1], bfr[1], acc, 0, 0, 0);
-    uint32_t pk[4][2];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int e = 0; e < 2; ++e) pk[q][e] = pack_bf16x2(acc[4 * q + 2 * e], acc[4 * q + 2 * e + 1]);
-#pragma unroll
-    for (int q = 0; q < 4; q += 2)
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(pk[q][e], pk[q + 1][e], false, false);
-        pk[q][e] = sw[0];
-        pk[q + 1][e] = sw[1];
-      }
-    // through LDS so that each store instruction writes 1 KB contiguous (the tile is 32 voxels x 64 B)
-#pragma unroll
-    for (int u2 = 0; u2 < 2; ++u2)
-      *reinterpret_cast<u32x4*>(ot + r * 64 + 32 * u2 + 16 * hh) =
-          (u32x4){pk[2 * u2][0], pk[2 * u2][1], pk[2 * u2 + 1][0], pk[2 * u2 + 1][1]};
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    const int nv = min(32, w - x0);
-#pragma unroll
-    for (int u2 = 0; u2 < 2; ++u2) {
-      const int q = lane + 64 * u2;  // 16-B chunk of the tile
-      const u32x4 v = *reinterpret_cast<const u32x4*>(ot + q * 16);
-      if ((q >> 2) < nv) *reinterpret_cast<u32x4*>(y + ((long long)row * w + x0) * 32 + q * 8) = v;
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-  }
-  }
-}
-
-// Off by default: 83 -> 59 us per launch in isolation but step-neutral (same-box A/B 6.961 vs 6.957 ms: in the step the
-// stem is bound by its 113 MB of output stores), and the VALU kernel keeps the fp32 input. U3D_STEM_MFMA=1 enables it.
-static bool stem1_mfma_on() {
-  static const bool on = [] {
-    const char* e = getenv("U3D_STEM_MFMA");
-    return e && atoi(e) != 0;
-  }();
-  return on;
-}
-
 extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                             int stride, void* y, u3d_stream_t stream) {
   U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "stem_fwd: bad dtype");
@@ -542,15 +339,6 @@ extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, in
   hipStream_t s = (hipStream_t)stream;
   const int od = sdim(d, stride), oh = sdim(h, stride), ow = sdim(w, stride);
   const long long total = (long long)n * od * oh * ow;
-  if (dtype == U3D_BF16 && cin == 1 && stride == 1 && cout == 32 && stem1_mfma_on()) {
-    const int tpr = cdiv(w, 32);
-    const long long tiles = (long long)n * d * h * tpr;
-    U3D_REQUIRE((long long)n * d * h < (1LL << 31), "stem_fwd: too many rows");
-    const unsigned grid = (unsigned)std::min<long long>(8192, ((long long)n * d * h + 3) / 4);
-    hipLaunchKernelGGL(stem1_mfma_fwd_kernel, dim3(grid), dim3(256), 0, s, x, (const bf16*)wpk, (bf16*)y, d, h, w,
-                       round_up(cin, 32), tiles, tpr);
-    return check_launch("stem1_mfma_fwd_kernel");
-  }
   if (cin == 1 && stride == 1 && cout == 32 && w % 4 == 0 && (long long)n * d * h < 2147483647LL && stem1_on()) {
     const long long rows = (long long)n * d * h, items = rows * (w / 4);
     const dim3 grid((unsigned)((items + ST - 1) / ST));

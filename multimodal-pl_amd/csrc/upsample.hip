@@ -6,7 +6,6 @@
 #include <cstdlib>
 
 #include "common.h"
-#include "gnpart.h"
 
 namespace u3d {
 
@@ -201,61 +200,6 @@ __global__ __launch_bounds__(256) void up_bwd_blk_kernel(const T* __restrict__ d
     }
 }
 
-// Forward with the GroupNorm(16) statistics of the stored (bf16-rounded) output accumulated in the epilogue
-// (gnpart.h): the decoder's upsample + skip output feeds the next block's gn1 and downsample GN (unet3D.py:56-73).
-// grid (NB, n): block b of sample n walks output rows (od, oh) b, b + NB, ...; thread t keeps the 8-channel chunk
-// t % chn of every row position it writes.
-template <int GS>
-__global__ __launch_bounds__(256) void up_fwd_stats_kernel(const bf16* __restrict__ x, const bf16* __restrict__ skip,
-                                                          bf16* __restrict__ y, int c, int d, int h, int w,
-                                                          double* __restrict__ part, unsigned* __restrict__ cnt,
-                                                          float* __restrict__ stats) {
-  constexpr int VEC = 8;
-  const int chn = c / VEC, D = 2 * d, H = 2 * h, W = 2 * w, nn = blockIdx.y, NB = gridDim.x;
-  const int cpg = c / 16, j = threadIdx.x % chn;
-  const bf16* xb = x + (long long)nn * d * h * w * c + j * VEC;
-  double acc[GS][2];
-#pragma unroll
-  for (int s = 0; s < GS; ++s) acc[s][0] = acc[s][1] = 0;
-  for (int row = blockIdx.x; row < D * H; row += NB) {
-    const int od = row / H, oh = row - od * H;
-    const Lerp Ld = lerp_of(od, d), Lh = lerp_of(oh, h);
-    for (int i = threadIdx.x; i < W * chn; i += 256) {
-      const int ow = i / chn;
-      const Lerp Lw = lerp_of(ow, w);
-      auto at = [&](int a, int b_, int e, float (&v)[VEC]) {
-        load16<bf16>(xb + ((long long)(a * h + b_) * w + e) * c, v);
-      };
-      float v000[VEC], v001[VEC], v010[VEC], v011[VEC], v100[VEC], v101[VEC], v110[VEC], v111[VEC];
-      at(Ld.i0, Lh.i0, Lw.i0, v000); at(Ld.i0, Lh.i0, Lw.i1, v001);
-      at(Ld.i0, Lh.i1, Lw.i0, v010); at(Ld.i0, Lh.i1, Lw.i1, v011);
-      at(Ld.i1, Lh.i0, Lw.i0, v100); at(Ld.i1, Lh.i0, Lw.i1, v101);
-      at(Ld.i1, Lh.i1, Lw.i0, v110); at(Ld.i1, Lh.i1, Lw.i1, v111);
-      const long long off = ((((long long)nn * D + od) * H + oh) * W + ow) * c + j * VEC;
-      float sv[VEC];
-      if (skip) load16<bf16>(skip + off, sv);
-      float o[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e)  // same expression (and order) as up_fwd_kernel
-        o[e] = Ld.l0 * (Lh.l0 * (Lw.l0 * v000[e] + Lw.l1 * v001[e]) + Lh.l1 * (Lw.l0 * v010[e] + Lw.l1 * v011[e])) +
-               Ld.l1 * (Lh.l0 * (Lw.l0 * v100[e] + Lw.l1 * v101[e]) + Lh.l1 * (Lw.l0 * v110[e] + Lw.l1 * v111[e]));
-      if (skip)
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) o[e] += sv[e];
-      u32x4 pk;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) pk[e] = pack_bf16x2(o[2 * e], o[2 * e + 1]);
-      *reinterpret_cast<u32x4*>(y + off) = pk;
-      float r[VEC];  // the stored values
-      load16<bf16>(reinterpret_cast<const bf16*>(&pk), r);
-      gn_part_add8<GS>(acc, r, cpg);
-    }
-  }
-  gn_part_block<GS, 256>(acc, chn, cpg, 16, part + ((long long)nn * NB + blockIdx.x) * 32);
-  if (!gn_part_is_last(cnt, (unsigned)(NB * gridDim.y))) return;
-  gn_part_finalize<256>(part, gridDim.y, NB, 16, (double)D * H * W * cpg, stats);
-}
-
 }  // namespace u3d
 
 using namespace u3d;
@@ -279,38 +223,6 @@ extern "C" int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d,
     else hipLaunchKernelGGL((up_fwd_kernel<float, 1>), gr, bl, 0, s, (const float*)x, (const float*)skip, (float*)y, n, c, d, h, w);
   }
   return check_launch("up_fwd_kernel");
-}
-
-static int up_stats_blocks(int n, int c, int d) { return std::max(1, std::min(2 * d * 4, 256 / n)); }
-
-extern "C" long long u3d_upsample2x_stats_ws_bytes(int n, int c, int d) {
-  return 256 + (long long)n * up_stats_blocks(n, c, d) * 32 * 8;
-}
-
-extern "C" int u3d_upsample2x_add_stats(const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
-                                        float* stats, void* ws, u3d_stream_t stream) {
-  U3D_REQUIRE(x && y && stats && ws && n > 0 && d > 0 && h > 0 && w > 0, "upsample_stats: bad args");
-  U3D_REQUIRE(c % 16 == 0 && c >= 16 && c <= 256 && (c & (c - 1)) == 0,
-              "upsample_stats: channels %d must be a power of two in [16, 256] (GroupNorm(16) chunks)", c);
-  const int nb = up_stats_blocks(n, c, d);
-  unsigned* cnt = reinterpret_cast<unsigned*>(ws);
-  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256);
-  const dim3 gr(nb, n), bl(256);
-  hipStream_t s = (hipStream_t)stream;
-  const int cpg = c / 16;
-  if (cpg >= 8)
-    hipLaunchKernelGGL(up_fwd_stats_kernel<1>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, c, d, h, w,
-                       part, cnt, stats);
-  else if (cpg == 4)
-    hipLaunchKernelGGL(up_fwd_stats_kernel<2>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, c, d, h, w,
-                       part, cnt, stats);
-  else if (cpg == 2)
-    hipLaunchKernelGGL(up_fwd_stats_kernel<4>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, c, d, h, w,
-                       part, cnt, stats);
-  else
-    hipLaunchKernelGGL(up_fwd_stats_kernel<8>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, c, d, h, w,
-                       part, cnt, stats);
-  return check_launch("up_fwd_stats_kernel");
 }
 
 extern "C" int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d, int h, int w, void* dx, int accumulate,

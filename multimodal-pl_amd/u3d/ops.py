@@ -198,14 +198,6 @@ def wstd_bwd(partials, nsplit, w, wstats, standardize, dw=None, accumulate=False
 USE_CONV1X1 = os.environ.get("U3D_CONV1X1", "1") != "0"
 
 
-# bf16 stride-2 3^3 forward convs: halo-brick kernel (conv_s2.hip) when the output is at least S2_FWD_MIN_W wide.
-# Parity-tested but measured no faster than the implicit GEMM (96^3 -> 48^3: 94.8 vs 96.6 us; 48^3: 68 vs 65;
-# 24^3: 51 vs 51): each 2x4x16-voxel unit stages a 95 KB halo for 7 MFLOP, so the walk is bound by halo traffic
-# (~3.5 TB/s). Off by default (U3D_S2_FWD=1 enables it).
-USE_S2_FWD = os.environ.get("U3D_S2_FWD", "0") != "0"
-S2_FWD_MIN_W = int(os.environ.get("U3D_S2_FWD_MIN_W", "12"))
-
-
 def _use_conv1x1(dtype, cx, cy, k, n):
     return USE_CONV1X1 and k == 1 and dtype == torch.bfloat16 and cx % 8 == 0 and cy % 8 == 0 and max(cx, cy) <= 256 \
         and n <= 65535
@@ -218,11 +210,6 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
     od, oh, ow = out_dim(d, k, stride), out_dim(h, k, stride), out_dim(w_, k, stride)
     y = torch.empty((n, od, oh, ow, cout), dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
     st, ga, be, G = gn if gn is not None else (None, None, None, 0)
-    if (USE_S2_FWD and k == 3 and stride == 2 and x.dtype == torch.bfloat16 and residual is None and bias is None
-            and not out_f32 and cin % 8 == 0 and cout % 8 == 0 and ow >= S2_FWD_MIN_W):
-        call("u3d_conv_fwd_s2", x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be), G,
-             y.data_ptr(), _stream())
-        return y
     if _use_conv1x1(x.dtype, cin, cout, k, n) and residual is None and bias is None and not out_f32:
         call("u3d_conv1x1", x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), wpk.shape[-1], cout, stride, _ptr(st),
              _ptr(ga), _ptr(be), G, y.data_ptr(), _stream())
@@ -522,22 +509,6 @@ def stem_fwd(x_ncdhw, wpk, cout, stride, dtype):
     return y
 
 
-def stem_fwd_stats(x_ncdhw, wpk, cout, stride, dtype):
-    """stem_fwd that also returns the GroupNorm(16) statistics of its output (bf16, cin 1 -> 32, stride 1,
-    w % 4 == 0); otherwise (stem_fwd(...), None)."""
-    n, cin, d, h, w_ = x_ncdhw.shape
-    if not (STEM_STATS and dtype == torch.bfloat16 and cin == 1 and cout == 32 and stride == 1 and w_ % 4 == 0
-            and d * h * (w_ // 4) >= 256):
-        return stem_fwd(x_ncdhw, wpk, cout, stride, dtype), None
-    require_device(x_ncdhw)
-    y = torch.empty((n, d, h, w_, cout), dtype=dtype, device=x_ncdhw.device)
-    st = torch.empty((n, 16, 2), dtype=torch.float32, device=x_ncdhw.device)
-    ws = WS.get(query("u3d_stem_fwd_stats_ws_bytes", n, d, h, w_), x_ncdhw.device, slot=STATS_SLOT + 1)
-    call("u3d_stem_fwd_stats", x_ncdhw.data_ptr(), n, d, h, w_, wpk.data_ptr(), y.data_ptr(), st.data_ptr(),
-         ws.data_ptr(), _stream())
-    return y, st
-
-
 def stem_wgrad(dy, x_ncdhw, stride):
     n, cin, d, h, w_ = x_ncdhw.shape
     cout = dy.shape[-1]
@@ -621,32 +592,6 @@ def upsample2x_add(x, skip=None):
     y = torch.empty((n, 2 * d, 2 * h, 2 * w_, c), dtype=x.dtype, device=x.device)
     call("u3d_upsample2x_add", dt_code(x.dtype), x.data_ptr(), n, c, d, h, w_, _ptr(skip), y.data_ptr(), _stream())
     return y
-
-
-# GroupNorm statistics from producer epilogues (csrc/gnpart.h). Measured (tools/kbench.py, one box): the decoder
-# upsample + skip with statistics wins where the separate statistics pass is launch/latency-bound (24^3 output:
-# 17.8 us vs 8 + 16 us) but loses at 96^3 (one 256-thread block per CU is too little memory parallelism for the
-# 8-tap gather: 175 vs 86 + 28 us), so it runs up to UP_STATS_MAX_BYTES of output; the stem variant loses at 96^3
-# (153 vs 98 us: the per-thread 16-group reductions) and is off (U3D_STEM_STATS=1 turns it on).
-EPI_STATS = os.environ.get("U3D_EPI_STATS", "0") != "0"  # A/B on one box: 8.01 vs 7.99 ms/step (off)
-STEM_STATS = os.environ.get("U3D_STEM_STATS", "0") != "0"
-UP_STATS_MAX_BYTES = 2 * 48 ** 3 * 64 * 2
-STATS_SLOT = 41  # last-block counters of the epilogue-statistics kernels (zero between launches)
-
-
-def upsample2x_add_stats(x, skip=None):
-    """upsample2x_add that also returns the GroupNorm(16) statistics [n,16,2] of its output (bf16, c a power of two
-    in [16, 256]); otherwise (upsample2x_add(...), None)."""
-    n, d, h, w_, c = x.shape
-    if not (EPI_STATS and x.dtype == torch.bfloat16 and 16 <= c <= 256 and c & (c - 1) == 0
-            and x.numel() * 8 * 2 <= UP_STATS_MAX_BYTES):
-        return upsample2x_add(x, skip), None
-    y = torch.empty((n, 2 * d, 2 * h, 2 * w_, c), dtype=x.dtype, device=x.device)
-    st = torch.empty((n, 16, 2), dtype=torch.float32, device=x.device)
-    ws = WS.get(query("u3d_upsample2x_stats_ws_bytes", n, c, d), x.device, slot=STATS_SLOT)
-    call("u3d_upsample2x_add_stats", x.data_ptr(), n, c, d, h, w_, _ptr(skip), y.data_ptr(), st.data_ptr(),
-         ws.data_ptr(), _stream())
-    return y, st
 
 
 def upsample2x_bwd(dy, in_shape, dx=None, accumulate=False):

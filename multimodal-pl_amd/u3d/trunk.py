@@ -114,19 +114,11 @@ class Tape:
             self.sink.done(name)
 
     # ------------------------------------------------------------------ ops
-    def stem(self, x, key, stride, groups=0):
-        """conv with cin <= 4 from the fp32 NCDHW input volume (unet3D.py:1632 / :1514); with groups == 16 the
-        GroupNorm statistics of the output come from the kernel's epilogue (layer0's gn1 reads them)."""
+    def stem(self, x, key, stride):
+        """conv with cin <= 4 from the fp32 NCDHW input volume (unet3D.py:1632 / :1514)."""
         W = self.P[key + ".weight"]
         pf, _, st = self.packed(key, self.std, need_dgrad=False)
-        g16 = None
-        if groups == 16:
-            y, g16 = ops.stem_fwd_stats(x, pf, W.shape[0], stride, self.dtype)
-        else:
-            y = ops.stem_fwd(x, pf, W.shape[0], stride, self.dtype)
-        out = Act(y)
-        if g16 is not None:
-            out.stats[16] = g16
+        out = Act(ops.stem_fwd(x, pf, W.shape[0], stride, self.dtype))
         if self.record:
             def bwd():
                 if out.grad is None:
@@ -214,17 +206,9 @@ class Tape:
         self.grad_done(gn_key + ".weight")
         self.grad_done(gn_key + ".bias")
 
-    def up_add(self, x, skip, groups=0):
-        """upsamplex2 (trilinear, align_corners=False) + skip, unet3D.py:1646 / :1764-1783. With groups == 16 the
-        GroupNorm statistics of the output come from the kernel's epilogue (the decoder block's gn1 reads them)."""
-        st = None
-        if groups == 16:
-            y, st = ops.upsample2x_add_stats(x.t, skip.t if skip is not None else None)
-        else:
-            y = ops.upsample2x_add(x.t, skip.t if skip is not None else None)
-        out = Act(y)
-        if st is not None:
-            out.stats[16] = st
+    def up_add(self, x, skip):
+        """upsamplex2 (trilinear, align_corners=False) + skip, unet3D.py:1646 / :1764-1783."""
+        out = Act(ops.upsample2x_add(x.t, skip.t if skip is not None else None))
         if self.record:
             def bwd():
                 dy = out.grad
@@ -257,7 +241,7 @@ class Tape:
             t = self.stem(x, "conv0", 2)
             t = self.gn_conv(t, "conv1", 3, 1)
         else:
-            t = self.stem(x, "conv1", 1, cfg.groups)
+            t = self.stem(x, "conv1", 1)
         skips = []
         for i in range(5):
             for b in range(cfg.layers[i]):
@@ -268,7 +252,7 @@ class Tape:
         bott = f
         self.dec = []  # decoder features after x8/x4/x2/x1_resb (unet3D_with_feam3 heads read the first three)
         for name, s in zip(["x8_resb", "x4_resb", "x2_resb", "x1_resb"], [skips[3], skips[2], skips[1], skips[0]]):
-            u = self.up_add(f, s, cfg.groups)
+            u = self.up_add(f, s)
             f = self.block(u, name + ".0.", 1, cfg.groups)
             self.dec.append(f)
         return f, bott

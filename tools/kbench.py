@@ -117,22 +117,6 @@ def _queue(fn):
 CASES["fwd96q"] = _queue(CASES["fwd96"])
 CASES["dgrad96q"] = _queue(CASES["dgrad96"])
 
-def _up(stats, n=2, s=48, c=32):
-    x = torch.randn((n, s, s, s, c), device=dev).to(bf)
-    sk = torch.randn((n, 2 * s, 2 * s, 2 * s, c), device=dev).to(bf)
-    fn = (lambda: ops.upsample2x_add_stats(x, sk)) if stats else (lambda: (ops.upsample2x_add(x, sk), ops.gn_stats(
-        ops.upsample2x_add(x, sk), 16)))
-    return t_(fn), 2.0 * n * (2 * s) ** 3 * c * 2
-
-
-def _stem(stats, n=2, s=96):
-    x = torch.rand((n, 1, s, s, s), device=dev)
-    w = torch.randn(32, 1, 3, 3, 3, device=dev)
-    pf, _, _ = ops.wstd_fwd(w, bf, True, need_dgrad=False)
-    fn = (lambda: ops.stem_fwd_stats(x, pf, 32, 1, bf)) if stats else (lambda: ops.gn_stats(ops.stem_fwd(x, pf, 32, 1, bf), 16))
-    return t_(fn), 2.0 * n * s ** 3 * 27 * 32
-
-
 def _stem_plain(n=2, s=96):
     x = torch.rand((n, 1, s, s, s), device=dev)
     w = torch.randn(32, 1, 3, 3, 3, device=dev)
@@ -146,9 +130,7 @@ CASES_EXTRA = {"fwd_s2_96": lambda: _fwd(2, 32, 64, 96, 3, 2, True, False),
                "fwd48_plain": lambda: _fwd(2, 64, 64, 48, 3, 1, False, False),
                "fwd48_gn": lambda: _fwd(2, 64, 64, 48, 3, 1, True, False),
                "fwd48_res": lambda: _fwd(2, 64, 64, 48, 3, 1, False, True),
-               "fwd24_plain": lambda: _fwd(2, 128, 128, 24, 3, 1, False, False),"up96_stats": lambda: _up(True), "up96_plain_then_stats": lambda: _up(False),
-               "up24_stats": lambda: _up(True, 2, 12, 128), "up24_plain_then_stats": lambda: _up(False, 2, 12, 128),
-               "stem96_stats": lambda: _stem(True), "stem96_plain_then_stats": lambda: _stem(False),
+               "fwd24_plain": lambda: _fwd(2, 128, 128, 24, 3, 1, False, False),
                "stem96": lambda: _stem_plain()}
 CASES.update(CASES_EXTRA)
 
