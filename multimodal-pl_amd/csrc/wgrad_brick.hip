@@ -41,7 +41,7 @@ __device__ __forceinline__ bf16x8 frag_from(v4i16 lo, v4i16 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int BD, int BH, int BW, int S>
+template <int BD, int BH, int BW, int S, int NCO = 1>
 __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                             const float* __restrict__ gstat,
                                                             const float* __restrict__ gamma,
@@ -49,30 +49,35 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
                                                             WBGeom g) {
   constexpr int NV = BD * BH * BW, NKS = NV / 16;
   constexpr int HD = (BD - 1) * S + 3, HH = (BH - 1) * S + 3, HW = (BW - 1) * S + 3, NH = HD * HH * HW;
-  constexpr int ROWB = 64;  // 32 bf16 channels per LDS row
+  constexpr int ROWB = 64;           // 32 bf16 channels per LDS halo row
+  constexpr int DROWB = 64 * NCO;    // dy rows: the NCO output-channel tiles of the workgroup side by side
   constexpr int NT = 512;
-  constexpr int RPP = NT / 4;                       // rows per pass (thread t: chunk t&3 of row t>>2)
-  constexpr int DYL = (NV + RPP - 1) / RPP;         // dy loads per thread
+  constexpr int RPP = NT / 4;                       // halo rows per pass (thread t: chunk t&3 of row t>>2)
+  constexpr int DCH = 4 * NCO, DRPP = NT / DCH;     // dy: 8-channel chunks per row, rows per pass
+  constexpr int DYL = (NV + DRPP - 1) / DRPP;       // dy loads per thread
   constexpr int HLL = (NH + RPP - 1) / RPP;         // halo loads per thread
   static_assert(NV % 32 == 0, "brick voxels (an even number of 16-voxel k-steps)");
-  __shared__ __attribute__((aligned(16))) char lds[(NV + NH) * ROWB];
+  __shared__ __attribute__((aligned(16))) char lds[NV * DROWB + NH * ROWB];
   char* dyt = lds;
-  char* hal = lds + NV * ROWB;
+  char* hal = lds + NV * DROWB;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ch = tid & 3, row0 = tid >> 2;  // fixed channel chunk per thread
+  const int ch = tid & 3, row0 = tid >> 2;  // fixed halo channel chunk per thread
+  const int dch = tid % DCH, drow0 = tid / DCH;
   const TileSplit ts = xcd_tile_split();  // XCD-aware: the channel tiles of neighbouring brick ranges share an L2
-  const int ci0 = ts.tx * 32, co0 = ts.ty * 32;
+  const int ci0 = ts.tx * 32, co0 = ts.ty * 32 * NCO;
   const long long b0 = (long long)ts.split * g.per_split;
   const long long b1 = min(g.nbricks, b0 + g.per_split);
   const bool has_gn = gstat != nullptr;
 
   constexpr int MAXT = 4;  // taps per wave: t = wave + 8j
-  f32x16 acc[MAXT];
+  f32x16 acc[MAXT][NCO];
 #pragma unroll
   for (int j = 0; j < MAXT; ++j)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    for (int c = 0; c < NCO; ++c)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][c][e] = 0.f;
   int tap_off[MAXT];
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
@@ -103,10 +108,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
     decode(b, n, od0, oh0, ow0);
 #pragma unroll
     for (int i = 0; i < DYL; ++i) {
-      const int v = row0 + i * RPP;
+      const int v = drow0 + i * DRPP;
       u32x4 val = {0u, 0u, 0u, 0u};
       const int vw = v % BW, vh = (v / BW) % BH, vd = v / (BW * BH);
-      const int zd = od0 + vd, zh = oh0 + vh, zw = ow0 + vw, co = co0 + ch * 8;
+      const int zd = od0 + vd, zh = oh0 + vh, zw = ow0 + vw, co = co0 + dch * 8;
       if (v < NV && zd < g.od && zh < g.oh && zw < g.ow && co < g.cout)
         val = *reinterpret_cast<const u32x4*>(dy + ((((long long)n * g.od + zd) * g.oh + zh) * g.ow + zw) * g.cout + co);
       pdy[i] = val;
@@ -133,8 +138,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
     }
 #pragma unroll
     for (int i = 0; i < DYL; ++i) {
-      const int v = row0 + i * RPP;
-      if (v < NV) *reinterpret_cast<u32x4*>(dyt + v * ROWB + ch * 16) = pdy[i];
+      const int v = drow0 + i * DRPP;
+      if (v < NV) *reinterpret_cast<u32x4*>(dyt + v * DROWB + dch * 16) = pdy[i];
     }
     const int id0 = od0 * S - 1, ih0 = oh0 * S - 1, iw0 = ow0 * S - 1;
 #pragma unroll
@@ -171,28 +176,43 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
         for (int m = 0; m < 2; ++m) {
           const int k = ks * 16 + 8 * h + 4 * m + q;
           const int vw = k % BW, vh = (k / BW) % BH, vd = k / (BW * BH);
-          ar[m] = k * ROWB + colb;
+          ar[m] = k * DROWB + colb;
           hr[m] = ((vd * S * HH + vh * S) * HW + vw * S) * ROWB + colb;
         }
       };
-      auto frags = [&](int ks, bf16x8& a, bf16x8 (&bb)[NT]) {
+      auto frags = [&](int ks, bf16x8 (&a)[NCO], bf16x8 (&bb)[NT]) {
         int ar[2], hr[2];
         rows(ks, ar, hr);
-        a = frag_from(tr_read(dyt, ar[0]), tr_read(dyt, ar[1]));
+#pragma unroll
+        for (int c = 0; c < NCO; ++c) a[c] = frag_from(tr_read(dyt, ar[0] + 64 * c), tr_read(dyt, ar[1] + 64 * c));
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           bb[j] = frag_from(tr_read(hal, hr[0] + tap_off[j]), tr_read(hal, hr[1] + tap_off[j]));
       };
-      bf16x8 a0, a1, b0[NT], b1[NT];
-      frags(0, a0, b0);
+      auto mfmas = [&](const bf16x8 (&a)[NCO], const bf16x8 (&bb)[NT]) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int c = 0; c < NCO; ++c)
+            acc[j][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[c], bb[j], acc[j][c], 0, 0, 0);
+      };
+      if constexpr (NCO == 1) {
+        bf16x8 a0[NCO], a1[NCO], b0[NT], b1[NT];
+        frags(0, a0, b0);
 #pragma unroll 1
-      for (int ks = 0; ks < NKS; ks += 2) {
-        frags(ks + 1, a1, b1);  // NKS is even
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0[j], acc[j], 0, 0, 0);
-        if (ks + 2 < NKS) frags(ks + 2, a0, b0);
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1[j], acc[j], 0, 0, 0);
+        for (int ks = 0; ks < NKS; ks += 2) {
+          frags(ks + 1, a1, b1);  // NKS is even
+          mfmas(a0, b0);
+          if (ks + 2 < NKS) frags(ks + 2, a0, b0);
+          mfmas(a1, b1);
+        }
+      } else {  // twice the accumulators: no fragment lookahead (the other wave of the SIMD covers the LDS reads)
+#pragma unroll 1
+        for (int ks = 0; ks < NKS; ++ks) {
+          bf16x8 a0[NCO], b0[NT];
+          frags(ks, a0, b0);
+          mfmas(a0, b0);
+        }
       }
     };
     if (ntap == 4)
@@ -213,15 +233,18 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
   for (int j = 0; j < MAXT; ++j) {
     if (j < ntap) {
       const int tt = w8 + 8 * j;
-      const int base = ((ts.split * 27 + tt) * g.cout_p + co0 + 4 * h8) * g.cin_p + ci0 + r;
-      // (the whole accumulator is bit-cast first: a bit_cast of a single element of the fp32 vector fed to
-      // raw_buffer_store_b32 is miscompiled by ROCm 7.2 clang into stores of element 0)
-      typedef __attribute__((ext_vector_type(16))) uint32_t u32x16;
-      const u32x16 ua = __builtin_bit_cast(u32x16, acc[j]);
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        __builtin_amdgcn_raw_buffer_store_b32(ua[i], prs, (unsigned)((base + ((i & 3) + 8 * (i >> 2)) * g.cin_p) * 4),
-                                              0, 0);
+      for (int c = 0; c < NCO; ++c) {
+        const int base = ((ts.split * 27 + tt) * g.cout_p + co0 + 32 * c + 4 * h8) * g.cin_p + ci0 + r;
+        // (the whole accumulator is bit-cast first: a bit_cast of a single element of the fp32 vector fed to
+        // raw_buffer_store_b32 is miscompiled by ROCm 7.2 clang into stores of element 0)
+        typedef __attribute__((ext_vector_type(16))) uint32_t u32x16;
+        const u32x16 ua = __builtin_bit_cast(u32x16, acc[j][c]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          __builtin_amdgcn_raw_buffer_store_b32(ua[i], prs, (unsigned)((base + ((i & 3) + 8 * (i >> 2)) * g.cin_p) * 4),
+                                                0, 0);
+      }
     }
   }
 }
@@ -360,6 +383,10 @@ using namespace u3d;
 
 static int wgrad_bd() { return opt(OPT_WGRAD_BD) == 2 ? 2 : 3; }  // brick depth of the stride-1 kernel
 
+// stride 2: a workgroup covers two 32-wide output-channel tiles, so the 8x-larger input halo of a stride-2 brick is
+// staged (and GroupNorm'd) once for 64 output channels
+static int wb_nco(int stride, int cout) { return stride == 2 && opt(OPT_WB_S2CO64) != 0 && round_up(cout, 32) % 64 == 0 ? 2 : 1; }
+
 static void brick_dims(int stride, int* bd, int* bh, int* bw) {
   if (stride == 1) { *bd = wgrad_bd(); *bh = 8; *bw = 16; }
   else { *bd = 2; *bh = 4; *bw = 8; }
@@ -370,7 +397,7 @@ extern "C" int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, 
   brick_dims(stride, &bd, &bh, &bw);
   const int od = (d - 1) / stride + 1, oh = (h - 1) / stride + 1, ow = (w - 1) / stride + 1;
   const long long nb = (long long)n * cdiv(od, bd) * cdiv(oh, bh) * cdiv(ow, bw);
-  const long long tiles = (long long)cdiv(cin, 32) * cdiv(cout, 32);
+  const long long tiles = (long long)cdiv(cin, 32) * (cdiv(cout, 32) / wb_nco(stride, cout));
   const long long target = std::max(1, opt(OPT_WB_WGS));  // workgroups aimed at
   long long want = std::max(1LL, target / tiles);
   const long long ns = std::max(1LL, std::min(want, nb));
@@ -403,8 +430,12 @@ extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int ci
   if (ns_eff < nsplit)  // trailing slabs would stay unwritten
     U3D_HIP(hipMemsetAsync(partials + (long long)ns_eff * 27 * g.cout_p * g.cin_p, 0,
                            (size_t)(nsplit - ns_eff) * 27 * g.cout_p * g.cin_p * 4, s));
-  dim3 grid(g.cin_p / 32, g.cout_p / 32, ns_eff);
-  if (stride == 1 && bd == 2)
+  const int nco = wb_nco(stride, cout);
+  dim3 grid(g.cin_p / 32, g.cout_p / 32 / nco, ns_eff);
+  if (stride == 2 && nco == 2)
+    hipLaunchKernelGGL((wgrad_brick_kernel<2, 4, 8, 2, 2>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
+                       gn_stats, gn_gamma, gn_beta, partials, g);
+  else if (stride == 1 && bd == 2)
     hipLaunchKernelGGL((wgrad_brick_kernel<2, 8, 16, 1>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
                        gn_stats, gn_gamma, gn_beta, partials, g);
   else if (stride == 1)

@@ -120,6 +120,23 @@ def test_bf16_conv_wgrad(gpu, n, cin, cout, dims, s, brick):
     assert err < 2e-3 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("n,cin,cout,dims", [(1, 32, 64, (8, 12, 18)), (2, 64, 128, (12, 10, 16)), (1, 40, 48, (6, 10, 14))])
+def test_wgrad_brick_s2_two_co_tiles_matches_one(gpu, n, cin, cout, dims):
+    """Stride-2 brick weight gradient with two 32-wide co tiles per workgroup (one staged halo for 64 output channels,
+    the default) against one co tile per workgroup (OPT WB_S2CO64 = 0): each output element is the same MFMA chain
+    over the same bricks; only the split boundaries (the split count follows the workgroup count) and so the fp32
+    order of the split sums differ: <= 1e-5 of max |dW|."""
+    from u3d import ops
+    x, w, st, ga, be, G = _case(gpu, n, cin, cout, dims, True, 7)
+    od = tuple(ops.out_dim(d, 3, 2) for d in dims)
+    dy = torch.randn((n,) + od + (cout,), device=gpu).to(torch.bfloat16)
+    part, _ = ops.conv_wgrad(dy, x, 3, 2, (st, ga, be, G), brick=True)
+    with ops.option("WB_S2CO64", 0):
+        part1, _ = ops.conv_wgrad(dy, x, 3, 2, (st, ga, be, G), brick=True)
+    a, b = part.double().sum(0), part1.double().sum(0)
+    assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item()
+
+
 def test_bf16_gn_bwd_and_upsample(gpu):
     from u3d import ops
     torch.manual_seed(4)
