@@ -9,6 +9,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 tail -1 $O/pytest.log
 bash tools/kab.sh r03k/kab 3 stem96 wgrad_s2_96 wgrad_s2_48 wgrad_s2_24 || exit 1
 for i in 1 2 3; do
+  timeout -k 10 300 python tools/kbench.py fwd96_nores fwd96 2>&1 | grep -v amdgpu.ids | sed 's/^/KR16 /' | tee -a $O/kr.log || exit 1
   U3D_LIB=$R/multimodal-pl_amd/u3d/libu3d_kr.so timeout -k 10 300 python tools/kbench.py fwd96_nores fwd96 2>&1 | grep -v amdgpu.ids | sed 's/^/KR12 /' | tee -a $O/kr.log || exit 1
 done
 bash tools/ab.sh r03k/ab "U3D_NONE=0" "U3D_LIB=$R/multimodal-pl_amd/u3d/libu3d_ab.so" 3 || exit 1
