@@ -227,9 +227,11 @@ int u3d_conv_wgrad1(const void* dy, const void* x, int n, int cin, int d, int h,
                     float* partials, int nsplit, u3d_stream_t stream);
 
 /* Stem conv with cin <= 4 (conv1 1->32, unet3D.py:1632; conv0 2->f stride 2, :1514): fp32 NCDHW input, NDHWC
- * output, direct VALU conv with fp32 input (conv1 1 -> 32 stride 1: packed FMAs with wave-uniform weights). */
+ * output, direct VALU conv with fp32 input (conv1 1 -> 32 stride 1: packed FMAs with scalar-loaded weights from a
+ * contiguous fp32 table written into ws, u3d_stem_fwd_ws_bytes() bytes; ws may be NULL for the other shapes). */
+long long u3d_stem_fwd_ws_bytes(void);
 int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
-                 int stride, void* y, u3d_stream_t stream);
+                 int stride, void* y, void* ws, u3d_stream_t stream);
 /* split count for u3d_stem_wgrad given its dtype/channels (the bf16 1->32 stride-1 stem runs on MFMA) */
 int u3d_stem_wgrad_splits2(int dtype, int n, int cin, int d, int h, int w, int cout, int stride);
 int u3d_stem_wgrad_splits(int n, int d, int h, int w, int stride);

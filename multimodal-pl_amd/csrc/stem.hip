@@ -59,24 +59,21 @@ __global__ __launch_bounds__(ST) void stem_fwd_kernel(const float* __restrict__ 
 }
 
 // cin = 1, stride 1, cout = 32 (conv1 of every trunk, unet3D.py:1632): a thread computes FOUR consecutive w voxels
-// x 32 channels from the 3 x 6 input window of each (kd, kh) row. The weights are wave-uniform: they are read with
-// scalar loads (the 27 x 32 values sit in the scalar cache) and fed to v_pk_fma_f32 as an SGPR pair, the input
-// value broadcast to both halves, so the kernel is bound by packed FMAs (864 per voxel, two per lane-instruction)
-// and the 64 B/voxel output stores; no LDS. Same fp32 FMA chain per output (taps in order, fma(x, w, acc)) as
+// x 32 channels from the 3 x 6 input window of each (kd, kh) row. The weights are wave-uniform: a one-block kernel
+// first writes them as a contiguous fp32 [27][32] table (the packed image holds them at a 32-element stride), which
+// the main kernel reads with wide scalar loads (scalar cache) and feeds to v_pk_fma_f32 as SGPR pairs with the input
+// value broadcast to both halves: the kernel is bound by packed FMAs (864 per voxel, two per lane-instruction) and
+// the 64 B/voxel output stores; no LDS. Same fp32 FMA chain per output (taps in order, fma(x, w, acc)) as
 // stem_fwd_kernel, so results are bitwise those of the generic kernel. One thread per (output row, 4-voxel group).
 template <typename T>
-__device__ __forceinline__ float stem_w(const T* __restrict__ wpk, int idx) {
-  if constexpr (sizeof(T) == 2) {  // bf16: the dword holding (ci 0, ci 1) of the packed image; ci 0 = low half
-    return __uint_as_float(reinterpret_cast<const uint32_t*>(wpk)[idx >> 1] << 16);
-  } else {
-    return wpk[idx];
-  }
+__global__ __launch_bounds__(1024) void stem1_wtab_kernel(const T* __restrict__ wpk, int cin_p, float* __restrict__ wt) {
+  const int i = threadIdx.x;  // (t, co)
+  if (i < 27 * 32) wt[i] = to_f(wpk[(long long)i * cin_p]);
 }
 
 template <typename T>
-__global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__ x, const T* __restrict__ wpk,
-                                                      T* __restrict__ y, int d, int h, int w, int cin_p,
-                                                      long long rows) {
+__global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                                                      T* __restrict__ y, int d, int h, int w, long long rows) {
   const int w4 = w >> 2;
   const long long item = (long long)blockIdx.x * ST + threadIdx.x;  // (output row, 4-voxel group)
   const long long row = item / w4;
@@ -109,10 +106,10 @@ __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__
       const int t0 = (kd * 3 + kh) * 3;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const int wb = (t0 + kw) * 32 * cin_p;
+        const float* wr = wt + (t0 + kw) * 32;
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
-          const f32x2 wv = {stem_w(wpk, wb + (2 * c) * cin_p), stem_w(wpk, wb + (2 * c + 1) * cin_p)};
+          const f32x2 wv = {wr[2 * c], wr[2 * c + 1]};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const f32x2 xv = {in[j + kw], in[j + kw]};
@@ -332,22 +329,27 @@ static int sdim(int d, int s) { return (d - 1) / s + 1; }  // k3 pad1: (d + 2 - 
 
 static bool stem1_on() { return opt(OPT_STEM1) != 0; }  // 0: the generic one-voxel kernel
 
+extern "C" long long u3d_stem_fwd_ws_bytes(void) { return 27 * 32 * 4; }
+
 extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
-                            int stride, void* y, u3d_stream_t stream) {
+                            int stride, void* y, void* ws, u3d_stream_t stream) {
   U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "stem_fwd: bad dtype");
   U3D_REQUIRE(x && wpk && y && cin >= 1 && cin <= 4 && cout >= 1 && (stride == 1 || stride == 2), "stem_fwd: bad args");
   hipStream_t s = (hipStream_t)stream;
   const int od = sdim(d, stride), oh = sdim(h, stride), ow = sdim(w, stride);
   const long long total = (long long)n * od * oh * ow;
   if (cin == 1 && stride == 1 && cout == 32 && w % 4 == 0 && (long long)n * d * h < 2147483647LL && stem1_on()) {
+    U3D_REQUIRE(ws, "stem_fwd: the conv1 kernel needs a workspace of u3d_stem_fwd_ws_bytes()");
     const long long rows = (long long)n * d * h, items = rows * (w / 4);
     const dim3 grid((unsigned)((items + ST - 1) / ST));
-    if (dtype == U3D_BF16)
-      hipLaunchKernelGGL(stem1_fwd_kernel<bf16>, grid, dim3(ST), 0, s, x, (const bf16*)wpk, (bf16*)y, d, h, w,
-                         round_up(cin, 32), rows);
-    else
-      hipLaunchKernelGGL(stem1_fwd_kernel<float>, grid, dim3(ST), 0, s, x, (const float*)wpk, (float*)y, d, h, w,
-                         round_up(cin, 32), rows);
+    float* wt = static_cast<float*>(ws);
+    if (dtype == U3D_BF16) {
+      hipLaunchKernelGGL(stem1_wtab_kernel<bf16>, dim3(1), dim3(1024), 0, s, (const bf16*)wpk, round_up(cin, 32), wt);
+      hipLaunchKernelGGL(stem1_fwd_kernel<bf16>, grid, dim3(ST), 0, s, x, wt, (bf16*)y, d, h, w, rows);
+    } else {
+      hipLaunchKernelGGL(stem1_wtab_kernel<float>, dim3(1), dim3(1024), 0, s, (const float*)wpk, round_up(cin, 32), wt);
+      hipLaunchKernelGGL(stem1_fwd_kernel<float>, grid, dim3(ST), 0, s, x, wt, (float*)y, d, h, w, rows);
+    }
     return check_launch("stem1_fwd_kernel");
   }
   const int nb = (int)std::min<long long>(8192, (total + ST - 1) / ST);

@@ -56,7 +56,8 @@ _SIGS = {
     "u3d_conv_wgrad_brick": [P, P, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_conv_wgrad1_splits": [I, I, I, I, I, I, I],
     "u3d_conv_wgrad1": [P, P, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
-    "u3d_stem_fwd": [I, P, I, I, I, I, I, P, I, I, P, P],
+    "u3d_stem_fwd": [I, P, I, I, I, I, I, P, I, I, P, P, P],
+    "u3d_stem_fwd_ws_bytes": [],
     "u3d_stem_wgrad_splits": [I, I, I, I, I],
     "u3d_stem_wgrad_splits2": [I, I, I, I, I, I, I, I],
     "u3d_stem_wgrad": [I, P, P, I, I, I, I, I, I, I, P, I, P],
@@ -107,7 +108,7 @@ _SIGS = {
     "u3d_aug_affine": [P, L, F, F, P],
     "u3d_aug_contrast": [P, L, F, P, I, P],
 }
-_RESTYPE = {"u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
+_RESTYPE = {"u3d_stem_fwd_ws_bytes": L, "u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
             "u3d_eam_attn_bwd_part_floats": L, "u3d_upsample_trilinear_bwd_ws_floats": L, "u3d_renew_token_ws_bytes": L,
             "u3d_consistency_ws_bytes": L, "u3d_volume_stats_ws_bytes": L, "u3d_convg_brick_stats_ws_floats": L}
 

@@ -499,13 +499,17 @@ def head_bwd(dy, wpk_dgrad, cin, dbias=None):
     return dA, dyb
 
 
+STEM_SLOT = 13  # the conv1 kernel's fp32 weight table
+
+
 def stem_fwd(x_ncdhw, wpk, cout, stride, dtype):
     require_device(x_ncdhw)
     n, cin, d, h, w_ = x_ncdhw.shape
     od, oh, ow = out_dim(d, 3, stride), out_dim(h, 3, stride), out_dim(w_, 3, stride)
     y = torch.empty((n, od, oh, ow, cout), dtype=dtype, device=x_ncdhw.device)
+    ws = WS.get(query("u3d_stem_fwd_ws_bytes"), x_ncdhw.device, slot=STEM_SLOT)
     call("u3d_stem_fwd", dt_code(dtype), x_ncdhw.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, stride,
-         y.data_ptr(), _stream())
+         y.data_ptr(), ws.data_ptr(), _stream())
     return y
 
 
