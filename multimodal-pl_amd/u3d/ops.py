@@ -500,6 +500,7 @@ def head_bwd(dy, wpk_dgrad, cin, dbias=None):
 
 
 STEM_SLOT = 13  # the conv1 kernel's fp32 weight table
+STEM_WS_BYTES = 27 * 32 * 4  # = u3d_stem_fwd_ws_bytes() (tests/test_host.py); a constant so A/B runs load older builds
 
 
 def stem_fwd(x_ncdhw, wpk, cout, stride, dtype):
@@ -507,7 +508,7 @@ def stem_fwd(x_ncdhw, wpk, cout, stride, dtype):
     n, cin, d, h, w_ = x_ncdhw.shape
     od, oh, ow = out_dim(d, 3, stride), out_dim(h, 3, stride), out_dim(w_, 3, stride)
     y = torch.empty((n, od, oh, ow, cout), dtype=dtype, device=x_ncdhw.device)
-    ws = WS.get(query("u3d_stem_fwd_ws_bytes"), x_ncdhw.device, slot=STEM_SLOT)
+    ws = WS.get(STEM_WS_BYTES, x_ncdhw.device, slot=STEM_SLOT)
     call("u3d_stem_fwd", dt_code(dtype), x_ncdhw.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, stride,
          y.data_ptr(), ws.data_ptr(), _stream())
     return y

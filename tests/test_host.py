@@ -32,6 +32,13 @@ def test_library_exports_every_header_symbol():
     assert h.u3d_abi_version() == 1
 
 
+def test_workspace_size_constants_match_the_library():
+    from u3d import _lib, ops
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libu3d.so not built")
+    assert _lib.query("u3d_stem_fwd_ws_bytes") == ops.STEM_WS_BYTES
+
+
 def test_header_compiles_as_c():
     import subprocess
     r = subprocess.run(["gcc", "-fsyntax-only", "-x", "c", os.path.join(REPO, "include", "u3d.h")],
