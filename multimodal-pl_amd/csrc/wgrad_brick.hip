@@ -78,12 +78,17 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
     for (int c = 0; c < NCO; ++c)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[j][c][e] = 0.f;
+  // stride 2: every halo w line is stored parity-split (even w first, then odd), so the lanes of a fragment read,
+  // for any tap, CONSECUTIVE rows (w = 2 vw + tw -> vw, HWE + vw, vw + 1 for tw = 0, 1, 2) instead of every other row
+  // (2-way bank conflicts)
+  constexpr int HWE = S == 2 ? (HW + 1) / 2 : 0;
+  auto wpos = [&](int hw) { return S == 2 ? ((hw & 1) ? HWE + (hw >> 1) : (hw >> 1)) : hw; };
   int tap_off[MAXT];
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
     const int t = min(wave + 8 * j, 26);
     const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
-    tap_off[j] = ((td * HH + th) * HW + tw) * ROWB;
+    tap_off[j] = ((td * HH + th) * HW + (S == 2 ? (tw == 1 ? HWE : tw >> 1) : tw)) * ROWB;
   }
   const int ntap = (27 - wave + 7) / 8;  // 4 for waves 0-2, 3 for 3-7
 
@@ -147,13 +152,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
       const int v = row0 + i * RPP;
       if (v < NH) {
         u32x4 val = phl[i];
+        const int hw = v % HW, hl = v - hw;  // hl = (hd * HH + hh) * HW
         if (has_gn) {
-          const int hw = v % HW, hh = (v / HW) % HH, hd = v / (HW * HH);
+          const int hh = (v / HW) % HH, hd = v / (HW * HH);
           const int zd = id0 + hd, zh = ih0 + hh, zw = iw0 + hw;
           if ((unsigned)zd < (unsigned)g.id && (unsigned)zh < (unsigned)g.ih && (unsigned)zw < (unsigned)g.iw)
             val = gn_relu8(val, sc, sh);
         }
-        *reinterpret_cast<u32x4*>(hal + v * ROWB + ch * 16) = val;
+        *reinterpret_cast<u32x4*>(hal + (hl + wpos(hw)) * ROWB + ch * 16) = val;
       }
     }
   };
@@ -177,7 +183,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
           const int k = ks * 16 + 8 * h + 4 * m + q;
           const int vw = k % BW, vh = (k / BW) % BH, vd = k / (BW * BH);
           ar[m] = k * DROWB + colb;
-          hr[m] = ((vd * S * HH + vh * S) * HW + vw * S) * ROWB + colb;
+          hr[m] = ((vd * S * HH + vh * S) * HW + (S == 2 ? vw : vw * S)) * ROWB + colb;
         }
       };
       auto frags = [&](int ks, bf16x8 (&a)[NCO], bf16x8 (&bb)[NT]) {
