@@ -13,7 +13,8 @@
 //     the chunk are staged once in LDS (chunk-planar, padded planes: conflict-free staging writes); each of
 //     the 8 shifted A fragments is read once per k16 step and feeds the 1..8 taps that use that shift;
 //   * the next chunk is prefetched into registers while the MFMAs of the current one run;
-//   * epilogue through LDS: (pw = 0, 1) of consecutive q are adjacent dx voxels -> 128-B contiguous rows.
+//   * the MFMA is issued transposed (A = weights, B = dy rows), so a lane's accumulators are dx channels of one voxel:
+//     the epilogue stores them as 16-B chunks straight from registers (one v_permlane32_swap per pair).
 #include "common.h"
 
 namespace u3d {
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(S2_NT, 1) void dgrad_s2_kernel(const bf16* __restri
                 const int p = ((td != 1) << 2) | ((th != 1) << 1) | (tw != 1);
                 const int t = (td * 3 + th) * 3 + tw;
                 const bf16x8 bv = *reinterpret_cast<const bf16x8*>(bb + t * 32 * 16);
-                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[p], 0, 0, 0);
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bv, a, acc[p], 0, 0, 0);  // D[dx ch][voxel]
               }
         }
       }
@@ -158,42 +159,37 @@ __global__ __launch_bounds__(S2_NT, 1) void dgrad_s2_kernel(const bf16* __restri
     }
   }
 
-  // epilogue, one half (pd) at a time: wave tile [ph][pw][32 q rows][32 co] bf16 = 8 KB, read back as 16-B
-  // chunks ordered (row, pw, part) so 8 lanes write one q row's two adjacent dx voxels (128 B contiguous)
-  char* const ept = smem + wave * 8192;
+  // epilogue straight from the accumulators (the MFMA is issued transposed: A = weights, B = dy rows): lane (r, hh)
+  // holds dx channels 8q + 4hh + e (q, e < 4) of q voxel r in every parity class; one v_permlane32_swap per pair
+  // leaves it channels 8hh..8hh+7 and 16+8hh..16+8hh+7, stored as two 16-B chunks per class (no LDS pass)
+  const int vv = wave * 32 + r;
+  const int uw = vv % g.bw, uh = (vv / g.bw) % g.bh, ud = vv / (g.bw * g.bh);
+  const bool qok = active && vv < g.nvq && q0d + ud < g.qd && q0h + uh < g.qh && q0w + uw < g.qw;
 #pragma unroll
-  for (int pd = 0; pd < 2; ++pd) {
-    if (pd) __syncthreads();  // all waves done reading the pd = 0 tiles
-    if (active) {
+  for (int p = 0; p < 8; ++p) {
+    uint32_t pk[4][2];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-          *reinterpret_cast<bf16*>(ept + ((j >> 1) * 2048 + (row * 2 + (j & 1)) * 32 + r) * 2) =
-              from_f<bf16>(acc[pd * 4 + j][i]);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    if (active) {
+      for (int e = 0; e < 2; ++e) pk[q][e] = pack_bf16x2(acc[p][4 * q + 2 * e], acc[p][4 * q + 2 * e + 1]);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int qi = lane + 64 * u;               // (ph, row, pw, part)
-        const int part = qi & 3, pw = (qi >> 2) & 1, row = (qi >> 3) & 31, ph = qi >> 8;
-        const int vv = wave * 32 + row;
-        const int uw = vv % g.bw, uh = (vv / g.bw) % g.bh, ud = vv / (g.bw * g.bh);
-        const int xd = 2 * (q0d + ud) + pd, xh = 2 * (q0h + uh) + ph, xw = 2 * (q0w + uw) + pw;
-        const int co = co0 + part * 8;
-        if (vv < g.nvq && q0d + ud < g.qd && q0h + uh < g.qh && q0w + uw < g.qw && xd < g.D && xh < g.H &&
-            xw < g.W && co < g.cx) {
-          const u32x4 val = *reinterpret_cast<const u32x4*>(ept + qi * 16);
-          *reinterpret_cast<u32x4*>(dx + ((((long long)nn * g.D + xd) * g.H + xh) * g.W + xw) * g.cx + co) = val;
-        }
+    for (int q = 0; q < 4; q += 2)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(pk[q][e], pk[q + 1][e], false, false);
+        pk[q][e] = sw[0];
+        pk[q + 1][e] = sw[1];
+      }
+    const int xd = 2 * (q0d + ud) + (p >> 2), xh = 2 * (q0h + uh) + ((p >> 1) & 1), xw = 2 * (q0w + uw) + (p & 1);
+    if (qok && xd < g.D && xh < g.H && xw < g.W) {
+      bf16* const row = dx + ((((long long)nn * g.D + xd) * g.H + xh) * g.W + xw) * g.cx;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int co = co0 + 16 * u + 8 * hh;
+        if (co < g.cx)
+          *reinterpret_cast<u32x4*>(row + co) = (u32x4){pk[2 * u][0], pk[2 * u][1], pk[2 * u + 1][0], pk[2 * u + 1][1]};
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
   }
 }
 
