@@ -33,6 +33,11 @@ def main():
     side = torch.cuda.Stream(device=dev)
     cases = {"fwd": lambda: ops.conv_fwd_stats(x, pf, 32, 3, 1, gn, r),
              "dgrad": lambda: ops.conv_dgrad(x, pd, 32, (n, s, s, s), 3, 1)}
+    # the persistent brick data gradients at 48^3 x 64 and 24^3 x 128 (round 3: u3d_convg_brick_q)
+    for s2, c2 in ((48, 64), (24, 128)):
+        x2 = (torch.randn((n, s2, s2, s2, c2), device=dev) * 0.5).to(bf)
+        _, pd2, _ = ops.wstd_fwd(torch.randn(c2, c2, 3, 3, 3, device=dev), bf, True)
+        cases[f"dgrad{s2}"] = (lambda x2=x2, pd2=pd2, s2=s2, c2=c2: ops.conv_dgrad(x2, pd2, c2, (n, s2, s2, s2), 3, 1))
 
     def timed(fn, reps=10):
         for _ in range(3):
@@ -70,13 +75,13 @@ def main():
     res = {"occupy_us_per_8wg_200k": round(t_occ, 1), "occupy_iters": iters, "cases": {}}
     for name, fn in cases.items():
         for mode in ("static", "queue"):
-            ops.RING_QUEUE = mode == "queue"
+            ops.RING_QUEUE = ops.PBRICK_QUEUE = mode == "queue"
             row = {"alone_us": round(timed(fn), 1)}
             for k in ks:
                 row[f"with_{k}_cus_held_us"] = round(with_hog(fn, k), 1)
             res["cases"][f"{name}_{mode}"] = row
             print(name, mode, row, file=sys.stderr, flush=True)
-    ops.RING_QUEUE = True
+    ops.RING_QUEUE = ops.PBRICK_QUEUE = False
     print(json.dumps(res))
 
 
