@@ -190,6 +190,11 @@ int u3d_conv32_ring_q_stats_finalize(const float* stats_ws, int n, int d, int h,
  * u3d_conv_wgrad_brick ([nsplit][27][cout_p][cin_p] fp32, summed by the caller in fixed order); a split is a
  * contiguous range of 16x16-voxel output planes walked down d. */
 int u3d_conv_wgrad_ring_splits(int n, int cin, int d, int h, int w, int cout);
+/* Split count aimed at `wgs` workgroups instead of one per CU. With wgs = 3 x the CU count the launch is a grid of
+ * short plane ranges that the hardware dispatcher hands to whichever CU is free, so a concurrent kernel holding CUs
+ * (the data-parallel all-reduce of train_amos_atlas_final.py:375) delays a third of a range, not a whole one; every
+ * split still owns a fixed contiguous range and its own slab (deterministic sums), at 3x the slab bytes. */
+int u3d_conv_wgrad_ring_splits_target(int n, int cin, int d, int h, int w, int cout, int wgs);
 int u3d_conv_wgrad_ring(const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout,
                         const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                         float* partials, int nsplit, u3d_stream_t stream);

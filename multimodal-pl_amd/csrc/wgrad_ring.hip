@@ -344,14 +344,19 @@ static void wr_geom(int n, int cin, int d, int h, int w, int cout, WRGeom& g) {
   g.ybytes = (long long)n * d * h * w * cout * 2;
 }
 
-extern "C" int u3d_conv_wgrad_ring_splits(int n, int cin, int d, int h, int w, int cout) {
+extern "C" int u3d_conv_wgrad_ring_splits_target(int n, int cin, int d, int h, int w, int cout, int wgs) {
   WRGeom g;
   wr_geom(n, cin, d, h, w, cout, g);
   const long long tiles = (long long)(g.cin_p / 32) * (g.cout_p / 32);
-  const long long target = std::max(1, opt(OPT_WR_WGS));  // workgroups aimed at
+  const long long target = std::max(1, wgs);  // workgroups aimed at
   const long long want = std::max(1LL, std::min(g.planes, target / tiles));
   const long long per = (g.planes + want - 1) / want;
   return (int)((g.planes + per - 1) / per);  // every split receives planes: no zero-filled slabs
+}
+
+// one workgroup per CU (OPT_WR_WGS, default 256): each split's plane range is walked by one resident workgroup
+extern "C" int u3d_conv_wgrad_ring_splits(int n, int cin, int d, int h, int w, int cout) {
+  return u3d_conv_wgrad_ring_splits_target(n, cin, d, h, w, cout, opt(OPT_WR_WGS));
 }
 
 extern "C" int u3d_conv_wgrad_ring(const void* dy, const void* x, int n, int cin, int d, int h, int w, int cout,

@@ -48,6 +48,7 @@ _SIGS = {
     "u3d_conv32_ring_q": [I, P, I, I, I, I, P, P, P, P, I, P, P, P, P, P],
     "u3d_conv32_ring_q_stats_finalize": [P, I, I, I, I, P, P],
     "u3d_conv_wgrad_ring_splits": [I, I, I, I, I, I],
+    "u3d_conv_wgrad_ring_splits_target": [I, I, I, I, I, I, I],
     "u3d_conv_wgrad_ring": [P, P, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_convg_brick": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P],
     "u3d_convg_brick_queue_bytes": [],

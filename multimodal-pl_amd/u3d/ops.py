@@ -321,6 +321,7 @@ def _queue(device, shape):
 # persistent brick data gradient on its work queue (u3d_convg_brick_q): while a collective may be in flight, or always
 # with U3D_PBRICK_QUEUE=1
 PBRICK_QUEUE = os.environ.get("U3D_PBRICK_QUEUE", "0") != "0"
+SMALL_Q_WGS = 768  # conv_small data-gradient workgroups aimed at while a collective may hold CUs
 PBRICK_QUEUE_SLOT = 41  # workspace slot of its counters (zero between launches; nothing else uses it)
 
 
@@ -393,8 +394,12 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
         return dx
     if _use_small(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
         ws = WS.get(SPLITK_WS_BYTES, dy.device, slot=4)
-        call("u3d_conv_small", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None, 0,
-             None, dx.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        # while a collective may hold CUs: ~3x the CUs in (tile, contraction split) workgroups, dealt by the
+        # dispatcher to free CUs (each split keeps its own slab and the fixed-order reduce: same dx every run)
+        with (option("SMALL_WGS", SMALL_Q_WGS) if (PBRICK_QUEUE or COLLECTIVE_IN_FLIGHT[0]) else
+              contextlib.nullcontext()):
+            call("u3d_conv_small", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None,
+                 0, None, dx.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         return dx
     if _use_gen_brick(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
         if PBRICK_QUEUE or COLLECTIVE_IN_FLIGHT[0]:
@@ -437,6 +442,10 @@ USE_BRICK_WGRAD = True
 USE_RING_WGRAD = True      # stride-1 3^3 weight gradients: depth-streaming ring kernel (wgrad_ring.hip)
 RING_WGRAD_MIN_HW = 8      # h, w extents below this use the brick kernel (measured faster from 12^3 up)
 USE_S2_BRICK = True  # stride-2 3^3 bf16 data gradient: one-launch parity-merged kernel (dgrad_s2.hip)
+# stride-1 weight-gradient ring while a collective may hold CUs (or always with U3D_WGRAD_QUEUE=1): a grid of ~3x the
+# CUs in short plane ranges instead of one resident range per CU (each range keeps its own slab: same sums every run)
+WGRAD_QUEUE = os.environ.get("U3D_WGRAD_QUEUE", "0") != "0"
+WGRAD_Q_WGS = 768
 
 
 def conv_wgrad(dy, x, k, stride, gn=None, brick=None):
@@ -451,7 +460,10 @@ def conv_wgrad(dy, x, k, stride, gn=None, brick=None):
             brick = "ring"  # (the ring addresses its operands with 32-bit buffer offsets; larger ones: bricks)
     if brick == "ring":
         assert k == 3 and stride == 1 and x.dtype == torch.bfloat16
-        ns = query("u3d_conv_wgrad_ring_splits", n, cin, d, h, w_, cout)
+        if WGRAD_QUEUE or COLLECTIVE_IN_FLIGHT[0]:  # short ranges the dispatcher deals to whichever CU is free
+            ns = query("u3d_conv_wgrad_ring_splits_target", n, cin, d, h, w_, cout, WGRAD_Q_WGS)
+        else:
+            ns = query("u3d_conv_wgrad_ring_splits", n, cin, d, h, w_, cout)
         part = torch.empty((ns, 27, round32(cout), round32(cin)), dtype=torch.float32, device=x.device)
         call("u3d_conv_wgrad_ring", dy.data_ptr(), x.data_ptr(), n, cin, d, h, w_, cout, _ptr(st), _ptr(ga), _ptr(be),
              G, part.data_ptr(), ns, _stream())

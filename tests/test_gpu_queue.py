@@ -1,0 +1,48 @@
+"""Concurrency-robust launch forms used while a data-parallel all-reduce may hold CUs (u3d.ddp sets
+ops.COLLECTIVE_IN_FLIGHT): the stride-1 weight-gradient ring on short plane ranges (~3x the CUs in splits, dealt by
+the hardware dispatcher to whichever CU is free). Each split still owns a fixed contiguous range and its own fp32
+slab, so the summed gradient is deterministic (bitwise equal run to run) and equals the one-range-per-CU form up to
+fp32 reassociation. Reference: the autograd of F.conv3d in Conv3d.forward (unet3D.py:27) while
+train_amos_atlas_final.py:375's DDP all-reduce runs."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # n, cin, cout, size, gn
+    (2, 32, 32, 48, True),
+    (2, 64, 64, 24, False),
+    (1, 32, 64, 20, True),
+]
+
+
+def _operands(gpu, n, cin, cout, s, gn):
+    torch.manual_seed(3)
+    x = (torch.randn((n, s, s, s, cin), device=gpu) * 0.7 + 0.1).to(torch.bfloat16)
+    dy = (torch.randn((n, s, s, s, cout), device=gpu) * 0.3).to(torch.bfloat16)
+    g = None
+    if gn:
+        from u3d import ops
+        g = (ops.gn_stats(x, 16), 1 + 0.1 * torch.randn(cin, device=gpu), 0.1 * torch.randn(cin, device=gpu), 16)
+    return x, dy, g
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"n{c[0]}_{c[1]}to{c[2]}_{c[3]}{'_gn' if c[4] else ''}")
+def test_wgrad_ring_short_ranges_match(gpu, case):
+    from u3d import ops
+    x, dy, g = _operands(gpu, *case)
+    assert not ops.WGRAD_QUEUE
+    pa, na = ops.conv_wgrad(dy, x, 3, 1, g)
+    try:
+        ops.WGRAD_QUEUE = True
+        pb, nb = ops.conv_wgrad(dy, x, 3, 1, g)
+        pc, nc = ops.conv_wgrad(dy, x, 3, 1, g)
+    finally:
+        ops.WGRAD_QUEUE = False
+    torch.cuda.synchronize()
+    assert nb > na and nb == nc, (na, nb)
+    assert torch.equal(pb, pc)  # fixed ranges, fixed slabs: deterministic
+    a, b = pa.double().sum(0), pb.double().sum(0)
+    err = ((a - b).norm() / a.norm()).item()
+    assert err < 1e-6, err

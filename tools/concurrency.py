@@ -38,6 +38,19 @@ def main():
         x2 = (torch.randn((n, s2, s2, s2, c2), device=dev) * 0.5).to(bf)
         _, pd2, _ = ops.wstd_fwd(torch.randn(c2, c2, 3, 3, 3, device=dev), bf, True)
         cases[f"dgrad{s2}"] = (lambda x2=x2, pd2=pd2, s2=s2, c2=c2: ops.conv_dgrad(x2, pd2, c2, (n, s2, s2, s2), 3, 1))
+    # conv_small data gradient at 12^3 x 256, the stride-2 data gradients 96^3 -> 48^3 and 48^3 -> 24^3, and the
+    # stride-1 weight-gradient rings at 96^3 and 48^3 (queue mode: short ranges, u3d.ops.WGRAD_QUEUE)
+    x12 = (torch.randn((n, 12, 12, 12, 256), device=dev) * 0.5).to(bf)
+    _, pd12, _ = ops.wstd_fwd(torch.randn(256, 256, 3, 3, 3, device=dev), bf, True)
+    cases["dgrad12"] = lambda: ops.conv_dgrad(x12, pd12, 256, (n, 12, 12, 12), 3, 1)
+    for s3, ci, co in ((96, 32, 64), (48, 64, 128)):
+        dy3 = (torch.randn((n, s3 // 2, s3 // 2, s3 // 2, co), device=dev) * 0.5).to(bf)
+        _, pd3, _ = ops.wstd_fwd(torch.randn(co, ci, 3, 3, 3, device=dev), bf, True)
+        cases[f"dgrad_s2_{s3}"] = (lambda dy3=dy3, pd3=pd3, ci=ci, s3=s3: ops.conv_dgrad(dy3, pd3, ci, (n, s3, s3, s3), 3, 2))
+    dyw = (torch.randn((n, s, s, s, 32), device=dev) * 0.5).to(bf)
+    cases["wgrad96"] = lambda: ops.conv_wgrad(dyw, x, 3, 1, gn)
+    x48 = (torch.randn((n, 48, 48, 48, 64), device=dev) * 0.5).to(bf)
+    cases["wgrad48"] = lambda: ops.conv_wgrad(x48, x48, 3, 1, None)
 
     def timed(fn, reps=10):
         for _ in range(3):
@@ -75,13 +88,13 @@ def main():
     res = {"occupy_us_per_8wg_200k": round(t_occ, 1), "occupy_iters": iters, "cases": {}}
     for name, fn in cases.items():
         for mode in ("static", "queue"):
-            ops.RING_QUEUE = ops.PBRICK_QUEUE = mode == "queue"
+            ops.RING_QUEUE = ops.PBRICK_QUEUE = ops.WGRAD_QUEUE = mode == "queue"
             row = {"alone_us": round(timed(fn), 1)}
             for k in ks:
                 row[f"with_{k}_cus_held_us"] = round(with_hog(fn, k), 1)
             res["cases"][f"{name}_{mode}"] = row
             print(name, mode, row, file=sys.stderr, flush=True)
-    ops.RING_QUEUE = ops.PBRICK_QUEUE = False
+    ops.RING_QUEUE = ops.PBRICK_QUEUE = ops.WGRAD_QUEUE = False
     print(json.dumps(res))
 
 
