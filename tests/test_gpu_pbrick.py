@@ -113,7 +113,7 @@ def test_persistent_brick_queue_bitwise_equal_static(gpu, case):
     the counters are left zero for the next launch (three launches in a row reuse them)."""
     from u3d import _lib, ops
     n, cin, cout, dims, gn, res, flip = case
-    ref = _run(gpu, *case, persist=True)
+    ref = _run(gpu, n, cin, cout, dims, gn, False, flip, persist=True)  # (the queue form takes no residual)
     torch.manual_seed(7)
     x = (torch.randn((n,) + dims + (cin,), device=gpu) * 1.3 + 0.2).to(torch.bfloat16)
     cin_p, cout_p = -(-cin // 32) * 32, -(-cout // 32) * 32
