@@ -19,10 +19,6 @@
 
 #include "common.h"
 
-#ifndef U3D_RING_PF
-#define U3D_RING_PF 2
-#endif
-
 namespace u3d {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -110,9 +106,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float* __restrict__ spart,
                                                               RGGeom g, int* __restrict__ queue = nullptr) {
-  // staging loads issued PF steps before their plane is written to LDS (2: two planes of loads in flight per
-  // workgroup; the work-stealing walk keeps 1)
-  constexpr int PF = Q ? 1 : U3D_RING_PF;
   __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024 + 512];
   char* const ring = smem;
   char* const wts = smem + 4 * RG_SS;
@@ -408,8 +401,8 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
 
   // step s: load plane s+1 into registers, write plane s (loaded during step s-1) into slot s&3, compute the
   // output whose triple ends at plane s-1, barrier. Unrolled by two so the register sets swap statically.
-  u32x4 va[RG_LD], vb[RG_LD], vc[RG_LD];
-  unsigned ma = 0, mb = 0, mc = 0;
+  u32x4 va[RG_LD], vb[RG_LD];
+  unsigned ma = 0, mb = 0;
   auto set_range = [&](long long o0, long long o1) {
     walk.o_next = o0;
     walk.o_end = o1;
@@ -487,11 +480,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   };
   RGPlane pw = next_plane();  // plane 0
   load_plane(pw, va, ma);
-  RGPlane pn{};               // PF = 2: plane s+1, its loads in flight
-  if constexpr (PF == 2) {
-    pn = next_plane();
-    load_plane(pn, vb, mb);
-  }
   __syncthreads();            // weights visible
   RGPlane pc{};               // plane s-1 (compute)
   int s = 0;
@@ -525,7 +513,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
     gn_table(pw);
     const int slot = s & 3;
-    const RGPlane pl = next_plane();  // plane s+PF
+    const RGPlane pl = next_plane();  // plane s+1
     // side work of the step, k = 0 .. 2 RG_LD - 1: even k writes staged piece k/2 of plane s into slot s & 3 (its
     // loads were issued a full step ago), odd k issues the load of piece k/2 of plane s + 1
     auto side = [&](auto kc) __attribute__((always_inline)) {
@@ -545,28 +533,13 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
     if constexpr ((EXP & 1) == 0) __syncthreads();
     pc = pw;
-    if constexpr (PF == 2) {
-      pw = pn;
-      pn = pl;
-    } else {
-      pw = pl;
-    }
+    pw = pl;
     ++s;
   };
-  if constexpr (PF == 2) {  // three register sets: plane s is written from the set its loads (step s-2) filled
-    while (pw.valid || (pc.valid && pc.out)) {
-      step(va, ma, vc, mc);
-      if (!(pw.valid || (pc.valid && pc.out))) break;
-      step(vb, mb, va, ma);
-      if (!(pw.valid || (pc.valid && pc.out))) break;
-      step(vc, mc, vb, mb);
-    }
-  } else {
-    while (pw.valid || (pc.valid && pc.out)) {
-      step(va, ma, vb, mb);
-      if (!(pw.valid || (pc.valid && pc.out))) break;
-      step(vb, mb, va, ma);
-    }
+  while (pw.valid || (pc.valid && pc.out)) {
+    step(va, ma, vb, mb);
+    if (!(pw.valid || (pc.valid && pc.out))) break;
+    step(vb, mb, va, ma);
   }
   epilogue(pend);  // the last computed plane (ok = false if none)
   if constexpr (Q) {
@@ -713,7 +686,7 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
   if (flip) RG_KR(true, false, false, 27);
   else if (gn_stats && residual) RG_KR(false, true, true, 12);  // + the statistics accumulators: 12 steps
   else if (gn_stats) RG_KR(false, true, false, 16);  // (12 measured equal: 124.6 vs 124.8 us)
-  else if (residual) RG_KR(false, false, true, 20);  // 27 spills with the third staging register set
+  else if (residual) RG_KR(false, false, true, 27);
   else RG_KR(false, false, false, 27);
 #undef RG_KR
 #undef RG_LAUNCH

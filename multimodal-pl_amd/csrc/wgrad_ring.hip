@@ -18,10 +18,6 @@
 
 #include "common.h"
 
-#ifndef U3D_RING_PF
-#define U3D_RING_PF 2
-#endif
-
 namespace u3d {
 namespace {
 
@@ -251,17 +247,10 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     });
   };
 
-  // staging loads are issued PF planes before the plane is written to LDS (2: two planes of loads in flight)
-  constexpr int PF = U3D_RING_PF;
-  u32x4 xa[WR_LX], xb[WR_LX], xc[WR_LX], ya[WR_LY], yb[WR_LY], yc[WR_LY];
-  unsigned ma = 0, mb = 0, mc3 = 0;
+  u32x4 xa[WR_LX], xb[WR_LX], ya[WR_LY], yb[WR_LY];
+  unsigned ma = 0, mb = 0;
   WRPlane pw = walk.next(g);
   load_plane(pw, xa, ya, ma);
-  WRPlane pn{};  // PF = 2: plane s+1, loads in flight
-  if constexpr (PF == 2) {
-    pn = walk.next(g);
-    load_plane(pn, xb, yb, mb);
-  }
   WRPlane pc{};
   int s = 0;
   auto step = [&](u32x4 (&cx)[WR_LX], u32x4 (&cy)[WR_LY], unsigned& mc, u32x4 (&nx)[WR_LX], u32x4 (&ny)[WR_LY],
@@ -277,28 +266,13 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     }
     __syncthreads();
     pc = pw;
-    if constexpr (PF == 2) {
-      pw = pn;
-      pn = pl;
-    } else {
-      pw = pl;
-    }
+    pw = pl;
     ++s;
   };
-  if constexpr (PF == 2) {  // three register sets: plane s is written from the set its loads (step s-2) filled
-    while (pw.valid || (pc.valid && pc.out)) {
-      step(xa, ya, ma, xc, yc, mc3);
-      if (!(pw.valid || (pc.valid && pc.out))) break;
-      step(xb, yb, mb, xa, ya, ma);
-      if (!(pw.valid || (pc.valid && pc.out))) break;
-      step(xc, yc, mc3, xb, yb, mb);
-    }
-  } else {
-    while (pw.valid || (pc.valid && pc.out)) {
-      step(xa, ya, ma, xb, yb, mb);
-      if (!(pw.valid || (pc.valid && pc.out))) break;
-      step(xb, yb, mb, xa, ya, ma);
-    }
+  while (pw.valid || (pc.valid && pc.out)) {
+    step(xa, ya, ma, xb, yb, mb);
+    if (!(pw.valid || (pc.valid && pc.out))) break;
+    step(xb, yb, mb, xa, ya, ma);
   }
   // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h. Buffer stores with 32-bit
   // offsets computed here (the host keeps the slabs below 2 GiB): no 64-bit addresses held across the walk.
