@@ -206,17 +206,6 @@ int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, int h, int w
                     const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                     const void* residual, void* y, u3d_stream_t stream);
 
-/* u3d_convg_brick data gradient (flip = 1) with a work queue instead of the static unit ranges: every (brick, co
- * tile) unit is claimed with an atomic add on one of 8 per-XCD counters (an XCD's workgroups take its own range first,
- * then steal), so a workgroup that starts late because a concurrent kernel (the data-parallel all-reduce) holds its CU
- * finds its units taken by the others. Bitwise the same dx as u3d_convg_brick. queue = u3d_convg_brick_queue_bytes()
- * bytes of caller-owned device memory, zero on entry and left zero. Replaces the same op as u3d_convg_brick (the data
- * gradient of F.conv3d, unet3D.py:27) while train_amos_atlas_final.py:375's DDP all-reduce is in flight. */
-int u3d_convg_brick_queue_bytes(void);
-int u3d_convg_brick_q(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
-                      const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                      const void* residual, void* y, int* queue, u3d_stream_t stream);
-
 /* u3d_convg_brick forward (flip = 0) that also returns the GroupNorm(16) statistics [n][16][2] (mean, rstd) of its
  * output (after the residual add, of the stored bf16 values) — the input of the next GroupNorm in NoBottleneck
  * (unet3D.py:44-53) — from per-unit channel-pair partials accumulated in the persistent kernel's epilogue

@@ -286,24 +286,13 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
 // epilogue is register-only (permlane32 swap, residual add, two 16-B stores per lane and co block) and never
 // touches the LDS the next unit's halo is being written into. Same operands, same fp32 accumulation order per
 // output (chunk, tap plane, tap, k-half) as convg_brick_kernel: bitwise-equal results.
-//
-// Q (work queue, round 3): the units of the workgroups an XCD runs form that XCD's range; each workgroup starts on
-// unit (range start + its index on the XCD) and claims every further unit with one atomic add on its XCD's counter
-// (issued by one lane at the start of a unit, fire and forget; the verdict is published through LDS before the
-// barrier that precedes the unit's last step, where the next unit's staging starts). A workgroup whose range is
-// exhausted steals from the other XCDs' ranges (wave 0 reads the 8 counters in one load round). A workgroup that
-// starts late (its CU held by a concurrent kernel, e.g. RCCL's all-reduce in the data-parallel backward) finds the
-// others have taken its units instead of setting the launch's tail. Results are bitwise those of the static walk:
-// each unit's outputs and GroupNorm partials (slot = unit) do not depend on which workgroup ran it. The counters are
-// left zero: the last workgroup to exit resets them.
-template <int CO, bool FLIP, int BWX = 16, bool Q = false>
+template <int CO, bool FLIP, int BWX = 16>
 __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                                bf16* __restrict__ y, const bf16* __restrict__ res,
                                                                const float* __restrict__ gstat,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta, GBGeom g, int per,
-                                                               int nunits, float* __restrict__ spart = nullptr,
-                                                               int* __restrict__ queue = nullptr) {
+                                                               int nunits, float* __restrict__ spart = nullptr) {
   constexpr int TN = CO / 32;
   constexpr int WROWS = 9 * CO;
   constexpr int WLD = (WROWS * 4 + GB_NT - 1) / GB_NT;
@@ -327,7 +316,6 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   __shared__ __attribute__((aligned(16))) f32x2 gtab[2][GB_MAXC];
   // output GroupNorm statistics (spart != nullptr): per (wave, lane half, tn, run v, channel pair q) (sum, sum sq)
   __shared__ f32x2 sst[8][2][TN * 2 * 4];
-  __shared__ int qsl[2];  // Q: the next unit's claim verdict, the stolen unit
 
   // the data gradient never takes a residual or output statistics (convg_impl): dead at compile time, so its
   // epilogue's registers are not reserved
@@ -337,29 +325,12 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int nwg = gridDim.x, xq = nwg >> 3, xr = nwg & 7, xcd = blockIdx.x & 7, xloc = blockIdx.x >> 3;
-  auto xwg0 = [&](int xc) { return xc < xr ? xc * (xq + 1) : xr * (xq + 1) + (xc - xr) * xq; };  // first bid of XCD xc
-  const int bid = xwg0(xcd) + xloc;
+  int bid;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
   const int u_begin = bid * per, u_end = min(nunits, u_begin + per);
-  // Q: XCD xc's range [xlo, xhi) of units (those of its workgroups' static ranges); claim c -> unit xlo + c
-  auto xlo = [&](int xc) { return min(nunits, xwg0(xc) * per); };
-  auto xhi = [&](int xc) { return min(nunits, xwg0(xc + 1) * per); };
-  auto claim_unit = [&](int xc, int c) { const int u = xlo(xc) + c; return u < xhi(xc) ? u : -1; };
-  // wave 0 (all lanes): claim a unit from any XCD's range (own first), -1 when every range is exhausted
-  auto steal = [&]() -> int {
-    for (;;) {
-      const int xc = (xcd + lane) & 7;
-      bool cand = false;
-      if (lane < 8) cand = claim_unit(xc, __hip_atomic_load(&queue[xc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= 0;
-      const unsigned long long m = __ballot(cand);
-      if (!m) return -1;
-      const int xs = (xcd + __builtin_ctzll(m)) & 7;
-      int got = -1;
-      if (lane == 0) got = claim_unit(xs, atomicAdd(&queue[xs], 1));
-      got = __shfl(got, 0);
-      if (got >= 0) return got;  // else lost a race for the last unit of xs: rescan
-    }
-  };
   const int nct = g.nct;
   const bool has_gn = gstat != nullptr;
   const bool pro_gn = !FLIP && has_gn;             // GN + ReLU prologue on the staged input (forward only)
@@ -386,12 +357,12 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   unsigned hmask = 0;  // bit i: staged piece i is inside the volume (GroupNorm'd; padding stays zero)
   u32x4 wpre[WLD];
   const int sch = tid & 3, srow0 = tid >> 2;
-  int stg_slot = 0, stg_c = 0;  // GN table slot and chunk of the staged halo (lookup at commit)
+  int stg_nn = 0, stg_c = 0;  // sample and chunk of the staged halo (GN table lookup at commit)
   // (buffer loads: 32-bit offsets from scalar bases, no per-lane 64-bit addresses held across the unit loop)
   const auto srs = __builtin_amdgcn_make_buffer_rsrc((void*)gstat, 0, has_gn ? 0x7FFFFFFF : 0, 0x00020000);
   const auto grs = __builtin_amdgcn_make_buffer_rsrc((void*)gamma, 0, has_gn ? 0x7FFFFFFF : 0, 0x00020000);
   const auto brs = __builtin_amdgcn_make_buffer_rsrc((void*)beta, 0, has_gn ? 0x7FFFFFFF : 0, 0x00020000);
-  auto gtab_fill = [&](int nn, int slot) {
+  auto gtab_fill = [&](int nn) {
     if (has_gn && tid < gtc_p) {
       int t = tid;
       asm volatile("" : "+v"(t));  // recompute channel and group here (once per sample), not held across the loop
@@ -400,7 +371,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       const float mean = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, so, 0, 0));
       const float rstd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, so + 4, 0, 0));
       const float sc_ = rstd * __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, c * 4, 0, 0));
-      gtab[slot][tid] = f32x2{sc_, __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, c * 4, 0, 0)) - mean * sc_};
+      gtab[nn & 1][tid] = f32x2{sc_, __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, c * 4, 0, 0)) - mean * sc_};
     }
   };
   // buffer loads with 32-bit offsets (the host guarantees x, y / the residual and the weight pack below 2 GiB): the
@@ -413,9 +384,9 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, ybytes, 0x00020000);
   const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)spart, 0, spart ? 0x7FFFFFFF : 0, 0x00020000);
   typedef __attribute__((ext_vector_type(2))) uint32_t v2u32;
-  auto halo_load = [&](const Unit& q, int c, int slot) {
+  auto halo_load = [&](const Unit& q, int c) {
     hmask = 0;
-    stg_slot = slot;
+    stg_nn = q.nn;
     stg_c = c;
     const int cc = c * 32 + sch * 8;
 #pragma unroll
@@ -434,7 +405,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   auto halo_commit = [&]() {
     f32x2 sc[4], sh[4];
     if (pro_gn) {
-      const f32x2* t = &gtab[stg_slot][stg_c * 32 + sch * 8];
+      const f32x2* t = &gtab[stg_nn & 1][stg_c * 32 + sch * 8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const f32x2 a0 = t[2 * e], a1 = t[2 * e + 1];
@@ -486,52 +457,22 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     arow[tm] = (vd * HH + vh) * HW + vw;
   }
 
-  int ucur = u_begin;
-  if constexpr (Q) {  // every unit is claimed, the first one too: a workgroup that starts late finds its work taken
-    if (tid == 0) qsl[0] = claim_unit(xcd, atomicAdd(&queue[xcd], 1));
-    __syncthreads();
-    ucur = __builtin_amdgcn_readfirstlane(qsl[0]);
-    if (ucur < 0) {
-      if (wave == 0) {
-        const int st_ = steal();
-        if (lane == 0) qsl[1] = st_;
-      }
-      __syncthreads();
-      ucur = __builtin_amdgcn_readfirstlane(qsl[1]);
-    }
-    if (ucur < 0) {  // nothing left: count the exit (the claims above have returned) and leave
-      if (tid == 0 && atomicAdd(&queue[8], 1) == (int)gridDim.x - 1)
-        for (int i = 0; i < 9; ++i) atomicExch(&queue[i], 0);
-      return;
-    }
-  }
-  Unit cu = unit_geo(ucur);
-  int cslot = 0;  // GN table slot of the current unit's sample
-  gtab_fill(cu.nn, 0);
+  Unit cu = unit_geo(u_begin);
+  gtab_fill(cu.nn);
   __syncthreads();
-  halo_load(cu, 0, 0);
+  halo_load(cu, 0);
   w_load(cu.co0, 0);
   halo_commit();
   w_commit(0);
   __syncthreads();
   int par = 0;
 
-  for (;;) {
-    // static: the next unit is known now; Q: after the claim's verdict (start of the last step)
-    bool more = !Q && ucur + 1 < u_end;
-    int unext = Q ? -1 : ucur + 1;
-    Unit nu = more ? unit_geo(unext) : cu;
-    // the next unit's sample table goes to the other slot: that slot was last read before this unit's first barrier,
-    // and is first read at the commit in this unit's last step (>= 1 barrier later)
-    int nslot = cslot;
-    if (more && nu.nn != cu.nn) {
-      nslot = cslot ^ 1;
-      gtab_fill(nu.nn, nslot);
-    }
-    int claim_old = 0;
-    if constexpr (Q) {
-      if (tid == 0) claim_old = atomicAdd(&queue[xcd], 1);  // fire and forget: read before the barrier of step nsteps-2
-    }
+  for (int u = u_begin; u < u_end; ++u) {
+    const bool more = u + 1 < u_end;
+    const Unit nu = more ? unit_geo(u + 1) : cu;
+    // the next unit's sample table: its slot was last read before this unit's first barrier, and is first read at
+    // the commit in this unit's last step (>= 1 barrier later)
+    if (more && nu.nn != cu.nn) gtab_fill(nu.nn);
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
@@ -542,32 +483,11 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     for (int s = 0; s < nsteps; ++s) {
       const int td = s % 3;
       const bool last = s + 1 == nsteps;
-      if constexpr (Q) {
-        if (last) {  // the claim's verdict (published before the previous barrier); steal when the own range is done
-          unext = __builtin_amdgcn_readfirstlane(qsl[0]);
-          if (unext < 0) {
-            if (wave == 0) {
-              const int st_ = steal();
-              if (lane == 0) qsl[1] = st_;
-            }
-            __syncthreads();
-            unext = __builtin_amdgcn_readfirstlane(qsl[1]);
-          }
-          more = unext >= 0;
-          if (more) {
-            nu = unit_geo(unext);
-            if (nu.nn != cu.nn) {  // before the staging loads: this wait drains nothing but the table loads
-              nslot = cslot ^ 1;
-              gtab_fill(nu.nn, nslot);
-            }
-          }
-        }
-      }
       const bool next = !last || more;
       if (next) {  // one call site each (the next step is (u, s + 1) or (u + 1, 0))
         const Unit& lq = last ? nu : cu;
         w_load(lq.co0, last ? 0 : s + 1);
-        if (td == 2) halo_load(lq, last ? 0 : s / 3 + 1, last ? nslot : cslot);
+        if (td == 2) halo_load(lq, last ? 0 : s / 3 + 1);
       }
       const char* wb = wbuf[par];
       const int od = FLIP ? 2 - td : td;
@@ -604,9 +524,6 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
         });
       }
       if (last) break;  // the last step's staging commit runs after the residual loads are issued (below)
-      if constexpr (Q) {
-        if (s + 2 == nsteps && tid == 0) qsl[0] = claim_unit(xcd, claim_old);  // visible after this step's barrier
-      }
       w_commit(par ^ 1);  // the other buffer: its readers finished before the previous barrier
       if (td == 2) {
         __syncthreads();  // everyone done with this chunk's halo
@@ -726,19 +643,10 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
         const int c = 2 * tid, tn = c >> 5, w32 = c & 31, v = w32 >> 4, h_ = (w32 >> 3) & 1, q = (w32 & 7) >> 1;
         f32x2 t = {0.f, 0.f};
         for (int w = 0; w < 8; ++w) t += sst[w][h_][(tn * 2 + v) * 4 + q];
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, t), prs, (ucur * CO + c) * 4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, t), prs, (u * CO + c) * 4, 0, 0);
       }
     }
-    if (!more) break;
     cu = nu;
-    ucur = unext;
-    cslot = nslot;
-  }
-  if constexpr (Q) {
-    // every claim of this workgroup has been consumed (its verdict read), so the exit count orders after them
-    if (tid == 0 && atomicAdd(&queue[8], 1) == (int)gridDim.x - 1) {
-      for (int i = 0; i < 9; ++i) atomicExch(&queue[i], 0);
-    }
   }
 }
 
@@ -789,8 +697,7 @@ static int convg_num_cus() {
 
 static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                       const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                      const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream,
-                      int* queue = nullptr) {
+                      const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && n <= GB_MAXN, "convg_brick: bad args");
   U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "convg_brick: channels must be multiples of 8");
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "convg_brick: bad GN");
@@ -820,10 +727,6 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
   // (a data gradient with a residual add — not a trunk routing, kept for the ABI — runs the one-shot kernel: the
   // persistent data gradient has no residual path, so its epilogue reserves no registers for one)
   const bool pers = pers_on && small && (!gn_stats || g.cin_p <= GB_MAXC) && !(flip && residual);
-  // (the queue serves the data gradient: the backward is where a data-parallel all-reduce runs beside the convs; the
-  // one-shot kernel, used when the persistent one cannot be, needs none: it is not persistent)
-  U3D_REQUIRE(!queue || flip, "convg_brick_q: the work queue is the data gradient's");
-  if (!pers) queue = nullptr;
   U3D_REQUIRE(!spart || (pers && !flip && cout % 32 == 0), "convg_brick_stats: needs the persistent forward, cout %% 32 == 0");
   if (pers) {
     // 8-wide bricks where the plane width is a multiple of 8 but not of 16 (24^3: the 16-wide bricks' second
@@ -842,26 +745,23 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
     }
     const int nunits = n * gp.nbd * gp.nbh * gp.nbw * gp.nct, per = cdiv(nunits, convg_num_cus()),
               nwg = cdiv(nunits, per);
-#define U3D_PB2(C, F, B, QQ)                                                                                       \
-  hipLaunchKernelGGL((convg_pbrick_kernel<C, F, B, QQ>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,             \
-                     (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per, nunits, \
-                     spart, queue)
-#define U3D_PB(C, F, QQ)                             \
-  do {                                               \
-    if (bw8) U3D_PB2(C, F, 8, QQ);                   \
-    else U3D_PB2(C, F, 16, QQ);                      \
+#define U3D_PB(C, F)                                                                                               \
+  do {                                                                                                             \
+    if (bw8)                                                                                                       \
+      hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 8>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,          \
+                         (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
+                         nunits, spart);                                                                           \
+    else                                                                                                           \
+      hipLaunchKernelGGL((convg_pbrick_kernel<C, F>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,                \
+                         (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
+                         nunits, spart);                                                                           \
   } while (0)
     if (co64) {
-      if (flip && queue) U3D_PB(64, true, true);
-      else if (flip) U3D_PB(64, true, false);
-      else U3D_PB(64, false, false);
+      if (flip) U3D_PB(64, true); else U3D_PB(64, false);
     } else {
-      if (flip && queue) U3D_PB(32, true, true);
-      else if (flip) U3D_PB(32, true, false);
-      else U3D_PB(32, false, false);
+      if (flip) U3D_PB(32, true); else U3D_PB(32, false);
     }
 #undef U3D_PB
-#undef U3D_PB2
     int rc = check_launch("convg_pbrick_kernel");
     if (rc) return rc;
     if (!spart) return rc;
@@ -907,14 +807,4 @@ extern "C" int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h
   U3D_REQUIRE(ws_floats >= u3d_convg_brick_stats_ws_floats(n, d, h, w, cout), "convg_brick_stats: workspace too small");
   return convg_impl(0, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
                     stats_out, stream);
-}
-
-extern "C" int u3d_convg_brick_queue_bytes(void) { return 9 * 4; }
-
-extern "C" int u3d_convg_brick_q(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
-                                 const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                                 const void* residual, void* y, int* queue, u3d_stream_t stream) {
-  U3D_REQUIRE(queue, "convg_brick_q: null queue");
-  return convg_impl(flip, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, nullptr,
-                    nullptr, stream, queue);
 }

@@ -51,8 +51,6 @@ _SIGS = {
     "u3d_conv_wgrad_ring_splits_target": [I, I, I, I, I, I, I],
     "u3d_conv_wgrad_ring": [P, P, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_convg_brick": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P],
-    "u3d_convg_brick_queue_bytes": [],
-    "u3d_convg_brick_q": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, P],
     "u3d_convg_brick_stats_ws_floats": [I, I, I, I, I],
     "u3d_convg_brick_stats": [P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P, P],
     "u3d_conv_wgrad_brick_splits": [I, I, I, I, I, I, I],

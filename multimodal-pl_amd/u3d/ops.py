@@ -318,17 +318,6 @@ def _queue(device, shape):
     return WS.get(query("u3d_conv32_ring_q_queue_bytes", *shape), device, slot=QUEUE_SLOT).data_ptr()
 
 
-# persistent brick data gradient on its work queue (u3d_convg_brick_q): while a collective may be in flight, or always
-# with U3D_PBRICK_QUEUE=1
-PBRICK_QUEUE = os.environ.get("U3D_PBRICK_QUEUE", "0") != "0"
-SMALL_Q_WGS = 768  # conv_small data-gradient workgroups aimed at while a collective may hold CUs
-PBRICK_QUEUE_SLOT = 41  # workspace slot of its counters (zero between launches; nothing else uses it)
-
-
-def _pbrick_queue(device):
-    return WS.get(query("u3d_convg_brick_queue_bytes"), device, slot=PBRICK_QUEUE_SLOT).data_ptr()
-
-
 BRICK_STATS = os.environ.get("U3D_BRICK_STATS", "1") != "0"  # GN statistics from the persistent brick's epilogue
 RING_STATS = os.environ.get("U3D_RING_STATS", "1") != "0"  # GroupNorm statistics from the ring conv epilogue (False: separate u3d_gn_stats pass)
 SPLITK_WS_BYTES = 64 << 20
@@ -394,20 +383,12 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
         return dx
     if _use_small(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
         ws = WS.get(SPLITK_WS_BYTES, dy.device, slot=4)
-        # while a collective may hold CUs: ~3x the CUs in (tile, contraction split) workgroups, dealt by the
-        # dispatcher to free CUs (each split keeps its own slab and the fixed-order reduce: same dx every run)
-        with (option("SMALL_WGS", SMALL_Q_WGS) if (PBRICK_QUEUE or COLLECTIVE_IN_FLIGHT[0]) else
-              contextlib.nullcontext()):
-            call("u3d_conv_small", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None,
-                 0, None, dx.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        call("u3d_conv_small", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None, 0,
+             None, dx.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         return dx
     if _use_gen_brick(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
-        if PBRICK_QUEUE or COLLECTIVE_IN_FLIGHT[0]:
-            call("u3d_convg_brick_q", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None,
-                 0, None, dx.data_ptr(), _pbrick_queue(dy.device), _stream())
-        else:
-            call("u3d_convg_brick", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None,
-                 0, None, dx.data_ptr(), _stream())
+        call("u3d_convg_brick", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None, 0,
+             None, dx.data_ptr(), _stream())
         return dx
     ws = WS.get(SPLITK_WS_BYTES, dy.device, slot=4)
     call("u3d_conv_dgrad", dt_code(dy.dtype), dy.data_ptr(), n, cout, wpk_dgrad.data_ptr(), cin, d, h, w_, k, stride,

@@ -101,33 +101,3 @@ def test_persistent_brick_epilogue_gn_stats(gpu, case):
 
 BG_CASES = [(2, 64, 64, (48, 48, 48)), (2, 128, 128, (24, 24, 24)), (2, 64, 96, (16, 23, 40)), (4, 96, 64, (12, 24, 19))]
 
-
-QUEUE_CASES = [c for c in CASES if c[6]] + [(2, 64, 32, (48, 48, 48), False, False, True),
-                                           (1, 64, 64, (4, 8, 16), False, False, True)]  # one unit only
-
-
-@pytest.mark.parametrize("case", QUEUE_CASES, ids=lambda c: f"n{c[0]}_{c[1]}to{c[2]}_{'x'.join(map(str, c[3]))}")
-def test_persistent_brick_queue_bitwise_equal_static(gpu, case):
-    """u3d_convg_brick_q (the data gradient on per-XCD claim counters, used while a data-parallel all-reduce may hold
-    CUs) against the static walk: the same units, each computed by whichever workgroup claimed it — bitwise equal dx;
-    the counters are left zero for the next launch (three launches in a row reuse them)."""
-    from u3d import _lib, ops
-    n, cin, cout, dims, gn, res, flip = case
-    ref = _run(gpu, n, cin, cout, dims, gn, False, flip, persist=True)  # (the queue form takes no residual)
-    torch.manual_seed(7)
-    x = (torch.randn((n,) + dims + (cin,), device=gpu) * 1.3 + 0.2).to(torch.bfloat16)
-    cin_p, cout_p = -(-cin // 32) * 32, -(-cout // 32) * 32
-    wpk = torch.zeros((27, cout_p, cin_p), device=gpu, dtype=torch.bfloat16)
-    wpk[:, :cout, :cin] = (torch.randn((27, cout, cin), device=gpu) * 0.05).to(torch.bfloat16)
-    q = torch.zeros(_lib.lib().u3d_convg_brick_queue_bytes() // 4, dtype=torch.int32, device=gpu)
-    for _ in range(3):
-        y = torch.full((n,) + dims + (cout,), 7.0, device=gpu, dtype=torch.bfloat16)
-        with ops.option("CONVG_PERSIST", 1):
-            rc = _lib.lib().u3d_convg_brick_q(1, x.data_ptr(), n, cin, *dims, wpk.data_ptr(), cout, None, None, None,
-                                              0, None, y.data_ptr(), q.data_ptr(),
-                                              torch.cuda.current_stream().cuda_stream)
-            assert rc == 0, _lib.lib().u3d_last_error()
-        torch.cuda.synchronize()
-        assert torch.equal(y.view(torch.int16), ref.view(torch.int16)), \
-            f"max diff {(y.float() - ref.float()).abs().max().item()}"
-        assert int(q.abs().sum().item()) == 0, q.tolist()

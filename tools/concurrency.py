@@ -88,13 +88,13 @@ def main():
     res = {"occupy_us_per_8wg_200k": round(t_occ, 1), "occupy_iters": iters, "cases": {}}
     for name, fn in cases.items():
         for mode in ("static", "queue"):
-            ops.RING_QUEUE = ops.PBRICK_QUEUE = ops.WGRAD_QUEUE = mode == "queue"
+            ops.RING_QUEUE = ops.WGRAD_QUEUE = mode == "queue"
             row = {"alone_us": round(timed(fn), 1)}
             for k in ks:
                 row[f"with_{k}_cus_held_us"] = round(with_hog(fn, k), 1)
             res["cases"][f"{name}_{mode}"] = row
             print(name, mode, row, file=sys.stderr, flush=True)
-    ops.RING_QUEUE = ops.PBRICK_QUEUE = ops.WGRAD_QUEUE = False
+    ops.RING_QUEUE = ops.WGRAD_QUEUE = False
     print(json.dumps(res))
 
 
