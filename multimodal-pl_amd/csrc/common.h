@@ -41,7 +41,6 @@ enum Opt : int {
   OPT_WR_WGS,         // weight-gradient ring workgroups aimed at
   OPT_RING_EXP,       // ring conv timing ablations (only in a -DU3D_RING_EXP diagnostic build; 0 = off)
   OPT_WB_S2CO64,      // stride-2 brick weight gradient: two co tiles per workgroup (0: one)
-  OPT_WG_SLAB_KB,     // 3^3 weight gradients: cap on the fp32 split-K slab bytes per launch, KB (0: no cap)
   OPT_COUNT
 };
 int opt(Opt o);
@@ -218,9 +217,5 @@ __device__ __forceinline__ TileSplit xcd_tile_split() {
 
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 __host__ __device__ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
-
-// split count `ns` of a 3^3 weight gradient limited so that its fp32 slabs (ns x 27 x cout_p x cin_p) stay under the
-// OPT_WG_SLAB_KB cap (deep levels: 7 MB per 256 x 256 slab against a few hundred KB of operands)
-int wg_slab_cap(int ns, int cin, int cout);
 
 }  // namespace u3d

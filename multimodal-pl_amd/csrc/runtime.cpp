@@ -43,7 +43,6 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"CONVG_PERSIST", 1},  {"CONVG_BW8", -1},   {"RING_KR", -1},       {"RING_WGS", 256}, {"RING_SC", 0},
     {"SMALL_WGS", 256},    {"GN_MAXBLK", 256},  {"HEAD_TR", 1},        {"STEM1", 1},      {"UP_BWD_BLK", -1},
     {"WGRAD_BD", 3},       {"WB_WGS", 256},     {"WR_TILE16", 0},      {"WR_WGS", 256},     {"RING_EXP", 0}, {"WB_S2CO64", 1},
-    {"WG_SLAB_KB", 0},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
@@ -89,11 +88,3 @@ extern "C" int u3d_get_option(const char* name, int* value) {
 extern "C" const char* u3d_last_error(void) { return u3d::g_last_error.c_str(); }
 extern "C" int u3d_abi_version(void) { return 1; }
 
-namespace u3d {
-int wg_slab_cap(int ns, int cin, int cout) {
-  const long long cap = (long long)opt(OPT_WG_SLAB_KB) << 10;
-  const long long slab = 27LL * round_up(cout, 32) * round_up(cin, 32) * 4;
-  if (cap <= 0 || (long long)ns * slab <= cap) return ns;
-  return (int)std::max<long long>(1, cap / slab);
-}
-}  // namespace u3d

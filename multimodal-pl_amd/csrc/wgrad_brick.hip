@@ -406,7 +406,7 @@ extern "C" int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, 
   const long long tiles = (long long)cdiv(cin, 32) * (cdiv(cout, 32) / wb_nco(stride, cout));
   const long long target = std::max(1, opt(OPT_WB_WGS));  // workgroups aimed at
   long long want = std::max(1LL, target / tiles);
-  const long long ns = wg_slab_cap((int)std::max(1LL, std::min(want, nb)), cin, cout);
+  const long long ns = std::max(1LL, std::min(want, nb));
   const long long per = (nb + ns - 1) / ns;
   return (int)((nb + per - 1) / per);  // splits that all receive bricks: no zero-filled slabs
 }

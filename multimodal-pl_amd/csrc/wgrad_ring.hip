@@ -323,7 +323,7 @@ extern "C" int u3d_conv_wgrad_ring_splits_target(int n, int cin, int d, int h, i
   wr_geom(n, cin, d, h, w, cout, g);
   const long long tiles = (long long)(g.cin_p / 32) * (g.cout_p / 32);
   const long long target = std::max(1, wgs);  // workgroups aimed at
-  const long long want = wg_slab_cap((int)std::max(1LL, std::min(g.planes, target / tiles)), cin, cout);
+  const long long want = std::max(1LL, std::min(g.planes, target / tiles));
   const long long per = (g.planes + want - 1) / want;
   return (int)((g.planes + per - 1) / per);  // every split receives planes: no zero-filled slabs
 }

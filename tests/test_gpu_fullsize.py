@@ -351,9 +351,21 @@ def test_conv32_beyond_2gib_routes_off_the_ring(gpu):
         got = y[0, z, :63, :63].double().cpu()
         assert (got - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
     del y
-    dy = torch.randn_like(x)
-    part, ns = ops.conv_wgrad(dy[:, :, :, :, :32], x, 3, 1)
+    # weight gradient through the brick path on the same > 2 GiB operands: dy is zero outside one 4 x 64 x 64 block
+    # placed past the 2 GiB offset, so the exact dW is the fp64 weight gradient of that block and its input halo
+    z0, h0, w0 = d - 6, 440, 440
+    assert ((z0 * h + h0) * w + w0) * 32 * 2 >= (1 << 31)
+    dy = torch.zeros_like(x)
+    dy[0, z0:z0 + 4, h0:h0 + 64, w0:w0 + 64] = torch.randn((4, 64, 64, 32), device=gpu).to(torch.bfloat16)
+    part, ns = ops.conv_wgrad(dy, x, 3, 1)
     assert part.shape[1:] == (27, 32, 32) and torch.isfinite(part).all()
+    got = part.double().sum(0).cpu()  # [t][co][ci]
+    xs = x[0, z0 - 1:z0 + 5, h0 - 1:h0 + 65, w0 - 1:w0 + 65].double().cpu().permute(3, 0, 1, 2)[None]
+    gs = dy[0, z0:z0 + 4, h0:h0 + 64, w0:w0 + 64].double().cpu().permute(3, 0, 1, 2)[None]
+    ref = torch.nn.grad.conv3d_weight(xs, (32, 32, 3, 3, 3), gs)  # [co][ci][kd][kh][kw]
+    ref = ref.permute(2, 3, 4, 0, 1).reshape(27, 32, 32)
+    err = ((got - ref).norm() / ref.norm()).item()
+    assert err <= 1e-4, err
 
 
 # wgrad ring plane tiles 12 x 24 (24-wide planes) and 12 x 12 (12-wide): flattened k over the tile's voxels, partial
