@@ -42,19 +42,31 @@ __device__ __forceinline__ void sfor(F&& f) {
   }
 }
 
+#ifndef U3D_WRING_M16
+#define U3D_WRING_M16 1
+#endif
 constexpr int WR_ROWB = 64;
 constexpr int WR_NT = 512;
 // plane tile PH x PW (16 x 16; 12 x 24 for 24-wide planes and 12 x 12 for 12-wide ones, so that no k step is
 // spent on voxels past the volume): the k index of an output plane runs over its PH*PW voxels flattened (h, w), 16
 // per MFMA; each lane addresses its own voxel's (shifted) halo row, so any tile shape works.
-template <int PH, int PW>
+template <int PH, int PW, bool MM>
 struct WRT {
   static constexpr int HH = PH + 2, HW = PW + 2;
   static constexpr int NR = HH * HW;                 // halo rows per input plane (324 at 16 x 16)
   static constexpr int NV = PH * PW;                 // voxels per output plane (256 = 16 k16 steps)
   static constexpr int KS = NV / 16;
-  static constexpr int SLOT = NR * WR_ROWB;
-  static constexpr int DSLOT = NV * WR_ROWB;
+  // M16 (default where the plane tile holds whole 32-voxel k steps: 16 x 16, 12 x 24): v_mfma_f32_16x16x32_bf16, the
+  // same cycles per flop as 32x32x16 at a higher held clock (MI355X_MICROARCH.md, DVFS item 7). Its fragments are 16
+  // channels x 8 voxels, so the rows are stored half-planar: plane = 16 channels (32 B per row); the 8 consecutive
+  // rows a half-wave reads per ds_read_b64_tr_b16 are then 256 contiguous bytes (conflict-free), and the plane
+  // stride = 128 mod 256 B keeps the staging writes (two rows x two planes per 8-lane group) conflict-free too.
+  static constexpr bool M16 = MM;
+  static constexpr int RP = M16 ? 32 : WR_ROWB;                               // row pitch within a plane
+  static constexpr int HP = M16 ? (NR * 32 + 255) / 256 * 256 + 128 : 0;      // input half-plane stride
+  static constexpr int DHP = M16 ? (NV * 32 + 255) / 256 * 256 + 128 : 0;     // dy half-plane stride
+  static constexpr int SLOT = M16 ? 2 * HP : NR * WR_ROWB;
+  static constexpr int DSLOT = M16 ? 2 * DHP : NV * WR_ROWB;
   static constexpr int LX = (NR * 4 + WR_NT - 1) / WR_NT;  // input pieces per thread and plane
   static constexpr int LY = (NV * 4 + WR_NT - 1) / WR_NT;  // dy pieces
   static_assert(NV % 16 == 0, "k steps of 16 voxels");
@@ -113,7 +125,8 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, float* __restrict__ part,
                                                              WRGeom g) {
-  using T = WRT<PH, PW>;
+  // (the 12 x 24 tile without the GroupNorm prologue keeps 32x32x16: its 16x16x32 form spills)
+  using T = WRT<PH, PW, U3D_WRING_M16 != 0 && (PH * PW) % 32 == 0 && (GN || PW == 16)>;
   constexpr int WR_HW = T::HW, WR_NR = T::NR, WR_NV = T::NV, WR_SLOT = T::SLOT, WR_DSLOT = T::DSLOT, WR_LX = T::LX,
                 WR_LY = T::LY, WR_PW = PW;
   __shared__ __attribute__((aligned(16))) char lds[4 * WR_SLOT + 2 * WR_DSLOT + 1024];
@@ -175,7 +188,8 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
         val = gn_relu8(val, sc, sh);
         if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
       }
-      char* dst = row < WR_NR ? ring + slot * WR_SLOT + row * WR_ROWB + ch * 16 : junk + (tid & 63) * 16;
+      const int lo = T::M16 ? (ch >> 1) * T::HP + row * 32 + (ch & 1) * 16 : row * WR_ROWB + ch * 16;
+      char* dst = row < WR_NR ? ring + slot * WR_SLOT + lo : junk + (tid & 63) * 16;
       *reinterpret_cast<u32x4*>(dst) = val;
     }
     if (p.out) {
@@ -183,23 +197,28 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
       for (int i = 0; i < WR_LY; ++i) {
         const int v = (tid >> 2) + i * (WR_NT / 4);
         if (WR_NV % (WR_NT / 4) == 0 || v < WR_NV)
-          *reinterpret_cast<u32x4*>(dyr + dslot * WR_DSLOT + v * WR_ROWB + ch * 16) = vy[i];
+          *reinterpret_cast<u32x4*>(dyr + dslot * WR_DSLOT +
+                                    (T::M16 ? (ch >> 1) * T::DHP + v * 32 + (ch & 1) * 16 : v * WR_ROWB + ch * 16)) = vy[i];
       }
     }
   };
 
   constexpr int MAXT = 4;  // taps per wave: t = wave + 8j
-  f32x16 acc[MAXT];
+  f32x16 acc[MAXT];    // 32x32x16: D[co 32][ci 32] per tap
+  f32x4 acc4[MAXT][4];  // M16: [tap][co block cb * 2 + ci block cib] (16 x 16 each)
 #pragma unroll
-  for (int j = 0; j < MAXT; ++j)
+  for (int j = 0; j < MAXT; ++j) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc4[j][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   int tap_row[MAXT], tap_d[MAXT];
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
     const int t = min(wave + 8 * j, 26);
     tap_d[j] = t / 9;
-    tap_row[j] = (((t / 3) % 3) * WR_HW + t % 3) * WR_ROWB;
+    tap_row[j] = (((t / 3) % 3) * WR_HW + t % 3) * T::RP;
   }
   const int ntap = (27 - wave + 7) / 8;  // 4 for waves 0-2, 3 for 3-7
   // fragment lane geometry: group gq = lane>>4, in-group lane i = lane&15 -> (q = i>>2, p = i&3)
@@ -225,6 +244,50 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
 #pragma unroll
     for (int j = 0; j < NTP; ++j) tb[j] = ((s0 + tap_d[j]) & 3) * WR_SLOT + tap_row[j];
     const char* dbase = dyr + dslot * WR_DSLOT;
+    if constexpr (T::M16) {
+      // 32-voxel k steps; sub-step u = (k step u >> 1, ci block u & 1): per sub-step NTP x 2 MFMAs (taps x co blocks).
+      // A = dy^T (co rows), B = the tap's input rows (ci columns). Lane (group g4 = lane >> 4, q, pp) addresses voxel
+      // rows 4 g4 + q (m = 0) and 16 + 4 g4 + q (m = 1) of the k step — the K order of a weight gradient is free, and
+      // each half-wave's tr read then covers 8 consecutive voxels (never across a tile row for PW = 16, 24).
+      constexpr int KS2 = T::NV / 32;
+      const int g4 = lane >> 4;
+      const int v16[2] = {4 * g4 + q, 16 + 4 * g4 + q};
+      auto dyo = [&](int ks, int m, int cb) { return cb * T::DHP + (32 * ks + v16[m]) * 32 + 8 * pp; };
+      auto xo = [&](int ks, int m) {  // halo row of voxel 32 ks + v: 32 ks = a PW + b, one wrap at most (PW >= 16)
+        const int a = 32 * ks / WR_PW, b = 32 * ks % WR_PW, v = v16[m];
+        return (a * WR_HW + b + v + (v >= WR_PW - b ? 2 : 0)) * 32 + 8 * pp;
+      };
+      bf16x8 fa2[2][2], fb2[2][NTP];
+      auto rdA = [&](int ks) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          fa2[ks & 1][cb] = frag2(trd(dbase, dyo(ks, 0, cb)), trd(dbase, dyo(ks, 1, cb)));
+      };
+      auto rdB = [&](int u) {
+        const int x0 = xo(u >> 1, 0) + (u & 1) * T::HP, x1 = xo(u >> 1, 1) + (u & 1) * T::HP;
+#pragma unroll
+        for (int j = 0; j < NTP; ++j) fb2[u & 1][j] = frag2(trd(ring, tb[j] + x0), trd(ring, tb[j] + x1));
+      };
+      rdA(0);
+      rdB(0);
+      __builtin_amdgcn_sched_barrier(0);
+      sfor<0, 2 * KS2>([&](auto uc) {
+        constexpr int u = decltype(uc)::value, ks = u >> 1, cib = u & 1;
+        if constexpr (u + 1 < 2 * KS2) {
+          if constexpr (((u + 1) & 1) == 0) rdA((u + 1) >> 1);
+          rdB(u + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < NTP; ++j)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+            acc4[j][cb * 2 + cib] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa2[ks & 1][cb], fb2[u & 1][j], acc4[j][cb * 2 + cib], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      return;
+    }
     constexpr int LA = GN ? (PW == 16 ? 1 : 0) : 2;  // fragment lookahead (k16 steps): what the registers allow
     bf16x8 fa[LA + 1], fb[LA + 1][NTP];
     auto rd = [&](int ks, int k) {
@@ -280,6 +343,25 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
   asm volatile("" : "+v"(t0));
   const int r = t0 & 31, w8 = t0 >> 6;
   const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFFF, 0x00020000);
+  if constexpr (T::M16) {  // lane: D[co 16 cb + 4 (lane >> 4) + k][ci 16 cib + (lane & 15)] of each (cb, cib) block
+    const int l16 = t0 & 15, g4 = (t0 >> 4) & 3;
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      if (j < ntap) {
+        const int tt = w8 + 8 * j;
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+          const int cb = blk >> 1, cib = blk & 1;
+          const int base = ((split * 27 + tt) * g.cout_p + co0 + 16 * cb + 4 * g4) * g.cin_p + ci0 + 16 * cib + l16;
+          const u32x4 ua = __builtin_bit_cast(u32x4, acc4[j][blk]);  // (whole-vector bit_cast: see below)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            __builtin_amdgcn_raw_buffer_store_b32(ua[k], prs, (unsigned)((base + k * g.cin_p) * 4), 0, 0);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < MAXT; ++j) {
     if (j < ntap) {
