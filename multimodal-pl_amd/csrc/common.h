@@ -39,7 +39,6 @@ enum Opt : int {
   OPT_WB_WGS,         // brick weight-gradient workgroups aimed at
   OPT_WR_TILE16,      // 1: 16 x 16 weight-gradient ring tiles everywhere
   OPT_WR_WGS,         // weight-gradient ring workgroups aimed at
-  OPT_RING_EXP,       // ring conv timing ablations (only in a -DU3D_RING_EXP diagnostic build; 0 = off)
   OPT_WB_S2CO64,      // stride-2 brick weight gradient: two co tiles per workgroup (0: one)
   OPT_COUNT
 };

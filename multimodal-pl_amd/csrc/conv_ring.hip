@@ -8,10 +8,11 @@
 //     z+1 while the fourth slot receives the next plane, so staging (global loads one step ahead in
 //     registers, GroupNorm + ReLU applied once per element, LDS writes issued between the MFMAs) overlaps the
 //     MFMAs and each output plane costs ONE barrier;
-//   * the weights of all 27 taps stay in LDS (55 KB), the first KR k16 steps' weights also in registers;
-//   * the MFMA is issued transposed (A = weights, B = input rows): a lane's accumulators are 16 output
-//     channels of ONE voxel, so after one permlane32 swap every lane stores two 16-B chunks straight from
-//     registers (no LDS epilogue tile), and the residual is added in the same layout.
+//   * the weights of all 27 taps stay in LDS (55 KB), the first KR (tap, co block) fragments also in registers;
+//   * v_mfma_f32_16x16x32_bf16 issued transposed (A = weights, B = input rows): a lane's accumulators are 4
+//     consecutive output channels of one voxel per (voxel block, co block), so after one permlane16 swap per pair
+//     every lane stores 16-B chunks straight from registers (no LDS epilogue tile), and the residual is added in
+//     the same layout. (Rounds 1-2 ran 32x32x16; the 16x16x32 form holds a higher clock, round 3.)
 // Data gradient = the same kernel with the flipped tap offsets and the [t][ci][co] weight pack.
 // Reference: F.conv3d in Conv3d.forward (unet3D.py:27) via NoBottleneck (:56-73) and its autograd.
 #include <cstdlib>
@@ -25,17 +26,10 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
 constexpr int RG_BH = 8, RG_BW = 32, RG_HH = RG_BH + 2, RG_HW = RG_BW + 2;
 constexpr int RG_NR = RG_HH * RG_HW;                 // 340 halo rows per plane
-#ifndef U3D_RING_M16
-#define U3D_RING_M16 1
-#endif
-// M16 (default): the MFMA is v_mfma_f32_16x16x32_bf16 (K = one tap's 32 input channels, 4 MFMAs per tap and wave:
-// 2 voxel blocks x 2 output-channel blocks), the same cycles per flop as v_mfma_f32_32x32x16_bf16 (the -DU3D_RING_M16=0
-// build) but the chip holds a higher clock under it (MI355X_MICROARCH.md, DVFS item 7).
-constexpr bool RG_M16 = U3D_RING_M16 != 0;
-// chunk-plane stride. 32x32x16: 1360 dwords = 16 mod 64 banks (the 4 lanes staging one voxel's 64 B write 4 planes
-// conflict-free). 16x16x32: a multiple of 64 dwords, because one 16-lane ds_read_b128 group spans two chunk planes;
-// the staging then writes 8 consecutive rows of one plane per 8-lane group (conflict-free as well).
-constexpr int RG_PS = RG_M16 ? (RG_NR * 16 + 255) / 256 * 256 : RG_NR * 16;
+// chunk-plane stride (plane = 8 channels of every halo row): a multiple of 64 dwords, because one 16-lane ds_read_b128
+// group of a v_mfma_f32_16x16x32_bf16 fragment spans two chunk planes; the staging writes 8 consecutive rows of one
+// plane per 8-lane group, conflict-free as well
+constexpr int RG_PS = (RG_NR * 16 + 255) / 256 * 256;
 constexpr int RG_SS = 4 * RG_PS;                     // ring slot stride
 constexpr int RG_NT = 512;
 constexpr int RG_LD = (RG_NR * 4 + RG_NT - 1) / RG_NT;  // 3 staged 16-B pieces per thread and plane
@@ -106,10 +100,10 @@ struct RGWalk {
 // tail is one sub-chunk instead of a whole range; uncontended, the walk is the static one. GroupNorm statistics go
 // to per-(sub-chunk, wave) slots (fixed-order finalize: deterministic whatever the assignment). The last workgroup
 // to exit resets the words and the exit counter to zero for the next launch.
-// EXP (diagnostic builds only, -DU3D_RING_EXP; results are wrong when set): 1 no per-step barrier, 2 no x staging
-// loads, 4 no MFMAs (a dependent VALU op keeps the fragment reads live), 8 no LDS fragment reads after the first
-// steps, 16 no residual loads / y stores, 32 both SIMD partners use the same side-work schedule (no stagger).
-template <bool FLIP, bool GN, bool RES, int KR, bool Q = false, int EXP = 0>
+// The MFMA is v_mfma_f32_16x16x32_bf16 (round 3: the same cycles per flop as 32x32x16, but the chip holds a higher
+// clock under it, MI355X_MICROARCH.md DVFS item 7): per tap (K = its 32 input channels) 4 MFMAs per wave = 2 voxel
+// blocks x 2 output-channel blocks. KR = weight fragments (tap, co block) held in registers.
+template <bool FLIP, bool GN, bool RES, int KR, bool Q = false>
 __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                               bf16* __restrict__ y, const bf16* __restrict__ res,
                                                               const float* __restrict__ gstat,
@@ -121,12 +115,11 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   char* const wts = smem + 4 * RG_SS;
   char* const junk = wts + 4 * RG_NWR * 16;  // target of the staging lanes past the plane's last row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  // staging: fixed 8-channel chunk (plane) per thread. 32x32x16: 4 threads = one voxel's 64 B; 16x16x32: 8 threads =
-  // 8 consecutive rows of one plane (a wave still covers 16 whole rows = 1 KB of contiguous voxels)
-  const int ch = RG_M16 ? (tid >> 3) & 3 : tid & 3;
-  const int srow = RG_M16 ? (tid & 7) + 8 * (tid >> 5) : tid >> 2;
-  const int l16 = lane & 15, q4 = lane >> 4;  // 16x16x32 fragment lane geometry: row / column, k group
+  // staging: fixed 8-channel chunk (plane) per thread, 8 threads = 8 consecutive rows of one plane (a wave covers 16
+  // whole rows = 1 KB of contiguous voxels per load)
+  const int ch = (tid >> 3) & 3;
+  const int srow = (tid & 7) + 8 * (tid >> 5);
+  const int l16 = lane & 15, q4 = lane >> 4;  // fragment lane geometry: row / column, k group
 
   // XCD-aware range order: XCD x (= blockIdx % 8) runs a contiguous eighth of the output planes, so the
   // columns it works on at a time are neighbours whose halo rows meet in its L2.
@@ -201,13 +194,12 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     *reinterpret_cast<u32x4*>(wts + (c * RG_NWR + row) * 16) = *reinterpret_cast<const u32x4*>(wpk + row * 32 + c * 8);
   }
   // k16 step st = (tap t = st >> 1, half s = st & 1): this lane's weight fragment is W[t][co = r][16s + 8h ..]
-  // 16x16x32: fragment st = (tap st >> 1, co block st & 1): W[t][co = 16 (st & 1) + l16][8 q4 ..] (whole taps only)
-  constexpr int KRX = RG_M16 ? KR & ~1 : KR;
+  // weight fragment st = (tap st >> 1, co block st & 1): W[t][co = 16 (st & 1) + l16][8 q4 ..] (whole taps only)
+  constexpr int KRX = KR & ~1;
   bf16x8 wreg[KRX > 0 ? KRX : 1];
 #pragma unroll
   for (int st = 0; st < KRX; ++st)
-    wreg[st] = RG_M16 ? *reinterpret_cast<const bf16x8*>(wpk + ((st >> 1) * 32 + 16 * (st & 1) + l16) * 32 + 8 * q4)
-                      : *reinterpret_cast<const bf16x8*>(wpk + ((st >> 1) * 32 + r) * 32 + (st & 1) * 16 + 8 * h);
+    wreg[st] = *reinterpret_cast<const bf16x8*>(wpk + ((st >> 1) * 32 + 16 * (st & 1) + l16) * 32 + 8 * q4);
 
   // buffer loads: out-of-range offsets return zeros with no branch around the load (no exec-masked paths whose
   // merge would make the wait-count insertion pessimistic)
@@ -224,10 +216,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     const bool ok = p.valid && row < RG_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
                     (unsigned)zw < (unsigned)g.w;
     const unsigned off = ok ? (unsigned)((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * 64 + ch * 16) : 0xFFFFFFF0u;
-    if constexpr ((EXP & 2) != 0)
-      v[i] = u32x4{off, off >> 3, off >> 5, 0x3f80u};
-    else
-      v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     m = (i == 0 ? 0u : m) | ((ok ? 1u : 0u) << i);
   };
   auto load_plane = [&](const RGPlane& p, u32x4 (&v)[RG_LD], unsigned& m) {
@@ -252,11 +241,10 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   // A computed output plane waiting for its epilogue: the epilogue (bf16 pack, permlane swap, residual add,
   // stores) of plane k runs between the MFMAs of plane k+1, so it is off the per-plane critical path.
   struct Pending {
-    f32x16 acc;    // 32x32x16
-    f32x4 a4[4];   // 16x16x32: [voxel block vb * 2 + co block cb]
-    u32x4 rv[2];
+    f32x4 a4[4];   // [voxel block vb * 2 + co block cb]
+    u32x4 rv[2];   // residual of voxel blocks 0, 1
     long long vox;
-    bool ok, ok1;  // (16x16x32: voxel blocks 0 and 1)
+    bool ok, ok1;  // voxel blocks 0 and 1 inside the volume
     int chunk;
   };
   Pending pend;
@@ -265,23 +253,17 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   pend.chunk = -1;
   // GroupNorm(16, 32) statistics of the output (GN variants = the forward convs whose outputs feed the next
   // GroupNorm), from the fp32 values just before the final bf16 rounding (no unpack; the voxel's in-volume flag
-  // selects): 8 (sum, sum of squares) pairs per lane, fp32 over the lane's voxels, reduced per workgroup at
-  // the end. Without residual the lane's accumulators acc[4q + e] are channels 8q + 4h + e -> slot 2q + e/2 =
-  // group 4q + 2h + e/2; with residual the post-swap values are channels 16u + 8h + e -> slot 4u + e/2 = group
-  // 8u + 4h + e/2.
-  // 16x16x32: 4 pairs per lane. Without residual acc a4[vb*2 + cb][k] is channel 16 cb + 4 q4 + k -> slot 2 cb + k/2
-  // = group 8 cb + 2 q4 + k/2; with residual the post-swap values are channels 16 (q4 & 1) + 8 (q4 >> 1) + e -> slot
-  // e/2 = group 8 (q4 & 1) + 4 (q4 >> 1) + e/2. Lanes with the same q4 hold the same groups.
-  constexpr int NSL = RG_M16 ? 4 : 8;  // statistics slots per lane
-  constexpr int XR = RG_M16 ? 16 : 32; // lanes sharing a slot's group (xor-reduced)
-  auto slot_group = [&](int j) {
-    if constexpr (RG_M16) return RES ? 8 * (q4 & 1) + 4 * (q4 >> 1) + j : 8 * (j >> 1) + 2 * q4 + (j & 1);
-    else return RES ? 8 * (j >> 2) + 4 * h + (j & 3) : 4 * (j >> 1) + 2 * h + (j & 1);
-  };
+  // selects): 4 (sum, sum of squares) pairs per lane, fp32 over the lane's voxels, reduced per workgroup at the end.
+  // Without residual acc a4[vb*2 + cb][k] is channel 16 cb + 4 q4 + k -> slot 2 cb + k/2 = group 8 cb + 2 q4 + k/2;
+  // with residual the post-swap values are channels 16 (q4 & 1) + 8 (q4 >> 1) + e -> slot e/2 = group
+  // 8 (q4 & 1) + 4 (q4 >> 1) + e/2. Lanes with the same q4 hold the same groups.
+  constexpr int NSL = 4;  // statistics slots per lane
+  constexpr int XR = 16;  // lanes sharing a slot's group (xor-reduced)
+  auto slot_group = [&](int j) { return RES ? 8 * (q4 & 1) + 4 * (q4 >> 1) + j : 8 * (j >> 1) + 2 * q4 + (j & 1); };
   const bool slot_writer = (lane & (XR - 1)) == 0;
-  float gs[8], gq[8];
+  float gs[NSL], gq[NSL];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) gs[j] = gq[j] = 0.f;
+  for (int j = 0; j < NSL; ++j) gs[j] = gq[j] = 0.f;
   int acc_chunk = -1;
   // work-queue mode: the statistics of one chunk, per wave: reduce over the wave's voxels (xor within the 32-lane
   // halves) and write slot (chunk, wave); no barrier, so it can run inside the MFMA chain
@@ -311,105 +293,53 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         acc_chunk = p.chunk;
       }
     }
-    if constexpr (RG_M16) {
-      // lane (l16, q4): a4[vb*2 + cb][k] = channel 16 cb + 4 q4 + k of voxel 16 vb + l16. Pack to bf16 pairs, then
-      // one permlane16 swap per pair (odd 16-lane rows of the co-block-0 value <-> even rows of the co-block-1
-      // value): an even-row lane then holds channels 8m..8m+7 (m = q4 >> 1), an odd-row lane 16+8m..16+8m+7, of its
-      // voxel -> one 16-B store per voxel block.
-      const int cbase = 16 * (q4 & 1) + 8 * (q4 >> 1);
+    // lane (l16, q4): a4[vb*2 + cb][k] = channel 16 cb + 4 q4 + k of voxel 16 vb + l16. Pack to bf16 pairs, then
+    // one permlane16 swap per pair (odd 16-lane rows of the co-block-0 value <-> even rows of the co-block-1
+    // value): an even-row lane then holds channels 8m..8m+7 (m = q4 >> 1), an odd-row lane 16+8m..16+8m+7, of its
+    // voxel -> one 16-B store per voxel block.
+    const int cbase = 16 * (q4 & 1) + 8 * (q4 >> 1);
 #pragma unroll
-      for (int vb = 0; vb < 2; ++vb) {
-        const bool okv = vb ? p.ok1 : p.ok;
-        if constexpr (GN && !RES) {
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const float t = okv ? p.a4[vb * 2 + cb][k] : 0.f;  // select: rows past the volume may be non-finite
-              gs[2 * cb + (k >> 1)] += t;
-              gq[2 * cb + (k >> 1)] = fmaf(t, t, gq[2 * cb + (k >> 1)]);
-            }
-        }
-        uint32_t pk[2][2];
+    for (int vb = 0; vb < 2; ++vb) {
+      const bool okv = vb ? p.ok1 : p.ok;
+      if constexpr (GN && !RES) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-          for (int e = 0; e < 2; ++e) pk[cb][e] = pack_bf16x2(p.a4[vb * 2 + cb][2 * e], p.a4[vb * 2 + cb][2 * e + 1]);
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][e], pk[1][e], false, false);
-          pk[0][e] = sw[0];
-          pk[1][e] = sw[1];
-        }
-        u32x4 v = {pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
-        if constexpr (RES) {
-          float a[8], c[8];
-          load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
-          load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[vb]), c);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) a[e] += c[e];
-          if constexpr (GN) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float t = okv ? a[e] : 0.f;
-              gs[e >> 1] += t;
-              gq[e >> 1] = fmaf(t, t, gq[e >> 1]);
-            }
+          for (int k = 0; k < 4; ++k) {
+            const float t = okv ? p.a4[vb * 2 + cb][k] : 0.f;  // select: rows past the volume may be non-finite
+            gs[2 * cb + (k >> 1)] += t;
+            gq[2 * cb + (k >> 1)] = fmaf(t, t, gq[2 * cb + (k >> 1)]);
           }
-          store16<bf16>(reinterpret_cast<bf16*>(&v), a);
-        }
-        if (okv) *reinterpret_cast<u32x4*>(y + (p.vox + 16 * vb) * 32 + cbase) = v;
       }
-      return;
-    }
-    if constexpr (GN && !RES) {
+      uint32_t pk[2][2];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const float t = p.ok ? p.acc[k] : 0.f;  // select, not a multiply: rows past the volume may hold non-finite
-        gs[2 * (k >> 2) + ((k & 3) >> 1)] += t;
-        gq[2 * (k >> 2) + ((k & 3) >> 1)] = fmaf(t, t, gq[2 * (k >> 2) + ((k & 3) >> 1)]);
-      }
-    }
-    // lane (r, h): acc[4q + e] = channel 8q + 4h + e of voxel r. Pack to bf16 pairs, then swap halves so that
-    // lane (r, h) holds channels 8h..8h+7 (pk[0..1]) and 16+8h..16+8h+7 (pk[2..3]).
-    uint32_t pk[4][2];
+      for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-        pk[q][e] = pack_bf16x2(p.acc[4 * q + 2 * e], p.acc[4 * q + 2 * e + 1]);
-#pragma unroll
-    for (int q = 0; q < 4; q += 2)
+        for (int e = 0; e < 2; ++e) pk[cb][e] = pack_bf16x2(p.a4[vb * 2 + cb][2 * e], p.a4[vb * 2 + cb][2 * e + 1]);
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(pk[q][e], pk[q + 1][e], false, false);
-        pk[q][e] = sw[0];
-        pk[q + 1][e] = sw[1];
+        const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][e], pk[1][e], false, false);
+        pk[0][e] = sw[0];
+        pk[1][e] = sw[1];
       }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      u32x4 v = {pk[2 * u][0], pk[2 * u][1], pk[2 * u + 1][0], pk[2 * u + 1][1]};
+      u32x4 v = {pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
       if constexpr (RES) {
         float a[8], c[8];
         load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
-        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[u]), c);
+        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[vb]), c);
 #pragma unroll
         for (int e = 0; e < 8; ++e) a[e] += c[e];
         if constexpr (GN) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float t = p.ok ? a[e] : 0.f;
-            gs[4 * u + (e >> 1)] += t;
-            gq[4 * u + (e >> 1)] = fmaf(t, t, gq[4 * u + (e >> 1)]);
+            const float t = okv ? a[e] : 0.f;
+            gs[e >> 1] += t;
+            gq[e >> 1] = fmaf(t, t, gq[e >> 1]);
           }
         }
         store16<bf16>(reinterpret_cast<bf16*>(&v), a);
       }
-      if constexpr ((EXP & 16) != 0) {
-        if (p.ok && v[0] == 0x7fc17fc1u) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
-      } else {
-        if (p.ok) *reinterpret_cast<u32x4*>(y + p.vox * 32 + 16 * u + 8 * h) = v;
-      }
+      if (okv) *reinterpret_cast<u32x4*>(y + (p.vox + 16 * vb) * 32 + cbase) = v;
     }
   };
 
@@ -419,128 +349,68 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   // (waves >= 4 on H = 1, MI355X_MICROARCH.md two waves per SIMD, item 9) measured equal or 2-3% slower at 96^3
   // (profiles/r03_ring_ablations.log), so every wave runs H = 0.
   auto compute = [&](const RGPlane& pc, int s0, int s1, int s2, auto hc, auto&& side) __attribute__((always_inline)) {
-    if constexpr (RG_M16) {
-      // 16x16x32: per tap (K = 32 input channels) 4 MFMAs = (voxel block vb: row voxels 16 vb..) x (co block cb);
-      // A = weights (rows = output channels), B = input rows (columns = voxels): a lane's accumulators are 4
-      // consecutive channels of one voxel per (vb, cb). Fragments: lane (l16, q4) reads 16 B of chunk plane q4
-      // (channels 8 q4 ..) of row l16 of the block: the 4 chunk planes of one row are one tap's K.
-      const int zo = pc.zin - 1;
-      const int zh = pc.h0 + wave, zw = pc.w0 + l16;
-      Pending nw;
-      nw.chunk = pc.chunk;
-      nw.ok = zh < g.h && zw < g.w;
-      nw.ok1 = zh < g.h && zw + 16 < g.w;
-      nw.vox = (((long long)pc.n * g.d + zo) * g.h + zh) * g.w + zw;
-      nw.rv[0] = nw.rv[1] = u32x4{0u, 0u, 0u, 0u};
-      if constexpr (RES) {  // the 16 B this lane stores after the swap, per voxel block
-        const int cb2 = 2 * (16 * (q4 & 1) + 8 * (q4 >> 1));
-        const unsigned r0 = nw.ok ? (unsigned)(nw.vox * 64 + cb2) : 0xFFFFFFC0u;
-        const unsigned r1 = nw.ok1 ? (unsigned)((nw.vox + 16) * 64 + cb2) : 0xFFFFFFC0u;
-        nw.rv[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, r0, 0, 0));
-        nw.rv[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, r1, 0, 0));
-      }
-      const int sl[3] = {FLIP ? s2 : s0, s1, FLIP ? s0 : s2};
-      const char* ibase = ring + q4 * RG_PS + (wave * RG_HW + l16) * 16;
-      const char* wbase = wts + (q4 * RG_NWR + l16) * 16;
-      auto ioff = [&](int t) {
-        const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
-        const int oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
-        return sl[td] * RG_SS + (oh * RG_HW + ow) * 16;
-      };
-#pragma unroll
-      for (int i = 0; i < 4; ++i) nw.a4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      constexpr int LA = 2;  // taps of fragments in flight
-      bf16x8 fi[LA + 1][2], fw[LA + 1][2];
-      auto rd = [&](int t, int k) {
-        const int o = ioff(t);
-        fi[k][0] = *reinterpret_cast<const bf16x8*>(ibase + o);
-        fi[k][1] = *reinterpret_cast<const bf16x8*>(ibase + o + 16 * 16);
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          const int st = 2 * t + cb;
-          if (st < KRX)
-            fw[k][cb] = wreg[st < KRX ? st : 0];
-          else
-            fw[k][cb] = *reinterpret_cast<const bf16x8*>(wbase + (t * 32 + 16 * cb) * 16);
-        }
-      };
-#pragma unroll
-      for (int k = 0; k < LA; ++k) rd(k, k);
-      auto tstep = [&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        if constexpr (t + LA < 27) rd(t + LA, (t + LA) % (LA + 1));
-        side(std::integral_constant<int, t - 1>{});
-        if constexpr (t == 15) epilogue(pend);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int vb = 0; vb < 2; ++vb)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
-            nw.a4[vb * 2 + cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t % (LA + 1)][cb], fi[t % (LA + 1)][vb],
-                                                                         nw.a4[vb * 2 + cb], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      __builtin_amdgcn_sched_barrier(0);
-      static_for<0, 27>(tstep);
-      pend = nw;
-      return;
-    }
-    constexpr int H = (EXP & 32) != 0 ? 0 : decltype(hc)::value;
-    constexpr int EPI = H ? 44 : 30;
+    // 16x16x32: per tap (K = 32 input channels) 4 MFMAs = (voxel block vb: row voxels 16 vb..) x (co block cb);
+    // A = weights (rows = output channels), B = input rows (columns = voxels): a lane's accumulators are 4
+    // consecutive channels of one voxel per (vb, cb). Fragments: lane (l16, q4) reads 16 B of chunk plane q4
+    // (channels 8 q4 ..) of row l16 of the block: the 4 chunk planes of one row are one tap's K.
     const int zo = pc.zin - 1;
-    const int zh = pc.h0 + wave, zw = pc.w0 + r;
+    const int zh = pc.h0 + wave, zw = pc.w0 + l16;
     Pending nw;
     nw.chunk = pc.chunk;
     nw.ok = zh < g.h && zw < g.w;
+    nw.ok1 = zh < g.h && zw + 16 < g.w;
     nw.vox = (((long long)pc.n * g.d + zo) * g.h + zh) * g.w + zw;
     nw.rv[0] = nw.rv[1] = u32x4{0u, 0u, 0u, 0u};
-    if constexpr (RES && (EXP & 16) == 0) {
-      const unsigned ro = nw.ok ? (unsigned)(nw.vox * 64 + 16 * h) : 0xFFFFFFC0u;
-      nw.rv[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
-      nw.rv[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro + 32, 0, 0));
+    if constexpr (RES) {  // the 16 B this lane stores after the swap, per voxel block
+      const int cb2 = 2 * (16 * (q4 & 1) + 8 * (q4 >> 1));
+      const unsigned r0 = nw.ok ? (unsigned)(nw.vox * 64 + cb2) : 0xFFFFFFC0u;
+      const unsigned r1 = nw.ok1 ? (unsigned)((nw.vox + 16) * 64 + cb2) : 0xFFFFFFC0u;
+      nw.rv[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, r0, 0, 0));
+      nw.rv[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, r1, 0, 0));
     }
     const int sl[3] = {FLIP ? s2 : s0, s1, FLIP ? s0 : s2};
-    const char* abase = ring + h * RG_PS + (wave * RG_HW + r) * 16;
-    const char* bbase = wts + (h * RG_NWR + r) * 16;
-    auto aoff = [&](int st) {
-      const int t = st >> 1, s = st & 1;
+    const char* ibase = ring + q4 * RG_PS + (wave * RG_HW + l16) * 16;
+    const char* wbase = wts + (q4 * RG_NWR + l16) * 16;
+    auto ioff = [&](int t) {
       const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
       const int oh = FLIP ? 2 - th : th, ow = FLIP ? 2 - tw : tw;
-      return sl[td] * RG_SS + (oh * RG_HW + ow) * 16 + 2 * s * RG_PS;
+      return sl[td] * RG_SS + (oh * RG_HW + ow) * 16;
     };
-    auto boff = [](int st) { return (2 * (st & 1) * RG_NWR + (st >> 1) * 32) * 16; };
 #pragma unroll
-    for (int e = 0; e < 16; ++e) nw.acc[e] = 0.f;
-    // fragments in flight: step st's MFMA consumes the reads issued LA steps earlier; one scheduling region
-    // per step (sched_barrier) keeps that order and spreads the staging writes / epilogue over the chain
-    constexpr int LA = 3;
-    bf16x8 fa[LA + 1], fb[LA + 1];
-    auto rd = [&](int st, int k) {
-      if constexpr ((EXP & 8) != 0) {
-        if (st >= LA + 1) return;
+    for (int i = 0; i < 4; ++i) nw.a4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int LA = 2;  // taps of fragments in flight
+    bf16x8 fi[LA + 1][2], fw[LA + 1][2];
+    auto rd = [&](int t, int k) {
+      const int o = ioff(t);
+      fi[k][0] = *reinterpret_cast<const bf16x8*>(ibase + o);
+      fi[k][1] = *reinterpret_cast<const bf16x8*>(ibase + o + 16 * 16);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int st = 2 * t + cb;
+        if (st < KRX)
+          fw[k][cb] = wreg[st < KRX ? st : 0];
+        else
+          fw[k][cb] = *reinterpret_cast<const bf16x8*>(wbase + (t * 32 + 16 * cb) * 16);
       }
-      fa[k] = *reinterpret_cast<const bf16x8*>(abase + aoff(st));
-      if (st < KR)
-        fb[k] = wreg[st < KR ? st : 0];
-      else
-        fb[k] = *reinterpret_cast<const bf16x8*>(bbase + boff(st));
     };
 #pragma unroll
     for (int k = 0; k < LA; ++k) rd(k, k);
-    auto mstep = [&](auto stc) {
-      constexpr int st = decltype(stc)::value;
-      if constexpr (st + LA < 54) rd(st + LA, (st + LA) % (LA + 1));
-      side(std::integral_constant<int, st - (H ? 15 : 1)>{});
-      if constexpr (st == EPI) epilogue(pend);
+    auto tstep = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      if constexpr (t + LA < 27) rd(t + LA, (t + LA) % (LA + 1));
+      side(std::integral_constant<int, t - 1>{});
+      if constexpr (t == 15) epilogue(pend);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((EXP & 4) != 0)
-        nw.acc[st & 15] += (float)fa[st % (LA + 1)][0] * (float)fb[st % (LA + 1)][1];
-      else
-        nw.acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[st % (LA + 1)], fa[st % (LA + 1)], nw.acc, 0, 0, 0);
+#pragma unroll
+      for (int vb = 0; vb < 2; ++vb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          nw.a4[vb * 2 + cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t % (LA + 1)][cb], fi[t % (LA + 1)][vb],
+                                                                       nw.a4[vb * 2 + cb], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     };
     __builtin_amdgcn_sched_barrier(0);
-    static_for<0, 54>(mstep);
+    static_for<0, 27>(tstep);
     pend = nw;
   };
 
@@ -676,7 +546,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     } else {
       static_for<0, 2 * RG_LD>(side);
     }
-    if constexpr ((EXP & 1) == 0) __syncthreads();
+    __syncthreads();
     pc = pw;
     pw = pl;
     ++s;
@@ -704,7 +574,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   }
   if constexpr (GN) {
     if (spart == nullptr) return;
-    // lanes with the same h hold the same groups: reduce over r (xor within 32-lane halves), then over the waves in
+    // lanes with the same q4 hold the same groups: reduce over l16 (xor within 16-lane rows), then over the waves in
     // fixed order through LDS (the ring is idle: every step ended with a barrier)
 #pragma unroll
     for (int j = 0; j < NSL; ++j)
@@ -796,42 +666,12 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
     else RG_LAUNCH(F, G, R, 0);            \
   } while (0)
   U3D_REQUIRE(!(flip && (gn_stats || residual)), "conv32_ring: the data gradient takes no prologue / residual");
-#ifdef U3D_RING_EXP
-  if (const int ex = opt(OPT_RING_EXP)) {  // diagnostic build: timing ablations of the static schedule
-#define RG_EX(F, G, R, K, E)                                                                                     \
-  hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K, false, E>), dim3((unsigned)grid), dim3(RG_NT), 0, s,  \
-                     (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta,  \
-                     sp, g)
-#define RG_EXS(E)                                                                   \
-  do {                                                                              \
-    if (flip) RG_EX(true, false, false, 27, E);                                     \
-    else if (gn_stats && residual) RG_EX(false, true, true, 12, E);                 \
-    else if (gn_stats) RG_EX(false, true, false, 16, E);                            \
-    else RG_EX(false, false, false, 27, E);                                         \
-  } while (0)
-    switch (ex) {
-      case 1: RG_EXS(1); break;
-      case 2: RG_EXS(2); break;
-      case 4: RG_EXS(4); break;
-      case 8: RG_EXS(8); break;
-      case 16: RG_EXS(16); break;
-      case 32: RG_EXS(32); break;
-      case 18: RG_EXS(18); break;
-      case 12: RG_EXS(12); break;
-      case 3: RG_EXS(3); break;
-      default: return fail(U3D_EINVAL, "RING_EXP: unknown ablation %d", ex);
-    }
-#undef RG_EXS
-#undef RG_EX
-    return check_launch("conv32_ring_kernel (ablation)");
-  }
-#endif
   // register budget (2 waves per SIMD): GN + residual holds 12 weight steps, GN 16, the others 27
   const bool kr = ring_kr(1) != 0;
   if (flip) RG_KR(true, false, false, 27);
   else if (gn_stats && residual) RG_KR(false, true, true, 12);  // + the statistics accumulators: 12 steps
   else if (gn_stats) RG_KR(false, true, false, 16);  // (12 measured equal: 124.6 vs 124.8 us)
-  else if (residual) RG_KR(false, false, true, RG_M16 ? 20 : 27);
+  else if (residual) RG_KR(false, false, true, 20);
   else RG_KR(false, false, false, 27);
 #undef RG_KR
 #undef RG_LAUNCH
@@ -891,11 +731,11 @@ extern "C" int u3d_conv32_ring_q(int flip, const void* x, int n, int d, int h, i
   hipLaunchKernelGGL((conv32_ring_kernel<F, G, R, K, true>), dim3(grid), dim3(RG_NT), 0, s, (const bf16*)x, \
                      (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, stats_ws, g, queue)
   // register budget: the claim state costs the weight steps of the static variants a few registers
-  if (flip) RQ_LAUNCH(true, false, false, RG_M16 ? 16 : 24);
+  if (flip) RQ_LAUNCH(true, false, false, 16);
   else if (gn_stats && residual) RQ_LAUNCH(false, true, true, 4);
   else if (gn_stats) RQ_LAUNCH(false, true, false, 8);
   else if (residual) RQ_LAUNCH(false, false, true, 16);
-  else RQ_LAUNCH(false, false, false, RG_M16 ? 16 : 24);
+  else RQ_LAUNCH(false, false, false, 16);
 #undef RQ_LAUNCH
   return check_launch("conv32_ring_kernel (work stealing)");
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the working tree's library with extra compiler flags into multimodal-pl_amd/u3d/<name>.so (diagnostic
-# builds, e.g. -DU3D_RING_EXP): tools/build_variant.sh NAME "FLAGS"
+# builds, e.g. -DU3D_WRING_M16=0): tools/build_variant.sh NAME "FLAGS"
 set -e
 NAME=$1; FLAGS=$2
 R=$(cd "$(dirname "$0")/.." && pwd)
