@@ -310,7 +310,10 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     }
   };
   __shared__ __attribute__((aligned(16))) char hal[4 * PS];
-  __shared__ __attribute__((aligned(16))) char wbuf[2][4 * WROWS * 16];
+  // weight planes (8 input channels each) padded by 64 B: the 4 lanes staging one row's 4 chunks write 4 planes
+  // conflict-free (plane stride = 64 mod 256 B)
+  constexpr int WPS = WROWS * 16 + 64;
+  __shared__ __attribute__((aligned(16))) char wbuf[2][4 * WPS];
   // GroupNorm (scale, shift) per input channel of the samples in flight, slot = sample & 1: filled once per sample
   // (the staging reads it from LDS — no global loads whose wait would drain the halo/weight prefetch)
   __shared__ __attribute__((aligned(16))) f32x2 gtab[2][GB_MAXC];
@@ -428,7 +431,9 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
 #pragma unroll
     for (int i = 0; i < WLD; ++i) {
       const int ci = tid + i * GB_NT;
-      const int ch = ci / WROWS, row = ci % WROWS;
+      // 4 consecutive lanes = one (tap, co) row's 4 chunks: 64 contiguous bytes of the pack per 4 lanes (the chunk-
+      // major order read 16 B per cache line and lane)
+      const int ch = ci & 3, row = ci >> 2;
       const int j = row / CO, co = co0 + row % CO;
       const int t = td * 9 + j;
       const unsigned off = ci < WROWS * 4 && co < g.cout_p
@@ -441,8 +446,8 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     for (int i = 0; i < WLD; ++i) {
       const int ci = tid + i * GB_NT;
       if (ci < WROWS * 4) {
-        const int ch = ci / WROWS, row = ci % WROWS;
-        *reinterpret_cast<u32x4*>(wbuf[buf] + (ch * WROWS + row) * 16) = wpre[i];
+        const int ch = ci & 3, row = ci >> 2;
+        *reinterpret_cast<u32x4*>(wbuf[buf] + ch * WPS + row * 16) = wpre[i];
       }
     }
   };
@@ -505,7 +510,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
           fa[slot][tm] = *reinterpret_cast<const bf16x8*>(hal + plane * PS + (arow[tm] + toff) * 16);
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
-          fb[slot][tn] = *reinterpret_cast<const bf16x8*>(wb + (plane * WROWS + j * CO + tn * 32 + r) * 16);
+          fb[slot][tn] = *reinterpret_cast<const bf16x8*>(wb + plane * WPS + (j * CO + tn * 32 + r) * 16);
       };
       rd(0, 0, 0);
 #pragma unroll 1
