@@ -71,25 +71,26 @@ __global__ __launch_bounds__(1024) void stem1_wtab_kernel(const T* __restrict__ 
   if (i < 27 * 32) wt[i] = to_f(wpk[(long long)i * cin_p]);
 }
 
+// conv1 (cin 1 -> 32, stride 1), one voxel per lane, packed FMAs (v_pk_fma_f32) with the weights from a contiguous fp32
+// table read by scalar loads: the 64-B output rows of consecutive lanes are consecutive, so each 16-B store
+// instruction of a wave covers 4 KB (round 3: a four-voxels-per-lane form, lanes 256 B apart, measured 91 vs 69 us at
+// 2x96^3); the three w-neighbours of a tap row are three coalesced loads. Same fp32 FMA chain per output as the
+// generic kernel (OPT_STEM1 = 0): bitwise equal.
 template <typename T>
 __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                                                      T* __restrict__ y, int d, int h, int w, long long rows) {
-  const int w4 = w >> 2;
-  const long long item = (long long)blockIdx.x * ST + threadIdx.x;  // (output row, 4-voxel group)
-  const long long row = item / w4;
-  if (row >= rows) return;
-  const int q = (int)(item - row * w4);
-  const int yy = (int)(row % h);
-  const long long nz = row / h;
+                                                       T* __restrict__ y, int d, int h, int w, long long nvox) {
+  const long long v = (long long)blockIdx.x * ST + threadIdx.x;
+  if (v >= nvox) return;
+  const int xx = (int)(v % w);
+  const long long r = v / w;
+  const int yy = (int)(r % h);
+  const long long nz = r / h;
   const int z = (int)(nz % d);
   const long long nn = nz / d;
-  const int x0 = 4 * q;
   const float* xb = x + nn * d * h * w;
-  f32x2 acc[4][16];
+  f32x2 acc[16];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int c = 0; c < 16; ++c) acc[j][c] = (f32x2){0.f, 0.f};
+  for (int c = 0; c < 16; ++c) acc[c] = (f32x2){0.f, 0.f};
 #pragma unroll 1
   for (int kd = 0; kd < 3; ++kd) {
     const int zd = z + kd - 1;
@@ -97,39 +98,31 @@ __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__
     for (int kh = 0; kh < 3; ++kh) {
       const int zh = yy + kh - 1;
       const bool rowok = (unsigned)zd < (unsigned)d && (unsigned)zh < (unsigned)h;
-      float in[6];
+      float in[3];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int zw = x0 + k - 1;
+      for (int k = 0; k < 3; ++k) {
+        const int zw = xx + k - 1;
         in[k] = rowok && (unsigned)zw < (unsigned)w ? xb[((long long)zd * h + zh) * w + zw] : 0.f;
       }
       const int t0 = (kd * 3 + kh) * 3;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
         const float* wr = wt + (t0 + kw) * 32;
+        const f32x2 xv = {in[kw], in[kw]};
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          const f32x2 wv = {wr[2 * c], wr[2 * c + 1]};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const f32x2 xv = {in[j + kw], in[j + kw]};
-            acc[j][c] = __builtin_elementwise_fma(xv, wv, acc[j][c]);
-          }
-        }
+        for (int c = 0; c < 16; ++c) acc[c] = __builtin_elementwise_fma(xv, (f32x2){wr[2 * c], wr[2 * c + 1]}, acc[c]);
       }
     }
   }
-  T* yr = y + (row * w + x0) * 32;
+  T* yr = y + v * 32;
   constexpr int VEC = 16 / sizeof(T);
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int c = 0; c < 32; c += VEC) {
+    float o[VEC];
 #pragma unroll
-    for (int c = 0; c < 32; c += VEC) {
-      float v[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) v[e] = acc[j][(c + e) >> 1][(c + e) & 1];
-      store16<T>(yr + j * 32 + c, v);
-    }
+    for (int e = 0; e < VEC; ++e) o[e] = acc[(c + e) >> 1][(c + e) & 1];
+    store16<T>(yr + c, o);
+  }
 }
 
 // dW[t][co][ci] partial over a voxel split: thread per (t, ci, co) output, loop over the split's voxels.
@@ -338,17 +331,18 @@ extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, in
   hipStream_t s = (hipStream_t)stream;
   const int od = sdim(d, stride), oh = sdim(h, stride), ow = sdim(w, stride);
   const long long total = (long long)n * od * oh * ow;
-  if (cin == 1 && stride == 1 && cout == 32 && w % 4 == 0 && (long long)n * d * h < 2147483647LL && stem1_on()) {
+  if (cin == 1 && stride == 1 && cout == 32 && stem1_on()) {
     U3D_REQUIRE(ws, "stem_fwd: the conv1 kernel needs a workspace of u3d_stem_fwd_ws_bytes()");
-    const long long rows = (long long)n * d * h, items = rows * (w / 4);
-    const dim3 grid((unsigned)((items + ST - 1) / ST));
+    const long long rows = (long long)n * d * h;
     float* wt = static_cast<float*>(ws);
+    const long long nvox = rows * w;
+    const dim3 g1((unsigned)((nvox + ST - 1) / ST));
     if (dtype == U3D_BF16) {
       hipLaunchKernelGGL(stem1_wtab_kernel<bf16>, dim3(1), dim3(1024), 0, s, (const bf16*)wpk, round_up(cin, 32), wt);
-      hipLaunchKernelGGL(stem1_fwd_kernel<bf16>, grid, dim3(ST), 0, s, x, wt, (bf16*)y, d, h, w, rows);
+      hipLaunchKernelGGL(stem1_fwd_kernel<bf16>, g1, dim3(ST), 0, s, x, wt, (bf16*)y, d, h, w, nvox);
     } else {
       hipLaunchKernelGGL(stem1_wtab_kernel<float>, dim3(1), dim3(1024), 0, s, (const float*)wpk, round_up(cin, 32), wt);
-      hipLaunchKernelGGL(stem1_fwd_kernel<float>, grid, dim3(ST), 0, s, x, wt, (float*)y, d, h, w, rows);
+      hipLaunchKernelGGL(stem1_fwd_kernel<float>, g1, dim3(ST), 0, s, x, wt, (float*)y, d, h, w, nvox);
     }
     return check_launch("stem1_fwd_kernel");
   }

@@ -304,9 +304,9 @@ def test_ring_epilogue_gn_stats_match_stats_pass(gpu, n, dims, res):
 
 
 @pytest.mark.parametrize("dims", [(5, 7, 16), (3, 9, 20), (4, 4, 6)])
-def test_stem_fwd_fp32_four_voxel_kernel(gpu, dims):
-    """cin=1 stride-1 32-channel stem: the four-voxels-per-thread kernel (w % 4 == 0) and the generic one (w = 6)
-    against fp64 on the same fp32 operands."""
+def test_stem_fwd_fp32_packed_kernel(gpu, dims):
+    """cin=1 stride-1 32-channel stem: the packed one-voxel-per-lane kernel (any w, here 16, 20 and 6) against fp64 on
+    the same fp32 operands."""
     from u3d import ops
     torch.manual_seed(4)
     x = torch.randn((2, 1) + dims, device=gpu)
@@ -321,8 +321,8 @@ def test_stem_fwd_fp32_four_voxel_kernel(gpu, dims):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("dims", [(5, 7, 16), (96, 96, 96)])
 def test_stem1_packed_kernel_bitwise_equals_generic(gpu, dt, dims):
-    """conv1 (cin 1 -> 32, stride 1): the four-voxel packed-FMA kernel (scalar-loaded weights, v_pk_fma_f32) runs the
-    same fp32 FMA chain per output as the generic one-voxel kernel (OPT STEM1 = 0), so the outputs are bitwise equal."""
+    """conv1 (cin 1 -> 32, stride 1): the packed-FMA kernel (scalar-loaded weights, v_pk_fma_f32) runs the same fp32 FMA
+    chain per output as the generic kernel (OPT STEM1 = 0), so the outputs are bitwise equal."""
     from u3d import ops
     torch.manual_seed(6)
     x = torch.randn((2, 1) + dims, device=gpu)
