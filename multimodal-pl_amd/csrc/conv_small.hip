@@ -80,22 +80,22 @@ __global__ __launch_bounds__(SC_NT, 1) void conv_small_kernel(const bf16* __rest
   const int sch = tid & 3, srow0 = tid >> 2;
   u32x4 hpre[SC_HLD], wpre[SC_WLD];
   unsigned hmask = 0;
+  // buffer loads with 32-bit offsets (host: operands below 2 GiB); a masked piece gets the out-of-range sentinel and
+  // reads zeros with no branch around the load (a branch merge pulls the prefetch's wait up ahead of the MFMAs)
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, g.n * g.d * g.h * g.w * g.cin * 2, 0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)wpk, 0, 27 * g.cout_p * g.cin_p * 2, 0x00020000);
   auto halo_load = [&](int c) {
     unsigned m = 0;
 #pragma unroll
     for (int i = 0; i < SC_HLD; ++i) {
       const int row = srow0 + i * (SC_NT / 4);
-      u32x4 val = {0u, 0u, 0u, 0u};
-      if (row < g.nh) {
-        const int xw = row % g.hw, xh = (row / g.hw) % g.hh, xd = row / (g.hw * g.hh);
-        const int zd = o0d - 1 + xd, zh = o0h - 1 + xh, zw = o0w - 1 + xw, cc = c * 32 + sch * 8;
-        if ((unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h && (unsigned)zw < (unsigned)g.w &&
-            cc < g.cin) {
-          val = *reinterpret_cast<const u32x4*>(x + ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc);
-          m |= 1u << i;
-        }
-      }
-      hpre[i] = val;
+      const int xw = row % g.hw, xh = (row / g.hw) % g.hh, xd = row / (g.hw * g.hh);
+      const int zd = o0d - 1 + xd, zh = o0h - 1 + xh, zw = o0w - 1 + xw, cc = c * 32 + sch * 8;
+      const bool ok = row < g.nh && (unsigned)zd < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
+                      (unsigned)zw < (unsigned)g.w && cc < g.cin;
+      const unsigned off = ok ? (unsigned)(((((nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cin + cc) * 2) : 0xFFFFFFF0u;
+      hpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      m |= (ok ? 1u : 0u) << i;
     }
     hmask = m;
   };
@@ -103,13 +103,10 @@ __global__ __launch_bounds__(SC_NT, 1) void conv_small_kernel(const bf16* __rest
 #pragma unroll
     for (int i = 0; i < SC_WLD; ++i) {
       const int id = tid + i * SC_NT;
-      u32x4 val = {0u, 0u, 0u, 0u};
-      if (id < SC_NWR * 4) {
-        const int row = id >> 2, t = row >> 5, co = co0 + (row & 31);
-        if (co < g.cout_p)
-          val = *reinterpret_cast<const u32x4*>(wpk + ((long long)t * g.cout_p + co) * g.cin_p + c * 32 + (id & 3) * 8);
-      }
-      wpre[i] = val;
+      const int row = id >> 2, t = row >> 5, co = co0 + (row & 31);
+      const bool ok = id < SC_NWR * 4 && co < g.cout_p;
+      const unsigned off = ok ? (unsigned)(((t * g.cout_p + co) * g.cin_p + c * 32 + (id & 3) * 8) * 2) : 0xFFFFFFF0u;
+      wpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
     }
   };
   // GN scale/shift of this workgroup's sample per input channel, in LDS (filled once): the staging reads its 8
@@ -313,6 +310,8 @@ extern "C" int u3d_conv_small(int flip, const void* x, int n, int cin, int d, in
   g.slab = g.nks > 1 ? ws : nullptr;
   const long long nwg = tiles * g.nks;
   U3D_REQUIRE(nwg < (1LL << 31), "conv_small: grid too large");
+  U3D_REQUIRE((long long)n * d * h * w * cin * 2 < (1LL << 31) - 64 && 27LL * g.cout_p * g.cin_p * 2 < (1LL << 31) - 64,
+              "conv_small: operands beyond the 2 GiB buffer-offset range");
   hipStream_t s = (hipStream_t)stream;
   if (flip)
     hipLaunchKernelGGL(conv_small_kernel<true>, dim3((unsigned)nwg), dim3(SC_NT), 0, s, (const bf16*)x,

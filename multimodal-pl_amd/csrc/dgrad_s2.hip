@@ -69,31 +69,30 @@ __global__ __launch_bounds__(S2_NT, 1) void dgrad_s2_kernel(const bf16* __restri
 
   const int sch = tid & 3, srow0 = tid >> 2;
   u32x4 hpre[S2_HLD], wpre[S2_WLD];
+  // buffer loads with 32-bit offsets (host: operands below 2 GiB); a masked piece gets the out-of-range sentinel and
+  // reads zeros with no branch around the load, so the prefetch's wait is not pulled up to a branch merge ahead of
+  // the MFMAs it should overlap
+  const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)dy, 0, g.n * g.qd * g.qh * g.qw * g.cy * 2, 0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)wpk, 0, 27 * g.cx_p * g.cy_p * 2, 0x00020000);
   auto halo_load = [&](int c) {
 #pragma unroll
     for (int i = 0; i < S2_HLD; ++i) {
       const int row = srow0 + i * (S2_NT / 4);
-      u32x4 val = {0u, 0u, 0u, 0u};
-      if (row < g.nh) {
-        const int xw = row % g.hw, xh = (row / g.hw) % g.hh, xd = row / (g.hw * g.hh);
-        const int zd = q0d + xd, zh = q0h + xh, zw = q0w + xw, cc = c * 32 + sch * 8;
-        if (zd < g.qd && zh < g.qh && zw < g.qw && cc < g.cy)
-          val = *reinterpret_cast<const u32x4*>(dy + ((((long long)nn * g.qd + zd) * g.qh + zh) * g.qw + zw) * g.cy + cc);
-      }
-      hpre[i] = val;
+      const int xw = row % g.hw, xh = (row / g.hw) % g.hh, xd = row / (g.hw * g.hh);
+      const int zd = q0d + xd, zh = q0h + xh, zw = q0w + xw, cc = c * 32 + sch * 8;
+      const bool ok = row < g.nh && zd < g.qd && zh < g.qh && zw < g.qw && cc < g.cy;
+      const unsigned off = ok ? (unsigned)(((((nn * g.qd + zd) * g.qh + zh) * g.qw + zw) * g.cy + cc) * 2) : 0xFFFFFFF0u;
+      hpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0));
     }
   };
   auto w_load = [&](int c) {  // rows (tap t, co): 4 consecutive threads read one row's 64 B
 #pragma unroll
     for (int i = 0; i < S2_WLD; ++i) {
       const int id = tid + i * S2_NT;
-      u32x4 val = {0u, 0u, 0u, 0u};
-      if (id < S2_NWR * 4) {
-        const int row = id >> 2, t = row >> 5, co = co0 + (row & 31);
-        if (co < g.cx_p)
-          val = *reinterpret_cast<const u32x4*>(wpk + ((long long)t * g.cx_p + co) * g.cy_p + c * 32 + (id & 3) * 8);
-      }
-      wpre[i] = val;
+      const int row = id >> 2, t = row >> 5, co = co0 + (row & 31);
+      const bool ok = id < S2_NWR * 4 && co < g.cx_p;
+      const unsigned off = ok ? (unsigned)(((t * g.cx_p + co) * g.cy_p + c * 32 + (id & 3) * 8) * 2) : 0xFFFFFFF0u;
+      wpre[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
     }
   };
   auto commit = [&]() {
@@ -223,6 +222,9 @@ extern "C" int u3d_conv_dgrad_s2(const void* dy, int n, int cout, const void* wp
   g.nct = g.cx_p / 32;
   const long long nwg = (long long)n * g.nbd * g.nbh * g.nbw * g.nct;
   U3D_REQUIRE(nwg < (1LL << 31), "conv_dgrad_s2: grid too large");
+  U3D_REQUIRE((long long)n * g.qd * g.qh * g.qw * g.cy * 2 < (1LL << 31) - 64 &&
+              27LL * g.cx_p * g.cy_p * 2 < (1LL << 31) - 64,
+              "conv_dgrad_s2: dy / weights beyond the 2 GiB buffer-offset range");
   hipLaunchKernelGGL(dgrad_s2_kernel, dim3((unsigned)nwg), dim3(S2_NT), 0, (hipStream_t)stream, (const bf16*)dy,
                      (const bf16*)wpk_dgrad, (bf16*)dx, g);
   return check_launch("dgrad_s2_kernel");

@@ -79,8 +79,13 @@ __global__ __launch_bounds__(1024) void stem1_wtab_kernel(const T* __restrict__ 
 template <typename T>
 __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                                                        T* __restrict__ y, int d, int h, int w, long long nvox) {
-  const long long v = (long long)blockIdx.x * ST + threadIdx.x;
-  if (v >= nvox) return;
+  __shared__ __attribute__((aligned(16))) char tr[sizeof(T) == 2 ? ST / 64 : 1][64 * 64];  // bf16: 4 KB per wave
+  const long long v0 = (long long)blockIdx.x * ST + (threadIdx.x & ~63);  // the wave's first voxel
+  const long long vr = (long long)blockIdx.x * ST + threadIdx.x;
+  if constexpr (sizeof(T) != 2) {
+    if (vr >= nvox) return;
+  }
+  const long long v = vr < nvox ? vr : nvox - 1;  // (bf16: every lane takes part in the wave's LDS transpose)
   const int xx = (int)(v % w);
   const long long r = v / w;
   const int yy = (int)(r % h);
@@ -114,14 +119,37 @@ __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__
       }
     }
   }
-  T* yr = y + v * 32;
   constexpr int VEC = 16 / sizeof(T);
+  if constexpr (sizeof(T) == 2) {
+    // through the wave's LDS block: lane l's 4 chunks go to row l (chunk slot XOR (l >> 2) & 3: conflict-free), then
+    // lane l reads linear chunks l + 64k, so each store instruction writes 1 KB of consecutive voxels
+    char* wb = tr[threadIdx.x >> 6];
+    const int l = threadIdx.x & 63;
 #pragma unroll
-  for (int c = 0; c < 32; c += VEC) {
-    float o[VEC];
+    for (int c4 = 0; c4 < 4; ++c4) {
+      float o[VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) o[e] = acc[(c + e) >> 1][(c + e) & 1];
-    store16<T>(yr + c, o);
+      for (int e = 0; e < VEC; ++e) o[e] = acc[(8 * c4 + e) >> 1][(8 * c4 + e) & 1];
+      u32x4 pk;
+      store16<T>(reinterpret_cast<T*>(&pk), o);
+      *reinterpret_cast<u32x4*>(wb + l * 64 + 16 * (c4 ^ ((l >> 2) & 3))) = pk;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = l + 64 * k, vx = p >> 2, c4 = p & 3;
+      const u32x4 pk = *reinterpret_cast<const u32x4*>(wb + vx * 64 + 16 * (c4 ^ ((vx >> 2) & 3)));
+      if (v0 + vx < nvox) *reinterpret_cast<u32x4*>(y + (v0 + vx) * 32 + 8 * c4) = pk;
+    }
+  } else {
+    T* yr = y + v * 32;
+#pragma unroll
+    for (int c = 0; c < 32; c += VEC) {
+      float o[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) o[e] = acc[(c + e) >> 1][(c + e) & 1];
+      store16<T>(yr + c, o);
+    }
   }
 }
 
