@@ -21,6 +21,7 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 struct WBGeom {
+  int n;
   int cin, cout, cin_p, cout_p;
   int id, ih, iw;
   int od, oh, ow;
@@ -41,7 +42,9 @@ __device__ __forceinline__ bf16x8 frag_from(v4i16 lo, v4i16 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int BD, int BH, int BW, int S, int NCO = 1>
+// BUF: operands below 2 GiB -> branch-free buffer loads with 32-bit offsets (a masked piece reads zeros at the
+// sentinel offset; a divergent branch around each prefetch load pulls its wait ahead of the MFMAs it should overlap)
+template <int BD, int BH, int BW, int S, int NCO = 1, bool BUF = false>
 __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                             const float* __restrict__ gstat,
                                                             const float* __restrict__ gamma,
@@ -108,30 +111,46 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
     n = (int)(t / g.nbd);
     od0 = bd_ * BD; oh0 = bh_ * BH; ow0 = bw_ * BW;
   };
+  const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)dy, 0, BUF ? g.n * g.od * g.oh * g.ow * g.cout * 2 : 0,
+                                                     0x00020000);
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, BUF ? g.n * g.id * g.ih * g.iw * g.cin * 2 : 0,
+                                                     0x00020000);
   auto prefetch = [&](long long b) {
     int n, od0, oh0, ow0;
     decode(b, n, od0, oh0, ow0);
 #pragma unroll
     for (int i = 0; i < DYL; ++i) {
       const int v = drow0 + i * DRPP;
-      u32x4 val = {0u, 0u, 0u, 0u};
       const int vw = v % BW, vh = (v / BW) % BH, vd = v / (BW * BH);
       const int zd = od0 + vd, zh = oh0 + vh, zw = ow0 + vw, co = co0 + dch * 8;
-      if (v < NV && zd < g.od && zh < g.oh && zw < g.ow && co < g.cout)
-        val = *reinterpret_cast<const u32x4*>(dy + ((((long long)n * g.od + zd) * g.oh + zh) * g.ow + zw) * g.cout + co);
-      pdy[i] = val;
+      const bool ok = v < NV && zd < g.od && zh < g.oh && zw < g.ow && co < g.cout;
+      if constexpr (BUF) {
+        const unsigned off = ok ? (unsigned)(((((n * g.od + zd) * g.oh + zh) * g.ow + zw) * g.cout + co) * 2) : 0xFFFFFFF0u;
+        pdy[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0));
+      } else {
+        u32x4 val = {0u, 0u, 0u, 0u};
+        if (ok)
+          val = *reinterpret_cast<const u32x4*>(dy + ((((long long)n * g.od + zd) * g.oh + zh) * g.ow + zw) * g.cout + co);
+        pdy[i] = val;
+      }
     }
     const int id0 = od0 * S - 1, ih0 = oh0 * S - 1, iw0 = ow0 * S - 1, c = ci0 + ch * 8;
 #pragma unroll
     for (int i = 0; i < HLL; ++i) {
       const int v = row0 + i * RPP;
-      u32x4 val = {0u, 0u, 0u, 0u};
       const int hw = v % HW, hh = (v / HW) % HH, hd = v / (HW * HH);
       const int zd = id0 + hd, zh = ih0 + hh, zw = iw0 + hw;
-      if (v < NH && (unsigned)zd < (unsigned)g.id && (unsigned)zh < (unsigned)g.ih && (unsigned)zw < (unsigned)g.iw &&
-          c < g.cin)
-        val = *reinterpret_cast<const u32x4*>(x + ((((long long)n * g.id + zd) * g.ih + zh) * g.iw + zw) * g.cin + c);
-      phl[i] = val;
+      const bool ok = v < NH && (unsigned)zd < (unsigned)g.id && (unsigned)zh < (unsigned)g.ih &&
+                      (unsigned)zw < (unsigned)g.iw && c < g.cin;
+      if constexpr (BUF) {
+        const unsigned off = ok ? (unsigned)(((((n * g.id + zd) * g.ih + zh) * g.iw + zw) * g.cin + c) * 2) : 0xFFFFFFF0u;
+        phl[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      } else {
+        u32x4 val = {0u, 0u, 0u, 0u};
+        if (ok)
+          val = *reinterpret_cast<const u32x4*>(x + ((((long long)n * g.id + zd) * g.ih + zh) * g.iw + zw) * g.cin + c);
+        phl[i] = val;
+      }
     }
   };
   auto commit = [&](long long b) {
@@ -274,7 +293,7 @@ struct W1Geom {
   int gn_groups;
 };
 
-template <int S>
+template <int S, bool BUF = false>
 __global__ __launch_bounds__(512, 1) void wgrad1_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                        const float* __restrict__ gstat,
                                                        const float* __restrict__ gamma,
@@ -302,10 +321,38 @@ __global__ __launch_bounds__(512, 1) void wgrad1_kernel(const bf16* __restrict__
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 
+  // BUF (operands below 2 GiB): branch-free buffer loads with 32-bit offsets and indices (a divergent branch around
+  // each prefetch load pulls its wait ahead of the MFMAs it should overlap)
+  const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)dy, 0, BUF ? (int)(g.nvox * g.cout * 2) : 0, 0x00020000);
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, 0, BUF ? (int)((long long)g.nvox / ((long long)g.od * g.oh * g.ow) * g.id * g.ih * g.iw * g.cin * 2) : 0,
+      0x00020000);
   auto prefetch = [&](long long c0) {
 #pragma unroll
     for (int i = 0; i < LD; ++i) {
       const long long v = c0 + row0 + i * RPP;
+      if constexpr (BUF) {
+        const int vi = (int)v, co = co0 + ch * 8, ci = ci0 + ch * 8;
+        const bool ok = v < v1;
+        int n, src;
+        if (S == 1) {
+          n = vi / (g.od * g.oh * g.ow);
+          src = vi;
+        } else {
+          int t = vi;
+          const int qw = t % g.ow; t /= g.ow;
+          const int qh = t % g.oh; t /= g.oh;
+          const int qd = t % g.od;
+          n = t / g.od;
+          src = ((n * g.id + 2 * qd) * g.ih + 2 * qh) * g.iw + 2 * qw;
+        }
+        const unsigned ob = ok && co < g.cout ? (unsigned)((vi * g.cout + co) * 2) : 0xFFFFFFF0u;
+        const unsigned oa = ok && ci < g.cin ? (unsigned)((src * g.cin + ci) * 2) : 0xFFFFFFF0u;
+        pdy[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, ob, 0, 0));
+        pa[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, oa, 0, 0));
+        pn[i] = ok ? n : -1;
+        continue;
+      }
       u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
       int n = -1;
       if (v < v1) {
@@ -422,6 +469,7 @@ extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int ci
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0),
               "wgrad_brick: bad GroupNorm prologue");
   WBGeom g{};
+  g.n = n;
   g.cin = cin; g.cout = cout; g.cin_p = round_up(cin, 32); g.cout_p = round_up(cout, 32);
   g.id = d; g.ih = h; g.iw = w;
   g.od = (d - 1) / stride + 1; g.oh = (h - 1) / stride + 1; g.ow = (w - 1) / stride + 1;
@@ -438,18 +486,23 @@ extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int ci
                            (size_t)(nsplit - ns_eff) * 27 * g.cout_p * g.cin_p * 4, s));
   const int nco = wb_nco(stride, cout);
   dim3 grid(g.cin_p / 32, g.cout_p / 32 / nco, ns_eff);
-  if (stride == 2 && nco == 2)
-    hipLaunchKernelGGL((wgrad_brick_kernel<2, 4, 8, 2, 2>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
-                       gn_stats, gn_gamma, gn_beta, partials, g);
-  else if (stride == 1 && bd == 2)
-    hipLaunchKernelGGL((wgrad_brick_kernel<2, 8, 16, 1>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
-                       gn_stats, gn_gamma, gn_beta, partials, g);
-  else if (stride == 1)
-    hipLaunchKernelGGL((wgrad_brick_kernel<3, 8, 16, 1>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
-                       gn_stats, gn_gamma, gn_beta, partials, g);
-  else
-    hipLaunchKernelGGL((wgrad_brick_kernel<2, 4, 8, 2>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,
-                       gn_stats, gn_gamma, gn_beta, partials, g);
+  // buffer loads where both operands fit the 32-bit offset range (the > 2 GiB whole-volume case keeps 64-bit loads)
+  const bool buf = (long long)n * g.od * g.oh * g.ow * cout * 2 < (1LL << 31) - 64 &&
+                   (long long)n * d * h * w * cin * 2 < (1LL << 31) - 64;
+#define U3D_WB(BD_, BH_, BW_, S_, NCO_)                                                                            \
+  do {                                                                                                             \
+    if (buf)                                                                                                       \
+      hipLaunchKernelGGL((wgrad_brick_kernel<BD_, BH_, BW_, S_, NCO_, true>), grid, dim3(512), 0, s,               \
+                         (const bf16*)dy, (const bf16*)x, gn_stats, gn_gamma, gn_beta, partials, g);               \
+    else                                                                                                           \
+      hipLaunchKernelGGL((wgrad_brick_kernel<BD_, BH_, BW_, S_, NCO_, false>), grid, dim3(512), 0, s,              \
+                         (const bf16*)dy, (const bf16*)x, gn_stats, gn_gamma, gn_beta, partials, g);               \
+  } while (0)
+  if (stride == 2 && nco == 2) U3D_WB(2, 4, 8, 2, 2);
+  else if (stride == 1 && bd == 2) U3D_WB(2, 8, 16, 1, 1);
+  else if (stride == 1) U3D_WB(3, 8, 16, 1, 1);
+  else U3D_WB(2, 4, 8, 2, 1);
+#undef U3D_WB
   return check_launch("wgrad_brick_kernel");
 }
 
@@ -484,11 +537,19 @@ extern "C" int u3d_conv_wgrad1(const void* dy, const void* x, int n, int cin, in
     U3D_HIP(hipMemsetAsync(partials + (long long)ns_eff * g.cout_p * g.cin_p, 0,
                            (size_t)(nsplit - ns_eff) * g.cout_p * g.cin_p * 4, s));
   dim3 grid(g.cin_p / 32, g.cout_p / 32, ns_eff);
-  if (stride == 1)
-    hipLaunchKernelGGL(wgrad1_kernel<1>, grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats, gn_gamma,
-                       gn_beta, partials, g);
-  else
-    hipLaunchKernelGGL(wgrad1_kernel<2>, grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x, gn_stats, gn_gamma,
-                       gn_beta, partials, g);
+  // buffer loads and 32-bit indices where both operands fit the 32-bit offset range
+  const bool buf = g.nvox * cout * 2 < (1LL << 31) - 64 && (long long)n * d * h * w * cin * 2 < (1LL << 31) - 64;
+#define U3D_W1(S_)                                                                                                \
+  do {                                                                                                            \
+    if (buf)                                                                                                      \
+      hipLaunchKernelGGL((wgrad1_kernel<S_, true>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,        \
+                         gn_stats, gn_gamma, gn_beta, partials, g);                                               \
+    else                                                                                                          \
+      hipLaunchKernelGGL((wgrad1_kernel<S_, false>), grid, dim3(512), 0, s, (const bf16*)dy, (const bf16*)x,       \
+                         gn_stats, gn_gamma, gn_beta, partials, g);                                               \
+  } while (0)
+  if (stride == 1) U3D_W1(1);
+  else U3D_W1(2);
+#undef U3D_W1
   return check_launch("wgrad1_kernel");
 }

@@ -98,6 +98,8 @@ CASES["dgrad1_s2_96"] = lambda: _dgrad(2, 32, 64, 96, 1, 2)
 CASES["dgrad1_s2_48"] = lambda: _dgrad(2, 64, 128, 48, 1, 2)
 CASES["fwd1_s2_96"] = lambda: _fwd(2, 32, 64, 96, 1, 2, True, False)
 CASES["fwd96_nores"] = lambda: _fwd(2, 32, 32, 96, 3, 1, True, False)
+CASES["wgrad1_96"] = lambda: _wgrad(2, 32, 16, 96, 1, 1)      # the head's 1^3 weight gradient
+CASES["wgrad1_s2_96"] = lambda: _wgrad(2, 32, 64, 96, 1, 2)   # layer1 downsample
 CASES["fwd96_nogn"] = lambda: _fwd(2, 32, 32, 96, 3, 1, False, True)
 CASES["fwd96_plain"] = lambda: _fwd(2, 32, 32, 96, 3, 1, False, False)
 CASES["head96"] = lambda: _fwd(2, 32, 16, 96, 1, 1, True, False)
