@@ -65,8 +65,10 @@ __global__ __launch_bounds__(HD_T) void head_fwd_kernel(const bf16* __restrict__
       const long long row = tile * 32 + r;
       const bool ok = tile < tiles && row < n * v;
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        a[s] = ok ? *reinterpret_cast<const u32x4*>(x + row * cin + 16 * s + 8 * h) : u32x4{0u, 0u, 0u, 0u};
+      for (int s = 0; s < KS; ++s) {  // clamped row, no branch around the load (its wait would land right after it)
+        const u32x4 t = *reinterpret_cast<const u32x4*>(x + (ok ? row : 0) * cin + 16 * s + 8 * h);
+        a[s] = ok ? t : u32x4{0u, 0u, 0u, 0u};
+      }
     };
     u32x4 a[KS], an[KS];
     load(wid, a);

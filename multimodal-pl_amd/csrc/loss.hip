@@ -104,12 +104,13 @@ __global__ __launch_bounds__(LT) void loss_partial_kernel(const float* __restric
       long long v = blockIdx.x * (long long)LT + threadIdx.x;
       f32x4 cur[NC / 4], nxt[NC / 4];
       float tcur = 0.f, tnxt = 0.f;
+      // (clamped index, no branch around the loads: a divergent branch makes the wait for the prefetch land at
+      // the branch merge, right after it is issued)
       auto load = [&](long long vv, f32x4 (&q)[NC / 4], float& t) {
-        if (vv < nvox) {
+        vv = vv < nvox ? vv : nvox - 1;
 #pragma unroll
-          for (int k = 0; k < NC / 4; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + vv * NC + 4 * k);
-          t = lab[vv];
-        }
+        for (int k = 0; k < NC / 4; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + vv * NC + 4 * k);
+        t = lab[vv];
       };
       load(v, cur, tcur);
       for (; v < nvox; v += stride) {
@@ -266,12 +267,11 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
       long long v = blockIdx.x * (long long)LT + threadIdx.x;
       f32x4 cur[4], nxt[4];
       float tcur = 0.f, tnxt = 0.f;
-      auto load = [&](long long vv, f32x4 (&q)[4], float& t) {
-        if (vv < nvox) {
+      auto load = [&](long long vv, f32x4 (&q)[4], float& t) {  // clamped index, no branch (see the forward)
+        vv = vv < nvox ? vv : nvox - 1;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + vv * 16 + 4 * k);
-          t = lab[vv];
-        }
+        for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + vv * 16 + 4 * k);
+        t = lab[vv];
       };
       load(v, cur, tcur);
       for (; v < nvox; v += stride) {
