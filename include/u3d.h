@@ -186,6 +186,15 @@ int u3d_conv32_ring_q(int flip, const void* x, int n, int d, int h, int w, const
                       float* stats_ws, int* queue, u3d_stream_t stream);
 int u3d_conv32_ring_q_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
                                      u3d_stream_t stream);
+/* Data gradient of conv(relu(gn(x))) (flip = 1 ring, wpk = the data-gradient pack) with the GroupNorm backward's
+ * partial pass fused into the epilogue: da = conv^T(dy) exactly as u3d_conv32_ring(1, ...), and parts receives
+ * [n][u3d_conv32_ring_wps(n, d, h, w)][32][2] floats = per workgroup and channel (sum g, sum g * xhat), g = da where
+ * the forward prologue's relu passed (x = that prologue's input, gn_* = its GroupNorm). u3d_gn_bwd_parts finishes
+ * the backward. Replaces u3d_gn_bwd's partial pass over (da, x) (NoBottleneck gn1/gn2 backward, unet3D.py:44-53). */
+int u3d_conv32_ring_wps(int n, int d, int h, int w);
+int u3d_conv32_ring_dgrad_gn(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad, const void* x,
+                             const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                             void* da, float* parts, u3d_stream_t stream);
 /* Stride-1 3^3 weight gradient, depth-streaming ring schedule (wgrad_ring.hip): same partial-slab contract as
  * u3d_conv_wgrad_brick ([nsplit][27][cout_p][cin_p] fp32, summed by the caller in fixed order); a split is a
  * contiguous range of 16x16-voxel output planes walked down d. */
@@ -261,6 +270,12 @@ int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v, int groups
 int u3d_gn_bwd(int dtype, const void* da, const void* x, int n, int c, long long v, int groups,
                const float* stats, const float* gamma, const float* beta, void* dx, int accumulate,
                float* dgamma, float* dbeta, int accumulate_params, float* ws, u3d_stream_t stream);
+/* u3d_gn_bwd (bf16) from per-channel partials already summed by the producer (u3d_conv32_ring_dgrad_gn): parts
+ * [n][nparts][c][2] = (sum g, sum g * xhat); a one-block fixed-order fp64 finalize writes the coefficients and
+ * dgamma/dbeta, then the same elementwise apply as u3d_gn_bwd. Same ws rules. */
+int u3d_gn_bwd_parts(const void* da, const void* x, int n, int c, long long v, int groups, const float* stats,
+                     const float* gamma, const float* beta, const float* parts, int nparts, void* dx, int accumulate,
+                     float* dgamma, float* dbeta, int accumulate_params, float* ws, u3d_stream_t stream);
 /* Backward of two GroupNorm+ReLU consumers of the same x with the same statistics (NoBottleneck gn1 and the
  * downsample GN of a stage's first block, unet3D.py:44-53, :1666-1686): dx (+)= GN-bwd(dA1; gamma1, beta1) +
  * GN-bwd(dA2; gamma2, beta2) in one partial pass and one apply pass; dgamma/dbeta of both (+= when acc). */

@@ -110,7 +110,12 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float* __restrict__ spart,
                                                               RGGeom g, int* __restrict__ queue = nullptr) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024 + 512];
+  // GN on the forward (!FLIP): GroupNorm + ReLU prologue on the staged input. GN on the data gradient (FLIP): the
+  // backward of that prologue's GroupNorm starts in the epilogue — res = x (the forward's pre-GroupNorm input), and
+  // per channel (sum g, sum g*xhat) of g = relu-mask * dA go to spart[workgroup][32][2] (u3d_gn_bwd_parts finishes)
+  constexpr bool PRO = GN && !FLIP, GB = GN && FLIP, LDR = RES || GB;
+  static_assert(!(GB && (Q || RES)), "the fused GroupNorm backward runs on the static data-gradient ring only");
+  __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024 + 512 + (GB ? 512 : 0)];
   char* const ring = smem;
   char* const wts = smem + 4 * RG_SS;
   char* const junk = wts + 4 * RG_NWR * 16;  // target of the staging lanes past the plane's last row
@@ -204,7 +209,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   // buffer loads: out-of-range offsets return zeros with no branch around the load (no exec-masked paths whose
   // merge would make the wait-count insertion pessimistic)
   const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)g.xbytes, 0x00020000);
-  const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, RES ? (int)g.xbytes : 0, 0x00020000);
+  const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, LDR ? (int)g.xbytes : 0, 0x00020000);
   f32x2 sc[4], sh[4];
   int gn_n = -1;
   // branch-free staging: out-of-volume rows load a valid dummy address and are zeroed when written
@@ -224,7 +229,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     for (int i = 0; i < RG_LD; ++i) load_piece(p, i, v, m);
   };
   auto gn_table = [&](const RGPlane& p) {
-    if (GN && p.valid && p.n != gn_n) {
+    if (PRO && p.valid && p.n != gn_n) {
       gn_n = p.n;
       gn_coef8(gstat, gamma, beta, g.gn_groups, 32, p.n, ch * 8, sc, sh);
     }
@@ -232,8 +237,8 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   auto write_piece = [&](int i, const u32x4& v, unsigned m, int slot) {
     const int row = srow + i * (RG_NT / 4);
     u32x4 val = v;
-    if constexpr (GN) val = gn_relu8(v, sc, sh);
-    if constexpr (GN) if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
+    if constexpr (PRO) val = gn_relu8(v, sc, sh);
+    if constexpr (PRO) if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
     char* dst = row < RG_NR ? ring + slot * RG_SS + ch * RG_PS + row * 16 : junk + (tid & 63) * 16;
     *reinterpret_cast<u32x4*>(dst) = val;
   };
@@ -251,6 +256,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   pend.ok = pend.ok1 = false;
   pend.vox = 0;
   pend.chunk = -1;
+  pend.rv[0] = pend.rv[1] = u32x4{0u, 0u, 0u, 0u};  // (GB reads them before the first computed plane)
   // GroupNorm(16, 32) statistics of the output (GN variants = the forward convs whose outputs feed the next
   // GroupNorm), from the fp32 values just before the final bf16 rounding (no unpack; the voxel's in-volume flag
   // selects): 4 (sum, sum of squares) pairs per lane, fp32 over the lane's voxels, reduced per workgroup at the end.
@@ -265,6 +271,21 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
 #pragma unroll
   for (int j = 0; j < NSL; ++j) gs[j] = gq[j] = 0.f;
   int acc_chunk = -1;
+  // GB: this lane's 8 channels after the swap (cbase..cbase+7) of the workgroup's one sample: mask coefficients
+  // (the forward prologue's x*sc + sh > 0 test), xhat = (x - mu)*rs, and (sum g, sum g*xhat) accumulators
+  // (table in LDS [channel][sc, sh, rs, -mu*rs]: registers are what the weight steps need)
+  float bs1[GB ? 8 : 1], bs2[GB ? 8 : 1];
+  f32x4* const gtab = reinterpret_cast<f32x4*>(smem + 4 * RG_SS + 4 * RG_NWR * 16 + 1536);
+  if constexpr (GB) {
+    if (tid < 32) {
+      const int smp = bid / g.wps, gr = tid / (32 / g.gn_groups);
+      const float mu = gstat[(smp * g.gn_groups + gr) * 2], rs = gstat[(smp * g.gn_groups + gr) * 2 + 1];
+      const float scv = rs * gamma[tid];
+      gtab[tid] = f32x4{scv, beta[tid] - mu * scv, rs, mu};
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bs1[e] = bs2[e] = 0.f;
+  }
   // work-queue mode: the statistics of one chunk, per wave: reduce over the wave's voxels (xor within the 32-lane
   // halves) and write slot (chunk, wave); no barrier, so it can run inside the MFMA chain
   auto flush = [&](int c) __attribute__((always_inline)) {
@@ -284,10 +305,10 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gs[j] = gq[j] = 0.f;
+    for (int j = 0; j < NSL; ++j) gs[j] = gq[j] = 0.f;
   };
   auto epilogue = [&](const Pending& p) __attribute__((always_inline)) {
-    if constexpr (Q && GN) {
+    if constexpr (Q && PRO) {
       if (spart != nullptr && p.chunk != acc_chunk) {
         if (acc_chunk >= 0) flush(acc_chunk);
         acc_chunk = p.chunk;
@@ -301,7 +322,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
 #pragma unroll
     for (int vb = 0; vb < 2; ++vb) {
       const bool okv = vb ? p.ok1 : p.ok;
-      if constexpr (GN && !RES) {
+      if constexpr (PRO && !RES) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -339,6 +360,18 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         }
         store16<bf16>(reinterpret_cast<bf16*>(&v), a);
       }
+      if constexpr (GB) {  // from the stored bf16 dA, as u3d_gn_bwd's partial pass reads it
+        float a[8], xv[8];
+        load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
+        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[vb]), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const f32x4 t = gtab[cbase + e];
+          const bool m = okv && fmaf(xv[e], t[0], t[1]) > 0.f;  // selects: rows past the volume may be non-finite
+          bs1[e] += m ? a[e] : 0.f;
+          bs2[e] = fmaf(m ? a[e] : 0.f, m ? (xv[e] - t[3]) * t[2] : 0.f, bs2[e]);
+        }
+      }
       if (okv) *reinterpret_cast<u32x4*>(y + (p.vox + 16 * vb) * 32 + cbase) = v;
     }
   };
@@ -361,7 +394,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     nw.ok1 = zh < g.h && zw + 16 < g.w;
     nw.vox = (((long long)pc.n * g.d + zo) * g.h + zh) * g.w + zw;
     nw.rv[0] = nw.rv[1] = u32x4{0u, 0u, 0u, 0u};
-    if constexpr (RES) {  // the 16 B this lane stores after the swap, per voxel block
+    if constexpr (LDR) {  // the 16 B this lane stores after the swap, per voxel block (residual, or GB's x)
       const int cb2 = 2 * (16 * (q4 & 1) + 8 * (q4 >> 1));
       const unsigned r0 = nw.ok ? (unsigned)(nw.vox * 64 + cb2) : 0xFFFFFFC0u;
       const unsigned r1 = nw.ok1 ? (unsigned)((nw.vox + 16) * 64 + cb2) : 0xFFFFFFC0u;
@@ -558,7 +591,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   }
   epilogue(pend);  // the last computed plane (ok = false if none)
   if constexpr (Q) {
-    if constexpr (GN) {
+    if constexpr (PRO) {
       if (spart != nullptr && acc_chunk >= 0) flush(acc_chunk);
     }
     int* const exits = reinterpret_cast<int*>(words + gridDim.x);
@@ -572,7 +605,32 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
     return;
   }
-  if constexpr (GN) {
+  if constexpr (GB) {
+    // lanes with the same q4 hold the same 8 channels: reduce over l16, then over the waves in fixed order (LDS)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 1; o < XR; o <<= 1) {
+        bs1[e] += __shfl_xor(bs1[e], o);
+        bs2[e] += __shfl_xor(bs2[e], o);
+      }
+    float* red = reinterpret_cast<float*>(ring);  // [wave][channel 32][2]
+    if (slot_writer) {
+      const int cb0 = 16 * (q4 & 1) + 8 * (q4 >> 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 32 + cb0 + e) * 2] = bs1[e];
+        red[(wave * 32 + cb0 + e) * 2 + 1] = bs2[e];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float t = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < RG_NT / 64; ++wv) t += red[wv * 64 + tid];
+      spart[(long long)bid * 64 + tid] = t;  // [sample][wps][channel][2]: bid = sample * wps + jw
+    }
+  } else if constexpr (GN) {
     if (spart == nullptr) return;
     // lanes with the same q4 hold the same groups: reduce over l16 (xor within 16-lane rows), then over the waves in
     // fixed order through LDS (the ring is idle: every step ended with a barrier)
@@ -628,6 +686,10 @@ __global__ __launch_bounds__(64) void ring_gn_finalize_kernel(const float* __res
 }  // namespace u3d
 
 using namespace u3d;
+
+#ifndef U3D_RING_GB_KR
+#define U3D_RING_GB_KR 8  // weight steps in registers beside the fused GroupNorm-backward state
+#endif
 
 static int ring_kr(int dflt) {  // RING_KR = 0: no weight steps in registers (experiments)
   const int kr = opt(OPT_RING_KR);
@@ -798,6 +860,49 @@ extern "C" int u3d_conv32_ring(int flip, const void* x, int n, int d, int h, int
                                const void* residual, void* y, u3d_stream_t stream) {
   return conv32_ring_impl(flip, x, n, d, h, w, wpk, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, nullptr,
                           nullptr, stream);
+}
+
+// Data gradient of conv(relu(gn(x))) with the GroupNorm backward's partial pass in its epilogue: dA = conv^T(dy) is
+// stored as by u3d_conv32_ring(flip = 1), and parts[n][wps][32][2] (wps = u3d_conv32_ring_wps(n, d, h, w)) receives
+// each workgroup's per-channel (sum g, sum g*xhat), g = dA where the forward prologue's relu passed (u3d_gn_bwd's
+// partial pass, groupnorm.hip). u3d_gn_bwd_parts then writes dx. Static schedule only (deterministic partials).
+extern "C" int u3d_conv32_ring_wps(int n, int d, int h, int w) {
+  if (n < 1 || d < 1 || h < 1 || w < 1) return -1;
+  const long long pps = (long long)cdiv(h, RG_BH) * cdiv(w, RG_BW) * d;
+  const long long wps0 = std::max<long long>(1, std::min<long long>(pps, ring_wgs() / n));
+  const long long per = (pps + wps0 - 1) / wps0;
+  return (int)((pps + per - 1) / per);
+}
+
+extern "C" int u3d_conv32_ring_dgrad_gn(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad,
+                                        const void* x, const float* gn_stats, const float* gn_gamma,
+                                        const float* gn_beta, int gn_groups, void* da, float* parts,
+                                        u3d_stream_t stream) {
+  U3D_REQUIRE(dy && wpk_dgrad && x && da && parts && n >= 1 && d >= 1 && h >= 1 && w >= 1,
+              "conv32_ring_dgrad_gn: bad args");
+  U3D_REQUIRE(gn_stats && gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0, "conv32_ring_dgrad_gn: bad GN");
+  RGGeom g{};
+  g.n = n; g.d = d; g.h = h; g.w = w;
+  g.nbh = cdiv(h, RG_BH); g.nbw = cdiv(w, RG_BW);
+  g.pps = (long long)g.nbh * g.nbw * d;
+  g.planes = (long long)n * g.pps;
+  g.xbytes = (long long)n * d * h * w * 64;
+  U3D_REQUIRE(g.xbytes < (1LL << 31), "conv32_ring_dgrad_gn: tensor of %lld bytes beyond the 2 GiB buffer-offset range",
+              g.xbytes);
+  const long long wps0 = std::max<long long>(1, std::min<long long>(g.pps, ring_wgs() / n));
+  g.per = (int)((g.pps + wps0 - 1) / wps0);
+  g.wps = (int)((g.pps + g.per - 1) / g.per);
+  g.gn_groups = gn_groups;
+  const long long grid = (long long)n * g.wps;
+  const bool kr = ring_kr(1) != 0;
+#define RG_GB(K)                                                                                               \
+  hipLaunchKernelGGL((conv32_ring_kernel<true, true, false, K>), dim3((unsigned)grid), dim3(RG_NT), 0,         \
+                     (hipStream_t)stream, (const bf16*)dy, (const bf16*)wpk_dgrad, (bf16*)da, (const bf16*)x,  \
+                     gn_stats, gn_gamma, gn_beta, parts, g)
+  if (kr) RG_GB(U3D_RING_GB_KR);
+  else RG_GB(0);
+#undef RG_GB
+  return check_launch("conv32_ring_dgrad_gn");
 }
 
 extern "C" int u3d_conv32_ring_stats_ws_floats(int n) { return 64 * std::max(256, n); }

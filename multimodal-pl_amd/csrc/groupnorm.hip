@@ -240,6 +240,43 @@ __global__ __launch_bounds__(GT) void gn_stats_kernel(const T* __restrict__ x, R
   }
 }
 
+// (2) apply coefficients per (n, c) from the per-(n, c) sums cs; (3) dgamma / dbeta per c (gn_bwd_partial's last
+// block and gn_bwd_parts_finalize)
+__device__ __forceinline__ void gn_bwd_coefs(const double (*cs)[2], const RedGeom& g, const float* __restrict__ stats,
+                                             const float* __restrict__ gamma, const float* __restrict__ beta,
+                                             float* __restrict__ coef, float* __restrict__ dgamma,
+                                             float* __restrict__ dbeta, int accp) {
+  const int tid = threadIdx.x, npairs = g.n * g.c;
+  const double M = (double)g.v * g.cpg;
+  for (int p = tid; p < npairs; p += GT) {
+    const int nn = p / g.c, c = p % g.c, gr = c / g.cpg;
+    double a = 0, bb = 0;
+    for (int k = 0; k < g.cpg; ++k) {
+      const int cc = gr * g.cpg + k;
+      a += (double)gamma[cc] * cs[nn * g.c + cc][0];
+      bb += (double)gamma[cc] * cs[nn * g.c + cc][1];
+    }
+    const float ca = (float)(a / M), cb = (float)(bb / M);
+    const float mu = stats[(nn * g.groups + gr) * 2], rs = stats[(nn * g.groups + gr) * 2 + 1];
+    const float scv = rs * gamma[c];
+    float* o = coef + (long long)nn * 5 * g.c;
+    o[c] = scv;
+    o[g.c + c] = beta[c] - mu * scv;
+    o[2 * g.c + c] = rs * gamma[c];
+    o[3 * g.c + c] = -rs * rs * cb;
+    o[4 * g.c + c] = -rs * ca + rs * rs * cb * mu;
+  }
+  for (int c = tid; c < g.c; c += GT) {
+    double tg = 0, tb = 0;
+    for (int nn = 0; nn < g.n; ++nn) {
+      tb += cs[nn * g.c + c][0];
+      tg += cs[nn * g.c + c][1];
+    }
+    if (dgamma) dgamma[c] = (accp ? dgamma[c] : 0.f) + (float)tg;
+    if (dbeta) dbeta[c] = (accp ? dbeta[c] : 0.f) + (float)tb;
+  }
+}
+
 // backward: per channel s1 = sum g, s2 = sum g*xhat (g = m*dA, m = the forward prologue's relu test
 // x*sc + sh > 0), then in the last block the apply coefficients of every (n, c), SoA coef[n][5][C]:
 //   sc, sh, alpha = rs*gamma_c, bx = -rs^2 * b_g, d = -rs*a_g + rs^2*b_g*mu
@@ -300,37 +337,63 @@ __global__ __launch_bounds__(GT) void gn_bwd_partial(const T* __restrict__ da, c
   block_channel_reduce<VEC, 2>(acc, lds, g, ws + ((long long)n * g.nblk + blk) * 2 * g.c);
   if (!block_is_last(cnt, (unsigned)(g.n * g.nblk))) return;
   // (1) per (n, c): fp64 sums over the blocks, fixed order
-  const int npairs = g.n * g.c;
   combine_channels(ws, g, cs);
-  // (2) apply coefficients per (n, c); (3) dgamma / dbeta per c
-  const double M = (double)g.v * g.cpg;
-  for (int p = tid; p < npairs; p += GT) {
-    const int nn = p / g.c, c = p % g.c, gr = c / g.cpg;
-    double a = 0, bb = 0;
-    for (int k = 0; k < g.cpg; ++k) {
-      const int cc = gr * g.cpg + k;
-      a += (double)gamma[cc] * cs[nn * g.c + cc][0];
-      bb += (double)gamma[cc] * cs[nn * g.c + cc][1];
+  gn_bwd_coefs(cs, g, stats, gamma, beta, coef, dgamma, dbeta, accp);
+}
+
+// The same backward when its per-channel partials come from the data-gradient ring's epilogue
+// (u3d_conv32_ring_dgrad_gn): parts [n][nparts][c][2] = (sum g, sum g*xhat) of one workgroup; one block sums them
+// per (n, c) in fp64 in a fixed order (deterministic) and writes the apply coefficients.
+__global__ __launch_bounds__(GT) void gn_bwd_parts_finalize(const float* __restrict__ parts, int nparts, RedGeom g,
+                                                            const float* __restrict__ stats,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float* __restrict__ coef,
+                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                            int accp) {
+  __shared__ double cs[GN_PAIRS_MAX][2];
+  __shared__ double red[GT][2];
+  // GT / npairs threads per (n, c) pair (fixed slices of the parts, independent loads in flight), then the slices
+  // in fixed order: deterministic, latency of ~nparts / slices loads instead of nparts dependent ones
+  const int tid = threadIdx.x, npairs = g.n * g.c;
+  const int spl = npairs >= GT ? 1 : GT / npairs;
+  for (int p0 = 0; p0 < npairs; p0 += GT) {
+    const int p = p0 + tid % min(npairs, GT), sl = tid / min(npairs, GT);
+    double s1 = 0, s2 = 0;
+    if (p < npairs && sl < spl) {
+      const int nn = p / g.c, c = p % g.c;
+      const float* q = parts + (long long)nn * nparts * 2 * g.c + 2 * c;
+      int b = sl;
+      for (; b + 3 * spl < nparts; b += 4 * spl) {
+        float2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float2*>(q + (long long)(b + u * spl) * 2 * g.c);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s1 += v[u].x;
+          s2 += v[u].y;
+        }
+      }
+      for (; b < nparts; b += spl) {
+        const float2 v = *reinterpret_cast<const float2*>(q + (long long)b * 2 * g.c);
+        s1 += v.x;
+        s2 += v.y;
+      }
     }
-    const float ca = (float)(a / M), cb = (float)(bb / M);
-    const float mu = stats[(nn * g.groups + gr) * 2], rs = stats[(nn * g.groups + gr) * 2 + 1];
-    const float scv = rs * gamma[c];
-    float* o = coef + (long long)nn * 5 * g.c;
-    o[c] = scv;
-    o[g.c + c] = beta[c] - mu * scv;
-    o[2 * g.c + c] = rs * gamma[c];
-    o[3 * g.c + c] = -rs * rs * cb;
-    o[4 * g.c + c] = -rs * ca + rs * rs * cb * mu;
-  }
-  for (int c = tid; c < g.c; c += GT) {
-    double tg = 0, tb = 0;
-    for (int nn = 0; nn < g.n; ++nn) {
-      tb += cs[nn * g.c + c][0];
-      tg += cs[nn * g.c + c][1];
+    red[tid][0] = s1;
+    red[tid][1] = s2;
+    __syncthreads();
+    if (tid < min(npairs - p0, GT)) {
+      double t1 = 0, t2 = 0;
+      for (int k = 0; k < spl; ++k) {
+        t1 += red[k * min(npairs, GT) + tid][0];
+        t2 += red[k * min(npairs, GT) + tid][1];
+      }
+      cs[p0 + tid][0] = t1;
+      cs[p0 + tid][1] = t2;
     }
-    if (dgamma) dgamma[c] = (accp ? dgamma[c] : 0.f) + (float)tg;
-    if (dbeta) dbeta[c] = (accp ? dbeta[c] : 0.f) + (float)tb;
+    __syncthreads();
   }
+  gn_bwd_coefs(cs, g, stats, gamma, beta, coef, dgamma, dbeta, accp);
 }
 
 // dx (+)= alpha*m*dA + bx*x + d per element; grid (blocks, n): a thread's 16-B channel chunk is fixed (the
@@ -616,6 +679,26 @@ extern "C" int u3d_gn_bwd(int dtype, const void* da, const void* x, int n, int c
                        (float*)dx, accumulate);
   }
   return check_launch("gn_bwd");
+}
+
+extern "C" int u3d_gn_bwd_parts(const void* da, const void* x, int n, int c, long long v, int groups, const float* stats,
+                                const float* gamma, const float* beta, const float* parts, int nparts, void* dx,
+                                int accumulate, float* dgamma, float* dbeta, int accumulate_params, float* ws,
+                                u3d_stream_t stream) {
+  U3D_REQUIRE(da && x && stats && gamma && beta && parts && nparts >= 1 && dx && ws && groups > 0 && c % groups == 0,
+              "gn_bwd_parts: bad args");
+  U3D_REQUIRE(c % 8 == 0 && c <= 256 && n * c <= GN_PAIRS_MAX, "gn_bwd_parts: channels %d unsupported", c);
+  RedGeom g = make_geom(n, c, v, groups, 8);
+  hipStream_t s = (hipStream_t)stream;
+  float* coef = gn_coef_ptr(ws, g);
+  const long long nvec = v * g.chn;
+  const int athr = GT / g.chn * g.chn;
+  const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + athr - 1) / athr);
+  hipLaunchKernelGGL(gn_bwd_parts_finalize, dim3(1), dim3(GT), 0, s, parts, nparts, g, stats, gamma, beta, coef, dgamma,
+                     dbeta, accumulate_params);
+  hipLaunchKernelGGL(gn_bwd_apply<bf16>, dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da, (const bf16*)x, g, coef,
+                     (bf16*)dx, accumulate);
+  return check_launch("gn_bwd_parts");
 }
 
 extern "C" int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v, int groups, const float* stats,

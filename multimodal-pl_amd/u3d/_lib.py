@@ -41,6 +41,8 @@ _SIGS = {
     "u3d_conv32_ring": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring_stats_ws_floats": [I],
     "u3d_conv32_ring_stats": [P, I, I, I, I, P, P, P, P, I, P, P, P, P],
+    "u3d_conv32_ring_wps": [I, I, I, I],
+    "u3d_conv32_ring_dgrad_gn": [P, I, I, I, I, P, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring_stats_finalize": [P, I, I, I, I, P, P],
     "u3d_conv32_ring_q_stats_ws_floats": [I, I, I, I],
     "u3d_conv32_ring_q_queue_bytes": [I, I, I, I],
@@ -66,6 +68,7 @@ _SIGS = {
     "u3d_gn_stats": [I, P, I, I, L, I, P, P, P],
     "u3d_gn_apply": [I, P, I, I, L, I, P, P, P, P, P],
     "u3d_gn_bwd": [I, P, P, I, I, L, I, P, P, P, P, I, P, P, I, P, P],
+    "u3d_gn_bwd_parts": [P, P, I, I, L, I, P, P, P, P, I, P, I, P, P, I, P, P],
     "u3d_gn_bwd2": [I, P, P, P, I, I, L, I, P, P, P, P, P, P, I, P, P, P, P, I, P, P],
     "u3d_gn_bwd2_s2": [I, P, P, P, I, I, I, I, I, I, P, P, P, P, P, P, I, P, P, P, P, I, P, P],
     "u3d_upsample2x_add": [I, P, I, I, I, I, I, P, P, P],

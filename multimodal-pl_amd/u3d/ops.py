@@ -361,6 +361,26 @@ def _use_gen_brick(dtype, cin, cout, k, stride, shape):
     return max(nb * max(1, -(-cout // 64)), nb * max(1, -(-cout // 32))) >= BRICK_MIN_WG
 
 
+GN_BWD_FUSED = os.environ.get("U3D_GN_BWD_FUSED", "1") != "0"  # GroupNorm-backward partials in the ring dgrad epilogue
+
+
+def conv_dgrad_gn(dy, wpk_dgrad, cin, x, k, stride, gn):
+    """Data gradient of conv(relu(gn(x))) with the GroupNorm backward's partial pass fused into the ring epilogue
+    (u3d_conv32_ring_dgrad_gn): returns (dA, parts) for gn_bwd_parts, or None where the static 32-channel ring does
+    not run this conv (the caller then takes conv_dgrad + gn_bwd)."""
+    n, d, h, w_ = x.shape[:4]
+    if not (GN_BWD_FUSED and gn is not None and dy.shape[-1] == 32 and _use_conv32(dy.dtype, cin, 32, k, stride, n, w_)
+            and CONV32_FN == "u3d_conv32_ring" and _conv32_fits(dy) and not _ring_queue(dgrad=True)):
+        return None
+    st, ga, be, G = gn
+    wps = query("u3d_conv32_ring_wps", n, d, h, w_)
+    da = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
+    parts = torch.empty((n, wps, 32, 2), dtype=torch.float32, device=dy.device)
+    call("u3d_conv32_ring_dgrad_gn", dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), x.data_ptr(), st.data_ptr(),
+         ga.data_ptr(), be.data_ptr(), G, da.data_ptr(), parts.data_ptr(), _stream())
+    return da, parts
+
+
 def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
     n, d, h, w_ = in_shape
     cout = dy.shape[-1]
@@ -568,6 +588,20 @@ def gn_bwd(da, x, stats, gamma, beta, groups, dx=None, accumulate=False, dgamma=
     call("u3d_gn_bwd", dt_code(x.dtype), da.data_ptr(), x.data_ptr(), n, c, v, groups, stats.data_ptr(),
          gamma.data_ptr(), beta.data_ptr(), dx.data_ptr(), int(accumulate), _ptr(dgamma), _ptr(dbeta), int(acc_params),
          _gn_ws(n, c, v, x.device).data_ptr(), _stream())
+    return dx
+
+
+def gn_bwd_parts(da, x, parts, stats, gamma, beta, groups, dx=None, accumulate=False, dgamma=None, dbeta=None,
+                 acc_params=False):
+    """gn_bwd from the per-workgroup partials of conv_dgrad_gn (no partial pass over da and x)."""
+    n, c = x.shape[0], x.shape[-1]
+    v = x.numel() // (n * c)
+    if dx is None:
+        dx = torch.empty_like(x)
+        accumulate = False
+    call("u3d_gn_bwd_parts", da.data_ptr(), x.data_ptr(), n, c, v, groups, stats.data_ptr(), gamma.data_ptr(),
+         beta.data_ptr(), parts.data_ptr(), parts.shape[1], dx.data_ptr(), int(accumulate), _ptr(dgamma), _ptr(dbeta),
+         int(acc_params), _gn_ws(n, c, v, x.device).data_ptr(), _stream())
     return dx
 
 

@@ -174,7 +174,14 @@ class Tape:
                 self.pend_wgrad(part, ns, W, st, std, key + ".weight")
                 s2c = (gn is not None and pair == "park" and k == 1 and stride == 2 and ops.S2_COMPACT
                        and ops._use_conv1x1(dyT.dtype, dyT.shape[-1], cin, 1, dyT.shape[0]))
-                if s2c:  # kept at the conv's output resolution: the paired GN backward reads it in place
+                parts = None
+                if gn is not None and not head and pair != "park" and not (pair == "finish" and x.gn_pend):
+                    fused = ops.conv_dgrad_gn(dyT, pd, cin, x.t, k, stride, gn)  # GN-bwd partials in the epilogue
+                    if fused is not None:
+                        dA, parts = fused
+                if parts is not None:
+                    pass
+                elif s2c:  # kept at the conv's output resolution: the paired GN backward reads it in place
                     dA = ops.conv_dgrad_1x1s2_compact(dyT, pd, cin)
                 elif not head:
                     dA = ops.conv_dgrad(dyT, pd, cin, x.t.shape[:4], k, stride)
@@ -192,17 +199,21 @@ class Tape:
                         self.grad_done(key_ + ".weight")
                         self.grad_done(key_ + ".bias")
                 elif gn is not None:
-                    self.gn_bwd_one(x, dA, gn, gn_key, G)
+                    self.gn_bwd_one(x, dA, gn, gn_key, G, parts)
                 else:
                     self.acc_grad(x, dA)
             self.ops.append(bwd)
         return out
 
-    def gn_bwd_one(self, x, dA, gn, gn_key, G):
+    def gn_bwd_one(self, x, dA, gn, gn_key, G, parts=None):
         dg = self.grad_out(gn_key + ".weight", gn[1])
         db = self.grad_out(gn_key + ".bias", gn[2])
-        x.grad = ops.gn_bwd(dA, x.t, gn[0], gn[1], gn[2], G, dx=x.grad,
-                            accumulate=x.grad is not None, dgamma=dg, dbeta=db)
+        if parts is not None:  # partial sums already taken by the data-gradient ring (ops.conv_dgrad_gn)
+            x.grad = ops.gn_bwd_parts(dA, x.t, parts, gn[0], gn[1], gn[2], G, dx=x.grad,
+                                      accumulate=x.grad is not None, dgamma=dg, dbeta=db)
+        else:
+            x.grad = ops.gn_bwd(dA, x.t, gn[0], gn[1], gn[2], G, dx=x.grad,
+                                accumulate=x.grad is not None, dgamma=dg, dbeta=db)
         self.grad_done(gn_key + ".weight")
         self.grad_done(gn_key + ".bias")
 
