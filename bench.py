@@ -5,10 +5,13 @@ Workload (BASELINE.json configs[1]; configs[2] at N=8): the reference's 16-organ
 synthetic CT-like volumes, random-init weights. One step = forward + EDiceLoss_partial(16) (uce) + backward
 (gradient all-reduce over RCCL inside the backward when N > 1) + SGD(momentum 0.9, wd 1e-4).
 
-Prints ONE JSON line on rank 0. `roofline` is the dominant kernel (the 32->32 3^3 conv at 96^3, 50.9% of
-forward FLOPs) timed with HIP events on the stream it is launched on; `cpu_baseline` times the oracle
-(plain-PyTorch fp32 restatement) on this host's cores on the same 2x96^3 step (warm-up + median of 3).
-`--gpus N` without WORLD_SIZE in the environment starts the N ranks itself (one process per GPU).
+Prints ONE JSON line on rank 0. `roofline` is the ring kernel with the largest time per step among the full-patch
+96^3 rings (the 32->32 3^3 convs: forward, data gradient with the fused GroupNorm-backward partials, and the stride-1
+weight gradient), each launch timed with HIP events on the stream it runs on; the others are listed in
+`roofline.rings`. `infer_cfg5` is BASELINE configs[4] (sliding-window inference of a 256x512x512 volume, 80 tiles,
+bf16 and fp32). `cpu_baseline` times the oracle (plain-PyTorch fp32 restatement) on this host's cores on the same
+2x96^3 step (warm-up + median of 3). `--gpus N` without WORLD_SIZE in the environment starts the N ranks itself (one
+process per GPU); `--force-buckets` runs the N>1 gradient-bucket machinery on one GPU (RCCL at world size 1).
 """
 import argparse
 import json
@@ -40,10 +43,14 @@ def parse():
                         "(MOTSDataset.py:171-185), the batch's mask[0] applied to both (loss_partial.py:87)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-infer", action="store_true", help="skip the configs[4] sliding-window inference leg")
+    p.add_argument("--force-buckets", action="store_true",
+                   help="N=1 only: RCCL (nccl backend) at world size 1 with U3DDataParallel(force_buckets=True), i.e. "
+                        "the bucketed all-reduces launched from inside the backward and the collective-tolerant kernel "
+                        "forms while they run (what N>1 pays for the overlap, measured on one GPU)")
     p.add_argument("--print-rank-env", action="store_true", help=argparse.SUPPRESS)  # launcher test (no GPU)
     p.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph (~1%% faster at "
-                   "N=1; the roofline kernel then falls back to a standalone timing: graph event nodes are not "
-                   "timeable)")
+                   "N=1; the roofline kernel then falls back to a standalone timing)")
     return p.parse_args()
 
 
@@ -62,42 +69,84 @@ def synthetic(batch, patch, device, seed, modality="ct"):
     return x, lab, mask
 
 
-def dominant_kernel_roofline(device, batch, patch, live=None, reps=20):
-    """The 32->32 3^3 stride-1 conv (GN+ReLU prologue, residual epilogue) at patch^3, bf16. `live` = (avg ms,
-    launches, voxels) from HIP events recorded around its launches inside the timed steps (on the stream it runs
-    on); a standalone timing of the same launch is reported beside it (and used when `live` is None)."""
+# the ring kernels the bench probes at the full patch, their committed-profile tag (profiles/rNN_pmc_<tag>.json) and the
+# substring of their rocprofv3 kernel name + grid in profiles/rNN_kernel_summary.txt (tools/prof_summary.py)
+RING_TAGS = {
+    "wgrad_ring 32->32 GN": ("wgrad96", "wgrad_ring_kernel<true, 16, 16>', 1, '1', '256'"),
+    "conv32_ring dgrad +GN-bwd partials": ("dgrad96gn", "conv32_ring_kernel<true, true, false, 8, false>', 256"),
+    "conv32_ring fwd GN +res +stats": ("fwd96", "conv32_ring_kernel<false, true, true, 12, false>', 256"),
+    "conv32_ring fwd GN +stats": ("fwd96_nores", "conv32_ring_kernel<false, true, false, 16, false>', 256"),
+}
+
+
+def ring_groups(probes, full, steps):
+    """Per (label) group of the full-patch ring launches recorded in the timed steps: launches, average event time,
+    time per step, achieved TFLOP/s and the fraction of the dense bf16 peak."""
+    groups = {}
+    for e0, e1, label, flop, vox in probes:
+        if vox == full:
+            groups.setdefault(label, []).append((e0.elapsed_time(e1), flop))
+    out = []
+    for label, v in groups.items():
+        avg = sum(t for t, _ in v) / len(v)
+        flop = v[0][1]
+        ach = flop / (avg * 1e-3) / 1e12
+        out.append({"kernel": label, "launches_per_step": round(len(v) / steps, 2), "avg_launch_ms": round(avg, 4),
+                    "ms_per_step": round(sum(t for t, _ in v) / steps, 4), "flop_per_launch": flop,
+                    "achieved": round(ach, 2), "frac": round(ach / PEAK_BF16_TFLOPS, 4)})
+    out.sort(key=lambda g: -g["ms_per_step"])
+    return out
+
+
+def standalone_ms(label, device, batch, patch, reps=20):
+    """The same launch outside the step (random bf16 operands; hipGraph-free back-to-back launches): reported beside
+    the live figure, and used for `achieved` when no live probe ran (e.g. --graph)."""
     from u3d import ops
     x = torch.randn((batch, patch, patch, patch, 32), device=device).to(torch.bfloat16)
+    dy = torch.randn_like(x)
     w = torch.randn(32, 32, 3, 3, 3, device=device)
-    pf, _, _ = ops.wstd_fwd(w, torch.bfloat16, True, need_dgrad=False)
+    pf, pd, _ = ops.wstd_fwd(w, torch.bfloat16, True)
     st = ops.gn_stats(x, 16)
-    ga = torch.ones(32, device=device)
-    be = torch.zeros(32, device=device)
-    for _ in range(3):  # the production launch: GroupNorm statistics accumulated in the epilogue
-        y, _ = ops.conv_fwd_stats(x, pf, 32, 3, 1, (st, ga, be, 16), residual=x)
+    gn = (st, torch.ones(32, device=device), torch.zeros(32, device=device), 16)
+    fns = {"wgrad_ring 32->32 GN": lambda: ops.conv_wgrad(dy, x, 3, 1, gn, brick="ring"),
+           "conv32_ring dgrad +GN-bwd partials": lambda: ops.conv_dgrad_gn(dy, pd, 32, x, 3, 1, gn),
+           "conv32_ring fwd GN +res +stats": lambda: ops.conv_fwd_stats(x, pf, 32, 3, 1, gn, residual=x),
+           "conv32_ring fwd GN +stats": lambda: ops.conv_fwd_stats(x, pf, 32, 3, 1, gn)}
+    fn = fns[label]
+    for _ in range(3):
+        fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        y, _ = ops.conv_fwd_stats(x, pf, 32, 3, 1, (st, ga, be, 16), residual=x)
+        fn()
     e1.record()
     torch.cuda.synchronize()
-    ms_alone = e0.elapsed_time(e1) / reps
+    return e0.elapsed_time(e1) / reps
+
+
+def dominant_kernel_roofline(device, batch, patch, groups):
+    """Roofline line of the ring kernel with the largest time per step (HIP events around each of its launches in the
+    timed steps, on the stream it runs on); the other full-patch rings are carried beside it in `rings`."""
+    if groups:
+        dom = groups[0]
+        label, ms, src = dom["kernel"], dom["avg_launch_ms"], "HIP events, every launch of the timed steps"
+    else:
+        label, ms, src = "wgrad_ring 32->32 GN", None, "standalone"
+    ms_alone = standalone_ms(label, device, batch, patch)
+    if ms is None:
+        ms = ms_alone
     flops = 2.0 * batch * patch ** 3 * 27 * 32 * 32
-    ms, src = ms_alone, "standalone"
-    if live is not None and live[2] == batch * patch ** 3:
-        ms, src = live[0], f"HIP events, {live[1]} launches, {live[3]}"
     achieved = flops / (ms * 1e-3) / 1e12
-    del y
-    traffic, tsrc = pmc_traffic(batch, patch)
-    kname = ops.CONV32_FN.replace("u3d_", "") + "_kernel"
-    return {"kernel": "%s (conv 32->32 3^3 s1 @%d^3, GN+ReLU prologue, residual)" % (kname, patch),
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-            "traffic_source": tsrc, "algorithmic_bytes": 3 * batch * patch ** 3 * 32 * 2,
+    tag, krx = RING_TAGS.get(label, (None, None))
+    traffic, tsrc = pmc_traffic(tag, batch, patch)
+    return {"kernel": label, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+            "traffic_unit": "bytes/launch", "traffic_source": tsrc,
+            "algorithmic_bytes": 3 * batch * patch ** 3 * 32 * 2,
             "avg_launch_ms": round(ms, 4), "timing": src, "standalone_launch_ms": round(ms_alone, 4),
-            "flop_per_launch": flops, "rocprof_check": timing_check(batch, patch, flops),
-            "peak_measured": measured_peak(achieved)}
+            "flop_per_launch": flops, "trace_check": trace_check(krx, flops) if (batch, patch) == (2, 96) else None,
+            "peak_measured": measured_peak(achieved), "rings": groups}
 
 
 def newest_profile(suffix):
@@ -115,11 +164,11 @@ def newest_profile(suffix):
     return None if best is None else best[1]
 
 
-def pmc_traffic(batch, patch):
-    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
-    (profiles/rNN_pmc_conv32_fwd.json, made by tools/pmc_traffic.py: 2*FETCH_SIZE + WRITE_SIZE, gfx950
-    FETCH_SIZE correction). Only valid for the configuration it was measured on (2x96^3)."""
-    f = newest_profile("pmc_conv32_fwd.json")
+def pmc_traffic(tag, batch, patch):
+    """HBM bytes per launch of a ring kernel from the newest committed rocprofv3 PMC summary
+    (profiles/rNN_pmc_<tag>.json, made by tools/pmc_traffic.py: 2*FETCH_SIZE + WRITE_SIZE, gfx950 FETCH_SIZE
+    correction). Only valid for the configuration it was measured on (2x96^3)."""
+    f = newest_profile(f"pmc_{tag}.json") if tag else None
     if f is None or (batch, patch) != (2, 96):
         return None, None
     with open(f) as fh:
@@ -138,19 +187,23 @@ def measured_peak(achieved):
             "hbm_read_gbs": c["hbm_read_gbs"], "frac_of_measured": round(achieved / c["mfma_bf16_dense_tflops"], 4)}
 
 
-def timing_check(batch, patch, flops):
-    """The newest committed cross-check of the live event timing against the rocprofv3 kernel trace of the same
-    run (profiles/rNN_conv32_timing_check.json, tools/timing_check.py): reported beside `achieved`, with the
-    roofline fraction the trace's in-step average gives. Only valid for the configuration it was measured on."""
-    f = newest_profile("conv32_timing_check.json")
-    if f is None or (batch, patch) != (2, 96):
+def trace_check(krx, flops):
+    """The same kernel's in-step average from the newest committed rocprofv3 kernel-trace summary of the bench
+    (profiles/rNN_kernel_summary.txt, tools/prof_summary.py) and the roofline fraction it gives: the live event
+    figure must agree with it (events carry the markers' own cost, a few %)."""
+    f = newest_profile("kernel_summary.txt")
+    if f is None or krx is None:
         return None
+    import re
     with open(f) as fh:
-        c = json.load(fh)
-    return {"file": os.path.relpath(f, REPO), "in_step_events_us": c["in_step_events_us"],
-            "in_step_trace_us": c["in_step_trace_us"], "standalone_events_us": c["standalone_events_us"],
-            "standalone_trace_us": c["standalone_trace_us"],
-            "frac_at_trace_in_step": round(flops / (c["in_step_trace_us"] * 1e-6) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+        for line in fh:
+            if krx in line:
+                m = re.search(r"avg=\s*([0-9.]+)us", line)
+                if m:
+                    us = float(m.group(1))
+                    return {"file": os.path.relpath(f, REPO), "in_step_trace_us": us,
+                            "frac_at_trace": round(flops / (us * 1e-6) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+    return None
 
 
 def _cpu_model():
@@ -196,6 +249,20 @@ def cpu_baseline(batch, patch, reps=3):
                       f"1 warm-up ({warm:.2f} s) + median of {reps} ({', '.join('%.2f' % t for t in ts)} s)"}
 
 
+def infer_cfg5(device):
+    """BASELINE configs[4] on this GPU: evaluate_amos.predict_sliding over one 1x1x256x512x512 volume, 64x192x192
+    tiles, overlap 1/4 (80 tiles), the 16-organ trunk, forward only (bench_infer.measure: one warm-up volume, then one
+    timed volume per dtype). fp32 is what the reference computes there (its --FP16 flag never casts:
+    evaluate_amos.py:594-601); bf16 (fp32 accumulation) is the fast mode."""
+    import bench_infer
+    out = {"workload": "predict_sliding 1x1x256x512x512, tile 64x192x192, overlap 1/4, unet3D_baseline(16)",
+           "data": "synthetic CT-like volume, random-init weights (resident on the device)"}
+    for dt in ("bf16", "fp32"):
+        out[dt] = bench_infer.measure(device, dt, reps=1)
+    torch.cuda.empty_cache()
+    return out
+
+
 def spawn_ranks(n):
     """`bench.py --gpus N` without a launcher: start N child ranks (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous on
     127.0.0.1) before this process touches the GPU, pass their output through, exit with the worst status."""
@@ -230,6 +297,12 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
         assert dist.get_world_size() == world
+    elif a.force_buckets:
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
 
     import unet3D
     from loss_functions.loss_partial import EDiceLoss_partial
@@ -237,7 +310,7 @@ def main():
 
     torch.manual_seed(0)
     model = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=16, weight_std=True).to(device).train()
-    net = U3DDataParallel(model) if world > 1 else model
+    net = U3DDataParallel(model, force_buckets=a.force_buckets) if (world > 1 or a.force_buckets) else model
     from u3d.optim import SGD  # drop-in for torch.optim.SGD: one fused launch per 48 tensors
     opt = SGD(model.parameters(), lr=5e-4, momentum=0.9, weight_decay=1e-4)
     crit = EDiceLoss_partial(16)
@@ -259,15 +332,12 @@ def main():
         return loss
 
     graphed = None
-    a.eager = not a.graph  # default: kernel-by-kernel launches (live HIP-event timing of the roofline kernel)
+    a.eager = not a.graph  # default: kernel-by-kernel launches (live HIP-event timing of the ring kernels)
     from u3d import ops as _ops
     if not a.eager:
         from u3d.graph import GraphedStep
         try:
-            _ops.PROBE = []  # the capture records event nodes around the dominant kernel; replays re-time them
             graphed = GraphedStep(step, (x, target, mask), warmup=3, optimizer=opt)
-            probes = _ops.PROBE[-4:]
-            _ops.PROBE = None
         except Exception as e:  # capture refused (e.g. a collective backend without graph support): run eager
             print(f"[bench] hipGraph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
             torch.cuda.synchronize()
@@ -284,8 +354,9 @@ def main():
 
     for i in range(a.warmup):
         run(i)
-    if a.eager:
-        _ops.PROBE = probes = []  # events around every dominant-kernel launch of the timed steps
+    probes = []
+    if a.eager and not a.no_roofline:
+        _ops.PROBE = probes  # events around every ring-kernel launch of the timed steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -304,26 +375,23 @@ def main():
         dt = t.item()
     loss_v = float(loss)
     _ops.PROBE = None
-    live = None
-    try:  # dominant kernel timed live over the timed region (eager: every launch; graph: the last replay)
-        # only the full-patch launches: the trunk also runs a 32->32 ring conv at half resolution, whose shorter
-        # launch must not enter an average priced at the full-patch FLOPs
-        full = a.batch * a.patch ** 3
-        durs = [e0.elapsed_time(e1) for e0, e1, v in probes if v == full]
-        if durs:
-            live = (sum(durs) / len(durs), len(durs), full,
-                    "every launch of the timed steps" if a.eager else "the last timed hipGraph replay")
-    except Exception as e:  # noqa: BLE001 - event nodes not timeable on this runtime: fall back below
+    groups = []
+    try:  # the full-patch ring launches only (the trunk also runs ring kernels at 48^3 and below)
+        groups = ring_groups(probes, a.batch * a.patch ** 3, a.steps)
+    except Exception as e:  # noqa: BLE001 - event timing unavailable: fall back to the standalone launch
         print(f"[bench] live kernel timing unavailable ({e}); using the standalone measurement", file=sys.stderr)
     ms = dt / a.steps * 1e3
     vox = world * a.batch * a.patch ** 3 * a.steps / dt
 
     roof = None
     cpu = None
+    infer = None
     if rank == 0 and not a.no_roofline:
-        roof = dominant_kernel_roofline(device, a.batch, a.patch, live)
+        roof = dominant_kernel_roofline(device, a.batch, a.patch, groups)
         step_gflop = STEP_GFLOP_PER_SAMPLE * a.batch * (a.patch / 96) ** 3
         roof["step_mfma_frac"] = round(step_gflop / (ms * 1e-3) / 1e3 / PEAK_BF16_TFLOPS, 4)
+    if rank == 0 and world == 1 and not a.no_infer:
+        infer = infer_cfg5(device)
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(a.batch, a.patch)
     if rank == 0:
@@ -335,13 +403,14 @@ def main():
             "config": {"workload": "unet3D_baseline([1,2,2,2,2],16,weight_std) fwd+EDiceLoss_partial+bwd+SGD",
                        "model": "unet3D_baseline-16", "global_batch": world * a.batch, "seq_len": a.patch ** 3,
                        "patch": [a.patch] * 3, "parallelism": f"dp{world}",
-                       "backend": dist.get_backend() if world > 1 else None,
-                       "world_size_seen": dist.get_world_size() if world > 1 else 1},
+                       "backend": dist.get_backend() if dist.is_initialized() else None,
+                       "world_size_seen": dist.get_world_size() if dist.is_initialized() else 1,
+                       "force_buckets": bool(a.force_buckets)},
             "loss": round(loss_v, 6), "launch": "eager" if a.eager else "hipgraph",
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "infer_cfg5": infer,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

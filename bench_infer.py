@@ -22,6 +22,58 @@ PEAK_BF16_TFLOPS = 2500.0
 GFLOP_PER_TILE = 1025.7
 
 
+def tile_count(volume, tile, tta=False):
+    """Tiles predict_sliding visits (evaluate_amos.py:215-221: overlap 1/4, ceil strides)."""
+    import math
+    D, H, W = volume
+    sHW, sD = math.ceil(tile[1] * 0.75), math.ceil(tile[0] * 0.75)
+    return ((math.ceil((D - tile[0]) / sD) + 1) * (math.ceil((H - tile[1]) / sHW) + 1)
+            * (math.ceil((W - tile[2]) / sHW) + 1)) * (8 if tta else 1)
+
+
+def measure(dev, dtype="bf16", reps=2, volume=(256, 512, 512), tile=(64, 192, 192), classes=16, tta=False, group=None):
+    """Seconds per volume of predict_sliding (min over ``reps`` timed runs after one warm-up) and the derived rates.
+    Forward only; the volume is resident on the device before the timed region (no host transfer inside it)."""
+    import unet3D
+    import evaluate_amos as E
+    from oracle.weights_recipe import apply_recipe
+    dist = None
+    if group is not None:
+        import torch.distributed as dist
+    m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=classes, weight_std=True)
+    apply_recipe(m, seed=0)
+    m = m.to(dev).eval()
+    m.compute_dtype = torch.bfloat16 if dtype == "bf16" else torch.float32
+    g = torch.Generator(device="cpu").manual_seed(0)
+    D, H, W = volume
+    vol = ((torch.rand((1, 1, D, H, W), generator=g) * 2000 - 1000).clamp(-325, 325) / 325).to(dev)
+    with torch.no_grad():
+        out = E.predict_sliding(None, [m], vol, list(tile), classes, None, tta=tta, group=group)  # warm-up
+        torch.cuda.synchronize()
+        del out
+        ts = []
+        for _ in range(reps):
+            if group is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = E.predict_sliding(None, [m], vol, list(tile), classes, None, tta=tta, group=group)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if group is not None:
+                tt = torch.tensor([dt], device=dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                dt = float(tt)
+            ts.append(dt)
+            del out
+    tiles = tile_count(volume, tile, tta)
+    t = min(ts)
+    gflop = GFLOP_PER_TILE * tiles * (tile[0] * tile[1] * tile[2]) / (64 * 192 * 192)
+    return {"dtype": dtype, "s_per_volume": round(t, 4), "voxels_per_s": round(D * H * W / t, 1), "tiles": tiles,
+            "ms_per_tile": round(1e3 * t / tiles, 3), "conv_tflops": round(gflop / t / 1e3, 2),
+            "mfma_frac": round(gflop / t / 1e3 / PEAK_BF16_TFLOPS, 4), "runs_s": [round(x, 4) for x in ts]}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--volume", type=int, nargs=3, default=[256, 512, 512])
@@ -31,9 +83,6 @@ def main():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--tta", action="store_true")
     a = p.parse_args()
-    import unet3D
-    import evaluate_amos as E
-    from oracle.weights_recipe import apply_recipe
     world = int(os.environ.get("WORLD_SIZE", "1"))
     group = None
     if world > 1:
@@ -44,46 +93,13 @@ def main():
         group = dist.group.WORLD
     else:
         dev = torch.device("cuda:0")
-    m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=a.classes, weight_std=True)
-    apply_recipe(m, seed=0)
-    m = m.to(dev).eval()
-    m.compute_dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
-    g = torch.Generator(device="cpu").manual_seed(0)
-    D, H, W = a.volume
-    vol = ((torch.rand((1, 1, D, H, W), generator=g) * 2000 - 1000).clamp(-325, 325) / 325).to(dev)
-    with torch.no_grad():
-        out = E.predict_sliding(None, [m], vol, a.tile, a.classes, None, tta=a.tta, group=group)  # warm-up
-        torch.cuda.synchronize()
-        del out
-        ts = []
-        for _ in range(a.reps):
-            if group is not None:
-                dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            out = E.predict_sliding(None, [m], vol, a.tile, a.classes, None, tta=a.tta, group=group)
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-            if group is not None:
-                tt = torch.tensor([dt], device=dev)
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                dt = float(tt)
-            ts.append(dt)
-            del out
-    import math
-    sHW, sD = math.ceil(a.tile[1] * 0.75), math.ceil(a.tile[0] * 0.75)
-    tiles = ((math.ceil((D - a.tile[0]) / sD) + 1) * (math.ceil((H - a.tile[1]) / sHW) + 1)
-             * (math.ceil((W - a.tile[2]) / sHW) + 1)) * (8 if a.tta else 1)
-    t = min(ts)
-    gflop = GFLOP_PER_TILE * tiles * (a.tile[0] * a.tile[1] * a.tile[2]) / (64 * 192 * 192)
+    r = measure(dev, a.dtype, a.reps, tuple(a.volume), tuple(a.tile), a.classes, a.tta, group)
     if group is not None and dist.get_rank() != 0:
         dist.destroy_process_group()
         return
-    print(json.dumps({"metric": "sliding-window inference voxels/sec (configs[4])", "value": D * H * W / t,
-                      "n_gpus": world,
-                      "unit": "voxels/s", "s_per_volume": t, "tiles": tiles, "ms_per_tile": 1e3 * t / tiles,
-                      "dtype": a.dtype, "data": "synthetic CT-like volume, random-init weights",
-                      "conv_tflops": gflop / t / 1e3, "mfma_frac": gflop / t / 1e3 / PEAK_BF16_TFLOPS,
+    print(json.dumps({"metric": "sliding-window inference voxels/sec (configs[4])", "value": r["voxels_per_s"],
+                      "n_gpus": world, "unit": "voxels/s", **r,
+                      "data": "synthetic CT-like volume, random-init weights",
                       "config": {"workload": "unet3D_baseline(16) predict_sliding", "volume": a.volume,
                                  "tile": a.tile, "tta": a.tta}}))
     if group is not None:

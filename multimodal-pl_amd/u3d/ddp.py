@@ -55,15 +55,32 @@ class GradBucketer:
         self.device = params[0][1].device if params else None
         self.active = False
         self.synced = set()
+        self.on_finish = None   # set by U3DDataParallel: queues its end-of-backward callback on every rank
 
     def begin(self):
         ops.COLLECTIVE_IN_FLIGHT[0] = False  # a backward that raised before finish() must not leave it set
+        ops.COLLECTIVE_POLL[0] = self.in_flight
         self.bufs = [torch.empty(nel, dtype=torch.float32, device=self.device) for _, nel in self.buckets]
         self.left = [len(names) for names, _ in self.buckets]
         self.done_names = set()
         self.synced = set()
         self.works = [None] * len(self.buckets)
+        self.completed = set()  # buckets whose all-reduce has finished on the device
         self.active = True
+
+    def in_flight(self):
+        """True while a launched bucket's all-reduce has not completed on the device (``work.is_completed()``, a
+        non-blocking event query). ops asks this before each launch that has a collective-tolerant form, so the slower
+        work-stealing / short-range kernels run only while a collective can actually hold CUs, not from the first
+        bucket to the end of the backward."""
+        live = False
+        for b, w in enumerate(self.works):
+            if w is not None and b not in self.completed:
+                if w.is_completed():
+                    self.completed.add(b)
+                else:
+                    live = True
+        return live
 
     def out(self, name):
         if not self.active or name not in self.where:
@@ -80,7 +97,7 @@ class GradBucketer:
     def _launch(self, b):
         op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
         self.works[b] = dist.all_reduce(self.bufs[b], op=op, group=self.group, async_op=True)
-        ops.COLLECTIVE_IN_FLIGHT[0] = True  # the ring data gradients switch to work stealing until finish()
+        ops.COLLECTIVE_IN_FLIGHT[0] = True  # ops polls in_flight() from here on and clears it when all have completed
 
     def needs_flush(self, pending):
         """True if producing the ``pending`` gradients would complete a bucket (so they must be written now)."""
@@ -119,6 +136,9 @@ class GradBucketer:
         self.synced = set(self.done_names)  # averaged here: the post-accumulate hooks skip these
         self.active = False
         ops.COLLECTIVE_IN_FLIGHT[0] = False
+        ops.COLLECTIVE_POLL[0] = None
+        if self.on_finish is not None:
+            self.on_finish()
 
     def average(self, t):
         """Mean over ranks of one flat tensor, in place (stream-ordered)."""
@@ -130,14 +150,40 @@ class GradBucketer:
 
     def check_same(self, names):
         """Every rank must average the same fallback gradients in the same order: a rank whose backward reached a
-        different set would otherwise block in (or mis-pair) the collective. One all-gather of (count, crc32)."""
-        key = torch.tensor([len(names), zlib.crc32("\0".join(names).encode())], dtype=torch.int64,
-                           device=self.device if self.avg_native else "cpu")
+        different set would otherwise block in (or mis-pair) the collective. One all-gather of (count, crc32), joined
+        by every rank at the end of every backward (also by a rank that collected nothing), so the
+        all-gathers always pair. A rank with gradients to average compares at once (it needs the values before its
+        all-reduce); an empty rank with a device key defers the comparison to its next forward (a pinned copy and an
+        event: no host sync in the backward) and raises there."""
+        self.verify_pending()
+        kv = (len(names), zlib.crc32("\0".join(names).encode()))
+        key = torch.tensor(kv, dtype=torch.int64)
+        if self.avg_native:  # RCCL gathers device tensors (a pinned staging copy: no blocking H2D copy)
+            key = key.pin_memory().to(self.device, non_blocking=True)
         got = [torch.empty_like(key) for _ in range(self.world)]
         dist.all_gather(got, key, group=self.group)
-        if any(not torch.equal(g, key) for g in got):
+        if not names and key.is_cuda:
+            host = torch.empty((self.world, 2), dtype=torch.int64, pin_memory=True)
+            host.copy_(torch.stack(got), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._deferred = (host, ev, kv, names)
+            return
+        self._compare([tuple(g.tolist()) for g in got], kv, names)
+
+    def verify_pending(self):
+        """Finish a deferred consistency check (see check_same)."""
+        d, self._deferred = getattr(self, "_deferred", None), None
+        if d is not None:
+            host, ev, key, names = d
+            ev.synchronize()
+            self._compare([tuple(r) for r in host.tolist()], tuple(key), names)
+
+    @staticmethod
+    def _compare(got, key, names):
+        if any(g != key for g in got):
             raise RuntimeError(f"U3DDataParallel: ranks reached different sets of non-native parameter gradients "
-                               f"({[tuple(g.tolist()) for g in got]} as (count, crc32)); this rank: {names}")
+                               f"({got} as (count, crc32)); this rank: {names}")
 
 
 class U3DDataParallel(torch.nn.Module):
@@ -159,7 +205,9 @@ class U3DDataParallel(torch.nn.Module):
         self.bucketer = GradBucketer(module.named_parameters(), bucket_mb, group) if self.distributed else None
         self.fallback_names = []  # parameters averaged by the hook in the last backward (tests / diagnostics)
         self._pending = []        # (name, param) collected by the hooks of the running backward
+        self._cb_queued = False   # the end-of-backward callback is queued for the running backward
         if self.distributed:
+            self.bucketer.on_finish = self._queue_flush
             with torch.no_grad():  # start from identical weights on every rank (DDP's init broadcast)
                 for p in module.parameters():
                     dist.broadcast(p.data, 0, group=group)
@@ -173,16 +221,26 @@ class U3DDataParallel(torch.nn.Module):
             if name in self.bucketer.synced:  # averaged in its bucket: exempt this one accumulation
                 self.bucketer.synced.discard(name)
                 return
-            if not self._pending:
-                torch.autograd.Variable._execution_engine.queue_callback(self._flush_fallback)
+            self._queue_flush()
             self._pending.append((name, p))
         return fn
 
+    def _queue_flush(self):
+        """Queue _flush_fallback once per backward: from the first fallback hook, and from the native backward's
+        finish() on every rank, so the rank-consistency all-gather runs even where no fallback gradient arrived."""
+        if not self._cb_queued:
+            self._cb_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._flush_fallback)
+
     def _flush_fallback(self):
-        """End of the backward: one all-reduce over every gradient the hooks collected (fixed hook order)."""
+        """End of the backward: the rank-consistency check (every rank, every backward) and one all-reduce over every
+        gradient the hooks collected (fixed hook order)."""
         pend, self._pending = self._pending, []
+        self._cb_queued = False
         names = [n for n, _ in pend]
         self.bucketer.check_same(names)
+        if not pend:
+            return
         grads = [p.grad for _, p in pend]
         flat = torch.cat([g.reshape(-1).float() for g in grads])
         self.bucketer.average(flat)
@@ -195,7 +253,10 @@ class U3DDataParallel(torch.nn.Module):
     def forward(self, *args, **kwargs):
         if self.bucketer is None or not torch.is_grad_enabled():
             return self.module(*args, **kwargs)
+        self.bucketer.verify_pending()  # a deferred rank-consistency check of the previous backward raises here
         self.fallback_names = []
         self.bucketer.synced = set()  # exemptions of a previous step whose accumulation never fired do not carry over
+        self._pending = []            # a backward that raised left its collected hooks (and its callback) behind
+        self._cb_queued = False
         with use_sink(self.bucketer):
             return self.module(*args, **kwargs)

@@ -27,14 +27,18 @@ def option(name, value):
     """Temporarily set a library tuning option (csrc/common.h ``Opt``; e.g. ``option("CONVG_PERSIST", 0)``) for a test
     that compares two routings in one process; restores the previous value."""
     h = _lib.lib()
-    old = ctypes.c_int(0)
-    if h.u3d_get_option(name.encode(), ctypes.byref(old)) != 0:
-        raise _lib.U3DError(h.u3d_last_error().decode())
-    h.u3d_set_option(name.encode(), int(value))
+    if not hasattr(h, "u3d_set_option"):
+        raise _lib.U3DError(f"u3d: this libu3d build has no option table (cannot set {name})")
+    old = get_option(name)
+
+    def put(v):
+        if h.u3d_set_option(name.encode(), int(v)) != 0:
+            raise _lib.U3DError(h.u3d_last_error().decode())
+    put(value)
     try:
         yield
     finally:
-        h.u3d_set_option(name.encode(), old.value)
+        put(old)
 
 def _ptr(t):
     return None if t is None else t.data_ptr()
@@ -215,19 +219,15 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
              _ptr(ga), _ptr(be), G, y.data_ptr(), _stream())
         return y
     if _use_conv32(x.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(x) and not out_f32 and bias is None:
-        probe = PROBE is not None
-        if probe:  # bench.py: HIP events around the dominant kernel, on the stream it runs on
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
+        pr = _probe0()
         if _ring_queue():
             call("u3d_conv32_ring_q", 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
                  _ptr(residual), y.data_ptr(), None, _queue(x.device, (n, d, h, w_)), _stream())
         else:
             call(CONV32_FN, 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), _ptr(st), _ptr(ga), _ptr(be), G,
                  _ptr(residual), y.data_ptr(), _stream())
-        if probe:
-            e1.record()
-            PROBE.append((e0, e1, n * d * h * w_))
+        _probe1(pr, "conv32_ring fwd" + (" GN" if st is not None else "") + (" +res" if residual is not None else ""),
+                2.0 * n * d * h * w_ * 27 * 32 * 32, n * d * h * w_)
         return y
     if _use_small(x.dtype, cin, cout, k, stride, (n, d, h, w_)) and not out_f32 and bias is None:
         ws = WS.get(SPLITK_WS_BYTES, x.device, slot=4)
@@ -263,19 +263,15 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
         q = _ring_queue()
         nws = query("u3d_conv32_ring_q_stats_ws_floats", n, d, h, w_) if q else query("u3d_conv32_ring_stats_ws_floats", n)
         ws = WS.get(4 * nws, x.device, slot=9)
-        probe = PROBE is not None
-        if probe:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
+        pr = _probe0()
         if q:
             call("u3d_conv32_ring_q", 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
                  be.data_ptr(), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), _queue(x.device, (n, d, h, w_)), _stream())
         else:
             call("u3d_conv32_ring_stats", x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
                  be.data_ptr(), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), _stream())
-        if probe:
-            e1.record()
-            PROBE.append((e0, e1, n * d * h * w_))
+        _probe1(pr, "conv32_ring fwd GN" + (" +res" if residual is not None else "") + " +stats",
+                2.0 * n * d * h * w_ * 27 * 32 * 32, n * d * h * w_)
         fin = "u3d_conv32_ring_q_stats_finalize" if q else "u3d_conv32_ring_stats_finalize"
         call(fin, ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
         return y, stats
@@ -298,15 +294,23 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
 
 # Work-stealing ring (u3d_conv32_ring_q): robust to a concurrent kernel holding CUs (a late workgroup's range is
 # taken over by the others instead of doubling the launch), but 10-25% slower alone (tools/concurrency.py,
-# profiles/r02_concurrency.json). Used for the data-gradient ring while a gradient all-reduce may be running
-# (COLLECTIVE_IN_FLIGHT, set by u3d.ddp between the first bucket launch and finish()); U3D_RING_QUEUE=1 forces it
-# for every ring launch.
+# profiles/r02_concurrency.json). Used for the data-gradient ring while a gradient all-reduce is running
+# (collective_in_flight()); U3D_RING_QUEUE=1 forces it for every ring launch.
 RING_QUEUE = os.environ.get("U3D_RING_QUEUE", "0") != "0"
-COLLECTIVE_IN_FLIGHT = [False]
+COLLECTIVE_IN_FLIGHT = [False]  # set by u3d.ddp at a bucket launch (tests may set it to force the collective forms)
+COLLECTIVE_POLL = [None]        # u3d.ddp: callable, True while a launched bucket all-reduce has not completed
+
+
+def collective_in_flight():
+    """Whether a gradient all-reduce may hold CUs now: the flag, cleared as soon as the poll (work.is_completed() of
+    every launched bucket) reports them all done, so the collective-tolerant kernel forms run only meanwhile."""
+    if COLLECTIVE_IN_FLIGHT[0] and COLLECTIVE_POLL[0] is not None and not COLLECTIVE_POLL[0]():
+        COLLECTIVE_IN_FLIGHT[0] = False
+    return COLLECTIVE_IN_FLIGHT[0]
 
 
 def _ring_queue(dgrad=False):
-    return CONV32_FN == "u3d_conv32_ring" and (RING_QUEUE or (dgrad and COLLECTIVE_IN_FLIGHT[0]))
+    return CONV32_FN == "u3d_conv32_ring" and (RING_QUEUE or (dgrad and collective_in_flight()))
 
 
 QUEUE_SLOT = 40  # workspace slot of the ring claim words (used by nothing else: the words must stay zero between launches)
@@ -321,7 +325,23 @@ def _queue(device, shape):
 BRICK_STATS = os.environ.get("U3D_BRICK_STATS", "1") != "0"  # GN statistics from the persistent brick's epilogue
 RING_STATS = os.environ.get("U3D_RING_STATS", "1") != "0"  # GroupNorm statistics from the ring conv epilogue (False: separate u3d_gn_stats pass)
 SPLITK_WS_BYTES = 64 << 20
-PROBE = None  # list -> conv32_brick forward launches record (start, end, voxels) HIP events (bench.py roofline)
+# bench.py roofline: while PROBE is a list, every launch of the 96^3-class ring kernels (conv fwd / dgrad and the
+# stride-1 weight-gradient ring) records (start event, end event, label, flop, voxels) on the stream it runs on
+PROBE = None
+
+
+def _probe0():
+    if PROBE is None:
+        return None
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    return e0, e1
+
+
+def _probe1(p, label, flop, vox):
+    if p is not None:
+        p[1].record()
+        PROBE.append((p[0], p[1], label, flop, vox))
 USE_CONV32_BRICK = True
 CONV32_FN = "u3d_conv32_ring"   # "u3d_conv32_brick": the earlier halo-brick schedule (same results)
 
@@ -376,8 +396,10 @@ def conv_dgrad_gn(dy, wpk_dgrad, cin, x, k, stride, gn):
     wps = query("u3d_conv32_ring_wps", n, d, h, w_)
     da = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
     parts = torch.empty((n, wps, 32, 2), dtype=torch.float32, device=dy.device)
+    pr = _probe0()
     call("u3d_conv32_ring_dgrad_gn", dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), x.data_ptr(), st.data_ptr(),
          ga.data_ptr(), be.data_ptr(), G, da.data_ptr(), parts.data_ptr(), _stream())
+    _probe1(pr, "conv32_ring dgrad +GN-bwd partials", 2.0 * n * d * h * w_ * 27 * 32 * 32, n * d * h * w_)
     return da, parts
 
 
@@ -390,12 +412,16 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
              None, None, 0, dx.data_ptr(), _stream())
         return dx
     if _use_conv32(dy.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(dy):
-        if _ring_queue(dgrad=True):
+        pr = _probe0()
+        q = _ring_queue(dgrad=True)
+        if q:
             call("u3d_conv32_ring_q", 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
                  dx.data_ptr(), None, _queue(dy.device, (n, d, h, w_)), _stream())
         else:
             call(CONV32_FN, 1, dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), None, None, None, 0, None,
                  dx.data_ptr(), _stream())
+        _probe1(pr, "conv32_ring dgrad" + (" (work stealing)" if q else ""), 2.0 * n * d * h * w_ * 27 * 32 * 32,
+                n * d * h * w_)
         return dx
     if USE_S2_BRICK and dy.dtype == torch.bfloat16 and k == 3 and stride == 2:
         call("u3d_conv_dgrad_s2", dy.data_ptr(), n, cout, wpk_dgrad.data_ptr(), cin, d, h, w_, dx.data_ptr(),
@@ -461,13 +487,16 @@ def conv_wgrad(dy, x, k, stride, gn=None, brick=None):
             brick = "ring"  # (the ring addresses its operands with 32-bit buffer offsets; larger ones: bricks)
     if brick == "ring":
         assert k == 3 and stride == 1 and x.dtype == torch.bfloat16
-        if WGRAD_QUEUE or COLLECTIVE_IN_FLIGHT[0]:  # short ranges the dispatcher deals to whichever CU is free
+        if WGRAD_QUEUE or collective_in_flight():  # short ranges the dispatcher deals to whichever CU is free
             ns = query("u3d_conv_wgrad_ring_splits_target", n, cin, d, h, w_, cout, WGRAD_Q_WGS)
         else:
             ns = query("u3d_conv_wgrad_ring_splits", n, cin, d, h, w_, cout)
         part = torch.empty((ns, 27, round32(cout), round32(cin)), dtype=torch.float32, device=x.device)
+        pr = _probe0()
         call("u3d_conv_wgrad_ring", dy.data_ptr(), x.data_ptr(), n, cin, d, h, w_, cout, _ptr(st), _ptr(ga), _ptr(be),
              G, part.data_ptr(), ns, _stream())
+        _probe1(pr, f"wgrad_ring {cin}->{cout}" + (" GN" if st is not None else ""),
+                2.0 * n * d * h * w_ * 27 * cin * cout, n * d * h * w_)
         return part, ns
     if brick and k == 1:
         ns = query("u3d_conv_wgrad1_splits", n, cin, d, h, w_, cout, stride)

@@ -123,7 +123,8 @@ def test_u3d_data_parallel_world2_equals_concatenated_batch(gpu, tmp_path):
 
 
 
-def test_rccl_world1_bucketed_step_matches_plain_step(gpu, monkeypatch):
+@pytest.mark.parametrize("hold", [True, False], ids=["collective-held", "polled"])
+def test_rccl_world1_bucketed_step_matches_plain_step(gpu, monkeypatch, hold):
     """The RCCL branch of the data-parallel path on the box's one GPU (never executed): torch.distributed
     backend "nccl" (= RCCL) at world size 1, U3DDataParallel forced onto its bucket machinery (1 MB buckets: the
     all-reduces are launched from inside the native backward), ReduceOp.AVG (avg_native), the async works waited on
@@ -132,14 +133,18 @@ def test_rccl_world1_bucketed_step_matches_plain_step(gpu, monkeypatch):
     (u3d_conv32_ring_q). bf16 step on 2 x 1 x 64^3 (the 32-channel convs run on the ring). Averaging over one rank is
     exact and the work-stealing ring is bitwise equal to the static one, so gradients and post-SGD weights must
     equal the plain single-process step (checked to <= 1e-6 relative; reference: train_amos_atlas_final.py:141-144,
-    375 and run_amos_atlas_final.sh:2)."""
+    375 and run_amos_atlas_final.sh:2). ``hold``: the bucketer's completion poll is pinned to "still running" (what a
+    slow all-reduce at N > 1 looks like), so the collective-tolerant kernel forms must run; "polled": the real
+    work.is_completed() poll, with which the static forms come back as soon as the world-1 all-reduces finish."""
     import torch.distributed as dist
     from loss_functions.loss_partial import EDiceLoss_partial
     from oracle.weights_recipe import input_volume, label_volume
     from u3d import _lib, ops
-    from u3d.ddp import U3DDataParallel
+    from u3d.ddp import GradBucketer, U3DDataParallel
     from u3d.optim import SGD
 
+    if hold:
+        monkeypatch.setattr(GradBucketer, "in_flight", lambda self: True)
     x = torch.from_numpy(input_volume((2, 1, 64, 64, 64), seed=61, kind="ct")).to(gpu)
     lab = torch.from_numpy(label_volume((2, 64, 64, 64), 16, seed=62)).to(gpu)
     mask = [torch.tensor(MASK)]
@@ -176,7 +181,10 @@ def test_rccl_world1_bucketed_step_matches_plain_step(gpu, monkeypatch):
     finally:
         dist.destroy_process_group()
     assert not ops.COLLECTIVE_IN_FLIGHT[0]
-    assert ("u3d_conv32_ring_q", True) in called, "no work-stealing data-gradient ring while a bucket was in flight"
+    if hold:
+        assert ("u3d_conv32_ring_q", True) in called, "no work-stealing data-gradient ring while a bucket was in flight"
+    else:
+        assert ("u3d_conv32_ring_dgrad_gn", False) in called, "the static fused ring never came back after completion"
     assert net.fallback_names == ["extra_scale"], net.fallback_names
     for k in g_ref:
         r = ((g[k] - g_ref[k]).norm() / g_ref[k].norm().clamp_min(1e-30)).item()

@@ -269,6 +269,126 @@ def test_ddp_fallback_mismatch_fails_loudly_gloo_world2():
         p.join(timeout=60)
     assert out == [(0, "raised"), (1, "raised")], out
 
+class _NativeScale(torch.autograd.Function):
+    """Stands in for a native tape (u3d.trunk._TrunkFn) in CPU tests: its parameter's gradient is written straight into
+    the DDP bucket and the bucketer's begin()/finish() run around it; ``boom`` makes its backward raise."""
+
+    @staticmethod
+    def forward(ctx, x, w, boom):
+        from u3d.ddp import current_sink
+        ctx.sink, ctx.boom = current_sink(), boom
+        ctx.save_for_backward(x)
+        if ctx.sink is not None:
+            ctx.sink.begin()
+        return x * w
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.boom:
+            raise RuntimeError("boom")
+        x, = ctx.saved_tensors
+        gw = (g * x).sum(0)
+        out = ctx.sink.out("w") if ctx.sink is not None else None
+        if out is not None:
+            out.copy_(gw)
+            ctx.sink.done("w")
+            ctx.sink.finish()
+            gw = out
+        return g * 0 + g, gw, None
+
+
+class _NativeModel(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.linspace(0.5, 1.5, 4))
+        self.lin = torch.nn.Linear(4, 3)
+        self.boom = False
+
+    def forward(self, x, extra=True):
+        y = _NativeScale.apply(x, self.w, self.boom)
+        return self.lin(y) if extra else y
+
+
+def _empty_set_worker(rank, world, port, q):
+    """Rank 0 reaches no non-native parameter at all (only the native one); rank 1 reaches the Linear: both ranks
+    must raise (rank 0 joins the consistency all-gather from the native finish()), none may hang."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    from u3d.ddp import U3DDataParallel
+    torch.manual_seed(0)
+    net = U3DDataParallel(_NativeModel())
+    try:
+        net(torch.randn(2, 4), extra=rank == 1).sum().backward()
+        q.put((rank, "no error"))
+    except RuntimeError as e:
+        q.put((rank, "raised" if "different sets" in str(e) else repr(e)))
+    dist.destroy_process_group()
+
+
+def test_ddp_fallback_mismatch_with_an_empty_rank_fails_loudly_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_set_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=60) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert out == [(0, "raised"), (1, "raised")], out
+
+
+def _raise_then_step_worker(rank, world, port, q):
+    """A backward that raises after the fallback hooks fired: the next step must still average both the
+    native bucket gradient and the fallback (Linear) gradients."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    from u3d.ddp import U3DDataParallel
+    torch.manual_seed(0)
+    m = _NativeModel()
+    net = U3DDataParallel(m)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(4, 4, generator=g)
+    m.boom = True
+    try:
+        net(x[2 * rank:2 * rank + 2]).square().sum().backward()
+        first = "no error"
+    except RuntimeError as e:
+        first = str(e)
+    m.boom = False
+    for p in m.parameters():
+        p.grad = None
+    net(x[2 * rank:2 * rank + 2]).square().sum().backward()
+    q.put((rank, first, {k: p.grad.tolist() for k, p in m.named_parameters()}, sorted(net.fallback_names)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_step_after_a_raised_backward_still_averages_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_raise_then_step_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=60) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    m = _NativeModel()
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(4, 4, generator=g)
+    (0.5 * (m(x[:2]).square().sum() + m(x[2:]).square().sum())).backward()
+    for rank, first, grads, fallback in out:
+        assert "boom" in first, first
+        assert fallback == ["lin.bias", "lin.weight"], fallback
+        for k, p in m.named_parameters():
+            assert np.allclose(grads[k], p.grad.numpy(), rtol=1e-6, atol=1e-7), (rank, k, grads[k], p.grad)
+
+
 def test_bench_gpus_flag_launches_ranks():
     """`python bench.py --gpus N` (the driver's SCALE command shape, no torchrun) starts N ranks itself, each with
     its own RANK / LOCAL_RANK / WORLD_SIZE and a 127.0.0.1 rendezvous, before any GPU call."""

@@ -74,6 +74,13 @@ def _dgrad(n, cin, cout, s, k, stride):
     return us, flop
 
 
+def _dgrad_gn(n, c, s):
+    """the production 96^3 data gradient: ring with the GroupNorm-backward partials fused in its epilogue"""
+    x, pf, pd, g, r, dy, flop = conv_case(n, c, c, s, 3, 1, True)
+    us = t_(lambda: ops.conv_dgrad_gn(dy, pd, c, x, 3, 1, g))
+    return us, flop
+
+
 def _wgrad(n, cin, cout, s, k, stride):
     x, pf, pd, g, r, dy, flop = conv_case(n, cin, cout, s, k, stride, True)
     us = t_(lambda: ops.conv_wgrad(dy, x, k, stride, g, brick={"ring": "ring", "brick": True}.get(os.environ.get("KB_WGRAD", ""))))
@@ -84,6 +91,7 @@ for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 
     CASES[f"fwd{lvl}"] = (lambda s=s, c=c: _fwd(2, c, c, s, 3, 1, True, True))
     CASES[f"dgrad{lvl}"] = (lambda s=s, c=c: _dgrad(2, c, c, s, 3, 1))
     CASES[f"wgrad{lvl}"] = (lambda s=s, c=c: _wgrad(2, c, c, s, 3, 1))
+CASES["dgrad96gn"] = lambda: _dgrad_gn(2, 32, 96)
 CASES["fwd12nogn"] = lambda: _fwd(2, 256, 256, 12, 3, 1, False, False)
 CASES["wgrad_s2_96"] = lambda: _wgrad(2, 32, 64, 96, 3, 2)
 CASES["wgrad_s2_48"] = lambda: _wgrad(2, 64, 128, 48, 3, 2)
