@@ -401,8 +401,10 @@ def get_loss_consistency(output, target, mask, attns, refine_output, label_t, co
 # ---------------------------------------------------------------------------------------------- next f4
 def truncate(ct, name):
     """AMOSDataSet_newatlas.truncate, MOTSDataset.py:171-186: CT (case id < 500) clipped to [-325, 325] and / 325;
-    MRI z-scored with np.mean / np.std (population) of the whole (padded) array. float64 as numpy computes it."""
-    ct = np.array(ct, dtype=np.float64, copy=True)
+    MRI z-scored with np.mean / np.std (population) of the whole (padded) array. numpy's own dtype rules, as the
+    reference computes (an int16 CT array is clipped in place and divided in float64; a float32 MRI array is z-scored
+    in float32 with numpy's pairwise sums): pinned bit-exact by G15."""
+    ct = np.array(ct, copy=True)
     if float(name) < 500:
         ct[ct <= -325] = -325
         ct[ct >= 325] = 325

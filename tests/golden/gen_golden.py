@@ -579,8 +579,77 @@ def g14():
          cmask=np.stack(outs))
 
 
+def _ref_lines(fname, first, last):
+    import textwrap
+    with open(os.path.join(REF, fname)) as f:
+        lines = f.read().splitlines()[first - 1:last]
+    return textwrap.dedent("\n".join(lines))
+
+
+def g15():
+    """f4 (deterministic half): AMOSDataSet_newatlas.__getitem__'s tensor work run from the reference's own lines
+    (MOTSDataset.py is not importable here: batchgenerators / SimpleITK absent). The methods ``truncate`` (:171-186),
+    ``pad_image`` (:269-282), ``pad_image2`` (:284-297) are exec'd into a class body and the getitem lines :370-397
+    (pad to crop + 5, truncate, random crop, transpose, astype) run on seeded synthetic volumes as sitk would return
+    them ([H, W, D]; CT int16 HU, MRI float32 intensities) and a 13-channel atlas already resized to the image
+    (:364). ``np.random`` is a seeded RandomState whose draws (b, c, a) are recorded; the device path draws from a
+    RandomState with the same seed. Cases: CT and MRI, volumes smaller and larger than crop + 5, train and valid."""
+    import math
+    src_methods = "\n".join(_ref_lines("MOTSDataset.py", a, b) for a, b in ((171, 186), (269, 282), (284, 297)))
+    src_get = _ref_lines("MOTSDataset.py", 370, 397).replace("return image.copy(), label.copy(), name, name, catlas",
+                                                           "out = (image.copy(), label.copy(), catlas)")
+    assert "def truncate(self, CT, task_id):" in src_methods and "def pad_image2" in src_methods
+    assert "image = self.truncate(image, name)" in src_get and "out = (" in src_get, "reference lines moved"
+    ns = {"np": np, "math": math}
+    exec(compile("class DS:\n" + "\n".join("    " + ln for ln in src_methods.splitlines()),
+                 "MOTSDataset.py:171-297", "exec"), ns)
+    cases = [  # tag, name, shape [H, W, D], crop (d, h, w), usage, seed
+        ("ct_small", "0007", (16, 30, 11), (8, 20, 16), "train", 151),
+        ("ct_big", "0123", (30, 34, 20), (8, 16, 24), "train", 152),
+        ("mri_small", "0541", (18, 20, 9), (8, 16, 16), "train", 153),
+        ("mri_big", "0598", (28, 26, 22), (12, 16, 20), "train", 154),
+        ("ct_valid", "0011", (14, 22, 12), (8, 16, 16), "valid", 155),
+        ("mri_valid", "0512", (24, 15, 13), (8, 16, 16), "valid", 156),
+    ]
+    out = {}
+    for tag, name, shp, crop, usage, seed in cases:
+        g = np.random.default_rng([15, seed])
+        if int(name) < 500:
+            image = g.integers(-1100, 1400, shp).astype(np.int16)
+        else:
+            image = (g.gamma(2.0, 150.0, shp)).astype(np.float32)
+        label = g.integers(0, 16, shp).astype(np.uint8)
+        catlas = (g.integers(0, 65, (13,) + shp) / 64.0).astype(np.float32)  # atlas probabilities (compressible)
+        ds = ns["DS"]()
+        ds.crop_d, ds.crop_h, ds.crop_w = crop
+        ds.usage = usage
+
+        class _Rec:
+            def __init__(self, seed):
+                self.rs, self.draws = np.random.RandomState(seed), []
+
+            def randint(self, *a):
+                v = self.rs.randint(*a)
+                self.draws.append(int(v))
+                return v
+        rec = _Rec(seed)
+        npx = types.SimpleNamespace(**{k: getattr(np, k) for k in ("newaxis", "float32")})
+        npx.random = rec
+        env = {"self": ds, "image": image.copy(), "label": label.copy(), "catlas": catlas.copy(), "name": name,
+               "np": npx}
+        exec(compile(src_get, "MOTSDataset.py:370-397", "exec"), env)
+        im, lb, ca = env["out"]
+        for k, v in (("image_in", image), ("label_in", label), ("catlas_in", catlas), ("image", im), ("label", lb),
+                     ("catlas", ca)):
+            out[f"{tag}_{k}"] = v
+        out[f"{tag}_name"], out[f"{tag}_crop"] = np.array(name), np.array(crop)
+        out[f"{tag}_usage"], out[f"{tag}_seed"] = np.array(usage), np.array(seed)
+        out[f"{tag}_draws"] = np.array(rec.draws, dtype=np.int64)
+    save("g15_crop_patch.npz", **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["g1", "g2", "g3", "g3b", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12", "g13",
-                             "g14"]
+                             "g14", "g15"]
     for w in which:
         globals()[w]()

@@ -34,6 +34,35 @@ def test_crop_patch_vs_reference_restatement(gpu, name, shape):
     np.testing.assert_allclose(gc.cpu().numpy(), rc.astype(np.float32), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("tag", ["ct_small", "ct_big", "mri_small", "mri_big", "ct_valid", "mri_valid"])
+def test_crop_patch_vs_reference_fixture(gpu, tag):
+    """f4 pinned on the reference's own lines (G15: MOTSDataset.py:171-186, :269-297, :370-397 exec'd in
+    tests/golden/gen_golden.py::g15 on CT int16 / MRI float32 volumes, train and valid): crop offsets drawn from the
+    same seeded RandomState in the reference's order (checked against the recorded draws), labels and atlas crops
+    bit-exact, the normalised image within 1e-6 (CT: one fp32 division vs numpy's float64 division then cast; MRI:
+    fp64 device statistics vs numpy's float32 pairwise mean / std)."""
+    from conftest import golden
+    from u3d import data
+    g = golden("g15_crop_patch.npz")
+    crop = tuple(int(v) for v in g[f"{tag}_crop"])
+    rs = np.random.RandomState(int(g[f"{tag}_seed"]))
+    draws = []
+
+    class Rec:
+        def randint(self, *a):
+            draws.append(int(rs.randint(*a)))
+            return draws[-1]
+    f = lambda k: torch.from_numpy(g[f"{tag}_{k}"].astype(np.float32)).to(gpu)  # noqa: E731 - host cast (exact)
+    gi, gl, gc = data.crop_patch(f("image_in"), f("label_in"), f("catlas_in"), str(g[f"{tag}_name"]), crop,
+                                 usage=str(g[f"{tag}_usage"]), rng=Rec())
+    assert draws == g[f"{tag}_draws"].tolist()
+    ri, rl, rc = g[f"{tag}_image"], g[f"{tag}_label"], g[f"{tag}_catlas"]
+    assert gi.shape == ri.shape and gl.shape == rl.shape and gc.shape == rc.shape
+    assert np.array_equal(gl.cpu().numpy(), rl)
+    assert np.array_equal(gc.cpu().numpy(), rc)
+    np.testing.assert_allclose(gi.cpu().numpy(), ri, rtol=0, atol=1e-6)
+
+
 @pytest.mark.parametrize("sigma,shape", [(0.5, (9, 10, 11)), (0.83, (16, 12, 20)), (1.0, (3, 17, 5))])
 def test_blur_vs_scipy(gpu, sigma, shape):
     from u3d import data

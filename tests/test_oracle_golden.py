@@ -343,3 +343,21 @@ def test_g14_partial_target_every_supervise_mask_row():
     assert len(g["names"]) == 240 and int((g["masks"].sum(1) == 0).sum()) == 40  # the all-zero MRI rows
     for i in range(len(g["names"])):
         np.testing.assert_array_equal(O.partial_target(g["labels"], g["masks"][i]).astype(np.uint8), g["cmask"][i])
+
+
+G15_CASES = ["ct_small", "ct_big", "mri_small", "mri_big", "ct_valid", "mri_valid"]
+
+
+@pytest.mark.parametrize("tag", G15_CASES)
+def test_g15_get_item_tensors_vs_reference_lines(tag):
+    """f4's deterministic half pinned on the reference's own lines (MOTSDataset.py:171-186 truncate, :269-297 pads,
+    :370-397 the getitem crop/transpose; G15): the restatement reproduces them, crops and labels bit-exact, the
+    normalised image bit-exact too (both compute in float64 and cast once)."""
+    g = golden("g15_crop_patch.npz")
+    crop = tuple(int(v) for v in g[f"{tag}_crop"])
+    ri, rl, rc = O.get_item_tensors(g[f"{tag}_image_in"], g[f"{tag}_label_in"], g[f"{tag}_catlas_in"],
+                                    str(g[f"{tag}_name"]), crop, np.random.RandomState(int(g[f"{tag}_seed"])),
+                                    usage=str(g[f"{tag}_usage"]))
+    np.testing.assert_array_equal(ri, g[f"{tag}_image"])
+    np.testing.assert_array_equal(rl, g[f"{tag}_label"])
+    np.testing.assert_array_equal(rc, g[f"{tag}_catlas"])
