@@ -33,7 +33,7 @@ enum Opt : int {
   OPT_SMALL_WGS,      // small-volume conv workgroups aimed at
   OPT_GN_MAXBLK,      // GroupNorm reduction blocks over all samples
   OPT_HEAD_TR,        // transposed classifier head (0: untransposed store path)
-  OPT_STEM1,          // four-voxel conv1 kernel (0: generic one-voxel kernel)
+  OPT_STEM1,          // conv1 (1 -> 32) one-voxel-per-lane kernel with LDS-transposed stores (0: generic kernel)
   OPT_UP_BWD_BLK,     // -1 auto, 0 / 1 force the one-row / 2x2-row trilinear backward
   OPT_WGRAD_BD,       // stride-1 brick weight-gradient brick depth (2 or 3)
   OPT_WB_WGS,         // brick weight-gradient workgroups aimed at
@@ -213,6 +213,21 @@ __device__ __forceinline__ TileSplit xcd_tile_split() {
   const int tile = N % nt;
   return TileSplit{tile % (int)gridDim.x, tile / (int)gridDim.x, N / nt};
 }
+
+// ------------------------------------------------------------------ diagnostic in-kernel stamps (never in the product)
+// A -DU3D_STAMPS build (tools/build_variant.sh) lets a kernel record s_memtime / s_memrealtime stamps and per-phase cycle
+// sums into a buffer of its own (a __device__ array of its translation unit, read back with u3d_diag_*_stamps): the
+// clock the chip holds inside the kernel (MI355X_MICROARCH.md, DVFS item 6) and where a persistent walk spends its
+// cycles. Nothing else reads the buffer and no output depends on it.
+#ifdef U3D_STAMPS
+__device__ __forceinline__ unsigned long long stamp_clk() {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+__device__ __forceinline__ unsigned long long stamp_real() { return __builtin_amdgcn_s_memrealtime(); }
+#endif
 
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 __host__ __device__ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }

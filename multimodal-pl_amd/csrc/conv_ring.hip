@@ -34,6 +34,11 @@ constexpr int RG_SS = 4 * RG_PS;                     // ring slot stride
 constexpr int RG_NT = 512;
 constexpr int RG_LD = (RG_NR * 4 + RG_NT - 1) / RG_NT;  // 3 staged 16-B pieces per thread and plane
 constexpr int RG_NWR = 27 * 32;                      // weight rows (t, co)
+#ifdef U3D_STAMPS
+// [workgroup][wave][8]: t0, t1 (s_memtime), r0, r1 (s_memrealtime), cycles in the compute steps (MFMAs + the staging
+// side work between them), in steps without compute, in the barriers, steps | compute steps << 32
+__device__ unsigned long long rg_stamps[2048 * 8 * 8];
+#endif
 
 struct RGGeom {
   int n, d, h, w;
@@ -526,6 +531,10 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
     return p;
   };
+#ifdef U3D_STAMPS
+  const unsigned long long st_t0 = stamp_clk(), st_r0 = stamp_real();
+  unsigned long long st_c = 0, st_s = 0, st_b = 0, st_n = 0;
+#endif
   RGPlane pw = next_plane();  // plane 0
   load_plane(pw, va, ma);
   __syncthreads();            // weights visible
@@ -574,12 +583,26 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         }
       }
     };
+#ifdef U3D_STAMPS
+    const unsigned long long a0 = stamp_clk();
+#endif
     if (pc.valid && pc.out) {
       compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 0>{}, side);
     } else {
       static_for<0, 2 * RG_LD>(side);
     }
+#ifdef U3D_STAMPS
+    const unsigned long long a1 = stamp_clk();
+    if (pc.valid && pc.out)
+      st_c += a1 - a0;
+    else
+      st_s += a1 - a0;
+    st_n += 1ull + ((pc.valid && pc.out) ? (1ull << 32) : 0ull);
+#endif
     __syncthreads();
+#ifdef U3D_STAMPS
+    st_b += stamp_clk() - a1;
+#endif
     pc = pw;
     pw = pl;
     ++s;
@@ -590,6 +613,15 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     step(vb, mb, va, ma);
   }
   epilogue(pend);  // the last computed plane (ok = false if none)
+#ifdef U3D_STAMPS
+  if (!Q) {
+    const unsigned long long t1 = stamp_clk(), r1 = stamp_real();
+    if (lane == 0) {
+      unsigned long long* o = rg_stamps + ((long long)(blockIdx.x & 2047) * 8 + wave) * 8;
+      o[0] = st_t0; o[1] = t1; o[2] = st_r0; o[3] = r1; o[4] = st_c; o[5] = st_s; o[6] = st_b; o[7] = st_n;
+    }
+  }
+#endif
   if constexpr (Q) {
     if constexpr (PRO) {
       if (spart != nullptr && acc_chunk >= 0) flush(acc_chunk);
@@ -762,6 +794,13 @@ static void ring_q_geom(int n, int d, int h, int w, RGGeom& g, bool stats = fals
   g.sc = std::min(g.per, std::max(3, env > 0 ? env : (g.per + parts - 1) / parts));
   g.rmax = (g.per + g.sc - 1) / g.sc;
 }
+
+#ifdef U3D_STAMPS
+extern "C" int u3d_diag_ring_stamps(void* out, long long nbytes) {
+  U3D_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(u3d::rg_stamps), std::min<long long>(nbytes, sizeof(u3d::rg_stamps))));
+  return 0;
+}
+#endif
 
 extern "C" int u3d_conv32_ring_q_stats_ws_floats(int n, int d, int h, int w) {
   RGGeom g;

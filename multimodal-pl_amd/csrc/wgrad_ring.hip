@@ -117,6 +117,11 @@ struct WRWalk {
   }
 };
 
+#ifdef U3D_STAMPS
+// [workgroup][wave][8]: t0, t1 (s_memtime), r0, r1 (s_memrealtime), cycles in write (incl. the staged loads' wait),
+// in compute, in the barrier, steps | compute steps << 32
+__device__ unsigned long long wr_stamps[4096 * 8 * 8];
+#endif
 }  // namespace
 
 template <bool GN, int PH = 16, int PW = 16>
@@ -312,22 +317,47 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
 
   u32x4 xa[WR_LX], xb[WR_LX], ya[WR_LY], yb[WR_LY];
   unsigned ma = 0, mb = 0;
+#ifdef U3D_STAMPS
+  const unsigned long long st_t0 = stamp_clk(), st_r0 = stamp_real();
+  unsigned long long st_w = 0, st_c = 0, st_b = 0, st_n = 0;
+#endif
   WRPlane pw = walk.next(g);
   load_plane(pw, xa, ya, ma);
   WRPlane pc{};
   int s = 0;
   auto step = [&](u32x4 (&cx)[WR_LX], u32x4 (&cy)[WR_LY], unsigned& mc, u32x4 (&nx)[WR_LX], u32x4 (&ny)[WR_LY],
                   unsigned& mn) {
+#ifdef U3D_STAMPS
+    const unsigned long long a0 = stamp_clk();
+#endif
     if (pw.valid) write_plane(pw, cx, cy, mc, s & 3, s & 1);
+#ifdef U3D_STAMPS
+    if (pw.valid) {  // the staged loads' wait (vmcnt) lands before the ds_writes
+      __builtin_amdgcn_s_waitcnt(0);
+    }
+    const unsigned long long a1 = stamp_clk();
+    st_w += a1 - a0;
+#endif
     const WRPlane pl = walk.next(g);
     load_plane(pl, nx, ny, mn);
+#ifdef U3D_STAMPS
+    const unsigned long long a2 = stamp_clk();
+    st_n += 1ull + ((pc.valid && pc.out) ? (1ull << 32) : 0ull);
+#endif
     if (pc.valid && pc.out) {
       if (ntap == 4)
         compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 4>{});
       else
         compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 3>{});
     }
+#ifdef U3D_STAMPS
+    const unsigned long long a3 = stamp_clk();
+    st_c += a3 - a2;
+#endif
     __syncthreads();
+#ifdef U3D_STAMPS
+    st_b += stamp_clk() - a3;
+#endif
     pc = pw;
     pw = pl;
     ++s;
@@ -337,6 +367,16 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     if (!(pw.valid || (pc.valid && pc.out))) break;
     step(xb, yb, mb, xa, ya, ma);
   }
+#ifdef U3D_STAMPS
+  {
+    const unsigned long long t1 = stamp_clk(), r1 = stamp_real();
+    const int wg = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & 4095;
+    if (lane == 0) {
+      unsigned long long* o = wr_stamps + ((long long)wg * 8 + wave) * 8;
+      o[0] = st_t0; o[1] = t1; o[2] = st_r0; o[3] = r1; o[4] = st_w; o[5] = st_c; o[6] = st_b; o[7] = st_n;
+    }
+  }
+#endif
   // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h. Buffer stores with 32-bit
   // offsets computed here (the host keeps the slabs below 2 GiB): no 64-bit addresses held across the walk.
   int t0 = tid;
@@ -399,6 +439,13 @@ static void wr_geom(int n, int cin, int d, int h, int w, int cout, WRGeom& g) {
   g.xbytes = (long long)n * d * h * w * cin * 2;
   g.ybytes = (long long)n * d * h * w * cout * 2;
 }
+
+#ifdef U3D_STAMPS
+extern "C" int u3d_diag_wgrad_stamps(void* out, long long nbytes) {
+  U3D_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(wr_stamps), std::min<long long>(nbytes, sizeof(wr_stamps))));
+  return 0;
+}
+#endif
 
 extern "C" int u3d_conv_wgrad_ring_splits_target(int n, int cin, int d, int h, int w, int cout, int wgs) {
   WRGeom g;

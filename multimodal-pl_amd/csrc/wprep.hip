@@ -66,7 +66,8 @@ __device__ __forceinline__ T block_sum(T v, T* red) {  // WB_T threads, fixed or
 
 // (1) mean / unbiased std of one row, as Conv3d.forward computes them. Rows up to WS_RV * 4 * WB_T floats (every trunk
 // conv: cin * 27 <= 6912) are read once, as 16-B vectors held in registers for both sums (K = cin * k3 is a multiple
-// of 8 and rows start 16-B aligned); longer rows take the two-pass scalar walk.
+// of 8 and rows start 16-B aligned); longer or unaligned rows (a weight view at an odd offset) take the two-pass scalar
+// walk.
 constexpr int WS_RV = 7;
 __global__ __launch_bounds__(WB_T) void wstd_stats_kernel(WBatch<WRow> bt) {
   __shared__ double red[WB_T / 64];
@@ -74,7 +75,7 @@ __global__ __launch_bounds__(WB_T) void wstd_stats_kernel(WBatch<WRow> bt) {
   const int co = blockIdx.x - D.b0;
   const int K = D.cin * D.k3;
   const float* wr = D.w + (long long)co * K;
-  if (K <= WS_RV * 4 * WB_T && K % 4 == 0) {
+  if (K <= WS_RV * 4 * WB_T && K % 4 == 0 && (((uintptr_t)D.w) & 15) == 0) {
     f32x4 r[WS_RV];
     double s = 0.0;
 #pragma unroll

@@ -423,7 +423,8 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
         _probe1(pr, "conv32_ring dgrad" + (" (work stealing)" if q else ""), 2.0 * n * d * h * w_ * 27 * 32 * 32,
                 n * d * h * w_)
         return dx
-    if USE_S2_BRICK and dy.dtype == torch.bfloat16 and k == 3 and stride == 2:
+    if (USE_S2_BRICK and dy.dtype == torch.bfloat16 and k == 3 and stride == 2
+            and dy.numel() * dy.element_size() < (1 << 31) - 64):  # (its dy reads use 32-bit buffer offsets)
         call("u3d_conv_dgrad_s2", dy.data_ptr(), n, cout, wpk_dgrad.data_ptr(), cin, d, h, w_, dx.data_ptr(),
              _stream())
         return dx

@@ -518,3 +518,23 @@ def test_no_kernel_spills_to_scratch():
     assert not bad, "kernels with VGPR spills / scratch: " + ", ".join(
         f"{n} ({v['.vgpr_spill_count']} spills, {v['.private_segment_fixed_size']} B)" for n, v in
         zip(KR.demangle(list(bad)), bad.values()))
+
+
+def test_stride2_dgrad_beyond_2gib_routes_to_the_64bit_kernel(monkeypatch):
+    """the stride-2 data-gradient kernel addresses dy with 32-bit buffer offsets, so a dy of 2 GiB or more
+    must route to the 64-bit implicit-GEMM data gradient instead of failing with EINVAL (routing only: meta tensors,
+    the library calls recorded, nothing launched)."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    from u3d import ops
+    calls = []
+    monkeypatch.setattr(ops, "call", lambda name, *a: calls.append(name))
+    monkeypatch.setattr(ops, "_stream", lambda: 0)
+    monkeypatch.setattr(ops.WS, "get", lambda *a, **k: torch.empty(256, dtype=torch.uint8, device="meta"))
+    wpk = torch.empty((27, 32, 64), dtype=torch.bfloat16, device="meta")
+    big = torch.empty((2, 48, 512, 512, 64), dtype=torch.bfloat16, device="meta")  # 3 GiB
+    assert big.numel() * 2 >= (1 << 31)
+    ops.conv_dgrad(big, wpk, 32, (2, 96, 1024, 1024), 3, 2)
+    ops.conv_dgrad(torch.empty((2, 24, 64, 64, 64), dtype=torch.bfloat16, device="meta"), wpk, 32, (2, 48, 128, 128),
+                   3, 2)
+    assert calls == ["u3d_conv_dgrad", "u3d_conv_dgrad_s2"], calls
