@@ -40,6 +40,7 @@ enum Opt : int {
   OPT_WR_TILE16,      // 1: 16 x 16 weight-gradient ring tiles everywhere
   OPT_WR_WGS,         // weight-gradient ring workgroups aimed at
   OPT_WB_S2CO64,      // stride-2 brick weight gradient: two co tiles per workgroup (0: one)
+  OPT_WR_DMA,         // 16 x 16-tile weight-gradient ring with LDS-DMA staging (0: register staging)
   OPT_COUNT
 };
 int opt(Opt o);

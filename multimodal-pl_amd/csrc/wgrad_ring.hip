@@ -419,6 +419,282 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Round 4: the 16 x 16-tile weight-gradient ring (96^3 and 48^3 levels) with LDS-DMA staging.
+// In-kernel stamps of the register-staged kernel above (r04, -DU3D_STAMPS): the younger wave of each SIMD pair spent
+// 18% of its time writing the staged plane (waiting for its loads, GroupNorm, ds_write) and 22% issuing the next plane's
+// loads, both between two barriers with no MFMA beside them, at a held clock of 2.31 GHz. Here every staging byte goes
+// global -> LDS by `buffer_load_dwordx4 ... lds` (no VGPRs, no write phase), issued between the MFMA sub-steps:
+//   * x: into a 5-slot ring in the final half-planar layout (row pitch 32 B, 16 channels per half-plane); the GroupNorm +
+//     ReLU prologue runs IN PLACE one step later (each lane transforms the 16 B its own DMA wrote, after a counted
+//     vmcnt: no barrier needed between the DMA and the transform);
+//   * dy: into a 3-slot ring, no transform;
+//   * 5 / 3 slots because a DMA lands while the step's MFMAs read their three (one) slots and one slot is being
+//     transformed; the plane barrier is a bare s_barrier behind an lgkmcnt(0) wait (a __syncthreads would drain the
+//     DMAs in flight: vmcnt(0)).
+// One DMA instruction = 32 rows x 32 B of one half-plane (1 KB, lane-contiguous: lane L -> row 32 i + L / 2, chunk L & 1).
+// x half-plane: 324 halo rows -> 11 instructions (the last one spills 28 rows into padding: 352 rows per half-plane);
+// waves 0-3 fill half 0, waves 4-7 half 1 (instructions wv, wv + 4, wv + 8; wave 3's third one is a dummy into junk);
+// dy half-plane: 256 voxels -> 8 instructions, two per wave. LDS: 5 x 22.5 KB + 3 x 16 KB + 1 KB = 159 KB.
+constexpr int WD_HROWS = 352;
+constexpr int WD_HP = WD_HROWS * 32;  // x half-plane
+constexpr int WD_SLOT = 2 * WD_HP;
+constexpr int WD_DHP = 256 * 32;      // dy half-plane
+constexpr int WD_DSLOT = 2 * WD_DHP;
+constexpr int WD_NXS = 5, WD_NDS = 3;
+constexpr int WD_LDS = WD_NXS * WD_SLOT + WD_NDS * WD_DSLOT + 1024;
+static_assert(WD_LDS <= 160 * 1024, "LDS");
+
+// buffer_load_dwordx4 ... lds as inline asm: the compiler's wait-count pass treats the builtin's LDS write as aliasing
+// every later ds_read and puts an s_waitcnt vmcnt(0) in front of the next MFMA fragment read (measured in the ISA),
+// which would serialise each DMA with the MFMA chain. The kernel orders the DMAs itself: a counted vmcnt before the
+// in-place transform and an lgkmcnt-only barrier (the hardware counts the asm loads in vmcnt like any other, so every
+// wait the compiler inserts for its own loads stays conservative). rsrc = the 4-dword buffer descriptor (SGPRs),
+// m0 = the wave-uniform LDS destination, off = this lane's byte offset.
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4s;
+__device__ __forceinline__ u32x4s buf_desc(const void* base, int bytes) {
+  const unsigned long long a = (unsigned long long)base;
+  return u32x4s{(unsigned)a, (unsigned)(a >> 32) & 0xffffu, (unsigned)bytes, 0x00020000u};
+}
+__device__ __forceinline__ void dma16(const u32x4s& rsrc, const char* lds_dst, unsigned off) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_dst);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, 0 offen lds" : : "v"(off), "s"(m0),
+               "s"(rsrc) : "memory", "m0");
+}
+
+template <bool GN>
+__global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                                 const float* __restrict__ gstat,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta,
+                                                                 float* __restrict__ part, WRGeom g) {
+  constexpr int HW = 18, NR = 324, PW = 16, KS2 = 8;  // 16 x 16 plane tile: 18 x 18 halo rows, 8 k steps of 32 voxels
+  __shared__ __attribute__((aligned(16))) char lds[WD_LDS];
+  char* const ring = lds;
+  char* const dyr = lds + WD_NXS * WD_SLOT;
+  char* const junk = dyr + WD_NDS * WD_DSLOT;
+  // (wave through readfirstlane: the compiler then knows every per-wave choice — tap count, DMA half — is uniform and
+  // emits scalar branches; an exec-masked branch makes its wait-count pass drain all loads at the join)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hf = wave >> 2, wv = wave & 3;  // DMA half-plane / wave within it
+  const int cofs = 16 * hf + 8 * (lane & 1);  // this lane's 8 channels (DMA + transform) within the 32-channel tile
+  const TileSplit ts = xcd_tile_split();
+  const int ci0 = ts.tx * 32, co0 = ts.ty * 32, split = ts.split;
+  WRWalk walk{};
+  walk.o_next = (long long)split * g.per;
+  walk.o_end = min(g.planes, walk.o_next + g.per);
+  walk.done = false;
+  walk.zin = 1;
+  walk.zlast = 0;
+  const u32x4s xrs = buf_desc(x, (int)g.xbytes), yrs = buf_desc(dy, (int)g.ybytes);
+  f32x2 sc[4], sh[4];
+  int gn_n = -1;
+  const bool cok = ci0 + cofs < g.cin, dok = co0 + cofs < g.cout;
+
+  // DMA of x piece j (instruction i = wv + 4 j) of plane p into slot xs; bit j of m = the lane's row is in the volume
+  auto dma_x = [&](const WRPlane& p, int j, int xs, unsigned& m) {
+    const int i = wv + 4 * j;
+    const int row = 32 * i + (lane >> 1);
+    const int hw = row % HW, hh = row / HW;
+    const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
+    const bool ok = p.valid && cok && row < NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
+                    (unsigned)zw < (unsigned)g.w;
+    const unsigned off =
+        ok ? (unsigned)(((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * g.cin + ci0 + cofs) * 2) : 0xFFFFFFF0u;
+    dma16(xrs, i < 11 ? ring + xs * WD_SLOT + hf * WD_HP + i * 1024 : junk, off);
+    m = (j == 0 ? 0u : m) | ((ok ? 1u : 0u) << j);
+  };
+  auto dma_y = [&](const WRPlane& p, int j, int ds) {
+    const int i = wv + 4 * j;
+    const int v = 32 * i + (lane >> 1);
+    const int zh = p.h0 + (v >> 4), zw = p.w0 + (v & 15), zo = p.zin - 1;
+    const bool ok = p.valid && p.out && dok && zh < g.h && zw < g.w;
+    const unsigned off =
+        ok ? (unsigned)(((((p.n * g.d + zo) * g.h + zh) * g.w + zw) * g.cout + co0 + cofs) * 2) : 0xFFFFFFF0u;
+    dma16(yrs, dyr + ds * WD_DSLOT + hf * WD_DHP + i * 1024, off);
+  };
+  // in-place GroupNorm + ReLU of x piece j in slot xs (the 16 B this lane's own DMA wrote; padding rows stay zero)
+  auto xform_x = [&](int j, int xs, unsigned m) {
+    const int i = wv + 4 * j;
+    char* a = (i < 11 ? ring + xs * WD_SLOT + hf * WD_HP + i * 1024 : junk) + lane * 16;
+    u32x4 v = *reinterpret_cast<u32x4*>(a);
+    v = gn_relu8(v, sc, sh);
+    if (!((m >> j) & 1u)) v = u32x4{0u, 0u, 0u, 0u};
+    *reinterpret_cast<u32x4*>(a) = v;
+  };
+  auto gn_refresh = [&](const WRPlane& p) {
+    if (GN && p.valid && p.n != gn_n) {
+      gn_n = p.n;
+      gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, p.n, ci0 + cofs, sc, sh);
+    }
+  };
+  auto bar = [&]() {  // plane barrier: the transforms' LDS writes done, the DMAs in flight stay in flight
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  constexpr int MAXT = 4;
+  f32x4 acc4[MAXT][4];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc4[j][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int tap_row[MAXT], tap_d[MAXT];
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    const int t = min(wave + 8 * j, 26);
+    tap_d[j] = t / 9;
+    tap_row[j] = (((t / 3) % 3) * HW + t % 3) * 32;
+  }
+  const int ntap = (27 - wave + 7) / 8;
+  const int q = (lane & 15) >> 2, pp = lane & 3, g4 = lane >> 4;
+  const int v16[2] = {4 * g4 + q, 16 + 4 * g4 + q};
+
+  // output plane from x slots s0, s0+1, s0+2 (mod 5) and dy slot ds; side(u) = the staging ops of sub-step u
+  auto compute = [&](int ds, int s0, auto ntc, auto&& side) __attribute__((always_inline)) {
+    constexpr int NTP = decltype(ntc)::value;
+    int tb[NTP];
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const int sl = s0 + tap_d[j];
+      tb[j] = (sl >= WD_NXS ? sl - WD_NXS : sl) * WD_SLOT + tap_row[j];
+    }
+    const char* dbase = dyr + ds * WD_DSLOT;
+    auto dyo = [&](int ks, int m, int cb) { return cb * WD_DHP + (32 * ks + v16[m]) * 32 + 8 * pp; };
+    auto xo = [&](int ks, int m) {
+      const int a = 32 * ks / PW, b = 32 * ks % PW, v = v16[m];
+      return (a * HW + b + v + (v >= PW - b ? 2 : 0)) * 32 + 8 * pp;
+    };
+    bf16x8 fa2[2][2], fb2[2][NTP];
+    auto rdA = [&](int ks) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) fa2[ks & 1][cb] = frag2(trd(dbase, dyo(ks, 0, cb)), trd(dbase, dyo(ks, 1, cb)));
+    };
+    auto rdB = [&](int u) {
+      const int x0 = xo(u >> 1, 0) + (u & 1) * WD_HP, x1 = xo(u >> 1, 1) + (u & 1) * WD_HP;
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) fb2[u & 1][j] = frag2(trd(ring, tb[j] + x0), trd(ring, tb[j] + x1));
+    };
+    rdA(0);
+    rdB(0);
+    __builtin_amdgcn_sched_barrier(0);
+    sfor<0, 2 * KS2>([&](auto uc) {
+      constexpr int u = decltype(uc)::value, ks = u >> 1, cib = u & 1;
+      if constexpr (u + 1 < 2 * KS2) {
+        if constexpr (((u + 1) & 1) == 0) rdA((u + 1) >> 1);
+        rdB(u + 1);
+      }
+      side(uc);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NTP; ++j)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          acc4[j][cb * 2 + cib] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa2[ks & 1][cb], fb2[u & 1][j], acc4[j][cb * 2 + cib], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+
+#ifdef U3D_STAMPS
+  const unsigned long long st_t0 = stamp_clk(), st_r0 = stamp_real();
+  unsigned long long st_w = 0, st_c = 0, st_b = 0, st_n = 0;
+#endif
+  // plane counter s: plane s sits in x slot s % 5 / dy slot s % 3 (DMA'd during step s-1, transformed at step s)
+  unsigned ma = 0, mb = 0;  // row masks of the planes in flight (rotating)
+  WRPlane pw = walk.next(g);  // plane 0
+  gn_refresh(pw);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) dma_x(pw, j, 0, ma);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) dma_y(pw, j, 0);
+  WRPlane pc{};
+  int x5 = 0, d3 = 0;  // s % 5, s % 3
+  auto step = [&](unsigned& mcur, unsigned& mnxt) __attribute__((always_inline)) {
+    const WRPlane pl = walk.next(g);  // plane s + 1
+    const int xn = x5 == WD_NXS - 1 ? 0 : x5 + 1, dn = d3 == WD_NDS - 1 ? 0 : d3 + 1;
+    gn_refresh(pw);
+    // sub-steps 0-4: DMA plane s+1; 6-8: transform plane s (its DMAs were issued a step ago: vmcnt(5) leaves only the
+    // five just issued in flight)
+    auto side = [&](auto uc) __attribute__((always_inline)) {
+      constexpr int u = decltype(uc)::value;
+      if constexpr (u < 3) dma_x(pl, u, xn, mnxt);
+      else if constexpr (u < 5) dma_y(pl, u - 3, dn);
+      else if constexpr (u >= 6 && u < 9) {
+        if constexpr (u == 6) {
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (GN) xform_x(u - 6, x5, mcur);
+      }
+    };
+#ifdef U3D_STAMPS
+    const unsigned long long a2 = stamp_clk();
+    st_n += 1ull + ((pc.valid && pc.out) ? (1ull << 32) : 0ull);
+#endif
+    if (pc.valid && pc.out) {
+      const int s0 = x5 >= 3 ? x5 - 3 : x5 + 2, dsc = d3 == 0 ? 2 : d3 - 1;  // planes s-3.. / dy of plane s-1
+      if (ntap == 4)
+        compute(dsc, s0, std::integral_constant<int, 4>{}, side);
+      else
+        compute(dsc, s0, std::integral_constant<int, 3>{}, side);
+    } else {
+      sfor<0, 2 * KS2>([&](auto uc) { side(uc); });
+    }
+#ifdef U3D_STAMPS
+    const unsigned long long a3 = stamp_clk();
+    st_c += a3 - a2;
+#endif
+    bar();
+#ifdef U3D_STAMPS
+    st_b += stamp_clk() - a3;
+#endif
+    pc = pw;
+    pw = pl;
+    x5 = xn;
+    d3 = dn;
+  };
+  while (pw.valid || (pc.valid && pc.out)) {
+    step(ma, mb);
+    if (!(pw.valid || (pc.valid && pc.out))) break;
+    step(mb, ma);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup's LDS is released
+#ifdef U3D_STAMPS
+  {
+    const unsigned long long t1 = stamp_clk(), r1 = stamp_real();
+    const int wg = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & 4095;
+    if (lane == 0) {
+      unsigned long long* o = wr_stamps + ((long long)wg * 8 + wave) * 8;
+      o[0] = st_t0; o[1] = t1; o[2] = st_r0; o[3] = r1; o[4] = st_w; o[5] = st_c; o[6] = st_b; o[7] = st_n;
+    }
+  }
+#endif
+  int t0 = tid;
+  asm volatile("" : "+v"(t0));
+  const int w8 = t0 >> 6;
+  const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFFF, 0x00020000);
+  const int l16 = t0 & 15, gq = (t0 >> 4) & 3;
+#pragma unroll
+  for (int j = 0; j < MAXT; ++j) {
+    if (j < ntap) {
+      const int tt = w8 + 8 * j;
+#pragma unroll
+      for (int blk = 0; blk < 4; ++blk) {
+        const int cb = blk >> 1, cib = blk & 1;
+        const int base = ((split * 27 + tt) * g.cout_p + co0 + 16 * cb + 4 * gq) * g.cin_p + ci0 + 16 * cib + l16;
+        const u32x4 ua = __builtin_bit_cast(u32x4, acc4[j][blk]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          __builtin_amdgcn_raw_buffer_store_b32(ua[k], prs, (unsigned)((base + k * g.cin_p) * 4), 0, 0);
+      }
+    }
+  }
+}
+
 }  // namespace u3d
 
 using namespace u3d;
@@ -488,6 +764,13 @@ extern "C" int u3d_conv_wgrad_ring(const void* dy, const void* x, int n, int cin
     if (gn) U3D_WR(true, 12, 24); else U3D_WR(false, 12, 24);
   } else if (g.pw == 12) {
     if (gn) U3D_WR(true, 12, 12); else U3D_WR(false, 12, 12);
+  } else if (opt(OPT_WR_DMA) != 0) {  // 16 x 16 tiles: LDS-DMA staging (round 4)
+    if (gn)
+      hipLaunchKernelGGL((wgrad_ring_dma_kernel<true>), grid, dim3(WR_NT), 0, s, (const bf16*)dy, (const bf16*)x,
+                         gn_stats, gn_gamma, gn_beta, partials, g);
+    else
+      hipLaunchKernelGGL((wgrad_ring_dma_kernel<false>), grid, dim3(WR_NT), 0, s, (const bf16*)dy, (const bf16*)x,
+                         gn_stats, gn_gamma, gn_beta, partials, g);
   } else {
     if (gn) U3D_WR(true, 16, 16); else U3D_WR(false, 16, 16);
   }

@@ -69,6 +69,8 @@ class Tape:
 
     def pend_wgrad(self, part, ns, W, st, std, name):
         self.pending.append((part, ns, W, st, std, self.grad_out(name, W), False, name))
+        if self.sink is not None:
+            self.sink.note_pending(name)  # sets sink.flush_due when the parked gradients complete a DDP bucket
 
     def flush_wgrads(self):
         """Slab sum + standardisation backward of the pending weight gradients, in one batched launch pair.
@@ -279,7 +281,8 @@ class Tape:
         out_act.grad = grad
         for fn in reversed(self.ops):
             fn()
-            if self.pending and self.sink is not None and self.sink.needs_flush([p[7] for p in self.pending]):
+            if self.sink is not None and self.sink.flush_due:
+                self.sink.flush_due = False
                 self.flush_wgrads()
         self.flush_wgrads()
         self.ops = []

@@ -4,7 +4,7 @@ batch"; reference: engine.data_parallel + DDP, train_amos_atlas_final.py:141-144
 Two ranks share cuda:0 (the pool's boxes have one GPU; RCCL refuses two ranks on one device), so the collective is
 gloo on device tensors. What runs is the production data-parallel machinery: U3DDataParallel around
 unet3D_baseline(16), the native backward writing parameter gradients straight into flat bucket views, the
-bucket-ordered weight-gradient flush (u3d/trunk.py Tape.backward: needs_flush -> flush_wgrads) with 1 MB buckets so
+bucket-ordered weight-gradient flush (u3d/trunk.py Tape.backward: sink.flush_due -> flush_wgrads) with 1 MB buckets so
 that ~70 buckets complete one after another inside the backward, the SUM + divide branch of the averaging, and the
 post-accumulate hook that averages a gradient the native tape did not produce (an extra parameter used by plain
 torch autograd). Rank r trains on sample r of a batch of two; the single-process reference trains on the whole
