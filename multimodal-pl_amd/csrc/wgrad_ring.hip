@@ -443,6 +443,10 @@ constexpr int WD_SLOT = 2 * WD_HP;
 constexpr int WD_DHP = 256 * 32;      // dy half-plane
 constexpr int WD_DSLOT = 2 * WD_DHP;
 constexpr int WD_NXS = 5, WD_NDS = 3;
+#ifndef U3D_WD_LA
+#define U3D_WD_LA 1
+#endif
+constexpr int WD_LA = U3D_WD_LA;  // MFMA sub-steps of fragment reads in flight
 constexpr int WD_LDS = WD_NXS * WD_SLOT + WD_NDS * WD_DSLOT + 1024;
 static_assert(WD_LDS <= 160 * 1024, "LDS");
 
@@ -457,11 +461,16 @@ __device__ __forceinline__ u32x4s buf_desc(const void* base, int bytes) {
   const unsigned long long a = (unsigned long long)base;
   return u32x4s{(unsigned)a, (unsigned)(a >> 32) & 0xffffu, (unsigned)bytes, 0x00020000u};
 }
+// (m0 is a reserved register: clang warns that the clobber may not be honoured. The kernel's own code never uses m0 —
+// checked in the ISA, tools/disasm.py — so the clobber only documents the asm's side effect.)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void dma16(const u32x4s& rsrc, const char* lds_dst, unsigned off) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_dst);
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, 0 offen lds" : : "v"(off), "s"(m0),
                "s"(rsrc) : "memory", "m0");
 }
+#pragma clang diagnostic pop
 
 template <bool GN>
 __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
@@ -492,26 +501,61 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
   int gn_n = -1;
   const bool cok = ci0 + cofs < g.cin, dok = co0 + cofs < g.cout;
 
-  // DMA of x piece j (instruction i = wv + 4 j) of plane p into slot xs; bit j of m = the lane's row is in the volume
+  // Per-lane DMA addressing, hoisted out of the walk: a lane's row of x piece j (instruction i = wv + 4 j) is the halo
+  // row (hh, hw) = divmod(32 i + lane / 2, 18) of every plane, its dy voxel (v / 16, v % 16), v = 32 i + lane / 2; so
+  // its byte offset is a per-lane constant plus a wave-uniform plane base, and its in-volume test changes only with
+  // the column (n, h0, w0). Per plane and piece that leaves one add and one select (the per-plane integer address math
+  // of the first version cost ~30 VALU + SALU per piece, issue slots the MFMA chain needs: r04 stamps / ISA).
+  int xlo[3], ylo[2], xhh[3], xhw[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int row = 32 * (wv + 4 * j) + (lane >> 1);
+    xhh[j] = row / HW;
+    xhw[j] = row % HW;
+    xlo[j] = ((xhh[j] * g.w + xhw[j]) * g.cin + ci0 + cofs) * 2;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int v = 32 * (wv + 4 * j) + (lane >> 1);
+    ylo[j] = (((v >> 4) * g.w + (v & 15)) * g.cout + co0 + cofs) * 2;
+  }
+  unsigned xin = 0, yin = 0;  // per column: bit j = x piece j's row / dy piece j's voxel inside the volume
+  int col_h0 = -1, col_w0 = -1;
+  auto column = [&](const WRPlane& p) {
+    if (p.valid && (p.h0 != col_h0 || p.w0 != col_w0)) {  // uniform: once per run of the walk
+      col_h0 = p.h0;
+      col_w0 = p.w0;
+      xin = yin = 0;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int i = wv + 4 * j, row = 32 * i + (lane >> 1);
+        const bool ok = cok && i < 11 && row < NR && (unsigned)(p.h0 - 1 + xhh[j]) < (unsigned)g.h &&
+                        (unsigned)(p.w0 - 1 + xhw[j]) < (unsigned)g.w;
+        xin |= (ok ? 1u : 0u) << j;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int v = 32 * (wv + 4 * j) + (lane >> 1);
+        const bool ok = dok && p.h0 + (v >> 4) < g.h && p.w0 + (v & 15) < g.w;
+        yin |= (ok ? 1u : 0u) << j;
+      }
+    }
+  };
+  // DMA of x piece j of plane p into slot xs; bit j of m = the lane's row is in the volume
   auto dma_x = [&](const WRPlane& p, int j, int xs, unsigned& m) {
     const int i = wv + 4 * j;
-    const int row = 32 * i + (lane >> 1);
-    const int hw = row % HW, hh = row / HW;
-    const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
-    const bool ok = p.valid && cok && row < NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
-                    (unsigned)zw < (unsigned)g.w;
-    const unsigned off =
-        ok ? (unsigned)(((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * g.cin + ci0 + cofs) * 2) : 0xFFFFFFF0u;
+    const bool pv = p.valid && (unsigned)p.zin < (unsigned)g.d;  // uniform
+    const int base = (((p.n * g.d + p.zin) * g.h + p.h0 - 1) * g.w + p.w0 - 1) * g.cin * 2;
+    const bool ok = pv && ((xin >> j) & 1u);
+    const unsigned off = ok ? (unsigned)(base + xlo[j]) : 0xFFFFFFF0u;
     dma16(xrs, i < 11 ? ring + xs * WD_SLOT + hf * WD_HP + i * 1024 : junk, off);
     m = (j == 0 ? 0u : m) | ((ok ? 1u : 0u) << j);
   };
   auto dma_y = [&](const WRPlane& p, int j, int ds) {
     const int i = wv + 4 * j;
-    const int v = 32 * i + (lane >> 1);
-    const int zh = p.h0 + (v >> 4), zw = p.w0 + (v & 15), zo = p.zin - 1;
-    const bool ok = p.valid && p.out && dok && zh < g.h && zw < g.w;
-    const unsigned off =
-        ok ? (unsigned)(((((p.n * g.d + zo) * g.h + zh) * g.w + zw) * g.cout + co0 + cofs) * 2) : 0xFFFFFFF0u;
+    const bool pv = p.valid && p.out;
+    const int base = (((p.n * g.d + p.zin - 1) * g.h + p.h0) * g.w + p.w0) * g.cout * 2;
+    const unsigned off = pv && ((yin >> j) & 1u) ? (unsigned)(base + ylo[j]) : 0xFFFFFFF0u;
     dma16(yrs, dyr + ds * WD_DSLOT + hf * WD_DHP + i * 1024, off);
   };
   // in-place GroupNorm + ReLU of x piece j in slot xs (the 16 B this lane's own DMA wrote; padding rows stay zero)
@@ -567,24 +611,29 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
       const int a = 32 * ks / PW, b = 32 * ks % PW, v = v16[m];
       return (a * HW + b + v + (v >= PW - b ? 2 : 0)) * 32 + 8 * pp;
     };
-    bf16x8 fa2[2][2], fb2[2][NTP];
+    // fragment lookahead: the reads of sub-step u + WD_LA are issued before the MFMAs of sub-step u
+    constexpr int NB = WD_LA + 1, NA = (WD_LA + 1) / 2 + 1;
+    bf16x8 fa2[NA][2], fb2[NB][NTP];
     auto rdA = [&](int ks) {
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) fa2[ks & 1][cb] = frag2(trd(dbase, dyo(ks, 0, cb)), trd(dbase, dyo(ks, 1, cb)));
+      for (int cb = 0; cb < 2; ++cb) fa2[ks % NA][cb] = frag2(trd(dbase, dyo(ks, 0, cb)), trd(dbase, dyo(ks, 1, cb)));
     };
     auto rdB = [&](int u) {
       const int x0 = xo(u >> 1, 0) + (u & 1) * WD_HP, x1 = xo(u >> 1, 1) + (u & 1) * WD_HP;
 #pragma unroll
-      for (int j = 0; j < NTP; ++j) fb2[u & 1][j] = frag2(trd(ring, tb[j] + x0), trd(ring, tb[j] + x1));
+      for (int j = 0; j < NTP; ++j) fb2[u % NB][j] = frag2(trd(ring, tb[j] + x0), trd(ring, tb[j] + x1));
     };
-    rdA(0);
-    rdB(0);
+    sfor<0, WD_LA>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if constexpr ((u & 1) == 0) rdA(u >> 1);
+      rdB(u);
+    });
     __builtin_amdgcn_sched_barrier(0);
     sfor<0, 2 * KS2>([&](auto uc) {
       constexpr int u = decltype(uc)::value, ks = u >> 1, cib = u & 1;
-      if constexpr (u + 1 < 2 * KS2) {
-        if constexpr (((u + 1) & 1) == 0) rdA((u + 1) >> 1);
-        rdB(u + 1);
+      if constexpr (u + WD_LA < 2 * KS2) {
+        if constexpr (((u + WD_LA) & 1) == 0) rdA((u + WD_LA) >> 1);
+        rdB(u + WD_LA);
       }
       side(uc);
       __builtin_amdgcn_sched_barrier(0);
@@ -592,8 +641,8 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
       for (int j = 0; j < NTP; ++j)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
-          acc4[j][cb * 2 + cib] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa2[ks & 1][cb], fb2[u & 1][j], acc4[j][cb * 2 + cib], 0, 0, 0);
+          acc4[j][cb * 2 + cib] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa2[ks % NA][cb], fb2[u % NB][j],
+                                                                          acc4[j][cb * 2 + cib], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     });
   };
@@ -606,6 +655,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
   unsigned ma = 0, mb = 0;  // row masks of the planes in flight (rotating)
   WRPlane pw = walk.next(g);  // plane 0
   gn_refresh(pw);
+  column(pw);
 #pragma unroll
   for (int j = 0; j < 3; ++j) dma_x(pw, j, 0, ma);
 #pragma unroll
@@ -616,6 +666,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
     const WRPlane pl = walk.next(g);  // plane s + 1
     const int xn = x5 == WD_NXS - 1 ? 0 : x5 + 1, dn = d3 == WD_NDS - 1 ? 0 : d3 + 1;
     gn_refresh(pw);
+    column(pl);
     // sub-steps 0-4: DMA plane s+1; 6-8: transform plane s (its DMAs were issued a step ago: vmcnt(5) leaves only the
     // five just issued in flight)
     auto side = [&](auto uc) __attribute__((always_inline)) {

@@ -82,6 +82,8 @@ class _DynFn(torch.autograd.Function):
         if tape.sink is not None:
             tape.sink.finish()
         grads = [tape.pgrad.get(nm) for nm in ctx.names]
+        if tape.sink is not None:
+            grads = tape.sink.returned(ctx.names, grads)
         ctx.state = None
         return (None, None, None, None, None, *grads)
 

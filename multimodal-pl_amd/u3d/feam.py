@@ -162,6 +162,8 @@ class _Feam3Fn(torch.autograd.Function):
         if tape.sink is not None:
             tape.sink.finish()
         pg = [tape.pgrad.get(nm) for nm in ctx.names]
+        if tape.sink is not None:
+            pg = tape.sink.returned(ctx.names, pg)
         ctx.state = None
         return (None, None, None, None, None, None, None, *pg)
 

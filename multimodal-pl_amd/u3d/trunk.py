@@ -321,6 +321,8 @@ class _TrunkFn(torch.autograd.Function):
         if tape.sink is not None:
             tape.sink.finish()
         grads = [tape.pgrad.get(n) for n in ctx.names]
+        if tape.sink is not None:
+            grads = tape.sink.returned(ctx.names, grads)
         ctx.tape = ctx.out = None
         return (None, None, None, None, *grads)
 
