@@ -317,8 +317,8 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   // GroupNorm (scale, shift) per input channel of the samples in flight, slot = sample & 1: filled once per sample
   // (the staging reads it from LDS — no global loads whose wait would drain the halo/weight prefetch)
   __shared__ __attribute__((aligned(16))) f32x2 gtab[2][GB_MAXC];
-  // output GroupNorm statistics (spart != nullptr): per (wave, lane half, tn, run v, channel pair q) (sum, sum sq)
-  __shared__ f32x2 sst[8][2][TN * 2 * 4];
+  // output GroupNorm statistics (spart != nullptr): per (wave, lane half, tn, run v, channel pair q) (sum, sum sq), fp64
+  __shared__ double sst[8][2][TN * 2 * 4][2];
 
   // the data gradient never takes a residual or output statistics (convg_impl): dead at compile time, so its
   // epilogue's registers are not reserved
@@ -386,7 +386,6 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, res ? ybytes : 0, 0x00020000);
   const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, ybytes, 0x00020000);
   const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)spart, 0, spart ? 0x7FFFFFFF : 0, 0x00020000);
-  typedef __attribute__((ext_vector_type(2))) uint32_t v2u32;
   auto halo_load = [&](const Unit& q, int c) {
     hmask = 0;
     stg_nn = q.nn;
@@ -577,7 +576,10 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     __syncthreads();
     par ^= 1;
     // (statistics of the stored bf16 outputs, per channel pair: the GN(16) groups of every cout % 32 == 0 hold
-    // whole pairs; fp32 per lane and unit, fixed-order reductions, fp64 across units in the finalize)
+    // whole pairs; fp32 over the 2-4 voxels of a lane — exact for bf16 squares, at most a rounding per add — then fp64
+    // for the fixed-order reductions over lanes, waves and units. Unshifted E[x^2] - mean^2 loses |mean|^2 / var digits
+    // to cancellation: with fp32 unit partials (rounds 2-3) that cost ~1e-3 relative rstd at |mean| / std = 50; with
+    // fp64 partials the loss stays below 1e-6 there (tests/test_gpu_pbrick.py, large-mean case; ADVICE r2 / VERDICT r3))
     // per co block tn: (sum, sum sq) of the 4 channel pairs q of each v half, over this lane's voxels; reduced over the
     // lane half (32 voxels) and stored per wave into the LDS before the next co block (8 pairs live, not 16)
     f32x2 ps[2 * 4];
@@ -629,26 +631,38 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
           }
         }
       }
-      if (spart != nullptr) {  // this tn's pairs: reduce over the 32 voxels of each lane half into the LDS
+      if (spart != nullptr) {  // this tn's pairs: reduce over the 32 voxels of each lane half into the LDS (fp64)
+        double dps[2 * 4][2];
 #pragma unroll
-        for (int i = 0; i < 2 * 4; ++i)
+        for (int i = 0; i < 2 * 4; ++i) {
+          dps[i][0] = ps[i][0];
+          dps[i][1] = ps[i][1];
 #pragma unroll
           for (int o = 1; o < 32; o <<= 1) {
-            ps[i][0] += __shfl_xor(ps[i][0], o);
-            ps[i][1] += __shfl_xor(ps[i][1], o);
+            dps[i][0] += __shfl_xor(dps[i][0], o);
+            dps[i][1] += __shfl_xor(dps[i][1], o);
           }
+        }
         if (r == 0)
 #pragma unroll
-          for (int i = 0; i < 2 * 4; ++i) sst[wave][hh][tn * 8 + i] = ps[i];
+          for (int i = 0; i < 2 * 4; ++i) {
+            sst[wave][hh][tn * 8 + i][0] = dps[i][0];
+            sst[wave][hh][tn * 8 + i][1] = dps[i][1];
+          }
       }
     }
     if (spart != nullptr) {  // the 8 waves in order, per channel pair of the tile
       __syncthreads();
       if (tid < CO / 2) {  // channel pair tid of the tile: c = 2 tid -> (tn, v, hh, q)
         const int c = 2 * tid, tn = c >> 5, w32 = c & 31, v = w32 >> 4, h_ = (w32 >> 3) & 1, q = (w32 & 7) >> 1;
-        f32x2 t = {0.f, 0.f};
-        for (int w = 0; w < 8; ++w) t += sst[w][h_][(tn * 2 + v) * 4 + q];
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, t), prs, (u * CO + c) * 4, 0, 0);
+        double t0 = 0.0, t1 = 0.0;
+        for (int w = 0; w < 8; ++w) {
+          t0 += sst[w][h_][(tn * 2 + v) * 4 + q][0];
+          t1 += sst[w][h_][(tn * 2 + v) * 4 + q][1];
+        }
+        typedef __attribute__((ext_vector_type(2))) double f64x2;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, (f64x2){t0, t1}), prs, (u * CO + c) * 8, 0,
+                                               0);
       }
     }
     cu = nu;
@@ -658,7 +672,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
 // GroupNorm(16) (mean, rstd) of the persistent brick conv's output from its per-unit channel-pair partials
 // spart[unit][CO / 2][2] (unit = brick * nct + co tile): one wave per (sample, group), lanes strided over the
 // sample's bricks, pairs summed in order, fp64 butterfly in fixed order (deterministic)
-__global__ __launch_bounds__(64) void pbrick_gn_finalize_kernel(const float* __restrict__ spart, int co_tile, int nct,
+__global__ __launch_bounds__(64) void pbrick_gn_finalize_kernel(const double* __restrict__ spart, int co_tile, int nct,
                                                                int bricks_per_sample, int cout, double m,
                                                                float* __restrict__ stats) {
   const int p = blockIdx.x, nn = p / 16, gr = p % 16, cpg = cout / 16;
@@ -667,7 +681,7 @@ __global__ __launch_bounds__(64) void pbrick_gn_finalize_kernel(const float* __r
     const long long brick = (long long)nn * bricks_per_sample + b;
     for (int c = gr * cpg; c < (gr + 1) * cpg; c += 2) {
       const int ct = c / co_tile, cl = c - ct * co_tile;
-      const float* q = spart + ((brick * nct + ct) * co_tile + cl);
+      const double* q = spart + ((brick * nct + ct) * co_tile + cl);
       s1 += q[0];
       s2 += q[1];
     }
@@ -770,7 +784,7 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
     int rc = check_launch("convg_pbrick_kernel");
     if (rc) return rc;
     if (!spart) return rc;
-    hipLaunchKernelGGL(pbrick_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, spart, co64 ? 64 : 32, gp.nct,
+    hipLaunchKernelGGL(pbrick_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, (const double*)spart, co64 ? 64 : 32, gp.nct,
                        gp.nbd * gp.nbh * gp.nbw, cout, (double)(cout / 16) * d * h * w, stats_out);
     return check_launch("pbrick_gn_finalize_kernel");
   }
@@ -800,8 +814,8 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
 }
 
 extern "C" long long u3d_convg_brick_stats_ws_floats(int n, int d, int h, int w, int cout) {
-  // upper bound over both brick widths and co tiles: units x 64 floats
-  return (long long)n * cdiv(d, GB_BD) * cdiv(h, GB_BH) * cdiv(w, 8) * cdiv(cout, 32) * 64;
+  // upper bound over both brick widths and co tiles: units x 32 channel pairs x 2 doubles (= 128 floats)
+  return (long long)n * cdiv(d, GB_BD) * cdiv(h, GB_BH) * cdiv(w, 8) * cdiv(cout, 32) * 128;
 }
 
 extern "C" int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,

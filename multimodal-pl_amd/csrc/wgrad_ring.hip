@@ -155,27 +155,85 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
   int gn_n = -1;
   const bool cok = ci0 + ch * 8 < g.cin, dok = co0 + ch * 8 < g.cout;
 
+  // per-lane staging offsets hoisted out of the walk (round 4): a lane's halo row / dy voxel of piece i is the same
+  // in every plane, so its byte offset is a per-lane constant plus a wave-uniform plane base, and its in-volume test
+  // changes only with the column (n, h0, w0) — per plane and piece one add and one select instead of ~30 VALU + SALU
+  int xlo[WR_LX], ylo[WR_LY];
+#pragma unroll
+  for (int i = 0; i < WR_LX; ++i) {  // (dead for the 12 x 24 / 12 x 12 tiles: see HOIST)
+    const int row = (tid >> 2) + i * (WR_NT / 4);
+    xlo[i] = (((row / WR_HW) * g.w + row % WR_HW) * g.cin + ci0 + ch * 8) * 2;
+  }
+#pragma unroll
+  for (int i = 0; i < WR_LY; ++i) {
+    const int v = (tid >> 2) + i * (WR_NT / 4);
+    ylo[i] = (((v / WR_PW) * g.w + v % WR_PW) * g.cout + co0 + ch * 8) * 2;
+  }
+  unsigned xin = 0, yin = 0;
+  int col_h0 = -1, col_w0 = -1;
+  auto column = [&](const WRPlane& p) {
+    if (p.valid && (p.h0 != col_h0 || p.w0 != col_w0)) {  // uniform: once per run of the walk
+      col_h0 = p.h0;
+      col_w0 = p.w0;
+      xin = yin = 0;
+#pragma unroll
+      for (int i = 0; i < WR_LX; ++i) {
+        const int row = (tid >> 2) + i * (WR_NT / 4);
+        const bool ok = cok && row < WR_NR && (unsigned)(p.h0 - 1 + row / WR_HW) < (unsigned)g.h &&
+                        (unsigned)(p.w0 - 1 + row % WR_HW) < (unsigned)g.w;
+        xin |= (ok ? 1u : 0u) << i;
+      }
+#pragma unroll
+      for (int i = 0; i < WR_LY; ++i) {
+        const int v = (tid >> 2) + i * (WR_NT / 4);
+        const bool ok = dok && v < WR_NV && p.h0 + v / WR_PW < g.h && p.w0 + v % WR_PW < g.w;
+        yin |= (ok ? 1u : 0u) << i;
+      }
+    }
+  };
+  // (hoisted only for the 16 x 16 tiles: the 12 x 24 tile's register budget has no room for the six offsets)
+  constexpr bool HOIST = PW == 16;
   auto load_plane = [&](const WRPlane& p, u32x4 (&vx)[WR_LX], u32x4 (&vy)[WR_LY], unsigned& m) {
     m = 0;
+    if constexpr (!HOIST) {
+#pragma unroll
+      for (int i = 0; i < WR_LX; ++i) {
+        const int row = (tid >> 2) + i * (WR_NT / 4);
+        const int hw = row % WR_HW, hh = row / WR_HW;
+        const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
+        const bool ok = p.valid && cok && row < WR_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
+                        (unsigned)zw < (unsigned)g.w;
+        const unsigned off =
+            ok ? (unsigned)(((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * g.cin + ci0 + ch * 8) * 2) : 0xFFFFFFF0u;
+        vx[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+        m |= (ok ? 1u : 0u) << i;
+      }
+#pragma unroll
+      for (int i = 0; i < WR_LY; ++i) {
+        const int v = (tid >> 2) + i * (WR_NT / 4);
+        const int zh = p.h0 + v / WR_PW, zw = p.w0 + v % WR_PW, zo = p.zin - 1;
+        const bool ok = p.valid && p.out && dok && v < WR_NV && zh < g.h && zw < g.w;
+        const unsigned off =
+            ok ? (unsigned)(((((p.n * g.d + zo) * g.h + zh) * g.w + zw) * g.cout + co0 + ch * 8) * 2) : 0xFFFFFFF0u;
+        vy[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0));
+      }
+      return;
+    }
+    column(p);
+    const bool pv = p.valid && (unsigned)p.zin < (unsigned)g.d;
+    const int xb = (((p.n * g.d + p.zin) * g.h + p.h0 - 1) * g.w + p.w0 - 1) * g.cin * 2;
 #pragma unroll
     for (int i = 0; i < WR_LX; ++i) {
-      const int row = (tid >> 2) + i * (WR_NT / 4);
-      const int hw = row % WR_HW, hh = row / WR_HW;
-      const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
-      const bool ok = p.valid && cok && row < WR_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
-                      (unsigned)zw < (unsigned)g.w;
-      const unsigned off =
-          ok ? (unsigned)(((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * g.cin + ci0 + ch * 8) * 2) : 0xFFFFFFF0u;
+      const bool ok = pv && ((xin >> i) & 1u);
+      const unsigned off = ok ? (unsigned)(xb + xlo[i]) : 0xFFFFFFF0u;
       vx[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
       m |= (ok ? 1u : 0u) << i;
     }
+    const bool po = p.valid && p.out;
+    const int yb = (((p.n * g.d + p.zin - 1) * g.h + p.h0) * g.w + p.w0) * g.cout * 2;
 #pragma unroll
     for (int i = 0; i < WR_LY; ++i) {
-      const int v = (tid >> 2) + i * (WR_NT / 4);
-      const int zh = p.h0 + v / WR_PW, zw = p.w0 + v % WR_PW, zo = p.zin - 1;
-      const bool ok = p.valid && p.out && dok && v < WR_NV && zh < g.h && zw < g.w;
-      const unsigned off =
-          ok ? (unsigned)(((((p.n * g.d + zo) * g.h + zh) * g.w + zw) * g.cout + co0 + ch * 8) * 2) : 0xFFFFFFF0u;
+      const unsigned off = po && ((yin >> i) & 1u) ? (unsigned)(yb + ylo[i]) : 0xFFFFFFF0u;
       vy[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0));
     }
   };

@@ -61,23 +61,28 @@ def test_persistent_brick_bitwise_equal_one_shot(gpu, case):
         f"max diff {(a.float() - b.float()).abs().max().item()}"
 
 
-STATS_CASES = [  # n, cin, cout, (d, h, w), residual (+ large mean), GN prologue
-    (2, 64, 64, (48, 48, 48), True, True),
-    (2, 128, 128, (24, 24, 24), True, True),
-    (2, 64, 64, (24, 24, 24), False, True),
-    (2, 64, 96, (16, 23, 40), True, True),
-    (4, 96, 64, (12, 24, 19), False, False),
+STATS_CASES = [  # n, cin, cout, (d, h, w), residual (+ offset), GN prologue, residual offset
+    (2, 64, 64, (48, 48, 48), True, True, 4.0),
+    (2, 128, 128, (24, 24, 24), True, True, 4.0),
+    (2, 64, 64, (24, 24, 24), False, True, 0.0),
+    (2, 64, 96, (16, 23, 40), True, True, 4.0),
+    (4, 96, 64, (12, 24, 19), False, False, 0.0),
+    # |mean| / std ~ 50 (VERDICT r3 / ADVICE r2): the conv output's std is ~25 here, so a +1250 residual
+    (2, 64, 64, (24, 24, 24), True, True, 1250.0),
+    (2, 64, 64, (48, 48, 48), True, True, -1250.0),
 ]
 
 
-@pytest.mark.parametrize("case", STATS_CASES, ids=lambda c: f"n{c[0]}_{c[1]}to{c[2]}_{'x'.join(map(str, c[3]))}")
+@pytest.mark.parametrize("case", STATS_CASES,
+                         ids=lambda c: f"n{c[0]}_{c[1]}to{c[2]}_{'x'.join(map(str, c[3]))}_off{c[6]:g}")
 def test_persistent_brick_epilogue_gn_stats(gpu, case):
     """GroupNorm(16) statistics accumulated in the persistent brick's epilogue (u3d_convg_brick_stats) against the
     statistics pass over the same stored output; the output itself bitwise equal to the plain launch. Residual
-    cases add a +4 offset (|mean| >> std: the unshifted E[x^2] - mean^2 form is checked where it is weakest).
-    Tolerance as the ring's epilogue statistics: |d mean| <= 2e-4 std, rstd relative <= 5e-4."""
+    cases add an offset to the output: +4, and +-1250 for |mean| / std ~ 50 (the unshifted E[x^2] - mean^2 form is
+    checked where it is weakest; fp64 partials since round 4). Tolerance as the ring's epilogue statistics:
+    |d mean| <= 2e-4 std, rstd relative <= 5e-4."""
     from u3d import ops
-    n, cin, cout, dims, res, gnp = case
+    n, cin, cout, dims, res, gnp, off = case
     torch.manual_seed(3)
     x = (torch.randn((n,) + dims + (cin,), device=gpu) * 1.2 + 0.1).to(torch.bfloat16)
     w = torch.randn(cout, cin, 3, 3, 3, device=gpu)
@@ -85,7 +90,7 @@ def test_persistent_brick_epilogue_gn_stats(gpu, case):
     G = 16
     gn = (ops.gn_stats(x, G), 1 + 0.1 * torch.randn(cin, device=gpu), 0.1 * torch.randn(cin, device=gpu), G) \
         if gnp else None
-    r = (torch.randn((n,) + dims + (cout,), device=gpu) + 4.0).to(torch.bfloat16) if res else None
+    r = (torch.randn((n,) + dims + (cout,), device=gpu) + off).to(torch.bfloat16) if res else None
     y, s16 = ops.conv_fwd_stats(x, pf, cout, 3, 1, gn, r)
     assert s16 is not None, "routing must take the persistent brick with epilogue statistics"
     y0 = ops.conv_fwd(x, pf, cout, 3, 1, gn, r)
@@ -93,6 +98,8 @@ def test_persistent_brick_epilogue_gn_stats(gpu, case):
     ref = ops.gn_stats(y, G)
     torch.cuda.synchronize()
     std = 1.0 / ref[..., 1]
+    if abs(off) > 100:
+        assert (ref[..., 0].abs() / std).min().item() >= 30, "the large-offset case must have |mean| / std >> 1"
     dm = ((s16[..., 0] - ref[..., 0]).abs() / std).max().item()
     dr = ((s16[..., 1] - ref[..., 1]).abs() / ref[..., 1]).max().item()
     assert dm <= 2e-4, f"epilogue GN mean error {dm:.2e} std"
