@@ -34,6 +34,9 @@ constexpr int RG_SS = 4 * RG_PS;                     // ring slot stride
 constexpr int RG_NT = 512;
 constexpr int RG_LD = (RG_NR * 4 + RG_NT - 1) / RG_NT;  // 3 staged 16-B pieces per thread and plane
 constexpr int RG_NWR = 27 * 32;                      // weight rows (t, co)
+#ifndef RG_HOIST
+#define RG_HOIST 1
+#endif
 #ifdef U3D_STAMPS
 // [workgroup][wave][8]: t0, t1 (s_memtime), r0, r1 (s_memrealtime), cycles in the compute steps (MFMAs + the staging
 // side work between them), in steps without compute, in the barriers, steps | compute steps << 32
@@ -219,13 +222,44 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   int gn_n = -1;
   // branch-free staging: out-of-volume rows load a valid dummy address and are zeroed when written
   // staged piece i of plane p (16 B of one halo row) into v[i]; bit i of m = the row is inside the volume
+  // (round 4, RG_HOIST) a lane's halo row of piece i is the same in every plane: its byte offset is a per-lane constant
+  // plus a wave-uniform plane base, and its in-volume test changes only with the column — per piece and plane one add
+  // and one select instead of the integer address math (r04 stamps / ISA: issue slots the MFMA chain needs)
+#if RG_HOIST
+  int plo[RG_LD];
+#pragma unroll
+  for (int i = 0; i < RG_LD; ++i) {
+    const int row = srow + i * (RG_NT / 4);
+    plo[i] = (((row / RG_HW) * g.w + row % RG_HW) * 64 + ch * 16);
+  }
+  unsigned pin = 0;
+  int col_h0 = -1, col_w0 = -1;
+#endif
   auto load_piece = [&](const RGPlane& p, int i, u32x4 (&v)[RG_LD], unsigned& m) {
+#if RG_HOIST
+    if (i == 0 && p.valid && (p.h0 != col_h0 || p.w0 != col_w0)) {  // uniform: once per run of the walk
+      col_h0 = p.h0;
+      col_w0 = p.w0;
+      pin = 0;
+#pragma unroll
+      for (int j = 0; j < RG_LD; ++j) {
+        const int row = srow + j * (RG_NT / 4);
+        const bool ok = row < RG_NR && (unsigned)(p.h0 - 1 + row / RG_HW) < (unsigned)g.h &&
+                        (unsigned)(p.w0 - 1 + row % RG_HW) < (unsigned)g.w;
+        pin |= (ok ? 1u : 0u) << j;
+      }
+    }
+    const int base = (((p.n * g.d + p.zin) * g.h + p.h0 - 1) * g.w + p.w0 - 1) * 64;
+    const bool ok = p.valid && (unsigned)p.zin < (unsigned)g.d && ((pin >> i) & 1u);
+    const unsigned off = ok ? (unsigned)(base + plo[i]) : 0xFFFFFFF0u;
+#else
     const int row = srow + i * (RG_NT / 4);
     const int hw = row % RG_HW, hh = row / RG_HW;
     const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
     const bool ok = p.valid && row < RG_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
                     (unsigned)zw < (unsigned)g.w;
     const unsigned off = ok ? (unsigned)((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * 64 + ch * 16) : 0xFFFFFFF0u;
+#endif
     v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     m = (i == 0 ? 0u : m) | ((ok ? 1u : 0u) << i);
   };
@@ -835,7 +869,7 @@ extern "C" int u3d_conv32_ring_q(int flip, const void* x, int n, int d, int h, i
   if (flip) RQ_LAUNCH(true, false, false, 16);
   else if (gn_stats && residual) RQ_LAUNCH(false, true, true, 4);
   else if (gn_stats) RQ_LAUNCH(false, true, false, 8);
-  else if (residual) RQ_LAUNCH(false, false, true, 16);
+  else if (residual) RQ_LAUNCH(false, false, true, 14);
   else RQ_LAUNCH(false, false, false, 16);
 #undef RQ_LAUNCH
   return check_launch("conv32_ring_kernel (work stealing)");
