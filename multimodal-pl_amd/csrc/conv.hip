@@ -794,7 +794,12 @@ static int launch_igemm(Geom g, int n, const T* x, const T* wpk, TO* y, const T*
   g.kps = (nk + ns - 1) / ns;
   g.slab = ns > 1 ? ws : nullptr;
   if constexpr (sizeof(T) == 2) {
-    g.mtiles = cdiv(Mq, 128);
+    // 256-row M tiles (8 MFMAs per wave per K step instead of 4: half the barriers and LDS stage writes per flop) for
+    // large unsplit BN = 64 launches (the stride-2 layer-1/2 forwards), IGEMM_BM = 128 / 256 forces (A/B)
+    const int env_bm = opt(OPT_IGEMM_BM);
+    const bool bm256 = BN == 64 && ns == 1 && (env_bm == 256 || (env_bm == 0 && (long long)cdiv(Mq, 256) *
+                                                                                 cdiv(g.cout, 64) * n >= 256));
+    g.mtiles = cdiv(Mq, bm256 ? 256 : 128);
     g.ntiles = cdiv(g.cout, BN);
     if (g.cin_p % 64 == 0) {  // 64-channel stages: twice the MFMAs per barrier
       g.kps = (g.ntaps * (g.cin_p / 64) + ns - 1) / ns;
@@ -808,6 +813,13 @@ static int launch_igemm(Geom g, int n, const T* x, const T* wpk, TO* y, const T*
                            ga, be, g);
       else
         hipLaunchKernelGGL((igemm_bf16_kernel<TO, 128, 32, 4, 1, 4>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st,
+                           ga, be, g);
+    } else if (BN == 64 && bm256) {
+      if (k64)
+        hipLaunchKernelGGL((igemm_bf16_kernel<TO, 256, 64, 2, 2, 8>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st,
+                           ga, be, g);
+      else
+        hipLaunchKernelGGL((igemm_bf16_kernel<TO, 256, 64, 2, 2, 4>), grid, dim3(NTHR), 0, s, x, wpk, y, res, bias, st,
                            ga, be, g);
     } else if (BN == 64) {
       if (k64)

@@ -16,3 +16,10 @@ for i in 1 2; do
 done
 grep -v amdgpu.ids $O/kab.log
 (cd /tmp && timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1) ; grep -o "SQ_[A-Z_0-9]*" $O/counters.txt | sort -u | tr '\n' ' ' | head -c 4000
+for i in 1 2; do
+  for v in "U3D_IGEMM_BM=128" "U3D_IGEMM_BM=0"; do
+    echo "== $v" >> $O/kab_igemm.log
+    env $v timeout -k 10 120 python tools/kbench.py fwd_s2_96 fwd_s2_48 fwd_s2_24 >> $O/kab_igemm.log 2>&1 || exit 1
+  done
+done
+grep -v amdgpu.ids $O/kab_igemm.log
