@@ -128,6 +128,10 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   char* const wts = smem + 4 * RG_SS;
   char* const junk = wts + 4 * RG_NWR * 16;  // target of the staging lanes past the plane's last row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef U3D_PRIO
+  // diagnostic: static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   // staging: fixed 8-channel chunk (plane) per thread, 8 threads = 8 consecutive rows of one plane (a wave covers 16
   // whole rows = 1 KB of contiguous voxels per load)
   const int ch = (tid >> 3) & 3;

@@ -140,6 +140,9 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
   char* const junk = dyr + 2 * WR_DSLOT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = tid & 3;
+#ifdef U3D_PRIO
+  if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);  // diagnostic (see conv_ring.hip)
+#endif
   const TileSplit ts = xcd_tile_split();  // XCD-aware: the channel tiles of neighbouring plane ranges share an L2
   const int ci0 = ts.tx * 32, co0 = ts.ty * 32, split = ts.split;
   WRWalk walk{};

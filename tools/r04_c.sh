@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_wgrad_dma.py tests/test_gpu
 tail -1 $O/pytest.log
 L=$R/multimodal-pl_amd/u3d
 for i in 1 2; do
-  for v in "U3D_WR_DMA=0" "U3D_LIB=$L/libu3d_ab.so U3D_WR_DMA=0" "U3D_WR_DMA=1" "U3D_LIB=$L/libu3d_la2.so" "U3D_LIB=$L/libu3d_la3.so"; do
+  for v in "U3D_WR_DMA=0" "U3D_LIB=$L/libu3d_ab.so U3D_WR_DMA=0" "U3D_WR_DMA=1" "U3D_LIB=$L/libu3d_la2.so" "U3D_LIB=$L/libu3d_la3.so" "U3D_LIB=$L/libu3d_prio.so U3D_WR_DMA=0"; do
     echo "== $v" >> $O/kab.log
     env $v timeout -k 10 120 python tools/kbench.py wgrad96 wgrad48 fwd96 fwd96_nores dgrad96gn >> $O/kab.log 2>&1 || exit 1
   done
