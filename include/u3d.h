@@ -226,6 +226,18 @@ int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h, int w, co
                           const void* residual, void* y, float* stats_ws, long long ws_floats, float* stats_out,
                           u3d_stream_t stream);
 
+/* Data gradient of conv(relu(gn(x))) for the persistent brick (48^3 / 24^3 levels) with the GroupNorm backward's
+ * partial pass (per channel sum g and sum g*xhat, g = relu-mask * dA) taken in its epilogue: dx = dA as
+ * u3d_convg_brick(flip = 1), parts[n][nparts][cin][2] per brick for u3d_gn_bwd_parts. cin / cout are the FORWARD
+ * conv's (dy has cout channels, x and dx cin); gn_* = the GroupNorm on x (unet3D.py:44-53). nparts =
+ * u3d_convg_brick_gn_nparts(...) (0: the persistent kernel does not run this shape; take u3d_convg_brick + u3d_gn_bwd).
+ * Replaces the gn_bwd_partial pass of u3d_gn_bwd at these levels (reference: the autograd of F.group_norm after
+ * Conv3d, unet3D.py:27, :44-73). */
+int u3d_convg_brick_gn_nparts(int n, int cin, int d, int h, int w, int cout);
+int u3d_convg_brick_dgrad_gn(const void* dy, int n, int cout, int d, int h, int w, const void* wpk_dgrad, int cin,
+                             const void* x, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
+                             int gn_groups, void* dx, float* parts, int nparts, u3d_stream_t stream);
+
 /* bf16 3^3 weight gradient in halo-brick form (ds_read_b64_tr_b16 operands, all 27 taps per workgroup);
  * same partial-slab output as u3d_conv_wgrad (nsplit from u3d_conv_wgrad_brick_splits). */
 int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, int cout, int stride);

@@ -97,6 +97,42 @@ __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t u) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0}));
 }
 
+// Sum of 8 per-lane values over the 32 lanes of each wave half, transposed: afterwards lane r (r = lane & 31) holds
+// the total of value (r >> 2) & 7 (fixed order, so deterministic; every lane of a group of 4 holds the same bits).
+// Butterfly where each step keeps the half of the values whose index bit equals the lane bit: lane bit 4 by
+// v_permlane16_swap (no selects), bit 3 by DPP row_ror:8 (= xor 8 within a row), bit 2 by ds_swizzle xor 4, then
+// the remaining lanes bits 1, 0 add by DPP quad_perm (xor 2, xor 1). 20 instructions for 8 values (the generic
+// __shfl_xor butterfly compiled to ~3x that: bpermute index math and exec-mask selects).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float half_sum8_transposed(float (&v)[8], int r) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // lane bit 4: rows 0 / 1 (and 2 / 3) exchange values i / i + 4
+    const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, v[i]),
+                                                     __builtin_bit_cast(uint32_t, v[i + 4]), false, false);
+    // (hipcc of ROCm 7.2 folds sw[0] + sw[1] into sw[0] + sw[0] — seen in the ISA of a two-line kernel; the empty
+    // asm hides the second result from that combine)
+    uint32_t hi = sw[1];
+    asm volatile("" : "+v"(hi));
+    v[i] = __builtin_bit_cast(float, sw[0]) + __builtin_bit_cast(float, hi);
+  }
+  const bool b3 = (r & 8) != 0, b2 = (r & 4) != 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // lane bit 3
+    const float keep = b3 ? v[i + 2] : v[i], send = b3 ? v[i] : v[i + 2];
+    v[i] = keep + dpp_mov<0x128>(send);  // row_ror:8
+  }
+  {  // lane bit 2
+    const float keep = b2 ? v[1] : v[0], send = b2 ? v[0] : v[1];
+    v[0] = keep + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, send), 0x101F));
+  }
+  v[0] += dpp_mov<0x4E>(v[0]);  // quad_perm [2,3,0,1]: xor 2 (a + b and b + a: the same bits)
+  v[0] += dpp_mov<0xB1>(v[0]);  // quad_perm [1,0,3,2]: xor 1
+  return v[0];
+}
+
 // 16-byte vector of T: 8 bf16 or 4 f32.
 template <typename T> struct Vec16 { static constexpr int N = 16 / sizeof(T); };
 

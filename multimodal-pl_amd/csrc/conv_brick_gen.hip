@@ -286,7 +286,11 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_brick_kernel(const bf16* __res
 // epilogue is register-only (permlane32 swap, residual add, two 16-B stores per lane and co block) and never
 // touches the LDS the next unit's halo is being written into. Same operands, same fp32 accumulation order per
 // output (chunk, tap plane, tap, k-half) as convg_brick_kernel: bitwise-equal results.
-template <int CO, bool FLIP, int BWX = 16>
+// GB (data gradient only, round 4): the epilogue also takes the GroupNorm backward's partial sums over the dA it
+// stores, as the 96^3 ring does (conv_ring.hip, GB): res = the GN input x (loaded at the stored dA's addresses, not
+// added), gstat / gamma / beta = that GroupNorm, spart = parts[n][bricks per sample][cout][2] of (sum g, sum g*xhat),
+// g = relu-mask * dA; u3d_gn_bwd_parts finishes (no partial pass over dA and x).
+template <int CO, bool FLIP, int BWX = 16, bool GB = false>
 __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                                bf16* __restrict__ y, const bf16* __restrict__ res,
                                                                const float* __restrict__ gstat,
@@ -317,15 +321,20 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   // GroupNorm (scale, shift) per input channel of the samples in flight, slot = sample & 1: filled once per sample
   // (the staging reads it from LDS — no global loads whose wait would drain the halo/weight prefetch)
   __shared__ __attribute__((aligned(16))) f32x2 gtab[2][GB_MAXC];
+  // GB: (scale, shift, rstd, mean) per dA channel of the samples in flight (the epilogue's relu test and xhat)
+  __shared__ __attribute__((aligned(16))) f32x4 gbt[GB ? 2 : 1][GB ? GB_MAXC : 1];
   // output GroupNorm statistics (spart != nullptr): per (wave, lane half, tn, run v, channel pair q) (sum, sum sq), fp64
   __shared__ double sst[8][2][TN * 2 * 4][2];
 
   // the data gradient never takes a residual or output statistics (convg_impl): dead at compile time, so its
-  // epilogue's registers are not reserved
-  if constexpr (FLIP) {
+  // epilogue's registers are not reserved (GB: res is the GN input x, spart the GN-backward partials)
+  static_assert(!GB || FLIP, "GB: data gradient only");
+  if constexpr (FLIP && !GB) {
     res = nullptr;
     spart = nullptr;
   }
+  float* const gbpart = GB ? spart : nullptr;
+  if constexpr (GB) spart = nullptr;  // (the forward's output-statistics path stays dead)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   int bid;
@@ -374,7 +383,11 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       const float mean = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, so, 0, 0));
       const float rstd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, so + 4, 0, 0));
       const float sc_ = rstd * __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, c * 4, 0, 0));
-      gtab[nn & 1][tid] = f32x2{sc_, __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, c * 4, 0, 0)) - mean * sc_};
+      const float sh_ = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, c * 4, 0, 0)) - mean * sc_;
+      if constexpr (GB)
+        gbt[nn & 1][tid] = f32x4{sc_, sh_, rstd, mean};
+      else
+        gtab[nn & 1][tid] = f32x2{sc_, sh_};
     }
   };
   // buffer loads with 32-bit offsets (the host guarantees x, y / the residual and the weight pack below 2 GiB): the
@@ -563,15 +576,15 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     };
     // the first co block's residual flies under the last step's staging commit (the next unit's first weights and
     // halo); the other blocks' are issued after it, when the staging registers are free
-    if (res) res_load(0);
+    if (!GB && res) res_load(0);
     if (more) {
       w_commit(par ^ 1);
       __syncthreads();
       halo_commit();
     }
-    if (res) {
+    if (res) {  // (GB: every block's x after the commit)
 #pragma unroll
-      for (int tn = 1; tn < TN; ++tn) res_load(tn);
+      for (int tn = GB ? 0 : 1; tn < TN; ++tn) res_load(tn);
     }
     __syncthreads();
     par ^= 1;
@@ -583,8 +596,67 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     // per co block tn: (sum, sum sq) of the 4 channel pairs q of each v half, over this lane's voxels; reduced over the
     // lane half (32 voxels) and stored per wave into the LDS before the next co block (8 pairs live, not 16)
     f32x2 ps[2 * 4];
+    float* const gred = reinterpret_cast<float*>(&sst[0][0][0][0]);  // GB: [wave][tn][hh][32] (sst is idle in FLIP)
+    static_assert(!GB || sizeof(sst) >= 8 * TN * 2 * 32 * sizeof(float), "GB reduction buffer");
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
+      if constexpr (GB) {
+        // per channel half v: (sum g, sum g*xhat) of this lane's 8 channels e over its voxels tm, from the stored bf16
+        // dA and x at the same address (as gn_bwd_partial reads them); v outer so that 16 sums are live, not 32
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
+          u32x4 o[TM];
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm) {
+            uint32_t pk[2][2];
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq)
+#pragma unroll
+              for (int e = 0; e < 2; ++e)
+                pk[qq][e] = pack_bf16x2(acc[tm][tn][4 * (2 * v + qq) + 2 * e], acc[tm][tn][4 * (2 * v + qq) + 2 * e + 1]);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const auto sw = __builtin_amdgcn_permlane32_swap(pk[0][e], pk[1][e], false, false);
+              pk[0][e] = sw[0];
+              pk[1][e] = sw[1];
+            }
+            o[tm] = u32x4{pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
+            if (ook[tm] && co < g.cout)
+              __builtin_amdgcn_raw_buffer_store_b128(o[tm], yrs, (unsigned)((ovox[tm] * g.cout + co) * 2), 0, 0);
+          }
+          // two passes of 4 channels (8 sums live), channel outer (one table entry live): holding more spilled
+          const f32x4* tb = &gbt[cu.nn & 1][co];
+          // dA of voxels past the volume / padded channels -> 0 (their x reads returned zeros: all terms finite)
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[tm][k] = (ook[tm] && co < g.cout) ? o[tm][k] : 0u;
+#pragma unroll
+          for (int eh = 0; eh < 2; ++eh) {
+            float gbs[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) gbs[i] = 0.f;
+#pragma unroll
+            for (int el = 0; el < 4; ++el) {
+              const int e = eh * 4 + el;
+              const f32x4 t = tb[e];
+#pragma unroll
+              for (int tm = 0; tm < TM; ++tm) {
+                const uint32_t ow = o[tm][e >> 1], xw = rv[tm][tn][v][e >> 1];
+                const float a = __builtin_bit_cast(float, (e & 1) ? (ow & 0xFFFF0000u) : (ow << 16));
+                const float xv = __builtin_bit_cast(float, (e & 1) ? (xw & 0xFFFF0000u) : (xw << 16));
+                const float gd = fmaf(xv, t[0], t[1]) > 0.f ? a : 0.f;  // the forward prologue's relu test
+                gbs[el * 2] += gd;
+                gbs[el * 2 + 1] = fmaf(gd, xv - t[3], gbs[el * 2 + 1]);  // sum g (x - mean); x rstd at the end
+              }
+            }
+            half_sum8_transposed(gbs, r);
+            if ((r & 3) == 0) gred[((wave * TN + tn) * 2 + hh) * 32 + v * 16 + eh * 8 + (r >> 2)] = gbs[0];
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < 2 * 4; ++i) ps[i] = f32x2{0.f, 0.f};
 #pragma unroll
@@ -651,6 +723,17 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
           }
       }
     }
+    if constexpr (GB) {  // the 8 waves in order, per (channel, sum) of the tile -> parts[brick][cout][2]
+      __syncthreads();
+      if (tid < CO * 2) {
+        const int cl = tid >> 1, k = tid & 1, tn = cl >> 5, v = (cl >> 4) & 1, h_ = (cl >> 3) & 1, e = cl & 7;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) t += gred[((w * TN + tn) * 2 + h_) * 32 + (v * 8 + e) * 2 + k];
+        const int co = cu.co0 + cl;
+        if (co < g.cout) gbpart[((long long)(u / nct) * g.cout + co) * 2 + k] = k ? t * gbt[cu.nn & 1][co][2] : t;
+      }
+    }
     if (spart != nullptr) {  // the 8 waves in order, per channel pair of the tile
       __syncthreads();
       if (tid < CO / 2) {  // channel pair tid of the tile: c = 2 tid -> (tn, v, hh, q)
@@ -714,12 +797,23 @@ static int convg_num_cus() {
   return n;
 }
 
+// 8-wide bricks where the plane width is a multiple of 8 but not of 16 (24^3: the 16-wide bricks' second column is
+// half empty); CONVG_BW8 = 0 / 1 forces the choice (A/B)
+static bool pbrick_bw8(int w) {
+  const int e8 = opt(OPT_CONVG_BW8);
+  return e8 >= 0 ? e8 != 0 : (w % 16 != 0 && w % 8 == 0);
+}
+
 static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                       const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                      const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream) {
+                      const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream,
+                      const void* gbx = nullptr, float* gbparts = nullptr) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && n <= GB_MAXN, "convg_brick: bad args");
+  U3D_REQUIRE(!gbparts || (flip && gbx && gn_stats && !residual && !spart && cout % gn_groups == 0),
+              "convg_brick_dgrad_gn: bad args");
   U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "convg_brick: channels must be multiples of 8");
-  U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0), "convg_brick: bad GN");
+  U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && (gbparts ? cout : cin) % gn_groups == 0),
+              "convg_brick: bad GN");
   GBGeom g{};
   g.n = n; g.d = d; g.h = h; g.w = w;
   g.cin = cin; g.cout = cout; g.cin_p = round_up(cin, 32); g.cout_p = round_up(cout, 32);
@@ -745,13 +839,11 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
                      27LL * g.cout_p * g.cin_p * 2 < (1LL << 31) - 64;
   // (a data gradient with a residual add — not a trunk routing, kept for the ABI — runs the one-shot kernel: the
   // persistent data gradient has no residual path, so its epilogue reserves no registers for one)
-  const bool pers = pers_on && small && (!gn_stats || g.cin_p <= GB_MAXC) && !(flip && residual);
+  const bool pers = pers_on && small && (!gn_stats || (gbparts ? g.cout_p : g.cin_p) <= GB_MAXC) && !(flip && residual);
   U3D_REQUIRE(!spart || (pers && !flip && cout % 32 == 0), "convg_brick_stats: needs the persistent forward, cout %% 32 == 0");
+  U3D_REQUIRE(!gbparts || pers, "convg_brick_dgrad_gn: needs the persistent data gradient (u3d_convg_brick_gn_nparts)");
   if (pers) {
-    // 8-wide bricks where the plane width is a multiple of 8 but not of 16 (24^3: the 16-wide bricks' second
-    // column is half empty); CONVG_BW8 = 0 / 1 forces the choice (A/B)
-    const int e8 = opt(OPT_CONVG_BW8);
-    const bool bw8 = e8 >= 0 ? e8 != 0 : (w % 16 != 0 && w % 8 == 0);
+    const bool bw8 = pbrick_bw8(w);
     GBGeom gp = g;
     if (bw8) {
       gp.nbw = cdiv(w, 8);
@@ -766,7 +858,16 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
               nwg = cdiv(nunits, per);
 #define U3D_PB(C, F)                                                                                               \
   do {                                                                                                             \
-    if (bw8)                                                                                                       \
+    if (F && gbparts) {                                                                                            \
+      if (bw8)                                                                                                     \
+        hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 8, F>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,       \
+                           (const bf16*)wpk, (bf16*)y, (const bf16*)gbx, gn_stats, gn_gamma, gn_beta, gp, per,     \
+                           nunits, gbparts);                                                                       \
+      else                                                                                                         \
+        hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 16, F>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,      \
+                           (const bf16*)wpk, (bf16*)y, (const bf16*)gbx, gn_stats, gn_gamma, gn_beta, gp, per,     \
+                           nunits, gbparts);                                                                       \
+    } else if (bw8)                                                                                                \
       hipLaunchKernelGGL((convg_pbrick_kernel<C, F, 8>), dim3(nwg), dim3(GB_NT), 0, s, (const bf16*)x,          \
                          (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, gp, per,  \
                          nunits, spart);                                                                           \
@@ -811,6 +912,27 @@ extern "C" int u3d_convg_brick(int flip, const void* x, int n, int cin, int d, i
                                const void* residual, void* y, u3d_stream_t stream) {
   return convg_impl(flip, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, nullptr,
                     nullptr, stream);
+}
+
+// Data gradient of conv(relu(gn(x))) with gn_bwd's partial pass fused into the persistent brick's epilogue
+// (convg_pbrick_kernel<.., GB>): dx = the data gradient dA (as u3d_convg_brick(flip = 1)), parts[n][nparts][cin][2]
+// (nparts = u3d_convg_brick_gn_nparts) = per brick (sum g, sum g*xhat) of g = relu-mask * dA for u3d_gn_bwd_parts.
+// Here cin / cout are the FORWARD conv's channels: dy has cout, x / dA have cin; gn_* is the GroupNorm on x.
+extern "C" int u3d_convg_brick_gn_nparts(int n, int cin, int d, int h, int w, int cout) {
+  const bool small = (long long)n * d * h * w * std::max(cin, cout) * 2 < (1LL << 31) - 64 &&
+                     27LL * round_up(cin, 32) * round_up(cout, 32) * 2 < (1LL << 31) - 64;
+  if (opt(OPT_CONVG_PERSIST) == 0 || !small || round_up(cin, 32) > GB_MAXC || n < 1 || n > GB_MAXN) return 0;
+  return cdiv(d, GB_BD) * cdiv(h, GB_BH) * cdiv(w, pbrick_bw8(w) ? 8 : GB_BW);
+}
+
+extern "C" int u3d_convg_brick_dgrad_gn(const void* dy, int n, int cout, int d, int h, int w, const void* wpk_dgrad,
+                                        int cin, const void* x, const float* gn_stats, const float* gn_gamma,
+                                        const float* gn_beta, int gn_groups, void* dx, float* parts, int nparts,
+                                        u3d_stream_t stream) {
+  U3D_REQUIRE(parts && x && nparts == u3d_convg_brick_gn_nparts(n, cin, d, h, w, cout) && nparts > 0,
+              "convg_brick_dgrad_gn: parts layout (u3d_convg_brick_gn_nparts) mismatch");
+  return convg_impl(1, dy, n, cout, d, h, w, wpk_dgrad, cin, gn_stats, gn_gamma, gn_beta, gn_groups, nullptr, dx,
+                    nullptr, nullptr, stream, x, parts);
 }
 
 extern "C" long long u3d_convg_brick_stats_ws_floats(int n, int d, int h, int w, int cout) {

@@ -55,6 +55,8 @@ _SIGS = {
     "u3d_convg_brick": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P],
     "u3d_convg_brick_stats_ws_floats": [I, I, I, I, I],
     "u3d_convg_brick_stats": [P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P, P],
+    "u3d_convg_brick_gn_nparts": [I, I, I, I, I, I],
+    "u3d_convg_brick_dgrad_gn": [P, I, I, I, I, I, P, I, P, P, P, P, I, P, P, I, P],
     "u3d_conv_wgrad_brick_splits": [I, I, I, I, I, I, I],
     "u3d_conv_wgrad_brick": [P, P, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_conv_wgrad1_splits": [I, I, I, I, I, I, I],

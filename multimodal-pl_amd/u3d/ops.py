@@ -391,7 +391,7 @@ def conv_dgrad_gn(dy, wpk_dgrad, cin, x, k, stride, gn):
     n, d, h, w_ = x.shape[:4]
     if not (GN_BWD_FUSED and gn is not None and dy.shape[-1] == 32 and _use_conv32(dy.dtype, cin, 32, k, stride, n, w_)
             and CONV32_FN == "u3d_conv32_ring" and _conv32_fits(dy) and not _ring_queue(dgrad=True)):
-        return None
+        return _conv_dgrad_gn_brick(dy, wpk_dgrad, cin, x, k, stride, gn)
     st, ga, be, G = gn
     wps = query("u3d_conv32_ring_wps", n, d, h, w_)
     da = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
@@ -400,6 +400,33 @@ def conv_dgrad_gn(dy, wpk_dgrad, cin, x, k, stride, gn):
     call("u3d_conv32_ring_dgrad_gn", dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), x.data_ptr(), st.data_ptr(),
          ga.data_ptr(), be.data_ptr(), G, da.data_ptr(), parts.data_ptr(), _stream())
     _probe1(pr, "conv32_ring dgrad +GN-bwd partials", 2.0 * n * d * h * w_ * 27 * 32 * 32, n * d * h * w_)
+    return da, parts
+
+
+GN_BWD_FUSED_BRICK = os.environ.get("U3D_GN_BWD_FUSED_BRICK", "1") != "0"  # the same in the persistent brick (48^3/24^3)
+
+
+def _conv_dgrad_gn_brick(dy, wpk_dgrad, cin, x, k, stride, gn):
+    """conv_dgrad_gn where conv_dgrad would run the persistent brick (u3d_convg_brick_dgrad_gn): parts per brick."""
+    if not (GN_BWD_FUSED and GN_BWD_FUSED_BRICK and gn is not None and dy.dtype == torch.bfloat16):
+        return None
+    shape = tuple(x.shape[:4])
+    cout = dy.shape[-1]
+    n, d, h, w_ = shape
+    # only where conv_dgrad itself runs the generic brick (not the 32-channel ring, e.g. its queue form under a
+    # collective, nor the small-volume kernel)
+    if _use_conv32(dy.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(dy):
+        return None
+    if _use_small(dy.dtype, cout, cin, k, stride, shape) or not _use_gen_brick(dy.dtype, cout, cin, k, stride, shape):
+        return None
+    nparts = query("u3d_convg_brick_gn_nparts", n, cin, d, h, w_, cout)
+    if nparts <= 0:
+        return None
+    st, ga, be, G = gn
+    da = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
+    parts = torch.empty((n, nparts, cin, 2), dtype=torch.float32, device=dy.device)
+    call("u3d_convg_brick_dgrad_gn", dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, x.data_ptr(),
+         st.data_ptr(), ga.data_ptr(), be.data_ptr(), G, da.data_ptr(), parts.data_ptr(), nparts, _stream())
     return da, parts
 
 

@@ -92,6 +92,29 @@ for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 
     CASES[f"dgrad{lvl}"] = (lambda s=s, c=c: _dgrad(2, c, c, s, 3, 1))
     CASES[f"wgrad{lvl}"] = (lambda s=s, c=c: _wgrad(2, c, c, s, 3, 1))
 CASES["dgrad96gn"] = lambda: _dgrad_gn(2, 32, 96)
+CASES["dgrad48gn"] = lambda: _dgrad_gn(2, 64, 48)   # persistent brick + GN-backward partials (round 4)
+CASES["dgrad24gn"] = lambda: _dgrad_gn(2, 128, 24)
+
+
+def _gnb(n, c, s, fused):
+    """data gradient + the whole GroupNorm backward (dx, dgamma, dbeta): fused partials + parts finalize + apply, or
+    the separate data gradient + partial pass + apply"""
+    x, pf, pd, g, r, dy, flop = conv_case(n, c, c, s, 3, 1, True)
+    dg, db = torch.zeros(c, device=dev), torch.zeros(c, device=dev)
+
+    def f():
+        if fused:
+            da, parts = ops.conv_dgrad_gn(dy, pd, c, x, 3, 1, g)
+            ops.gn_bwd_parts(da, x, parts, g[0], g[1], g[2], g[3], dgamma=dg, dbeta=db)
+        else:
+            da = ops.conv_dgrad(dy, pd, c, x.shape[:4], 3, 1)
+            ops.gn_bwd(da, x, g[0], g[1], g[2], g[3], dgamma=dg, dbeta=db)
+    return t_(f), flop
+
+
+for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128)]:
+    CASES[f"gnb{lvl}f"] = (lambda s=s, c=c: _gnb(2, c, s, True))
+    CASES[f"gnb{lvl}s"] = (lambda s=s, c=c: _gnb(2, c, s, False))
 CASES["fwd12nogn"] = lambda: _fwd(2, 256, 256, 12, 3, 1, False, False)
 CASES["wgrad_s2_96"] = lambda: _wgrad(2, 32, 64, 96, 3, 2)
 CASES["wgrad_s2_48"] = lambda: _wgrad(2, 64, 128, 48, 3, 2)

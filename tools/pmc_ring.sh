@@ -12,4 +12,5 @@ timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/w -o run
 mkdir -p $O/fd $O/wd
 cp $(find $O/f -name '*counter_collection.csv' | head -1) $O/fd/run_counter_collection.csv
 cp $(find $O/w -name '*counter_collection.csv' | head -1) $O/wd/run_counter_collection.csv
-python3 $R/tools/pmc_traffic.py $O/fd $O/wd "$KRX" $R/$OUTJ 20
+case "$OUTJ" in /*) OJ=$OUTJ;; *) OJ=$R/$OUTJ;; esac
+python3 $R/tools/pmc_traffic.py $O/fd $O/wd "$KRX" $OJ 20
