@@ -313,7 +313,14 @@ __global__ __launch_bounds__(NTHR) void igemm_bf16_kernel(const bf16* __restrict
                                                           const float* __restrict__ gstat,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, Geom g) {
-  constexpr int NCH = KC, ROWB = KC * 16, BKC = KC * 8, D = KC == 4 ? 3 : 2;
+#ifndef U3D_IGEMM_D4
+#define U3D_IGEMM_D4 3
+#endif
+#ifndef U3D_IGEMM_D8
+#define U3D_IGEMM_D8 2
+#endif
+  // register pipeline depth (K-steps of global loads in flight); -DU3D_IGEMM_D4 / _D8 override (diagnostic builds)
+  constexpr int NCH = KC, ROWB = KC * 16, BKC = KC * 8, D = KC == 4 ? U3D_IGEMM_D4 : U3D_IGEMM_D8;
   constexpr int A_LOADS = BM * NCH / NTHR;
   constexpr int B_CH = BN * NCH;
   constexpr int B_LOADS = (B_CH + NTHR - 1) / NTHR;

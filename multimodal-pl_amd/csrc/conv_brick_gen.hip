@@ -329,6 +329,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
   // the data gradient never takes a residual or output statistics (convg_impl): dead at compile time, so its
   // epilogue's registers are not reserved (GB: res is the GN input x, spart the GN-backward partials)
   static_assert(!GB || FLIP, "GB: data gradient only");
+  constexpr int GB_EARLY = TM == 1 ? TN : 1;  // GB: co blocks whose x loads go out in the last step (VGPR budget)
   if constexpr (FLIP && !GB) {
     res = nullptr;
     spart = nullptr;
@@ -497,6 +498,30 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.f;
+    // epilogue from registers: lane (r, hh) holds channels tn*32 + 8q + 4hh + e (acc[tm][tn][4q + e]) of voxel
+    // ovox[tm]; after the swap it holds channels tn*32 + 8hh .. +7 and tn*32 + 16 + 8hh .. +7
+    // this lane's output voxels (MFMA column r of row tiles 0, 1)
+    int ovox[TM];  // < 2^31 voxels x channels (host check): 32-bit buffer offsets
+    bool ook[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      int vd, vh, vw;
+      tile_vox(TM * wave + tm, r, vd, vh, vw);
+      const int zd = cu.d0 + vd, zh = cu.h0 + vh, zw = cu.w0 + vw;
+      ook[tm] = zd < g.d && zh < g.h && zw < g.w;
+      ovox[tm] = ((cu.nn * g.d + zd) * g.h + zh) * g.w + zw;
+    }
+    u32x4 rv[TM][TN][2];
+    auto res_load = [&](int tn) {  // the residual of co block tn (buffer loads: zeros where res is null)
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
+          const unsigned ro = (ook[tm] && co < g.cout) ? (unsigned)((ovox[tm] * g.cout + co) * 2) : 0xFFFFFFF0u;
+          rv[tm][tn][v] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
+        }
+    };
     for (int s = 0; s < nsteps; ++s) {
       const int td = s % 3;
       const bool last = s + 1 == nsteps;
@@ -505,6 +530,11 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
         const Unit& lq = last ? nu : cu;
         w_load(lq.co0, last ? 0 : s + 1);
         if (td == 2) halo_load(lq, last ? 0 : s / 3 + 1);
+      }
+      if constexpr (GB) {  // the GN input x (first co block; all with 8-wide bricks) flies under the last tap plane
+        if (last)
+#pragma unroll
+          for (int tn = 0; tn < GB_EARLY; ++tn) res_load(tn);
       }
       const char* wb = wbuf[par];
       const int od = FLIP ? 2 - td : td;
@@ -550,30 +580,6 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       par ^= 1;
     }
 
-    // epilogue from registers: lane (r, hh) holds channels tn*32 + 8q + 4hh + e (acc[tm][tn][4q + e]) of voxel
-    // ovox[tm]; after the swap it holds channels tn*32 + 8hh .. +7 and tn*32 + 16 + 8hh .. +7
-    // this lane's output voxels (MFMA column r of row tiles 0, 1)
-    int ovox[TM];  // < 2^31 voxels x channels (host check): 32-bit buffer offsets
-    bool ook[TM];
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-      int vd, vh, vw;
-      tile_vox(TM * wave + tm, r, vd, vh, vw);
-      const int zd = cu.d0 + vd, zh = cu.h0 + vh, zw = cu.w0 + vw;
-      ook[tm] = zd < g.d && zh < g.h && zw < g.w;
-      ovox[tm] = ((cu.nn * g.d + zd) * g.h + zh) * g.w + zw;
-    }
-    u32x4 rv[TM][TN][2];
-    auto res_load = [&](int tn) {  // the residual of co block tn (buffer loads: zeros where res is null)
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-          const int co = cu.co0 + tn * 32 + 16 * v + 8 * hh;
-          const unsigned ro = (ook[tm] && co < g.cout) ? (unsigned)((ovox[tm] * g.cout + co) * 2) : 0xFFFFFFF0u;
-          rv[tm][tn][v] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
-        }
-    };
     // the first co block's residual flies under the last step's staging commit (the next unit's first weights and
     // halo); the other blocks' are issued after it, when the staging registers are free
     if (!GB && res) res_load(0);
@@ -582,9 +588,9 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
       __syncthreads();
       halo_commit();
     }
-    if (res) {  // (GB: every block's x after the commit)
+    if (res) {  // (GB: the x of the blocks not loaded early, under the first block's epilogue)
 #pragma unroll
-      for (int tn = GB ? 0 : 1; tn < TN; ++tn) res_load(tn);
+      for (int tn = GB ? GB_EARLY : 1; tn < TN; ++tn) res_load(tn);
     }
     __syncthreads();
     par ^= 1;

@@ -21,8 +21,16 @@ namespace u3d {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
-constexpr int S2_NT = 512;
-constexpr int S2_HMAX = 512;                     // halo rows (max)
+// U3D_S2_NT = 512: one 8-wave workgroup per CU (236 VGPRs), the next chunk prefetched into registers under the MFMAs;
+// 256: 4-wave workgroups of up to 128 q voxels, two per CU (76 KB of LDS each), no register prefetch — the other
+// workgroup's MFMAs cover a workgroup's loads and dx stores
+#ifndef U3D_S2_NT
+#define U3D_S2_NT 512
+#endif
+constexpr int S2_NT = U3D_S2_NT;
+constexpr bool S2_PF = S2_NT == 512;             // register prefetch of the next chunk
+constexpr int S2_MAXQ = S2_NT / 2;               // q voxels per brick (32 per wave)
+constexpr int S2_HMAX = S2_NT == 512 ? 512 : 320;  // halo rows (max)
 constexpr int S2_PS = S2_HMAX * 16 + 64;         // halo plane stride
 constexpr int S2_NWR = 27 * 32;                  // weight rows (tap, co)
 constexpr int S2_WPS = S2_NWR * 16 + 64;         // weight plane stride
@@ -40,7 +48,7 @@ struct S2Geom {
   int nvq;                 // q voxels per brick (<= 256)
 };
 
-__global__ __launch_bounds__(S2_NT, 1) void dgrad_s2_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wpk,
+__global__ __launch_bounds__(S2_NT, 512 / S2_NT) void dgrad_s2_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wpk,
                                                            bf16* __restrict__ dx, S2Geom g) {
   __shared__ __attribute__((aligned(16))) char smem[S2_LDS];
   char* const hal = smem;
@@ -61,6 +69,7 @@ __global__ __launch_bounds__(S2_NT, 1) void dgrad_s2_kernel(const bf16* __restri
   const int nn = b / g.nbd;
   const int q0d = bd_ * g.bd, q0h = bh_ * g.bh, q0w = bw_ * g.bw;
 
+  static_assert(S2_NT == 512 || S2_NT == 256, "workgroup size");
   // this lane's q row (clamped into the brick for the idle rows of the last tile)
   const int v = min(wave * 32 + r, g.nvq - 1);
   const int vw = v % g.bw, vh = (v / g.bw) % g.bh, vd = v / (g.bw * g.bh);
@@ -121,7 +130,7 @@ __global__ __launch_bounds__(S2_NT, 1) void dgrad_s2_kernel(const bf16* __restri
   __syncthreads();
   for (int c = 0; c < nchunk; ++c) {
     const bool more = c + 1 < nchunk;
-    if (more) {
+    if (S2_PF && more) {
       halo_load(c + 1);
       w_load(c + 1);
     }
@@ -153,6 +162,10 @@ __global__ __launch_bounds__(S2_NT, 1) void dgrad_s2_kernel(const bf16* __restri
     }
     __syncthreads();
     if (more) {
+      if (!S2_PF) {
+        halo_load(c + 1);
+        w_load(c + 1);
+      }
       commit();
       __syncthreads();
     }
@@ -206,12 +219,12 @@ extern "C" int u3d_conv_dgrad_s2(const void* dy, int n, int cout, const void* wp
   g.D = d; g.H = h; g.W = w;
   g.qd = (d - 1) / 2 + 1; g.qh = (h - 1) / 2 + 1; g.qw = (w - 1) / 2 + 1;
   g.cy = cout; g.cy_p = round_up(cout, 32); g.cx = cin; g.cx_p = round_up(cin, 32);
-  // q-brick: up to 256 voxels, w extent first (contiguous dy rows), extents that tile the volume evenly,
+  // q-brick: up to S2_MAXQ voxels, w extent first (contiguous dy rows), extents that tile the volume evenly,
   // halo <= S2_HMAX rows
   auto even = [](int q, int mx) { return cdiv(q, cdiv(q, std::max(1, mx))); };
   g.bw = even(g.qw, 16);
-  g.bh = even(g.qh, 256 / (g.bw * 2));
-  g.bd = even(g.qd, std::min(g.qd, 256 / (g.bw * g.bh)));
+  g.bh = even(g.qh, S2_MAXQ / (g.bw * 2));
+  g.bd = even(g.qd, std::min(g.qd, S2_MAXQ / (g.bw * g.bh)));
   while ((g.bd + 1) * (g.bh + 1) * (g.bw + 1) > S2_HMAX && g.bd > 1) --g.bd;
   while ((g.bd + 1) * (g.bh + 1) * (g.bw + 1) > S2_HMAX && g.bh > 1) --g.bh;
   U3D_REQUIRE((g.bd + 1) * (g.bh + 1) * (g.bw + 1) <= S2_HMAX, "conv_dgrad_s2: halo too large");

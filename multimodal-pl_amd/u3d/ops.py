@@ -403,7 +403,11 @@ def conv_dgrad_gn(dy, wpk_dgrad, cin, x, k, stride, gn):
     return da, parts
 
 
-GN_BWD_FUSED_BRICK = os.environ.get("U3D_GN_BWD_FUSED_BRICK", "1") != "0"  # the same in the persistent brick (48^3/24^3)
+GN_BWD_FUSED_BRICK = os.environ.get("U3D_GN_BWD_FUSED_BRICK", "1") != "0"  # the same in the persistent brick
+# ... up to this many voxels (n*d*h*w): the fused epilogue pays where the separate partial pass is latency-bound. Kernel
+# A/B (tools/kbench.py gnb*, gpurun_out/r04_g): 2x24^3 x 128 ch 51.4 -> 47.9 us for the data gradient + GN backward,
+# 2x48^3 x 64 ch 89.7 -> 92.5 us (the x loads and the epilogue sums outweigh the 56 MB partial pass there)
+GN_BWD_FUSED_BRICK_MAX_VOX = int(os.environ.get("U3D_GN_BWD_FUSED_BRICK_MAX_VOX", str(2 * 32 ** 3)))
 
 
 def _conv_dgrad_gn_brick(dy, wpk_dgrad, cin, x, k, stride, gn):
@@ -413,6 +417,8 @@ def _conv_dgrad_gn_brick(dy, wpk_dgrad, cin, x, k, stride, gn):
     shape = tuple(x.shape[:4])
     cout = dy.shape[-1]
     n, d, h, w_ = shape
+    if n * d * h * w_ > GN_BWD_FUSED_BRICK_MAX_VOX:
+        return None
     # only where conv_dgrad itself runs the generic brick (not the 32-channel ring, e.g. its queue form under a
     # collective, nor the small-volume kernel)
     if _use_conv32(dy.dtype, cin, cout, k, stride, n, w_) and _conv32_fits(dy):

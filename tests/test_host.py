@@ -538,3 +538,34 @@ def test_stride2_dgrad_beyond_2gib_routes_to_the_64bit_kernel(monkeypatch):
     ops.conv_dgrad(torch.empty((2, 24, 64, 64, 64), dtype=torch.bfloat16, device="meta"), wpk, 32, (2, 48, 128, 128),
                    3, 2)
     assert calls == ["u3d_conv_dgrad", "u3d_conv_dgrad_s2"], calls
+
+
+def test_dgrad_gn_routing_brick_levels(monkeypatch):
+    """conv_dgrad_gn takes the persistent brick with the GN-backward partials in its epilogue
+    (u3d_convg_brick_dgrad_gn) where conv_dgrad runs that brick and the volume is small (24^3 level); at 48^3 and for
+    the 32-channel ring shapes it declines or takes the ring's own fused form (routing only: meta tensors, calls
+    recorded, nothing launched)."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    from u3d import ops
+    calls = []
+    monkeypatch.setattr(ops, "call", lambda name, *a: calls.append(name))
+    monkeypatch.setattr(ops, "_stream", lambda: 0)
+    monkeypatch.setattr(ops, "query", lambda name, *a: 54 if name == "u3d_convg_brick_gn_nparts" else 64)
+
+    def gn(c):
+        return (torch.empty((2, 16, 2), device="meta"), torch.empty(c, device="meta"), torch.empty(c, device="meta"), 16)
+
+    def run(s, c):
+        x = torch.empty((2, s, s, s, c), dtype=torch.bfloat16, device="meta")
+        dy = torch.empty((2, s, s, s, c), dtype=torch.bfloat16, device="meta")
+        wpk = torch.empty((27, c, c), dtype=torch.bfloat16, device="meta")
+        return ops.conv_dgrad_gn(dy, wpk, c, x, 3, 1, gn(c))
+
+    r = run(24, 128)
+    assert r is not None and r[1].shape == (2, 54, 128, 2) and calls == ["u3d_convg_brick_dgrad_gn"], calls
+    calls.clear()
+    assert run(48, 64) is None and calls == []          # 48^3: the separate partial pass measured faster
+    assert run(12, 256) is None and calls == []         # small-volume kernel level: no fused form
+    monkeypatch.setattr(ops, "GN_BWD_FUSED_BRICK", False)
+    assert run(24, 128) is None and calls == []
