@@ -6,13 +6,15 @@
 // dx[2q + p] = sum over the taps of parity class p of dy[q + delta] . W[tap]: per dim, p = 0 takes tap 1 at
 // delta 0, p = 1 takes tap 0 at delta 1 and tap 2 at delta 0 — the 27 taps split into 8 parity classes, and
 // the dy window a tap reads is one of 8 shifts delta in {0,1}^3 of a q-brick.
-//   * one workgroup (8 waves) = one q-brick of up to 256 dy voxels x one 32-channel dx tile; each wave owns
-//     32 q rows and ALL 8 parity accumulators (8 x 32x32 fp32), so one workgroup writes the whole 2x-sized
-//     dx region of its brick: every dx voxel is produced once, with no zero-fill and no per-class launches;
+//   * one workgroup (4 waves; 8 in the U3D_S2_NT = 512 build) = one q-brick of up to 128 (256) dy voxels x one
+//     32-channel dx tile; each wave owns 32 q rows and ALL 8 parity accumulators (8 x 32x32 fp32), so one
+//     workgroup writes the whole 2x-sized dx region of its brick: every dx voxel is produced once, with no
+//     zero-fill and no per-class launches;
 //   * K loop = 32-channel dy chunks: the dy halo ((bd+1)(bh+1)(bw+1) voxels) and the 27 taps' weights of
 //     the chunk are staged once in LDS (chunk-planar, padded planes: conflict-free staging writes); each of
 //     the 8 shifted A fragments is read once per k16 step and feeds the 1..8 taps that use that shift;
-//   * the next chunk is prefetched into registers while the MFMAs of the current one run;
+//   * two workgroups per CU: one's chunk loads and dx stores run under the other's MFMAs (the 512-thread build
+//     prefetches the next chunk into registers instead);
 //   * the MFMA is issued transposed (A = weights, B = dy rows), so a lane's accumulators are dx channels of one voxel:
 //     the epilogue stores them as 16-B chunks straight from registers (one v_permlane32_swap per pair).
 #include "common.h"
@@ -21,11 +23,12 @@ namespace u3d {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
-// U3D_S2_NT = 512: one 8-wave workgroup per CU (236 VGPRs), the next chunk prefetched into registers under the MFMAs;
-// 256: 4-wave workgroups of up to 128 q voxels, two per CU (76 KB of LDS each), no register prefetch — the other
-// workgroup's MFMAs cover a workgroup's loads and dx stores
+// U3D_S2_NT = 256 (default since round 4): 4-wave workgroups of up to 128 q voxels, two per CU (76 KB of LDS and 248
+// VGPRs each), no register prefetch — the other workgroup's MFMAs cover a workgroup's loads and dx stores; 512: one
+// 8-wave workgroup per CU (236 VGPRs), the next chunk prefetched into registers under its own MFMAs. Kernel A/B
+// (2 x 96^3 / 48^3 / 24^3 / 12^3 levels, gpurun_out/r04_h): 64 / 38.8 / 30.2 / 29.1 -> 62.6 / 28.2 / 26.9 / 24.3 us
 #ifndef U3D_S2_NT
-#define U3D_S2_NT 512
+#define U3D_S2_NT 256
 #endif
 constexpr int S2_NT = U3D_S2_NT;
 constexpr bool S2_PF = S2_NT == 512;             // register prefetch of the next chunk
@@ -45,7 +48,7 @@ struct S2Geom {
   int bd, bh, bw;          // q-brick
   int hh, hw, nh;          // halo pitch (bh+1, bw+1) and rows
   int nbd, nbh, nbw, nct;  // bricks per dim, 32-wide dx channel tiles
-  int nvq;                 // q voxels per brick (<= 256)
+  int nvq;                 // q voxels per brick (<= S2_MAXQ)
 };
 
 __global__ __launch_bounds__(S2_NT, 512 / S2_NT) void dgrad_s2_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ wpk,
