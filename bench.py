@@ -72,7 +72,8 @@ def synthetic(batch, patch, device, seed, modality="ct"):
 # the ring kernels the bench probes at the full patch, their committed-profile tag (profiles/rNN_pmc_<tag>.json) and the
 # substring of their rocprofv3 kernel name + grid in profiles/rNN_kernel_summary.txt (tools/prof_summary.py)
 RING_TAGS = {
-    "wgrad_ring 32->32 GN": ("wgrad96", "wgrad_ring_kernel<true, 16, 16>', 1, '1', '256'"),
+    "wgrad_ring 32->32 GN": ("wgrad96", ("wgrad_ring_dma_kernel<true>', 1, '1', '256'",  # U3D_WR_DMA=1 (default)
+                                         "wgrad_ring_kernel<true, 16, 16>', 1, '1', '256'")),
     "conv32_ring dgrad +GN-bwd partials": ("dgrad96gn", "conv32_ring_kernel<true, true, false, 8, false>', 256"),
     "conv32_ring fwd GN +res +stats": ("fwd96", "conv32_ring_kernel<false, true, true, 12, false>', 256"),
     "conv32_ring fwd GN +stats": ("fwd96_nores", "conv32_ring_kernel<false, true, false, 16, false>', 256"),
@@ -195,9 +196,10 @@ def trace_check(krx, flops):
     if f is None or krx is None:
         return None
     import re
+    krxs = (krx,) if isinstance(krx, str) else krx
     with open(f) as fh:
         for line in fh:
-            if krx in line:
+            if any(k in line for k in krxs):
                 m = re.search(r"avg=\s*([0-9.]+)us", line)
                 if m:
                     us = float(m.group(1))
