@@ -22,15 +22,22 @@ namespace u3d {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
-constexpr int SC_NT = 512;
-constexpr int SC_HMAX = 640;                     // halo rows (max)
+// U3D_SC_NT = 512: one 8-wave workgroup of up to 256 output voxels per CU (105 KB of LDS); 256: 4-wave workgroups
+// of up to 128 voxels, two per CU (<= 80 KB each: smaller halo, GN table for cin <= 640)
+#ifndef U3D_SC_NT
+#define U3D_SC_NT 512
+#endif
+constexpr int SC_NT = U3D_SC_NT;
+constexpr int SC_MAXV = SC_NT / 2;               // output voxels per brick (32 per wave)
+constexpr int SC_HMAX = SC_NT == 512 ? 640 : 320;  // halo rows (max)
 constexpr int SC_PS = SC_HMAX * 16 + 64;         // halo plane stride (+64 B: conflict-free staging writes)
 constexpr int SC_NWR = 27 * 32;                  // weight rows (tap, co)
 constexpr int SC_WPS = SC_NWR * 16 + 64;         // weight plane stride
 constexpr int SC_HLD = SC_HMAX * 4 / SC_NT;      // 5 halo loads per thread
 constexpr int SC_WLD = (SC_NWR * 4 + SC_NT - 1) / SC_NT;  // 7 weight loads per thread
 constexpr int SC_LDS = 4 * SC_PS + 4 * SC_WPS;
-constexpr int SC_MAXC = 1024;                    // GN prologue: cin_p <= SC_MAXC (per-channel table after SC_LDS)
+constexpr int SC_MAXC = SC_NT == 512 ? 1024 : 640;  // GN prologue: cin_p <= SC_MAXC (per-channel table after SC_LDS)
+static_assert(SC_NT == 512 || SC_LDS + SC_MAXC * 8 <= 81920, "two workgroups per CU");
 
 struct SCGeom {
   int n, d, h, w;
@@ -45,7 +52,7 @@ struct SCGeom {
 };
 
 template <bool FLIP>
-__global__ __launch_bounds__(SC_NT, 1) void conv_small_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
+__global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                              bf16* __restrict__ y, const bf16* __restrict__ res,
                                                              const float* __restrict__ gstat,
                                                              const float* __restrict__ gamma,
@@ -286,8 +293,8 @@ extern "C" int u3d_conv_small(int flip, const void* x, int n, int cin, int d, in
   g.gn_groups = gn_groups;
   auto even = [](int q, int mx) { return cdiv(q, cdiv(q, std::max(1, mx))); };
   g.bw = even(w, 16);
-  g.bh = even(h, 256 / (g.bw * 2));
-  g.bd = even(d, std::min(d, 256 / (g.bw * g.bh)));
+  g.bh = even(h, SC_MAXV / (g.bw * 2));
+  g.bd = even(d, std::min(d, SC_MAXV / (g.bw * g.bh)));
   while ((g.bd + 2) * (g.bh + 2) * (g.bw + 2) > SC_HMAX && g.bd > 1) --g.bd;
   while ((g.bd + 2) * (g.bh + 2) * (g.bw + 2) > SC_HMAX && g.bh > 1) --g.bh;
   while ((g.bd + 2) * (g.bh + 2) * (g.bw + 2) > SC_HMAX && g.bw > 1) --g.bw;

@@ -132,7 +132,8 @@ def test_rccl_world1_bucketed_step_matches_plain_step(gpu, monkeypatch, hold):
     parameter, and COLLECTIVE_IN_FLIGHT switching the 96^3-class data-gradient rings to the work-stealing kernel
     (u3d_conv32_ring_q). bf16 step on 2 x 1 x 64^3 (the 32-channel convs run on the ring). Averaging over one rank is
     exact and the work-stealing ring is bitwise equal to the static one, so gradients and post-SGD weights must
-    equal the plain single-process step (checked to <= 1e-6 relative; reference: train_amos_atlas_final.py:141-144,
+    equal the plain single-process step (<= 1e-6 relative on identical kernel paths, 5e-5 where the collective forms
+    reassociated a GroupNorm backward's sums, see below; reference: train_amos_atlas_final.py:141-144,
     375 and run_amos_atlas_final.sh:2). ``hold``: the bucketer's completion poll is pinned to "still running" (what a
     slow all-reduce at N > 1 looks like), so the collective-tolerant kernel forms must run; "polled": the real
     work.is_completed() poll, with which the static forms come back as soon as the world-1 all-reduces finish."""
@@ -186,7 +187,18 @@ def test_rccl_world1_bucketed_step_matches_plain_step(gpu, monkeypatch, hold):
     else:
         assert ("u3d_conv32_ring_dgrad_gn", False) in called, "the static fused ring never came back after completion"
     assert net.fallback_names == ["extra_scale"], net.fallback_names
+    # Identical kernel paths give identical gradients (1e-6: the averaging over one rank is exact). While a bucket is
+    # in flight the 32-channel data-gradient ring runs its work-stealing form, whose GroupNorm backward takes the
+    # separate partial pass instead of the epilogue partials: the same sums in another fp32 order. Through the bf16
+    # roundings downstream that moved layer0's gn1 / the stem weight gradient by up to 8e-6 (r04, tools/path_diff.py:
+    # the call sequences differ only there), so a step that switched forms is held to 5e-5 — DDP bugs (a missing
+    # average, a mis-mapped bucket slice, a stale gradient) are O(1).
+    switched = any(name == "u3d_conv32_ring_q" for name, _ in called)
+    tol = 5e-5 if switched else 1e-6
+    rel = {k: ((g[k] - g_ref[k]).norm() / g_ref[k].norm().clamp_min(1e-30)).item() for k in g_ref}
+    worst = sorted(rel.items(), key=lambda kv: -kv[1])[:6]
+    print(f"worst gradient rel L2 vs the plain step (tolerance {tol:g}):", ", ".join(f"{k} {r:.2e}" for k, r in worst))
+    bad = [f"{k} {r:.3e}" for k, r in worst if r > tol]
+    assert not bad, "gradient rel L2 vs the plain step: " + ", ".join(bad)
     for k in g_ref:
-        r = ((g[k] - g_ref[k]).norm() / g_ref[k].norm().clamp_min(1e-30)).item()
-        assert r <= 1e-6, f"{k}: gradient rel L2 {r:.3e} vs the plain step"
-        assert (w[k] - w_ref[k]).abs().max().item() <= 1e-6 * max(1.0, w_ref[k].abs().max().item()), k
+        assert (w[k] - w_ref[k]).abs().max().item() <= tol * max(1.0, w_ref[k].abs().max().item()), k
