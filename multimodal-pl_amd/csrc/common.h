@@ -42,6 +42,7 @@ enum Opt : int {
   OPT_WB_S2CO64,      // stride-2 brick weight gradient: two co tiles per workgroup (0: one)
   OPT_WR_DMA,         // 16 x 16-tile weight-gradient ring with LDS-DMA staging (0: register staging)
   OPT_IGEMM_BM,       // bf16 implicit GEMM M tile: 0 auto (256 for large unsplit BN 64 launches), 128 / 256 force
+  OPT_WSTD_ROW,       // weight-standardisation backward: one row per block from registers (0: chunked LDS kernel)
   OPT_COUNT
 };
 int opt(Opt o);

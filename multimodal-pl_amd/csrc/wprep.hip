@@ -378,6 +378,73 @@ __global__ __launch_bounds__(WG_T) void wstd_grad_kernel(WBatch<WPack> bt) {
     wgrad_rows<1>(D, co0);
 }
 
+// (4+5), one row per block (round 4): the row's K = cin * k^3 (w, g) pairs are loaded at once — NPT per thread,
+// straight into registers, w and dW in parameter order (coalesced), g gathered from its [t][co][ci] layout — then the
+// row sums (fp32 per thread in a fixed order, fp64 across the block in a fixed order) and dW from the same registers.
+// One load round-trip per row instead of the chunk stage / barrier chain of wstd_grad_kernel, whose 64-block launch
+// of a 256x256 layer took 44 us (latency-bound, r04 trace); wstd_grad_kernel stays for rows longer than 56 x 256.
+template <int NPT>
+__global__ __launch_bounds__(WB_T) void wstd_grad_row_kernel(WBatch<WPack> bt) {
+  __shared__ double red[WB_T / 64][2];
+  __shared__ float fs[2];
+  const WPack& D = bt.d[find_desc(bt, blockIdx.x)];
+  const int co = blockIdx.x - D.b0, tid = threadIdx.x;
+  const int K3 = D.k3, K = D.cin * K3, cout_p = round_up(D.cout, 32), cin_p = round_up(D.cin, 32);
+  const bool std_ = D.st != nullptr;
+  const float mu = std_ ? D.st[co * 2] : 0.f;
+  const float rsg = std_ ? 1.f / D.st[co * 2 + 1] : 1.f;
+  const float* wr = D.w + (long long)co * K;
+  float wv[NPT], gv[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int e = tid + i * WB_T;
+    const int ci = K3 == 27 ? e / 27 : e, t = e - ci * K3;
+    const bool in = e < K;
+    wv[i] = in && std_ ? wr[e] : 0.f;
+    gv[i] = in ? D.g[((long long)t * cout_p + co) * cin_p + ci] : 0.f;
+  }
+  float f1 = 0.f, f2 = 0.f;
+  if (std_) {
+    float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      m1 += gv[i];
+      m2 = fmaf(gv[i], (wv[i] - mu) * rsg, m2);
+    }
+    double d1 = m1, d2 = m2;
+    for (int o = 32; o > 0; o >>= 1) {
+      d1 += __shfl_xor(d1, o);
+      d2 += __shfl_xor(d2, o);
+    }
+    if ((tid & 63) == 0) {
+      red[tid >> 6][0] = d1;
+      red[tid >> 6][1] = d2;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double t1 = 0, t2 = 0;
+      for (int w = 0; w < WB_T / 64; ++w) {
+        t1 += red[w][0];
+        t2 += red[w][1];
+      }
+      fs[0] = (float)(t1 / K);
+      fs[1] = (float)(t2 / (K > 1 ? K - 1 : 1));
+    }
+    __syncthreads();
+    f1 = fs[0];
+    f2 = fs[1];
+  }
+  float* o = D.dw + (long long)co * K;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int e = tid + i * WB_T;
+    if (e < K) {
+      const float v = std_ ? (gv[i] - f1 - (wv[i] - mu) * rsg * f2) * rsg : gv[i];
+      o[e] = (D.acc ? o[e] : 0.f) + v;
+    }
+  }
+}
+
 }  // namespace u3d
 
 using namespace u3d;
@@ -431,7 +498,7 @@ extern "C" int u3d_wstd_bwd_batch(const u3d_wstd_desc* descs, int count, float* 
   hipStream_t st = (hipStream_t)stream;
   WBatch<WSum> sb{};
   WBatch<WPack> ab{};
-  int sblocks = 0, ablocks = 0;
+  int sblocks = 0, ablocks = 0, maxk = 0;
   for (int i = 0; i < count; ++i) {
     const u3d_wstd_desc& s = descs[i];
     U3D_REQUIRE(s.part && s.w && s.dw && s.nsplit >= 1 && s.cout > 0 && s.cin > 0 && (s.ksize == 1 || s.ksize == 3),
@@ -448,6 +515,29 @@ extern "C" int u3d_wstd_bwd_batch(const u3d_wstd_desc* descs, int count, float* 
     ab.d[ab.count++] = WPack{s.w, s.standardize ? s.wstats : nullptr, nullptr, nullptr, s.part, nullptr, s.dw,
                              s.cout, s.cin, k3, s.accumulate, ablocks};
     ablocks += cdiv(s.cout, WG_R);
+    maxk = std::max(maxk, s.cin * k3);
+  }
+  // one row per block where every row fits the register form (U3D_WSTD_ROW=0: the chunked kernel, A/B)
+  const int npt = cdiv(maxk, WB_T);
+  if (opt(OPT_WSTD_ROW) != 0 && npt <= 56) {
+    int rb = 0;
+    for (int i = 0; i < ab.count; ++i) {
+      ab.d[i].b0 = rb;
+      rb += ab.d[i].cout;
+    }
+    if (sb.count) {
+      hipLaunchKernelGGL(wstd_sum_slabs_kernel, dim3(sblocks), dim3(WB_T), 0, st, sb);
+      int rc = check_launch("wstd_sum_slabs_kernel");
+      if (rc) return rc;
+    }
+#define U3D_WROW(N) hipLaunchKernelGGL(wstd_grad_row_kernel<N>, dim3(rb), dim3(WB_T), 0, st, ab)
+    if (npt <= 4) U3D_WROW(4);
+    else if (npt <= 8) U3D_WROW(8);
+    else if (npt <= 16) U3D_WROW(16);
+    else if (npt <= 28) U3D_WROW(28);
+    else U3D_WROW(56);
+#undef U3D_WROW
+    return check_launch("wstd_grad_row_kernel");
   }
   if (sb.count) {
     hipLaunchKernelGGL(wstd_sum_slabs_kernel, dim3(sblocks), dim3(WB_T), 0, st, sb);

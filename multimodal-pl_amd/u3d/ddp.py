@@ -138,9 +138,7 @@ class GradBucketer:
             return
         for b, (names, _) in enumerate(self.buckets):
             if self.works[b] is None:
-                for n in names:
-                    if n not in self.done_names:
-                        self.out(n).zero_()
+                self._zero_missing(b, names)
                 self._launch(b)
         for b, w in enumerate(self.works):
             w.wait()
@@ -165,6 +163,26 @@ class GradBucketer:
         ops.COLLECTIVE_POLL[0] = None
         if self.on_finish is not None:
             self.on_finish()
+
+    def _zero_missing(self, b, names):
+        """Zero the slices of bucket b whose gradient this backward never produced, one fill per run of adjacent
+        slices (the slices follow the bucket's name order; a fill per parameter measured ~40 fills per step)."""
+        start = end = None
+        for n in names:
+            _, off, shape = self.where[n]
+            nel = 1
+            for d in shape:
+                nel *= d
+            if n in self.done_names:
+                if start is not None:
+                    self.bufs[b][start:end].zero_()
+                    start = None
+                continue
+            if start is None:
+                start = off
+            end = off + nel
+        if start is not None:
+            self.bufs[b][start:end].zero_()
 
     def returned(self, names, grads):
         """The gradients a native tape's autograd Function returns: None where finish() already set .grad."""

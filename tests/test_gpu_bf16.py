@@ -182,6 +182,32 @@ def test_wstd_batch_matches_single(gpu):
         assert (dw - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
 
 
+def test_wstd_bwd_row_kernel_matches_chunked(gpu):
+    """Weight-standardisation backward, one row per block from registers (WSTD_ROW=1, round 4) == the chunked LDS
+    kernel (WSTD_ROW=0): the same per-row sums in another fp32 order (rows up to 56 x 256 long), accumulate on/off."""
+    from u3d import ops
+    torch.manual_seed(9)
+    shapes = [(32, 1, 3, True), (32, 32, 3, True), (64, 64, 1, True), (256, 256, 3, True), (48, 512, 3, True),
+              (8, 32, 1, False), (24, 40, 3, True)]
+    ws = [torch.randn(co, ci, k, k, k, device=gpu) * 0.1 + 0.02 for co, ci, k, _ in shapes]
+    sts = [ops.wstd_fwd(w, torch.float32, std, need_dgrad=False)[2] for w, (_, _, _, std) in zip(ws, shapes)]
+    parts = [torch.randn((ns, k ** 3, ops.round32(co), ops.round32(ci)), device=gpu)
+             for (co, ci, k, _), ns in zip(shapes, [1, 3, 4, 9, 2, 1, 5])]
+    base = [torch.randn_like(w) for w in ws]
+    out = {}
+    for row in (0, 1):
+        for acc in (False, True):
+            dws = [b.clone() for b in base]
+            items = [(p.clone(), p.shape[0], w, st, std, dw, acc)
+                     for p, w, st, (_, _, _, std), dw in zip(parts, ws, sts, shapes, dws)]
+            with ops.option("WSTD_ROW", row):
+                ops.wstd_bwd_batch(items)
+            out[row, acc] = dws
+    for acc in (False, True):
+        for a, b in zip(out[0, acc], out[1, acc]):
+            assert (a - b).abs().max().item() <= 2e-6 * a.abs().max().item()
+
+
 @pytest.mark.parametrize("n,cin,cout,dims,s", [(2, 32, 16, (8, 10, 12), 1), (2, 32, 64, (8, 10, 12), 2),
                                                (1, 64, 128, (6, 6, 7), 2), (2, 320, 320, (3, 3, 3), 1),
                                                (1, 32, 8, (5, 7, 9), 1), (2, 32, 32, (40, 40, 40), 2)])
