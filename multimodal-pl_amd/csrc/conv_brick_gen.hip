@@ -503,14 +503,18 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     // this lane's output voxels (MFMA column r of row tiles 0, 1)
     int ovox[TM];  // < 2^31 voxels x channels (host check): 32-bit buffer offsets
     bool ook[TM];
+    auto out_vox = [&]() {
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-      int vd, vh, vw;
-      tile_vox(TM * wave + tm, r, vd, vh, vw);
-      const int zd = cu.d0 + vd, zh = cu.h0 + vh, zw = cu.w0 + vw;
-      ook[tm] = zd < g.d && zh < g.h && zw < g.w;
-      ovox[tm] = ((cu.nn * g.d + zd) * g.h + zh) * g.w + zw;
-    }
+      for (int tm = 0; tm < TM; ++tm) {
+        int vd, vh, vw;
+        tile_vox(TM * wave + tm, r, vd, vh, vw);
+        const int zd = cu.d0 + vd, zh = cu.h0 + vh, zw = cu.w0 + vw;
+        ook[tm] = zd < g.d && zh < g.h && zw < g.w;
+        ovox[tm] = ((cu.nn * g.d + zd) * g.h + zh) * g.w + zw;
+      }
+    };
+    // (GB: before the walk, its x loads go out in the last step; otherwise after it: nothing held across the MFMAs)
+    if constexpr (GB) out_vox();
     u32x4 rv[TM][TN][2];
     auto res_load = [&](int tn) {  // the residual of co block tn (buffer loads: zeros where res is null)
 #pragma unroll
@@ -582,6 +586,7 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
 
     // the first co block's residual flies under the last step's staging commit (the next unit's first weights and
     // halo); the other blocks' are issued after it, when the staging registers are free
+    if constexpr (!GB) out_vox();
     if (!GB && res) res_load(0);
     if (more) {
       w_commit(par ^ 1);

@@ -93,6 +93,17 @@ for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 
     CASES[f"wgrad{lvl}"] = (lambda s=s, c=c: _wgrad(2, c, c, s, 3, 1))
 CASES["dgrad96gn"] = lambda: _dgrad_gn(2, 32, 96)
 CASES["dgrad48gn"] = lambda: _dgrad_gn(2, 64, 48)   # persistent brick + GN-backward partials (round 4)
+
+
+def _fwd_stats(n, c, s, res):
+    """the production brick forward: GN prologue (+ residual) + GroupNorm(16) statistics of the output from its epilogue"""
+    x, pf, pd, g, r, dy, flop = conv_case(n, c, c, s, 3, 1, True, res)
+    return t_(lambda: ops.conv_fwd_stats(x, pf, c, 3, 1, g, r)), flop
+
+
+CASES["fwd48st"] = lambda: _fwd_stats(2, 64, 48, True)
+CASES["fwd48st_nores"] = lambda: _fwd_stats(2, 64, 48, False)
+CASES["fwd24st"] = lambda: _fwd_stats(2, 128, 24, True)
 CASES["dgrad24gn"] = lambda: _dgrad_gn(2, 128, 24)
 
 
