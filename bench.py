@@ -49,8 +49,11 @@ def parse():
                         "the bucketed all-reduces launched from inside the backward and the collective-tolerant kernel "
                         "forms while they run (what N>1 pays for the overlap, measured on one GPU)")
     p.add_argument("--print-rank-env", action="store_true", help=argparse.SUPPRESS)  # launcher test (no GPU)
-    p.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph (the ring kernels' "
-                   "live timing then comes from an eager pass of the same steps after the timed region)")
+    p.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph (the default at N=1 "
+                   "without --force-buckets; the ring kernels' live timing then comes from an eager pass of the same "
+                   "steps after the timed region)")
+    p.add_argument("--eager", action="store_true", help="launch the step kernel by kernel from Python (the default at "
+                   "N>1 and with --force-buckets, where the step holds collectives)")
     return p.parse_args()
 
 
@@ -334,7 +337,10 @@ def main():
         return loss
 
     graphed = None
-    a.eager = not a.graph  # default: kernel-by-kernel launches (live HIP-event timing of the ring kernels)
+    # N=1: the step replays as one hipGraph (the Python host launching ~180 library calls per step was measured
+    # slower than the GPU runs them: eager 6.03-6.19 vs graph 5.98-6.01 ms/step, gpurun_out/r04_k); with collectives
+    # in the step (N>1, --force-buckets) kernel by kernel
+    a.eager = a.eager or not (a.graph or (world == 1 and not a.force_buckets))
     from u3d import ops as _ops
     if not a.eager:
         from u3d.graph import GraphedStep

@@ -600,13 +600,16 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
     __syncthreads();
     par ^= 1;
     // (statistics of the stored bf16 outputs, per channel pair: the GN(16) groups of every cout % 32 == 0 hold
-    // whole pairs; fp32 over the 2-4 voxels of a lane — exact for bf16 squares, at most a rounding per add — then fp64
-    // for the fixed-order reductions over lanes, waves and units. Unshifted E[x^2] - mean^2 loses |mean|^2 / var digits
-    // to cancellation: with fp32 unit partials (rounds 2-3) that cost ~1e-3 relative rstd at |mean| / std = 50; with
-    // fp64 partials the loss stays below 1e-6 there (tests/test_gpu_pbrick.py, large-mean case; ADVICE r2 / VERDICT r3))
+    // whole pairs. Unshifted fp32 E[x^2] - mean^2 loses |mean|^2 / var digits to cancellation: ~1e-3 relative rstd at
+    // |mean| / std = 50 with the rounds 2-3 fp32 partials (ADVICE r2 / VERDICT r3). Sums of x - shift in fp32 (the
+    // shift: the pair's first channel at the half-wave's first voxel, so |x - shift| ~ std), reduced transposed over
+    // the half-wave, then un-shifted in fp64 for the fixed-order reductions over waves and units
+    // (tests/test_gpu_pbrick.py, |mean| / std ~ 50 cases). An fp64 shuffle reduction of unshifted sums (round 4,
+    // first form) cost 7 us per 2x48^3 launch (kbench fwd48st 76.5 -> 83.2 us).)
     // per co block tn: (sum, sum sq) of the 4 channel pairs q of each v half, over this lane's voxels; reduced over the
     // lane half (32 voxels) and stored per wave into the LDS before the next co block (8 pairs live, not 16)
     f32x2 ps[2 * 4];
+    float shv[2 * 4];  // output statistics: per channel pair of the co block, the shift of its sums
     float* const gred = reinterpret_cast<float*>(&sst[0][0][0][0]);  // GB: [wave][tn][hh][32] (sst is idle in FLIP)
     static_assert(!GB || sizeof(sst) >= 8 * TN * 2 * 32 * sizeof(float), "GB reduction buffer");
 #pragma unroll
@@ -704,34 +707,47 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
             float f8[8];
             load16<bf16>(reinterpret_cast<const bf16*>(&o), f8);
             const bool on = ook[tm] && co < g.cout;
+            if (tm == 0)  // the pair's shift: its first channel at the half-wave's lane 0 voxel (a brick origin: inside)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const int xb = __builtin_bit_cast(int, f8[2 * q]);
+                shv[v * 4 + q] = __builtin_bit_cast(float, hh ? __builtin_amdgcn_readlane(xb, 32)
+                                                                : __builtin_amdgcn_readlane(xb, 0));
+              }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const float a0 = on ? f8[2 * q] : 0.f, a1 = on ? f8[2 * q + 1] : 0.f;
+              const float a0 = f8[2 * q] - shv[v * 4 + q], a1 = f8[2 * q + 1] - shv[v * 4 + q];
               f32x2& t = ps[v * 4 + q];
-              t[0] += a0 + a1;
-              t[1] = fmaf(a0, a0, fmaf(a1, a1, t[1]));
+              t[0] += on ? a0 + a1 : 0.f;
+              t[1] = on ? fmaf(a0, a0, fmaf(a1, a1, t[1])) : t[1];
             }
           }
         }
       }
-      if (spart != nullptr) {  // this tn's pairs: reduce over the 32 voxels of each lane half into the LDS (fp64)
-        double dps[2 * 4][2];
+      if (spart != nullptr) {  // this tn's pairs: reduce over the 32 voxels of each lane half into the LDS
+        // shifted fp32 sums (|x - shift| ~ std, not |mean|), transposed over the half-wave (lane r ends with pair
+        // (r >> 2) & 7), then un-shifted in fp64: S = sum + n s, Q = sumsq + 2 s sum + n s^2 with n the pair's valid
+        // values in this half-wave (2 channels x the voxels inside the volume)
+        float s1[8], s2[8];
 #pragma unroll
-        for (int i = 0; i < 2 * 4; ++i) {
-          dps[i][0] = ps[i][0];
-          dps[i][1] = ps[i][1];
-#pragma unroll
-          for (int o = 1; o < 32; o <<= 1) {
-            dps[i][0] += __shfl_xor(dps[i][0], o);
-            dps[i][1] += __shfl_xor(dps[i][1], o);
-          }
+        for (int i = 0; i < 8; ++i) {
+          s1[i] = ps[i][0];
+          s2[i] = ps[i][1];
         }
-        if (r == 0)
+        const float t1 = half_sum8_transposed(s1, r), t2 = half_sum8_transposed(s2, r);
+        unsigned nvox = 0;
 #pragma unroll
-          for (int i = 0; i < 2 * 4; ++i) {
-            sst[wave][hh][tn * 8 + i][0] = dps[i][0];
-            sst[wave][hh][tn * 8 + i][1] = dps[i][1];
-          }
+        for (int tm = 0; tm < TM; ++tm) {
+          const unsigned long long b = __ballot(ook[tm]);
+          nvox += __builtin_popcount(hh ? (unsigned)(b >> 32) : (unsigned)b);
+        }
+        if ((r & 3) == 0) {
+          const int i = r >> 2, v = i >> 2;
+          const double sh = (double)shv[i];
+          const double nn = cu.co0 + tn * 32 + 16 * v + 8 * hh < g.cout ? 2.0 * nvox : 0.0;
+          sst[wave][hh][tn * 8 + i][0] = (double)t1 + nn * sh;
+          sst[wave][hh][tn * 8 + i][1] = (double)t2 + 2.0 * sh * (double)t1 + nn * sh * sh;
+        }
       }
     }
     if constexpr (GB) {  // the 8 waves in order, per (channel, sum) of the tile -> parts[brick][cout][2]

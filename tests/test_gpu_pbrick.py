@@ -79,7 +79,7 @@ def test_persistent_brick_epilogue_gn_stats(gpu, case):
     """GroupNorm(16) statistics accumulated in the persistent brick's epilogue (u3d_convg_brick_stats) against the
     statistics pass over the same stored output; the output itself bitwise equal to the plain launch. Residual
     cases add an offset to the output: +4, and +-1250 for |mean| / std ~ 50 (the unshifted E[x^2] - mean^2 form is
-    checked where it is weakest; fp64 partials since round 4). Tolerance as the ring's epilogue statistics:
+    checked where it is weakest; shifted fp32 sums + fp64 un-shift since round 4). Tolerance as the ring's epilogue statistics:
     |d mean| <= 2e-4 std, rstd relative <= 5e-4."""
     from u3d import ops
     n, cin, cout, dims, res, gnp, off = case
