@@ -743,7 +743,10 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
         }
         if ((r & 3) == 0) {
           const int i = r >> 2, v = i >> 2;
-          const double sh = (double)shv[i];
+          float shi = shv[0];  // (select, not a dynamic index: that would put shv in scratch)
+#pragma unroll
+          for (int j = 1; j < 8; ++j) shi = i == j ? shv[j] : shi;
+          const double sh = (double)shi;
           const double nn = cu.co0 + tn * 32 + 16 * v + 8 * hh < g.cout ? 2.0 * nvox : 0.0;
           sst[wave][hh][tn * 8 + i][0] = (double)t1 + nn * sh;
           sst[wave][hh][tn * 8 + i][1] = (double)t2 + 2.0 * sh * (double)t1 + nn * sh * sh;
