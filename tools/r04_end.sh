@@ -15,7 +15,7 @@ timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { echo "bench failed"; 
 grep '^{' $O/bench.log | tail -1 > $O/bench.json; cut -c1-300 $O/bench.json
 timeout -k 10 300 python bench.py --no-cpu --no-infer --no-roofline --force-buckets > $O/bench_fb.log 2>&1 || { echo "fb failed"; exit 1; }
 grep '^{' $O/bench_fb.log | tail -1 > $O/bench_fb.json; cut -c1-200 $O/bench_fb.json
-(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu --no-roofline --no-infer > $O/bench_kt.log 2>&1) || { echo "prof failed"; exit 1; }
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu --no-roofline --no-infer --eager > $O/bench_kt.log 2>&1) || { echo "prof failed"; exit 1; }
 f=$(find $O/kt -name '*kernel_trace.csv' | head -1); [ -n "$f" ] && cp $(dirname $f)/*.csv $O/
 python3 tools/prof_summary.py $O 13 > $O/kernel_summary.txt 2>&1 || true
 head -25 $O/kernel_summary.txt
