@@ -64,6 +64,79 @@ __global__ __launch_bounds__(256) void up_fwd_kernel(const T* __restrict__ x, co
   storev<T, VEC>(y + off, o);
 }
 
+// bf16 form with register reuse (round 4): a thread owns the 2 x 2 outputs (oh, ow) in {2ih, 2ih+1} x {2iw, 2iw+1} of
+// one output plane od and one 8-channel chunk. Along h and w those outputs read inputs i-1, i, i+1 only (2i reads
+// i-1 / i, 2i+1 reads i / i+1, clamped), so 2 x 3 x 3 = 18 loads serve 4 outputs instead of 32 — the one-output
+// kernel issued 8 gathered loads per output and was L2-load-bound (80 us at 2x48^3 -> 96^3 x 32). Every output is
+// computed with the same Lerp weights and the same expression as up_fwd_kernel: bitwise equal.
+// grid: x = (iw, chunk) pairs of one input row, y = ih, z = n * D + od
+__global__ __launch_bounds__(256) void up_fwd_quad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ skip,
+                                                         bf16* __restrict__ y, int n, int c, int d, int h, int w) {
+  const int chn = c / 8, D = 2 * d, H = 2 * h, W = 2 * w;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w * chn) return;
+  const int j = i % chn, iw = i / chn, ih = blockIdx.y, od = blockIdx.z % D, nn = blockIdx.z / D;
+  const Lerp Ld = lerp_of(od, d);
+  const bf16* xb = x + (long long)nn * d * h * w * c + j * 8;
+  const int hs[3] = {max(ih - 1, 0), ih, min(ih + 1, h - 1)}, ws[3] = {max(iw - 1, 0), iw, min(iw + 1, w - 1)};
+  u32x4 raw[2][3][3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        raw[a][b][e] = *reinterpret_cast<const u32x4*>(xb + ((long long)((a ? Ld.i1 : Ld.i0) * h + hs[b]) * w + ws[e]) * c);
+  // tap t (0: Lerp i0, 1: i1) of output 2i + q along a dim reads slot q + t of (i-1, i, i+1) — except tap 1 of
+  // output 2i at i = 0, where Lerp clamps i0 to 0 and i1 = 1 is slot 2 (selected below; all indices static)
+  const bool hz = ih == 0, wz = iw == 0;
+  auto pick = [&](int a, int qh, int th, int qw, int tw) -> u32x4 {
+    const int hsl = qh + th, wsl = qw + tw;
+    const bool halt = qh == 0 && th == 1, walt = qw == 0 && tw == 1;
+    u32x4 v = raw[a][hsl][wsl];
+    if (halt && walt) v = hz ? (wz ? raw[a][2][2] : raw[a][2][wsl]) : (wz ? raw[a][hsl][2] : v);
+    else if (halt) v = hz ? raw[a][2][wsl] : v;
+    else if (walt) v = wz ? raw[a][hsl][2] : v;
+    return v;
+  };
+  auto un = [](const u32x4& v, int k) {
+    const uint32_t u = v[k >> 1];
+    return __builtin_bit_cast(float, (k & 1) ? (u & 0xFFFF0000u) : (u << 16));
+  };
+#pragma unroll
+  for (int qh = 0; qh < 2; ++qh) {
+    const int oh = 2 * ih + qh;
+    if (oh >= H) continue;
+    const Lerp Lh = lerp_of(oh, h);
+#pragma unroll
+    for (int qw = 0; qw < 2; ++qw) {
+      const int ow = 2 * iw + qw;
+      const Lerp Lw = lerp_of(ow, w);
+      const long long off = ((((long long)nn * D + od) * H + oh) * W + ow) * c + j * 8;
+      float sv[8];
+      if (skip) loadv<bf16, 8>(skip + off, sv);
+      u32x4 t[2][2][2];  // [a][th][tw]
+#pragma unroll
+      for (int a_ = 0; a_ < 2; ++a_)
+#pragma unroll
+        for (int th = 0; th < 2; ++th)
+#pragma unroll
+          for (int tw = 0; tw < 2; ++tw) t[a_][th][tw] = pick(a_, qh, th, qw, tw);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)  // PyTorch CPU nesting order, as up_fwd_kernel
+        o[e] = Ld.l0 * (Lh.l0 * (Lw.l0 * un(t[0][0][0], e) + Lw.l1 * un(t[0][0][1], e)) +
+                        Lh.l1 * (Lw.l0 * un(t[0][1][0], e) + Lw.l1 * un(t[0][1][1], e))) +
+               Ld.l1 * (Lh.l0 * (Lw.l0 * un(t[1][0][0], e) + Lw.l1 * un(t[1][0][1], e)) +
+                        Lh.l1 * (Lw.l0 * un(t[1][1][0], e) + Lw.l1 * un(t[1][1][1], e)));
+      if (skip)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += sv[e];
+      storev<bf16, 8>(y + off, o);
+    }
+  }
+}
+
 // outputs o (and weights) that read input i along one dim of size n (output 2n): o in {2i-1, 2i, 2i+1, 2i+2}
 __device__ __forceinline__ int taps_of(int i, int n, int (&o)[4], float (&wt)[4]) {
   int k = 0;
@@ -215,6 +288,11 @@ extern "C" int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d,
   const int row = 2 * w * (vect ? c / vec : c);
   U3D_REQUIRE((long long)n * 2 * d < 65536 && 2 * h < 65536, "upsample: volume too large for the row grid");
   const dim3 gr(cdiv(row, 256), 2 * h, n * 2 * d), bl(256);
+  if (dtype == U3D_BF16 && vect && opt(OPT_UP_QUAD) != 0) {  // UP_QUAD = 0: the one-output kernel (A/B)
+    hipLaunchKernelGGL(up_fwd_quad_kernel, dim3(cdiv(w * (c / 8), 256), h, n * 2 * d), bl, 0, s, (const bf16*)x,
+                       (const bf16*)skip, (bf16*)y, n, c, d, h, w);
+    return check_launch("up_fwd_quad_kernel");
+  }
   if (dtype == U3D_BF16) {
     if (vect) hipLaunchKernelGGL((up_fwd_kernel<bf16, 8>), gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w);
     else hipLaunchKernelGGL((up_fwd_kernel<bf16, 1>), gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w);

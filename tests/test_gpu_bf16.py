@@ -425,3 +425,20 @@ def test_head_transposed_bitwise_equal(gpu, cin, cout, dims):
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1].view(torch.int16), out[1][1].view(torch.int16))
     assert torch.equal(out[0][2].view(torch.int16), out[1][2].view(torch.int16))
+
+
+@pytest.mark.parametrize("n,c,dims,skip", [(2, 32, (48, 48, 48), True), (1, 64, (5, 1, 7), True), (2, 16, (3, 4, 1), False),
+                                          (1, 128, (12, 12, 12), True), (1, 8, (1, 1, 1), True)])
+def test_upsample_quad_bitwise_equals_one_output(gpu, n, c, dims, skip):
+    """bf16 trilinear x2 upsample (+ skip): the 2 x 2-outputs-per-thread kernel (UP_QUAD=1, round 4) is bitwise equal
+    to the one-output kernel (same Lerp weights, same expression; boundary taps selected, not clamped differently)."""
+    from u3d import ops
+    torch.manual_seed(13)
+    x = torch.randn((n,) + dims + (c,), device=gpu).to(torch.bfloat16)
+    s = torch.randn((n,) + tuple(2 * v for v in dims) + (c,), device=gpu).to(torch.bfloat16) if skip else None
+    with ops.option("UP_QUAD", 0):
+        a = ops.upsample2x_add(x, s)
+    with ops.option("UP_QUAD", 1):
+        b = ops.upsample2x_add(x, s)
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16))

@@ -101,6 +101,15 @@ def _fwd_stats(n, c, s, res):
     return t_(lambda: ops.conv_fwd_stats(x, pf, c, 3, 1, g, r)), flop
 
 
+def _up(n, c, s):
+    """trilinear x2 upsample + skip add (decoder, unet3D.py:1646) into an s^3 output: (us, bytes moved)"""
+    x = torch.randn((n, s // 2, s // 2, s // 2, c), device=dev).to(bf)
+    sk = torch.randn((n, s, s, s, c), device=dev).to(bf)
+    return t_(lambda: ops.upsample2x_add(x, sk)), 2.0 * (x.numel() + 2 * sk.numel())
+
+
+CASES["up96"] = lambda: _up(2, 32, 96)
+CASES["up48"] = lambda: _up(2, 64, 48)
 CASES["fwd48st"] = lambda: _fwd_stats(2, 64, 48, True)
 CASES["fwd48st_nores"] = lambda: _fwd_stats(2, 64, 48, False)
 CASES["fwd24st"] = lambda: _fwd_stats(2, 128, 24, True)
