@@ -411,6 +411,8 @@ def main():
         roof = dominant_kernel_roofline(device, a.batch, a.patch, groups)
         if probe_pass:
             roof["probe_pass"] = probe_pass
+            if groups:
+                roof["timing"] = "HIP events, every launch of the " + probe_pass
         step_gflop = STEP_GFLOP_PER_SAMPLE * a.batch * (a.patch / 96) ** 3
         roof["step_mfma_frac"] = round(step_gflop / (ms * 1e-3) / 1e3 / PEAK_BF16_TFLOPS, 4)
     if rank == 0 and world == 1 and not a.no_infer:
