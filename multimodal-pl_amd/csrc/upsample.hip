@@ -209,9 +209,17 @@ __global__ __launch_bounds__(256) void up_bwd_blk_kernel(const T* __restrict__ d
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= w * chn) return;
   const int j = i % chn, iw = i / chn, ih0 = 2 * blockIdx.y, id0 = 2 * (blockIdx.z % dp), nn = blockIdx.z / dp;
+  // the w taps of input iw: outputs 2iw - 1 .. 2iw + 2 in order, zero weight where out of range or not read (skipped
+  // below, so the fmaf chain is taps_of's); static indices keep them in registers
   int ow_[4];
   float ww[4];
-  const int cw = taps_of(iw, w, ow_, ww);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int oo = 2 * iw - 1 + q;
+    const bool ok = oo >= 0 && oo < W;
+    ow_[q] = ok ? oo : 2 * iw;
+    ww[q] = ok ? wt_of(oo, iw, w) : 0.f;
+  }
   float acc[2][2][VEC];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
@@ -225,19 +233,31 @@ __global__ __launch_bounds__(256) void up_bwd_blk_kernel(const T* __restrict__ d
     if (od < 0 || od >= D) continue;
     const float wd0 = wt_of(od, id0, d), wd1 = v1d ? wt_of(od, id0 + 1, d) : 0.f;
     if (wd0 == 0.f && wd1 == 0.f) continue;
-    for (int oh = 2 * ih0 - 1; oh <= 2 * ih0 + 4; ++oh) {
-      if (oh < 0 || oh >= H) continue;
-      const float wh0 = wt_of(oh, ih0, h), wh1 = v1h ? wt_of(oh, ih0 + 1, h) : 0.f;
+    // the plane's 6 output rows x 4 w taps, loaded at once (clamped rows / taps are loaded but not used): one
+    // latency round per od instead of one per (od, oh) row (round 4; the adds below are unchanged)
+    u32x4 raw[6][4];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int ohc = min(max(2 * ih0 - 1 + k, 0), H - 1);
+      const T* yr = yb + ((long long)od * H + ohc) * W * c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        raw[k][q] = *reinterpret_cast<const u32x4*>(yr + ow_[q] * c);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int oh = 2 * ih0 - 1 + k;
+      const bool ohok = oh >= 0 && oh < H;
+      const float wh0 = ohok ? wt_of(oh, ih0, h) : 0.f, wh1 = ohok && v1h ? wt_of(oh, ih0 + 1, h) : 0.f;
       if (wh0 == 0.f && wh1 == 0.f) continue;
-      const T* yr = yb + ((long long)od * H + oh) * W * c;
       float part[VEC];
 #pragma unroll
       for (int e = 0; e < VEC; ++e) part[e] = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if (q < cw) {
+        if (ww[q] != 0.f) {
           float v[VEC];
-          loadv<T, VEC>(yr + ow_[q] * c, v);
+          load16<T>(reinterpret_cast<const T*>(&raw[k][q]), v);
 #pragma unroll
           for (int e = 0; e < VEC; ++e) part[e] = fmaf(ww[q], v[e], part[e]);
         }

@@ -108,7 +108,16 @@ def _up(n, c, s):
     return t_(lambda: ops.upsample2x_add(x, sk)), 2.0 * (x.numel() + 2 * sk.numel())
 
 
+def _upb(n, c, s):
+    """trilinear x2 upsample backward (adjoint gather) from an s^3 gradient"""
+    dy = torch.randn((n, s, s, s, c), device=dev).to(bf)
+    shape = (n, s // 2, s // 2, s // 2, c)
+    return t_(lambda: ops.upsample2x_bwd(dy, shape)), 2.0 * (dy.numel() + dy.numel() // 8)
+
+
 CASES["up96"] = lambda: _up(2, 32, 96)
+CASES["upb96"] = lambda: _upb(2, 32, 96)
+CASES["upb48"] = lambda: _upb(2, 64, 48)
 CASES["up48"] = lambda: _up(2, 64, 48)
 CASES["fwd48st"] = lambda: _fwd_stats(2, 64, 48, True)
 CASES["fwd48st_nores"] = lambda: _fwd_stats(2, 64, 48, False)
