@@ -363,8 +363,6 @@ def main():
     for i in range(a.warmup):
         run(i)
     probes = []
-    if a.eager and not a.no_roofline:
-        _ops.PROBE = probes  # events around every ring-kernel launch of the timed steps
     probe_pass = None
     torch.cuda.synchronize()
     if world > 1:
@@ -384,9 +382,10 @@ def main():
         dt = t.item()
     loss_v = float(loss)
     _ops.PROBE = None
-    if not a.eager and not a.no_roofline:  # (every rank: the step may hold collectives)
-        # graph replay has no per-launch events: the ring kernels' live timing comes from an eager pass of the same
-        # step right after the timed region (same kernels, same operands, launched one by one)
+    if not a.no_roofline:  # (every rank: the step may hold collectives)
+        # the ring kernels' live timing (HIP events around every launch) comes from an eager pass of the same step
+        # right after the timed region: graph replay has no per-launch events, and the events' host cost (~0.4 ms per
+        # eager step, r04) stays out of the timed steps
         _ops.PROBE = probes
         for i in range(a.steps):
             x.copy_(batches[i % 2][0], non_blocking=True)
@@ -395,7 +394,7 @@ def main():
             step()
         torch.cuda.synchronize()
         _ops.PROBE = None
-        probe_pass = f"eager pass of {a.steps} steps after the graph-timed region"
+        probe_pass = f"eager pass of {a.steps} steps after the timed region"
     groups = []
     try:  # the full-patch ring launches only (the trunk also runs ring kernels at 48^3 and below)
         groups = ring_groups(probes, a.batch * a.patch ** 3, a.steps)
