@@ -123,7 +123,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   // per channel (sum g, sum g*xhat) of g = relu-mask * dA go to spart[workgroup][32][2] (u3d_gn_bwd_parts finishes)
   constexpr bool PRO = GN && !FLIP, GB = GN && FLIP, LDR = RES || GB;
   static_assert(!(GB && (Q || RES)), "the fused GroupNorm backward runs on the static data-gradient ring only");
-  __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024 + 512 + (GB ? 512 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024 + 512 + (GB ? 576 : 0)];
   char* const ring = smem;
   char* const wts = smem + 4 * RG_SS;
   char* const junk = wts + 4 * RG_NWR * 16;  // target of the staging lanes past the plane's last row
@@ -316,7 +316,9 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   int acc_chunk = -1;
   // GB: this lane's 8 channels after the swap (cbase..cbase+7) of the workgroup's one sample: mask coefficients
   // (the forward prologue's x*sc + sh > 0 test), xhat = (x - mu)*rs, and (sum g, sum g*xhat) accumulators
-  // (table in LDS [channel][sc, sh, rs, -mu*rs]: registers are what the weight steps need)
+  // (table in LDS [channel][sc, sh, rs, -mu*rs]: registers are what the weight steps need; entry c at c + c / 8, so
+  // the 4 channel chunks a ds_read_b128 lane group reads sit in different banks: unpadded, chunks 0 and 16 collided,
+  // SQ_LDS_BANK_CONFLICT = 10% of the ring's LDS cycles, r04)
   float bs1[GB ? 8 : 1], bs2[GB ? 8 : 1];
   f32x4* const gtab = reinterpret_cast<f32x4*>(smem + 4 * RG_SS + 4 * RG_NWR * 16 + 1536);
   if constexpr (GB) {
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       const int smp = bid / g.wps, gr = tid / (32 / g.gn_groups);
       const float mu = gstat[(smp * g.gn_groups + gr) * 2], rs = gstat[(smp * g.gn_groups + gr) * 2 + 1];
       const float scv = rs * gamma[tid];
-      gtab[tid] = f32x4{scv, beta[tid] - mu * scv, rs, mu};
+      gtab[tid + (tid >> 3)] = f32x4{scv, beta[tid] - mu * scv, rs, mu};
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) bs1[e] = bs2[e] = 0.f;
@@ -409,7 +411,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[vb]), xv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const f32x4 t = gtab[cbase + e];
+          const f32x4 t = gtab[cbase + (cbase >> 3) + e];
           const bool m = okv && fmaf(xv[e], t[0], t[1]) > 0.f;  // selects: rows past the volume may be non-finite
           bs1[e] += m ? a[e] : 0.f;
           bs2[e] = fmaf(m ? a[e] : 0.f, m ? (xv[e] - t[3]) * t[2] : 0.f, bs2[e]);
