@@ -287,6 +287,14 @@ def spawn_ranks(n):
     return rc
 
 
+def launch_mode(a, world):
+    """'graph' (hipGraph replay of the step) at N=1 unless --eager or --force-buckets; 'eager' where the step holds
+    collectives (N>1, --force-buckets) unless --graph asks for a capture attempt."""
+    if a.eager:
+        return "eager"
+    return "graph" if a.graph or (world == 1 and not a.force_buckets) else "eager"
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -340,7 +348,7 @@ def main():
     # N=1: the step replays as one hipGraph (the Python host launching ~180 library calls per step was measured
     # slower than the GPU runs them: eager 6.03-6.19 vs graph 5.98-6.01 ms/step, gpurun_out/r04_k); with collectives
     # in the step (N>1, --force-buckets) kernel by kernel
-    a.eager = a.eager or not (a.graph or (world == 1 and not a.force_buckets))
+    a.eager = launch_mode(a, world) == "eager"
     from u3d import ops as _ops
     if not a.eager:
         from u3d.graph import GraphedStep

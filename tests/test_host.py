@@ -404,6 +404,24 @@ def test_bench_gpus_flag_launches_ranks():
         [(str(i), str(i), "3", "127.0.0.1") for i in range(3)]
 
 
+def test_bench_launch_mode_defaults():
+    """bench.py times hipGraph replays at N=1 and launches eagerly where the step holds collectives."""
+    import argparse
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+
+    def ns(**k):
+        d = dict(eager=False, graph=False, force_buckets=False)
+        d.update(k)
+        return argparse.Namespace(**d)
+    assert bench.launch_mode(ns(), 1) == "graph"
+    assert bench.launch_mode(ns(eager=True), 1) == "eager"
+    assert bench.launch_mode(ns(force_buckets=True), 1) == "eager"
+    assert bench.launch_mode(ns(), 8) == "eager"
+    assert bench.launch_mode(ns(graph=True), 8) == "graph"
+
+
 # ------------------------------------------------------------- f1: sliding-window tiles sharded over ranks
 def test_tile_plan_matches_reference_tiling_and_shards_partition_it():
     from evaluate_amos import shard_tiles, tile_plan
