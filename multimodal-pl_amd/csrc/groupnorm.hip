@@ -25,22 +25,55 @@ struct RedGeom {
   long long v;
   int fh, fw, ch, cw;  // u3d_gn_bwd2_s2: fine h, w (x) and compact h, w (da2 = a stride-2 1^3 data gradient)
   long long cv;        // compact voxels per sample
+  float rhw, rfw;      // 1 / (fh * fw), 1 / fw (s2_index; voxels per sample < 2^24)
 };
+
+// quotient of 0 <= x < 2^24 by d from x * (1/d) in fp32 (off by at most one, corrected): ~6 instructions instead of
+// the ~30 of a 32-bit integer division per voxel
+__device__ __forceinline__ int div_small(int x, int d, float rd) {
+  int q = (int)((float)x * rd);
+  q -= q * d > x;
+  q += (q + 1) * d <= x;
+  return q;
+}
 
 // da2 of u3d_gn_bwd2_s2 is the stride-2 1^3 conv's data gradient at the conv's OUTPUT resolution: nonzero only at
 // fine voxels with all coordinates even. Returns its compact index, or -1 (odd voxel: dA2 = 0).
 __device__ __forceinline__ long long s2_index(long long vv, const RedGeom& g) {
   const int vi = (int)vv, hw = g.fh * g.fw;
-  const int a = vi / hw, rem = vi - a * hw, b = rem / g.fw, c = rem - b * g.fw;
+  const int a = div_small(vi, hw, g.rhw), rem = vi - a * hw, b = div_small(rem, g.fw, g.rfw), c = rem - b * g.fw;
   return ((a | b | c) & 1) ? -1 : ((long long)(a >> 1) * g.ch + (b >> 1)) * g.cw + (c >> 1);
 }
 
+// U3D_GN2_COND (default 1): the compact operand is read with a buffer load whose offset is the out-of-range sentinel
+// for odd voxels — zeros with no memory request and no branch (a branch around a plain load made the compiler wait
+// for it inside the branch: one round trip per voxel); 0: a clamped straight-line load for every voxel (round 3).
+#ifndef U3D_GN2_COND
+#define U3D_GN2_COND 1
+#endif
 template <typename T, bool S2>
 __device__ __forceinline__ void load_da2(const T* __restrict__ da2, const RedGeom& g, int n, long long vv, int j,
                                          long long off, float (&d2)[16 / sizeof(T)]) {
   constexpr int VEC = 16 / sizeof(T);
   if constexpr (S2) {
     const long long ci = s2_index(vv, g);
+    if (U3D_GN2_COND) {  // host: n * cv * c * sizeof(T) < 2 GiB
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)da2, 0, (int)(g.n * g.cv * g.c * (int)sizeof(T)),
+                                                        0x00020000);
+      const unsigned bo = ci >= 0 ? (unsigned)((((long long)n * g.cv + ci) * g.c + j * VEC) * sizeof(T)) : 0xFFFFFFF0u;
+      const u32x4 r = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, bo, 0, 0));
+      if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d2[i] = __uint_as_float(r[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          d2[2 * i] = __uint_as_float(r[i] << 16);
+          d2[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
+        }
+      }
+      return;
+    }
     load16<T>(da2 + ((long long)n * g.cv + (ci < 0 ? 0 : ci)) * g.c + j * VEC, d2);  // clamped: straight-line load
     if (ci < 0)
 #pragma unroll
@@ -432,6 +465,9 @@ __global__ __launch_bounds__(GT) void gn_bwd_apply(const T* __restrict__ da, con
 }
 
 
+#ifndef U3D_GN2_PR
+#define U3D_GN2_PR 4
+#endif
 // Two GroupNorm consumers of the SAME activation x with the same statistics (NoBottleneck gn1 and the downsample
 // GN of the first block of a stage, unet3D.py:44-53 + _make_layer :1666-1686): one partial pass over x, dA1, dA2
 // (per set k: s1_k = sum m_k dA_k, s2_k = sum m_k dA_k xhat) and one apply writing
@@ -478,10 +514,11 @@ __global__ __launch_bounds__(GT) void gn_bwd2_partial(const T* __restrict__ da1,
         acc[3][e] = fmaf(g2, xh, acc[3][e]);
       }
     };
-    for (long long v = v0 + vl; v < v1; v += 2 * g.vlanes) {  // rounds of 6 predicated loads
-      float xv[2][VEC], d1[2][VEC], d2[2][VEC];
+    constexpr int PR = U3D_GN2_PR;  // voxels per round (3 predicated loads each)
+    for (long long v = v0 + vl; v < v1; v += PR * g.vlanes) {
+      float xv[PR][VEC], d1[PR][VEC], d2[PR][VEC];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < PR; ++u) {
         const long long vv = std::min(v + u * g.vlanes, v1 - 1);
         const long long off = base + vv * g.c + j * VEC;
         load16<T>(x + off, xv[u]);
@@ -489,7 +526,7 @@ __global__ __launch_bounds__(GT) void gn_bwd2_partial(const T* __restrict__ da1,
         load_da2<T, S2>(da2, g, n, vv, j, off, d2[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < PR; ++u) {
         if (v + u * g.vlanes >= v1)
 #pragma unroll
           for (int e = 0; e < VEC; ++e) d1[u][e] = d2[u][e] = 0.f;
@@ -720,6 +757,9 @@ extern "C" int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v,
   return check_launch("gn_apply_kernel");
 }
 
+#ifndef U3D_GN2_APV
+#define U3D_GN2_APV 16
+#endif
 template <bool S2>
 static int gn_bwd2_launch(int dtype, const void* da1, const void* da2, const void* x, int n, int c, long long v,
                           int fh, int fw, int groups, const float* stats, const float* gamma1, const float* beta1,
@@ -734,18 +774,25 @@ static int gn_bwd2_launch(int dtype, const void* da1, const void* da2, const voi
   U3D_REQUIRE(n * c <= GN_PAIRS_MAX, "gn_bwd2: n * c must be <= %d", GN_PAIRS_MAX);
   RedGeom g = make_geom(n, c, v, groups, vec);
   if (S2) {
-    U3D_REQUIRE(v < (1LL << 31) && fh > 0 && fw > 0 && v % ((long long)fh * fw) == 0, "gn_bwd2_s2: bad dims");
+    U3D_REQUIRE(v < (1LL << 24) && fh > 0 && fw > 0 && v % ((long long)fh * fw) == 0, "gn_bwd2_s2: bad dims");
     const int fd = (int)(v / ((long long)fh * fw));
     g.fh = fh; g.fw = fw;
     g.ch = (fh - 1) / 2 + 1; g.cw = (fw - 1) / 2 + 1;
     g.cv = (long long)((fd - 1) / 2 + 1) * g.ch * g.cw;
+    U3D_REQUIRE(n * g.cv * c * (dtype == U3D_BF16 ? 2 : 4) < (1LL << 31) - 64,
+                "gn_bwd2_s2: compact gradient beyond the 2 GiB buffer-offset range");
+    g.rhw = 1.f / (float)((long long)fh * fw);
+    g.rfw = 1.f / (float)fw;
   }
   hipStream_t s = (hipStream_t)stream;
   unsigned* cnt = reinterpret_cast<unsigned*>(ws) + 2;
   float* coef = gn_coef_ptr(ws, g);
   const long long nvec = v * g.chn;
   const int athr = GT / g.chn * g.chn;
-  const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + 4LL * athr - 1) / (4LL * athr));
+  // U3D_GN2_APV vectors per apply thread where that still leaves >= 200 blocks (its 2 x 5 x VEC coefficient loads
+  // amortised over more voxels: 2 x 96^3 x 32 160 -> 155 us, 48^3 48.2 -> 46.3), else 4 (24^3: 27 -> 37 us with 16)
+  const long long apv = n * ((nvec + U3D_GN2_APV * athr - 1) / (U3D_GN2_APV * athr)) >= 200 ? U3D_GN2_APV : 4;
+  const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + apv * athr - 1) / (apv * athr));
   if (dtype == U3D_BF16) {
     hipLaunchKernelGGL((gn_bwd2_partial<bf16, S2>), dim3(g.nblk, n), dim3(GT), 0, s, (const bf16*)da1,
                        (const bf16*)da2, (const bf16*)x, g, stats, gamma1, beta1, gamma2, beta2, gn_part_ptr(ws), cnt,

@@ -230,18 +230,21 @@ def _gn(kind, s, c, n=2, G=16):
     x = torch.randn((n, s, s, s, c), device=dev).to(bf)
     da = torch.randn_like(x)
     da2 = torch.randn_like(x)
+    h2 = ops.out_dim(s, 1, 2)
+    da2c = torch.randn((n, h2, h2, h2, c), device=dev).to(bf)
     ga, be = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.1
     st = ops.gn_stats(x, G)
     dx = torch.empty_like(x)
     fns = {"stats": lambda: ops.gn_stats(x, G),
            "apply": lambda: ops.gn_apply(x, st, ga, be, G),
            "bwd": lambda: ops.gn_bwd(da, x, st, ga, be, G, dx=dx, accumulate=True),
-           "bwd2": lambda: ops.gn_bwd2(da, da2, x, st, (ga, be), (ga, be), G, dx=dx, accumulate=True)}
+           "bwd2": lambda: ops.gn_bwd2(da, da2, x, st, (ga, be), (ga, be), G, dx=dx, accumulate=True),
+           "bwd2s": lambda: ops.gn_bwd2(da, da2c, x, st, (ga, be), (ga, be), G, dx=dx, accumulate=True, da2_s2=True)}
     return t_(fns[kind]), 0.0
 
 
 for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 256), ("6", 6, 256)]:
-    for kind in ("stats", "apply", "bwd", "bwd2"):
+    for kind in ("stats", "apply", "bwd", "bwd2", "bwd2s"):
         CASES[f"gn{kind}{lvl}"] = (lambda kind=kind, s=s, c=c: _gn(kind, s, c))
 
 
