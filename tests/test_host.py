@@ -32,6 +32,19 @@ def test_library_exports_every_header_symbol():
     assert h.u3d_abi_version() == 1
 
 
+def test_library_has_no_undefined_internal_symbols():
+    """Every u3d:: function the library calls is defined in it (a shared object links with undefined symbols, which
+    would only fail at load time on the GPU box)."""
+    import shutil
+    import subprocess
+    from u3d import _lib
+    if not os.path.exists(_lib.LIB_PATH) or shutil.which("nm") is None:
+        pytest.skip("libu3d.so or nm missing")
+    out = subprocess.run(["nm", "-DC", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    bad = [ln for ln in out.splitlines() if "u3d::" in ln or " u3d_" in ln]
+    assert not bad, bad
+
+
 def test_workspace_size_constants_match_the_library():
     from u3d import _lib, ops
     if not os.path.exists(_lib.LIB_PATH):
