@@ -454,7 +454,15 @@ __global__ __launch_bounds__(LT) void dice_binary_count_kernel(const float* __re
   if (threadIdx.x < 3 && h[threadIdx.x]) atomicAdd(&cnt[l * 3 + threadIdx.x], (unsigned long long)h[threadIdx.x]);
 }
 
-static int loss_blocks(long long nvox) { return (int)std::min<long long>(1024, std::max<long long>(1, (nvox + LT - 1) / LT)); }
+// Forward grid: at most 512 blocks = two per CU, all resident at once (the softmax path holds 161 VGPRs: 3 waves per
+// SIMD, so 1024 blocks ran as a full and a one-third round). 2 x 96^3 x 16 (tools/kbench.py loss96, gpurun_out/r04_u):
+// 1024 / 768 / 512 / 384 / 256 blocks -> 63.6 / 48.6 / 45.8 / 51.0 / 51.7 us
+#ifndef U3D_LOSS_NB
+#define U3D_LOSS_NB 512
+#endif
+static int loss_blocks(long long nvox) {
+  return (int)std::min<long long>(U3D_LOSS_NB, std::max<long long>(1, (nvox + LT - 1) / LT));
+}
 
 // dispatch on the class count: exact instantiations for the model heads, a guarded 32-wide fallback
 #define U3D_NC_DISPATCH(C, F)        \

@@ -216,6 +216,8 @@ CASES["upf96"] = lambda: _upp(False)
 CASES["upf48"] = lambda: _upp(False, 2, 24, 64)
 CASES["upb96"] = lambda: _upp(True)
 CASES["upb48"] = lambda: _upp(True, 2, 24, 64)
+CASES["upb24"] = lambda: _upp(True, 2, 12, 128)
+CASES["upb12"] = lambda: _upp(True, 2, 6, 256)
 CASES["dec24_c1"] = lambda: _fwd(2, 128, 64, 24, 3, 1, True, False)
 CASES["dec24_c2"] = lambda: _fwd(2, 64, 64, 24, 3, 1, True, True)
 CASES["ddec24_c1"] = lambda: _dgrad(2, 128, 64, 24, 3, 1)
@@ -246,6 +248,22 @@ def _gn(kind, s, c, n=2, G=16):
 for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 256), ("6", 6, 256)]:
     for kind in ("stats", "apply", "bwd", "bwd2", "bwd2s"):
         CASES[f"gn{kind}{lvl}"] = (lambda kind=kind, s=s, c=c: _gn(kind, s, c))
+
+
+def _loss(n, s, C, bwd):
+    """EDiceLoss_partial forward (per-class sums over the fp32 logits) / backward (dlogits), 2 x 96^3 x 16"""
+    lg = torch.randn((n, s, s, s, C), device=dev)
+    lab = torch.randint(0, C, (n, s, s, s), device=dev).float()
+    wt = torch.ones(C, device=dev)
+    if not bwd:
+        return t_(lambda: ops.partial_loss_fwd(lg, lab, wt)), 0.0
+    _, sums = ops.partial_loss_fwd(lg, lab, wt)
+    go = torch.ones(1, device=dev)
+    return t_(lambda: ops.partial_loss_bwd(lg, lab, wt, sums, go)), 0.0
+
+
+CASES["loss96"] = lambda: _loss(2, 96, 16, False)
+CASES["lossb96"] = lambda: _loss(2, 96, 16, True)
 
 
 if __name__ == "__main__":
