@@ -33,7 +33,7 @@ enum Opt : int {
   OPT_SMALL_WGS,      // small-volume conv workgroups aimed at
   OPT_GN_MAXBLK,      // GroupNorm reduction blocks over all samples
   OPT_HEAD_TR,        // transposed classifier head (0: untransposed store path)
-  OPT_STEM1,          // conv1 (1 -> 32) one-voxel-per-lane kernel with LDS-transposed stores (0: generic kernel)
+  OPT_STEM1,          // conv1 (1 -> 32) one-voxel-per-lane kernel, packed FMAs, scalar weight table (0: generic kernel)
   OPT_UP_BWD_BLK,     // -1 auto, 0 / 1 force the one-row / 2x2-row trilinear backward
   OPT_WGRAD_BD,       // stride-1 brick weight-gradient brick depth (2 or 3)
   OPT_WB_WGS,         // brick weight-gradient workgroups aimed at

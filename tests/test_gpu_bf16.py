@@ -226,9 +226,11 @@ def test_bf16_conv_wgrad_1x1(gpu, n, cin, cout, dims, s):
     assert err < 2e-3 * ref.abs().max().item(), err
 
 
-@pytest.mark.parametrize("dims", [(6, 10, 64), (3, 9, 32), (5, 7, 20)])
+@pytest.mark.parametrize("dims", [(6, 10, 64), (3, 9, 32), (5, 7, 20), (33, 48, 64), (48, 64, 96)])
 def test_bf16_stem_wgrad(gpu, dims):
-    """conv1 (1 -> 32, 3^3, stride 1) weight gradient: MFMA kernel (w % 32 == 0) and the VALU kernel."""
+    """conv1 (1 -> 32, 3^3, stride 1) weight gradient: MFMA kernel (w % 32 == 0) and the VALU kernel. The two large
+    volumes give the MFMA kernel's workgroups 2 and 5 bricks each (its two-deep register prefetch, odd brick counts,
+    a partial last d brick)."""
     from u3d import ops
     torch.manual_seed(7)
     n = 2

@@ -262,6 +262,13 @@ def _loss(n, s, C, bwd):
     return t_(lambda: ops.partial_loss_bwd(lg, lab, wt, sums, go)), 0.0
 
 
+def _stemw(n=2, s=96):
+    x = torch.randn((n, 1, s, s, s), device=dev)
+    dy = torch.randn((n, s, s, s, 32), device=dev).to(bf)
+    return t_(lambda: ops.stem_wgrad(dy, x, 1)), 2.0 * n * s ** 3 * 27 * 32
+
+
+CASES["stemw96"] = lambda: _stemw()
 CASES["loss96"] = lambda: _loss(2, 96, 16, False)
 CASES["lossb96"] = lambda: _loss(2, 96, 16, True)
 
