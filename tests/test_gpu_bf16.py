@@ -275,8 +275,8 @@ def test_head_fwd_bwd(gpu, cin, cout, dims):
 @pytest.mark.parametrize("cin,cout,dims,s", [(1, 32, (8, 10, 12), 1), (2, 24, (8, 6, 10), 2), (1, 8, (5, 7, 9), 1),
                                              (2, 32, (4, 4, 6), 1), (1, 32, (6, 9, 70), 1), (1, 32, (3, 4, 33), 1)])
 def test_bf16_stem_fwd(gpu, cin, cout, dims, s):
-    """Stem conv (fp32 input, bf16 packed weights, bf16 output; conv1 1 -> 32 on the MFMA kernel with the input rounded
-    to bf16, the others fp32 VALU math) against fp64 on the fp32 input."""
+    """Stem conv (fp32 input, bf16 packed weights, bf16 output; conv1 1 -> 32 on the packed-FMA kernel, the others on
+    the generic kernel, all fp32 VALU math) against fp64 on the fp32 input."""
     from u3d import ops
     torch.manual_seed(3)
     x = torch.randn((2, cin) + dims, device=gpu)
