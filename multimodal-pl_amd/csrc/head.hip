@@ -275,7 +275,15 @@ __global__ __launch_bounds__(HD_T) void head_bwd_kernel(const float* __restrict_
   }
 }
 
-static int head_blocks(long long rows) { return (int)std::min<long long>(2048, std::max<long long>(1, (rows + 127) / 128)); }
+// grid cap: 768 = three 4-wave blocks per CU, resident at once at the backward's 148 VGPRs (2048 ran it in 2.7
+// rounds). 2 x 96^3 x 32 -> 16 (tools/kbench.py headf96 / headb96, gpurun_out/r04_hd): forward 37.3 -> 36.0 us,
+// backward 62.2 -> 57.3 us; 1024 / 1280 blocks: backward 66-70 us
+#ifndef U3D_HEAD_NB
+#define U3D_HEAD_NB 768
+#endif
+static int head_blocks(long long rows) {
+  return (int)std::min<long long>(U3D_HEAD_NB, std::max<long long>(1, (rows + 127) / 128));
+}
 
 }  // namespace u3d
 

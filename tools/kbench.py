@@ -268,6 +268,19 @@ def _stemw(n=2, s=96):
     return t_(lambda: ops.stem_wgrad(dy, x, 1)), 2.0 * n * s ** 3 * 27 * 32
 
 
+def _head(bwd, n=2, s=96, cin=32, cout=16):
+    """precls head (head.hip): GN+ReLU+1^3 conv to fp32 logits (+ bias) / its data gradient from fp32 dlogits"""
+    x, pf, pd, g, r, dy, flop = conv_case(n, cin, cout, s, 1, 1, True)
+    b = torch.randn(cout, device=dev)
+    if not bwd:
+        return t_(lambda: ops.head_fwd(x, pf, cout, b, g)), flop
+    dyf = torch.randn((n, s, s, s, cout), device=dev)
+    db = torch.empty(cout, device=dev)
+    return t_(lambda: ops.head_bwd(dyf, pd, cin, dbias=db)), flop
+
+
+CASES["headf96"] = lambda: _head(False)
+CASES["headb96"] = lambda: _head(True)
 CASES["stemw96"] = lambda: _stemw()
 CASES["loss96"] = lambda: _loss(2, 96, 16, False)
 CASES["lossb96"] = lambda: _loss(2, 96, 16, True)
