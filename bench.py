@@ -22,6 +22,11 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(REPO, "multimodal-pl_amd"), REPO]
 
+# RCCL collectives are captured into the step's hipGraph (N>1, --force-buckets). torch's process-group event cache
+# can hand an event that was recorded inside the capture to the watchdog thread's completion query ("operation not
+# permitted on an event last recorded in a capturing stream", seen once in r05): no cached events (set before the
+# process group exists).
+os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -44,16 +49,18 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-infer", action="store_true", help="skip the configs[4] sliding-window inference leg")
+    p.add_argument("--no-mixed", action="store_true", help="skip the configs[3] (CT + MRI batch) step leg at N=1")
     p.add_argument("--force-buckets", action="store_true",
                    help="N=1 only: RCCL (nccl backend) at world size 1 with U3DDataParallel(force_buckets=True), i.e. "
                         "the bucketed all-reduces launched from inside the backward and the collective-tolerant kernel "
                         "forms while they run (what N>1 pays for the overlap, measured on one GPU)")
+    p.add_argument("--bucket-mb", type=float, default=40.0, help="gradient bucket cap (MB of fp32 gradients)")
+    p.add_argument("--tail-mb", type=float, default=2.0, help="cap of the last bucket (launched at the backward's end)")
     p.add_argument("--print-rank-env", action="store_true", help=argparse.SUPPRESS)  # launcher test (no GPU)
-    p.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph (the default at N=1 "
-                   "without --force-buckets; the ring kernels' live timing then comes from an eager pass of the same "
+    p.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph (the default, also at "
+                   "N>1 and with --force-buckets; the ring kernels' live timing comes from an eager pass of the same "
                    "steps after the timed region)")
-    p.add_argument("--eager", action="store_true", help="launch the step kernel by kernel from Python (the default at "
-                   "N>1 and with --force-buckets, where the step holds collectives)")
+    p.add_argument("--eager", action="store_true", help="launch the step kernel by kernel from Python")
     return p.parse_args()
 
 
@@ -129,6 +136,23 @@ def standalone_ms(label, device, batch, patch, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
+def algorithmic_bytes(label, batch, patch):
+    """HBM bytes one launch of a full-patch 96^3-class ring must move (bf16 NDHWC tensors of batch x patch^3 x 32):
+    * weight gradient: x and dy read + its fp32 split-K slabs written (splits x 27 x 32 x 32 x 4 B; 256 splits at
+      2 x 96^3 = 28.3 MB) -> 254 MB at 2 x 96^3;
+    * data gradient with the fused GroupNorm-backward partials: dy and x read, dA written -> 340 MB;
+    * forward with GN prologue + residual: x and the residual read, y written -> 340 MB;
+    * forward with GN prologue: x read, y written -> 226 MB."""
+    t = batch * patch ** 3 * 32 * 2
+    if label.startswith("wgrad_ring"):
+        from u3d import _lib
+        ns = _lib.query("u3d_conv_wgrad_ring_splits", batch, 32, patch, patch, patch, 32)
+        return 2 * t + ns * 27 * 32 * 32 * 4
+    if label == "conv32_ring fwd GN +stats":
+        return 2 * t
+    return 3 * t
+
+
 def dominant_kernel_roofline(device, batch, patch, groups):
     """Roofline line of the ring kernel with the largest time per step (HIP events around each of its launches in the
     timed steps, on the stream it runs on); the other full-patch rings are carried beside it in `rings`."""
@@ -147,7 +171,9 @@ def dominant_kernel_roofline(device, batch, patch, groups):
     return {"kernel": label, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
             "traffic_unit": "bytes/launch", "traffic_source": tsrc,
-            "algorithmic_bytes": 3 * batch * patch ** 3 * 32 * 2,
+            "algorithmic_bytes": algorithmic_bytes(label, batch, patch),
+            "traffic_over_algorithmic": (round(traffic / algorithmic_bytes(label, batch, patch), 3)
+                                         if traffic else None),
             "avg_launch_ms": round(ms, 4), "timing": src, "standalone_launch_ms": round(ms_alone, 4),
             "flop_per_launch": flops, "trace_check": trace_check(krx, flops) if (batch, patch) == (2, 96) else None,
             "peak_measured": measured_peak(achieved), "rings": groups}
@@ -268,6 +294,41 @@ def infer_cfg5(device):
     return out
 
 
+def mixed_leg(a, make_step, opt, device, rank):
+    """BASELINE configs[3] per GPU at N=1: the same step on the multimodal batch (one CT-normalised patch, one z-scored
+    MRI-like patch, MOTSDataset.py:171-185; the batch's mask[0] applied to both, loss_partial.py:87), same model and
+    optimizer, its own captured hipGraph (or eager with --eager); warm-up + the same number of timed steps, timed like
+    the main line (synchronize on both sides)."""
+    bm = []
+    for j in range(2):
+        xb, lb, mb = synthetic(a.batch, a.patch, device, 2000 + 17 * j + rank, "mixed")
+        bm.append((xb, lb.squeeze(1), mb.to(device)))
+    xm, tm, mm = (t.clone() for t in bm[0])
+    stepm = make_step(xm, tm, mm)
+    if a.eager:
+        def run(i):
+            for dst, src in zip((xm, tm, mm), bm[i % 2]):
+                dst.copy_(src, non_blocking=True)
+            return stepm()
+    else:
+        from u3d.graph import GraphedStep
+        g = GraphedStep(stepm, (xm, tm, mm), warmup=3, optimizer=opt)
+        def run(i):
+            return g(*bm[i % 2])
+    for i in range(a.warmup):
+        run(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = run(i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ms = dt / a.steps * 1e3
+    return {"workload": "configs[3] per GPU: same step, batch = 1 CT-normalised + 1 z-scored MRI-like 96^3 patch",
+            "ms_per_step": round(ms, 3), "value": round(a.batch * a.patch ** 3 * a.steps / dt, 1), "unit": "voxels/s",
+            "launch": "eager" if a.eager else "hipgraph", "loss": round(float(loss), 6)}
+
+
 def spawn_ranks(n):
     """`bench.py --gpus N` without a launcher: start N child ranks (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous on
     127.0.0.1) before this process touches the GPU, pass their output through, exit with the worst status."""
@@ -288,11 +349,9 @@ def spawn_ranks(n):
 
 
 def launch_mode(a, world):
-    """'graph' (hipGraph replay of the step) at N=1 unless --eager or --force-buckets; 'eager' where the step holds
-    collectives (N>1, --force-buckets) unless --graph asks for a capture attempt."""
-    if a.eager:
-        return "eager"
-    return "graph" if a.graph or (world == 1 and not a.force_buckets) else "eager"
+    """'graph' (hipGraph replay of the whole step, its bucketed RCCL all-reduces included at N>1 / --force-buckets)
+    unless --eager; a refused capture falls back to eager and says so in the line (`launch`, `graph_error`)."""
+    return "eager" if a.eager else "graph"
 
 
 def main():
@@ -323,7 +382,8 @@ def main():
 
     torch.manual_seed(0)
     model = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=16, weight_std=True).to(device).train()
-    net = U3DDataParallel(model, force_buckets=a.force_buckets) if (world > 1 or a.force_buckets) else model
+    net = (U3DDataParallel(model, force_buckets=a.force_buckets, bucket_mb=a.bucket_mb, tail_mb=a.tail_mb)
+           if (world > 1 or a.force_buckets) else model)
     from u3d.optim import SGD  # drop-in for torch.optim.SGD: one fused launch per 48 tensors
     opt = SGD(model.parameters(), lr=5e-4, momentum=0.9, weight_decay=1e-4)
     crit = EDiceLoss_partial(16)
@@ -335,19 +395,24 @@ def main():
     x, target, mask = (t.clone() for t in batches[0])
     amp = a.dtype == "bf16"
 
-    def step():
-        opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
-            logits, _, _ = net(x)
-        loss = crit(logits, target, mask=[mask])
-        loss.backward()
-        opt.step()
-        return loss
+    def make_step(x, target, mask):
+        def step():
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+                logits, _, _ = net(x)
+            loss = crit(logits, target, mask=[mask])
+            loss.backward()
+            opt.step()
+            return loss
+        return step
+
+    step = make_step(x, target, mask)
 
     graphed = None
-    # N=1: the step replays as one hipGraph (the Python host launching ~180 library calls per step was measured
-    # slower than the GPU runs them: eager 6.03-6.19 vs graph 5.98-6.01 ms/step, gpurun_out/r04_k); with collectives
-    # in the step (N>1, --force-buckets) kernel by kernel
+    graph_error = None
+    # the step replays as one hipGraph (the Python host launching ~180 library calls per step was measured slower than
+    # the GPU runs them: eager 6.03-6.19 vs graph 5.98-6.01 ms/step, gpurun_out/r04_k); at N>1 / --force-buckets the
+    # bucketed RCCL all-reduces are captured with it (their kernel forms are static: ops.DDP_TOLERANT)
     a.eager = launch_mode(a, world) == "eager"
     from u3d import ops as _ops
     if not a.eager:
@@ -355,7 +420,8 @@ def main():
         try:
             graphed = GraphedStep(step, (x, target, mask), warmup=3, optimizer=opt)
         except Exception as e:  # capture refused (e.g. a collective backend without graph support): run eager
-            print(f"[bench] hipGraph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
+            graph_error = f"{type(e).__name__}: {e}"[:300]
+            print(f"[bench] hipGraph capture failed ({graph_error}); running eager", file=sys.stderr)
             torch.cuda.synchronize()
             a.eager = True
     if a.eager:
@@ -411,6 +477,9 @@ def main():
     ms = dt / a.steps * 1e3
     vox = world * a.batch * a.patch ** 3 * a.steps / dt
 
+    mixed = None
+    if world == 1 and a.modality == "ct" and not a.no_mixed:
+        mixed = mixed_leg(a, make_step, opt, device, rank)
     roof = None
     cpu = None
     infer = None
@@ -438,8 +507,9 @@ def main():
                        "backend": dist.get_backend() if dist.is_initialized() else None,
                        "world_size_seen": dist.get_world_size() if dist.is_initialized() else 1,
                        "force_buckets": bool(a.force_buckets)},
-            "loss": round(loss_v, 6), "launch": "eager" if a.eager else "hipgraph",
-            "roofline": roof, "cpu_baseline": cpu, "infer_cfg5": infer,
+            "loss": round(loss_v, 6), "launch": "eager" if a.eager else "hipgraph", "graph_error": graph_error,
+            "ddp_tolerant_forms": bool(_ops.DDP_TOLERANT[0]),
+            "roofline": roof, "cpu_baseline": cpu, "infer_cfg5": infer, "mixed_cfg3": mixed,
         }
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

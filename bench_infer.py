@@ -36,12 +36,11 @@ def measure(dev, dtype="bf16", reps=2, volume=(256, 512, 512), tile=(64, 192, 19
     Forward only; the volume is resident on the device before the timed region (no host transfer inside it)."""
     import unet3D
     import evaluate_amos as E
-    from oracle.weights_recipe import apply_recipe
     dist = None
     if group is not None:
         import torch.distributed as dist
+    torch.manual_seed(0)  # random-init weights (the module's own init; nothing from oracle/)
     m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=classes, weight_std=True)
-    apply_recipe(m, seed=0)
     m = m.to(dev).eval()
     m.compute_dtype = torch.bfloat16 if dtype == "bf16" else torch.float32
     g = torch.Generator(device="cpu").manual_seed(0)

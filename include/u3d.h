@@ -134,6 +134,20 @@ int u3d_conv_small(int flip, const void* x, int n, int cin, int d, int h, int w,
                    const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                    const void* residual, void* y, float* ws, long long ws_bytes, u3d_stream_t stream);
 
+/* Round 5 form of u3d_conv_small: the split-K partials are combined INSIDE the launch by each output tile's
+ * last-arriving workgroup (fixed slab order: bitwise the two-kernel result; write-through slab stores, agent-scope
+ * arrival counters), and with stats_out (forward, cout in {64, 128, 256}) the output's GroupNorm(16) statistics
+ * [n][16][2] = (mean, rstd) from that combine: per-(sample, brick) fp32 partials in spart, fp64 fixed-order finalize
+ * by the workgroup completing the last tile. cnt: u3d_conv_small_cnt_bytes bytes, ZERO-FILLED before first use (every
+ * launch leaves it zeroed); spart: u3d_conv_small_spart_floats floats. *stats_made = 1 when stats_out was written
+ * (it needs the contraction split over 2..8 workgroups); 0: the caller takes u3d_gn_stats. */
+long long u3d_conv_small_cnt_bytes(int n, int d, int h, int w, int cout);
+long long u3d_conv_small_spart_floats(int n, int d, int h, int w);
+int u3d_conv_small2(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                    const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                    const void* residual, void* y, float* ws, long long ws_bytes, unsigned* cnt, float* spart,
+                    float* stats_out, int* stats_made, u3d_stream_t stream);
+
 /* Classifier head precls_conv (unet3D.py:1653-1657): GN+ReLU + 1^3 conv cin (16..64, %16) -> cout (<= 32) + bias,
  * bf16 NDHWC input, fp32 NDHWC logits [n*v][cout]; wpk = forward pack [1][cout_p][cin_p]. Streaming MFMA kernel
  * (operands straight from global memory in fragment layout). */
@@ -258,6 +272,13 @@ int u3d_conv_wgrad1(const void* dy, const void* x, int n, int cin, int d, int h,
 long long u3d_stem_fwd_ws_bytes(void);
 int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                  int stride, void* y, void* ws, u3d_stream_t stream);
+/* conv1 (bf16, cin 1 -> 32, stride 1) with the output's GroupNorm(16) statistics from its epilogue (round 5): per-block
+ * fp32 partials into spart (u3d_stem1_stats_ws_floats floats; 0 = shape not supported: d*h*w must be a multiple of
+ * 256), fp64 fixed-order finalize into stats[n][16][2] = (mean, rstd), as u3d_gn_stats computes them. Replaces
+ * u3d_stem_fwd + u3d_gn_stats for the trunk's stem (unet3D.py:1632 feeding layer0's GroupNorms, :44-53). */
+long long u3d_stem1_stats_ws_floats(int n, int d, int h, int w);
+int u3d_stem1_fwd_stats(const float* x, int n, int d, int h, int w, const void* wpk, void* y, void* ws, float* spart,
+                        float* stats, u3d_stream_t stream);
 /* split count for u3d_stem_wgrad given its dtype/channels (the bf16 1->32 stride-1 stem runs on MFMA) */
 int u3d_stem_wgrad_splits2(int dtype, int n, int cin, int d, int h, int w, int cout, int stride);
 int u3d_stem_wgrad_splits(int n, int d, int h, int w, int stride);
@@ -310,6 +331,13 @@ int u3d_gn_bwd2_s2(int dtype, const void* da1, const void* da2c, const void* x, 
  * (unet3D.py:1646, 1764-1783). x [n][d][h][w][c] -> y [n][2d][2h][2w][c]; skip nullable. */
 int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
                        u3d_stream_t stream);
+/* bf16 u3d_upsample2x_add with the output's GroupNorm(16) statistics from its epilogue (round 5): per-block fp32
+ * partials into spart (u3d_upsample2x_stats_ws_floats floats; 0 = shape not supported: c/16 in {2,4,8,16}), fp64
+ * fixed-order finalize into stats[n][16][2] = (mean, rstd). Replaces upsample + u3d_gn_stats for the decoder input
+ * of each x{8,4,2,1}_resb block (unet3D.py:1764-1783 feeding NoBottleneck's GroupNorms :44-53). */
+long long u3d_upsample2x_stats_ws_floats(int n, int c, int d, int h, int w);
+int u3d_upsample2x_add_stats(const void* x, int n, int c, int d, int h, int w, const void* skip, void* y, float* spart,
+                             float* stats, u3d_stream_t stream);
 int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d, int h, int w, void* dx, int accumulate,
                        u3d_stream_t stream);
 

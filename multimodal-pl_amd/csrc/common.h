@@ -135,6 +135,39 @@ __device__ __forceinline__ float half_sum8_transposed(float (&v)[8], int r) {
   return v[0];
 }
 
+// Sum of N (a power of two, <= 32) per-lane values over the 64 lanes of a wave, transposed: afterwards lane l holds
+// the wave total of value index (l >> (6 - log2 N)) & (N - 1) (for N = 32: l >> 1); the lanes of a group of 64 / N
+// hold the same bits. Each xor step keeps the half of the values whose index bit equals the lane bit, so the work
+// halves every step (N - 1 + 6 - log2 N shuffles instead of 6 N). Fixed order: deterministic.
+template <int N, int O = 32>
+__device__ __forceinline__ void wave_sum_transposed_step(float (&v)[N], int lane) {
+  if constexpr (O >= 1) {
+    constexpr int M = N >> (5 - (O == 32 ? 5 : O == 16 ? 4 : O == 8 ? 3 : O == 4 ? 2 : O == 2 ? 1 : 0));  // values left
+    if constexpr (M > 1) {
+      constexpr int H = M / 2;
+      const bool b = (lane & O) != 0;
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        const float keep = b ? v[i + H] : v[i], send = b ? v[i] : v[i + H];
+        v[i] = keep + __shfl_xor(send, O);
+      }
+    } else {
+      v[0] += __shfl_xor(v[0], O);
+    }
+    wave_sum_transposed_step<N, O / 2>(v, lane);
+  }
+}
+template <int N>
+__device__ __forceinline__ float wave_sum_transposed(float (&v)[N], int lane) {
+  static_assert(N >= 1 && N <= 32 && (N & (N - 1)) == 0, "N: power of two <= 32");
+  wave_sum_transposed_step<N, 32>(v, lane);
+  return v[0];
+}
+
+// GroupNorm(16) statistics from per-workgroup partials [sample][wps][16][2] (fp32 sums of values and squares): one
+// wave per (sample, group), fixed-order fp64 combine (conv_ring.hip). m = values per group and sample.
+int launch_gn16_finalize(const float* spart, int n, int wps, double m, float* stats, hipStream_t s);
+
 // 16-byte vector of T: 8 bf16 or 4 f32.
 template <typename T> struct Vec16 { static constexpr int N = 16 / sizeof(T); };
 

@@ -755,6 +755,11 @@ __global__ __launch_bounds__(64) void ring_gn_finalize_kernel(const float* __res
   }
 }
 
+int launch_gn16_finalize(const float* spart, int n, int wps, double m, float* stats, hipStream_t s) {
+  hipLaunchKernelGGL(ring_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, spart, n, wps, m, stats);
+  return check_launch("ring_gn_finalize_kernel");
+}
+
 }  // namespace u3d
 
 using namespace u3d;

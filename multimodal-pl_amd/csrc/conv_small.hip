@@ -49,6 +49,11 @@ struct SCGeom {
   int gn_groups;
   int nks, cpk;            // K split: workgroups per output tile, 32-channel chunks per split
   float* slab;             // fp32 partials [nks][n][d][h][w][cout] when nks > 1
+  // round 5: in-kernel split-K combine (cnt != nullptr, nks > 1) and optional output GroupNorm(16) statistics
+  unsigned* cnt;           // [tiles + 1] zeroed arrival counters (per output tile, then one for the statistics)
+  float* spart;            // [n][nbd*nbh*nbw][16][2] fp32 partials of the output statistics (stats != nullptr)
+  float* stats;            // [n][16][2] (mean, rstd) of the output, or nullptr
+  int cpg;                 // output channels per GroupNorm group (cout / 16; 4, 8 or 16)
 };
 
 template <bool FLIP>
@@ -204,18 +209,135 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
+    const long long per = (long long)g.n * g.d * g.h * g.w * g.cout;  // floats per slab
+    // (write-through sc1 16-B stores where the combine runs in this launch: the last-arriving workgroup of the tile
+    // reads them with sc1 loads, MI355X_MICROARCH.md visibility table, counter row)
+    const auto srs = __builtin_amdgcn_make_buffer_rsrc((void*)g.slab, 0, (int)(g.nks * per * 4), 0x00020000);
     if (active) {
-      float* const sl = g.slab + (long long)ks * g.n * g.d * g.h * g.w * g.cout;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int qi = lane + 64 * u, part = qi & 7, row = qi >> 3;
         const int vv = wave * 32 + row;
         const int uw = vv % g.bw, uh = (vv / g.bw) % g.bh, ud = vv / (g.bw * g.bh);
         const int zd = o0d + ud, zh = o0h + uh, zw = o0w + uw, co = co0 + part * 4;
-        if (vv < g.nv && zd < g.d && zh < g.h && zw < g.w && co < g.cout)
-          *reinterpret_cast<f32x4*>(sl + ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cout + co) =
-              *reinterpret_cast<const f32x4*>(ept + qi * 4);
+        if (vv < g.nv && zd < g.d && zh < g.h && zw < g.w && co < g.cout) {
+          const long long e = ks * per + ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cout + co;
+          const f32x4 val = *reinterpret_cast<const f32x4*>(ept + qi * 4);
+          if (g.cnt)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), srs, (int)(e * 4), 0, 16);
+          else
+            *reinterpret_cast<f32x4*>(g.slab + e) = val;
+        }
       }
+    }
+    if (!g.cnt) return;  // the separate small_reduce_kernel sums the slabs
+    // ---- in-kernel split-K combine (round 5): the workgroup that completes its output tile last sums the tile's
+    // nks slabs in slab order (bitwise the small_reduce_kernel sums), adds the residual and stores y
+    __shared__ unsigned s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    const int tile = bid / g.nks;
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(g.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == (unsigned)(g.nks - 1);
+      if (s_last) __hip_atomic_store(g.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    float ls[8], lq[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ls[k] = lq[k] = 0.f;
+    const int cpg = g.stats ? g.cpg : 32;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = tid + SC_NT * k, vv = q >> 3, part = q & 7;
+      if (vv >= SC_MAXV) break;
+      const int uw = vv % g.bw, uh = (vv / g.bw) % g.bh, ud = vv / (g.bw * g.bh);
+      const int zd = o0d + ud, zh = o0h + uh, zw = o0w + uw, co = co0 + part * 4;
+      const bool ok = vv < g.nv && zd < g.d && zh < g.h && zw < g.w && co < g.cout;
+      const long long vo = ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cout + co;
+      f32x4 t[8];
+#pragma unroll
+      for (int s_ = 0; s_ < 8; ++s_) {  // all slab loads in flight, then the adds in slab order
+        const bool in = ok && s_ < g.nks;
+        t[s_] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              srs, in ? (int)((s_ * per + vo) * 4) : (int)0xFFFFFFF0u, 0, 16));
+      }
+      if (!ok) continue;
+      f32x4 v = t[0];
+#pragma unroll
+      for (int s_ = 1; s_ < 8; ++s_)
+        if (s_ < g.nks) v += t[s_];
+      if (res) {
+        const uint2 rq = *reinterpret_cast<const uint2*>(res + vo);
+        v[0] += __uint_as_float(rq.x << 16);
+        v[1] += __uint_as_float(rq.x & 0xffff0000u);
+        v[2] += __uint_as_float(rq.y << 16);
+        v[3] += __uint_as_float(rq.y & 0xffff0000u);
+      }
+      uint2 o;
+      o.x = (uint32_t)from_f<bf16>(v[0]) | ((uint32_t)from_f<bf16>(v[1]) << 16);
+      o.y = (uint32_t)from_f<bf16>(v[2]) | ((uint32_t)from_f<bf16>(v[3]) << 16);
+      *reinterpret_cast<uint2*>(y + vo) = o;
+      if (g.stats) {  // the stored values' group sums (4 channels of one group: cpg >= 4)
+        const float a0 = __uint_as_float(o.x << 16), a1 = __uint_as_float(o.x & 0xffff0000u);
+        const float a2 = __uint_as_float(o.y << 16), a3 = __uint_as_float(o.y & 0xffff0000u);
+        const float ss = (a0 + a1) + (a2 + a3), qq = (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+        const int gi = (part * 4) / cpg;
+#pragma unroll
+        for (int k2 = 0; k2 < 8; ++k2) {
+          ls[k2] += gi == k2 ? ss : 0.f;
+          lq[k2] += gi == k2 ? qq : 0.f;
+        }
+      }
+    }
+    if (!g.stats) return;
+    // ---- output GroupNorm(16) statistics: this tile's groups reduced over the workgroup (fixed order), one partial
+    // row per (sample, brick); the workgroup completing the last tile combines them in fp64 (one launch, no pass)
+    float sv[16];
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      sv[2 * k2] = ls[k2];
+      sv[2 * k2 + 1] = lq[k2];
+    }
+    const float tot = wave_sum_transposed<16>(sv, lane);  // lane l: value l >> 2 = (group slot, sum | square)
+    float* const red = reinterpret_cast<float*>(smem);     // (LDS free: the MFMA loop is done)
+    __syncthreads();
+    if ((lane & 3) == 0) red[wave * 16 + (lane >> 2)] = tot;
+    __syncthreads();
+    const int gpt = 32 / cpg, nbr = g.nbd * g.nbh * g.nbw, brick = (bd_ * g.nbh + bh_) * g.nbw + bw_;
+    if (tid < 2 * gpt) {
+      float t2 = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < SC_NT / 64; ++wv) t2 += red[wv * 16 + tid];
+      const int gr = co0 / cpg + (tid >> 1);
+      __hip_atomic_store(g.spart + ((long long)nn * nbr + brick) * 32 + gr * 2 + (tid & 1), t2, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);  // sc1
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int ntiles = (int)(gridDim.x / g.nks);
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(g.cnt + ntiles, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == (unsigned)(ntiles - 1);
+      if (s_last) __hip_atomic_store(g.cnt + ntiles, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (tid < g.n * 16) {
+      const int n2 = tid >> 4, gr = tid & 15;
+      double s1 = 0, s2 = 0;
+      for (int b2 = 0; b2 < nbr; ++b2) {
+        const float* pp = g.spart + ((long long)n2 * nbr + b2) * 32 + gr * 2;
+        s1 += __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s2 += __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const double m = (double)g.cpg * g.d * g.h * g.w;
+      const double mean = s1 / m;
+      double var = s2 / m - mean * mean;
+      if (var < 0) var = 0;
+      g.stats[tid * 2] = (float)mean;
+      g.stats[tid * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
     }
     return;
   }
@@ -279,9 +401,46 @@ __global__ __launch_bounds__(256) void small_reduce_kernel(const float* __restri
 
 using namespace u3d;
 
+static int conv_small_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                           const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                           const void* residual, void* y, float* ws, long long ws_bytes, unsigned* cnt,
+                           float* spart, float* stats_out, int* nks_out, u3d_stream_t stream);
+
 extern "C" int u3d_conv_small(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                               const void* residual, void* y, float* ws, long long ws_bytes, u3d_stream_t stream) {
+  return conv_small_impl(flip, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, ws,
+                         ws_bytes, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+// Round 5 form: the split-K slabs are combined inside the conv launch by the last-arriving workgroup of each output
+// tile (no small_reduce_kernel), and with stats_out the output's GroupNorm(16) statistics come from that combine (no
+// statistics pass). cnt: u3d_conv_small_cnt_bytes() of ZEROED memory (left zeroed); spart: u3d_conv_small_spart_floats.
+// Statistics need the contraction split (nks > 1) and cout in {64, 128, 256} (4..16 channels per group); where a
+// launch cannot produce them it returns 0 with *stats_made = 0 and the caller takes the statistics pass.
+extern "C" long long u3d_conv_small_cnt_bytes(int n, int d, int h, int w, int cout) {
+  return 4LL * (n * cdiv(d, 1) * cdiv(h, 1) * cdiv(w, 1) * cdiv(cout, 32) + 1);  // >= tiles + 1 (bricks >= 1 voxel)
+}
+extern "C" long long u3d_conv_small_spart_floats(int n, int d, int h, int w) {
+  return 32LL * n * d * h * w;  // >= n * bricks * 32
+}
+extern "C" int u3d_conv_small2(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                               const void* residual, void* y, float* ws, long long ws_bytes, unsigned* cnt,
+                               float* spart, float* stats_out, int* stats_made, u3d_stream_t stream) {
+  U3D_REQUIRE(cnt && stats_made, "conv_small2: needs the counter workspace and stats_made");
+  int nks = 0;
+  const bool want = stats_out && spart && !flip && cout % 16 == 0 && (cout / 16 == 4 || cout / 16 == 8 || cout / 16 == 16);
+  const int rc = conv_small_impl(flip, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual,
+                                 y, ws, ws_bytes, cnt, want ? spart : nullptr, want ? stats_out : nullptr, &nks, stream);
+  *stats_made = rc == 0 && want && nks > 1 && nks <= 8;
+  return rc;
+}
+
+static int conv_small_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                           const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                           const void* residual, void* y, float* ws, long long ws_bytes, unsigned* cnt,
+                           float* spart, float* stats_out, int* nks_out, u3d_stream_t stream) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv_small: bad args");
   U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "conv_small: channels must be multiples of 8");
   U3D_REQUIRE(!gn_stats || (!flip && gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0),
@@ -315,6 +474,13 @@ extern "C" int u3d_conv_small(int flip, const void* x, int n, int cin, int d, in
   g.cpk = cdiv(nchunk, nks);
   g.nks = cdiv(nchunk, g.cpk);
   g.slab = g.nks > 1 ? ws : nullptr;
+  if (nks_out) *nks_out = g.nks;
+  g.cnt = g.nks > 1 && g.nks <= 8 ? cnt : nullptr;  // in-kernel combine where there are (<= 8) slabs to combine
+  g.stats = g.cnt ? stats_out : nullptr;
+  g.spart = g.stats ? spart : nullptr;
+  g.cpg = cout / 16;
+  U3D_REQUIRE(!g.stats || (n * 16 <= SC_NT && g.nks * (long long)n * d * h * w * cout * 4 < (1LL << 31)),
+              "conv_small2: statistics form limits");
   const long long nwg = tiles * g.nks;
   U3D_REQUIRE(nwg < (1LL << 31), "conv_small: grid too large");
   U3D_REQUIRE((long long)n * d * h * w * cin * 2 < (1LL << 31) - 64 && 27LL * g.cout_p * g.cin_p * 2 < (1LL << 31) - 64,
@@ -327,7 +493,7 @@ extern "C" int u3d_conv_small(int flip, const void* x, int n, int cin, int d, in
     hipLaunchKernelGGL(conv_small_kernel<false>, dim3((unsigned)nwg), dim3(SC_NT), 0, s, (const bf16*)x,
                        (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, g);
   int rc = check_launch("conv_small_kernel");
-  if (rc || g.nks == 1) return rc;
+  if (rc || g.nks == 1 || g.cnt) return rc;
   const long long per4 = slab1 / 16;
   hipLaunchKernelGGL(small_reduce_kernel, dim3((unsigned)std::min<long long>(4096, (per4 + 255) / 256)), dim3(256), 0,
                      s, ws, g.nks, per4, (const bf16*)residual, (bf16*)y);

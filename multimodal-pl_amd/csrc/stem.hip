@@ -76,10 +76,17 @@ __global__ __launch_bounds__(1024) void stem1_wtab_kernel(const T* __restrict__ 
 // instruction of a wave covers 4 KB (round 3: a four-voxels-per-lane form, lanes 256 B apart, measured 91 vs 69 us at
 // 2x96^3); the three w-neighbours of a tap row are three coalesced loads. Same fp32 FMA chain per output as the
 // generic kernel (OPT_STEM1 = 0): bitwise equal.
-template <typename T>
+// STATS (bf16 only, round 5): the output's GroupNorm(16) partial sums from the epilogue — per voxel the two channels
+// of each group (the stored bf16 values) summed and squared, reduced over the wave transposed (wave_sum_transposed:
+// lane l ends with value l >> 1 = (group, sum | square)) and over the block's 4 waves in order, one [16][2] row per
+// block into spart ([sample][wps][16][2]; blocks never straddle samples: the host requires d*h*w % ST == 0), then
+// launch_gn16_finalize: no separate statistics pass over the 2 x 96^3 x 32 output.
+template <typename T, bool STATS = false>
 __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                                                       T* __restrict__ y, int d, int h, int w, long long nvox) {
+                                                       T* __restrict__ y, int d, int h, int w, long long nvox,
+                                                       float* __restrict__ spart = nullptr) {
   __shared__ __attribute__((aligned(16))) char tr[sizeof(T) == 2 ? ST / 64 : 1][64 * 64];  // bf16: 4 KB per wave
+  __shared__ float red[STATS ? ST / 64 : 1][32];
   const long long v0 = (long long)blockIdx.x * ST + (threadIdx.x & ~63);  // the wave's first voxel
   const long long vr = (long long)blockIdx.x * ST + threadIdx.x;
   if constexpr (sizeof(T) != 2) {
@@ -140,6 +147,25 @@ __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__
       const int p = l + 64 * k, vx = p >> 2, c4 = p & 3;
       const u32x4 pk = *reinterpret_cast<const u32x4*>(wb + vx * 64 + 16 * (c4 ^ ((vx >> 2) & 3)));
       if (v0 + vx < nvox) *reinterpret_cast<u32x4*>(y + (v0 + vx) * 32 + 8 * c4) = pk;
+    }
+    if constexpr (STATS) {
+      float sv[32];
+      const bool ok = vr < nvox;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const float a = ok ? to_f(from_f<bf16>(acc[g][0])) : 0.f, b = ok ? to_f(from_f<bf16>(acc[g][1])) : 0.f;
+        sv[2 * g] = a + b;
+        sv[2 * g + 1] = a * a + b * b;
+      }
+      const float t = wave_sum_transposed<32>(sv, l);
+      if ((l & 1) == 0) red[threadIdx.x >> 6][l >> 1] = t;
+      __syncthreads();
+      if (threadIdx.x < 32) {
+        float r = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < ST / 64; ++wv) r += red[wv][threadIdx.x];
+        spart[(long long)blockIdx.x * 32 + threadIdx.x] = r;
+      }
     }
   } else {
     T* yr = y + v * 32;
@@ -351,6 +377,26 @@ static int sdim(int d, int s) { return (d - 1) / s + 1; }  // k3 pad1: (d + 2 - 
 static bool stem1_on() { return opt(OPT_STEM1) != 0; }  // 0: the generic one-voxel kernel
 
 extern "C" long long u3d_stem_fwd_ws_bytes(void) { return 27 * 32 * 4; }
+
+extern "C" long long u3d_stem1_stats_ws_floats(int n, int d, int h, int w) {
+  const long long v = (long long)d * h * w;
+  return v % ST == 0 ? (long long)n * (v / ST) * 32 : 0;  // 0: not supported (blocks would straddle samples)
+}
+
+extern "C" int u3d_stem1_fwd_stats(const float* x, int n, int d, int h, int w, const void* wpk, void* y, void* ws,
+                                   float* spart, float* stats, u3d_stream_t stream) {
+  U3D_REQUIRE(x && wpk && y && ws && spart && stats && n >= 1 && d >= 1 && h >= 1 && w >= 1, "stem1_fwd_stats: bad args");
+  const long long v = (long long)d * h * w;
+  U3D_REQUIRE(v % ST == 0, "stem1_fwd_stats: d*h*w = %lld not a multiple of %d", v, ST);
+  hipStream_t s = (hipStream_t)stream;
+  float* wt = static_cast<float*>(ws);
+  const long long nvox = (long long)n * v;
+  hipLaunchKernelGGL(stem1_wtab_kernel<bf16>, dim3(1), dim3(1024), 0, s, (const bf16*)wpk, 32, wt);
+  hipLaunchKernelGGL((stem1_fwd_kernel<bf16, true>), dim3((unsigned)(nvox / ST)), dim3(ST), 0, s, x, wt, (bf16*)y, d, h, w,
+                     nvox, spart);
+  if (check_launch("stem1_fwd_kernel<stats>")) return U3D_EHIP;
+  return launch_gn16_finalize(spart, n, (int)(v / ST), 2.0 * (double)v, stats, s);
+}
 
 extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                             int stride, void* y, void* ws, u3d_stream_t stream) {

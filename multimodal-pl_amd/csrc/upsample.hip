@@ -70,11 +70,23 @@ __global__ __launch_bounds__(256) void up_fwd_kernel(const T* __restrict__ x, co
 // kernel issued 8 gathered loads per output and was L2-load-bound (80 us at 2x48^3 -> 96^3 x 32). Every output is
 // computed with the same Lerp weights and the same expression as up_fwd_kernel: bitwise equal.
 // grid: x = (iw, chunk) pairs of one input row, y = ih, z = n * D + od
+// CPG > 0 (round 5; channels per GroupNorm(16) group = c / 16, 2 / 4 / 8 / 16): the output's GroupNorm statistics from
+// the epilogue. Each thread sums the stored bf16 values of its 4 outputs per group its 8-channel chunk covers (and
+// their squares), the block reduces them per (group, sum | square) over its threads in a fixed order (LDS), one
+// [16][2] fp32 row per block into spart ([sample][wps][16][2], wps = blocks per sample: a block never straddles
+// samples), and launch_gn16_finalize combines the rows in fp64: no statistics pass over the output.
+template <int CPG = 0>
 __global__ __launch_bounds__(256) void up_fwd_quad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ skip,
-                                                         bf16* __restrict__ y, int n, int c, int d, int h, int w) {
+                                                         bf16* __restrict__ y, int n, int c, int d, int h, int w,
+                                                         float* __restrict__ spart = nullptr) {
+  constexpr bool STATS = CPG > 0;
+  constexpr int NSL = STATS ? (CPG >= 8 ? 1 : 8 / CPG) : 1;  // group slots of one 8-channel chunk
   const int chn = c / 8, D = 2 * d, H = 2 * h, W = 2 * w;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= w * chn) return;
+  float gs[NSL], gq[NSL];
+#pragma unroll
+  for (int k = 0; k < NSL; ++k) gs[k] = gq[k] = 0.f;
+  if (i < w * chn) {
   const int j = i % chn, iw = i / chn, ih = blockIdx.y, od = blockIdx.z % D, nn = blockIdx.z / D;
   const Lerp Ld = lerp_of(od, d);
   const bf16* xb = x + (long long)nn * d * h * w * c + j * 8;
@@ -133,6 +145,40 @@ __global__ __launch_bounds__(256) void up_fwd_quad_kernel(const bf16* __restrict
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] += sv[e];
       storev<bf16, 8>(y + off, o);
+      if constexpr (STATS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float r = to_f(from_f<bf16>(o[e]));  // the stored value
+          gs[e / (CPG >= 8 ? 8 : CPG)] += r;
+          gq[e / (CPG >= 8 ? 8 : CPG)] += r * r;
+        }
+      }
+    }
+  }
+  }  // i < w * chn
+  if constexpr (STATS) {
+    __shared__ float red[256][2 * NSL];
+#pragma unroll
+    for (int k = 0; k < NSL; ++k) {
+      red[threadIdx.x][2 * k] = gs[k];
+      red[threadIdx.x][2 * k + 1] = gq[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      const int g = threadIdx.x >> 1, comp = threadIdx.x & 1;
+      const int nact = min(256, w * chn - (int)blockIdx.x * 256);  // 256 % chn == 0: local thread L has chunk L % chn
+      float t = 0.f;
+      if constexpr (CPG >= 16) {  // chunks 2g, 2g + 1 (slot 0 each), in order
+        for (int jj = 2 * g; jj < 2 * g + 2; ++jj)
+          for (int L = jj; L < nact; L += chn) t += red[L][comp];
+      } else {
+        const int jj = g / NSL, k = g - jj * NSL;
+        for (int L = jj; L < nact; L += chn) t += red[L][2 * k + comp];
+      }
+      const int D_ = 2 * d, od = blockIdx.z % D_, nn = blockIdx.z / D_;
+      const long long wps = (long long)gridDim.x * gridDim.y * D_;
+      const long long loc = ((long long)od * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+      spart[((long long)nn * wps + loc) * 32 + threadIdx.x] = t;
     }
   }
 }
@@ -371,8 +417,8 @@ extern "C" int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d,
   U3D_REQUIRE((long long)n * 2 * d < 65536 && 2 * h < 65536, "upsample: volume too large for the row grid");
   const dim3 gr(cdiv(row, 256), 2 * h, n * 2 * d), bl(256);
   if (dtype == U3D_BF16 && vect && opt(OPT_UP_QUAD) != 0) {  // UP_QUAD = 0: the one-output kernel (A/B)
-    hipLaunchKernelGGL(up_fwd_quad_kernel, dim3(cdiv(w * (c / 8), 256), h, n * 2 * d), bl, 0, s, (const bf16*)x,
-                       (const bf16*)skip, (bf16*)y, n, c, d, h, w);
+    hipLaunchKernelGGL(up_fwd_quad_kernel<0>, dim3(cdiv(w * (c / 8), 256), h, n * 2 * d), bl, 0, s, (const bf16*)x,
+                       (const bf16*)skip, (bf16*)y, n, c, d, h, w, nullptr);
     return check_launch("up_fwd_quad_kernel");
   }
   if (dtype == U3D_BF16) {
@@ -383,6 +429,34 @@ extern "C" int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d,
     else hipLaunchKernelGGL((up_fwd_kernel<float, 1>), gr, bl, 0, s, (const float*)x, (const float*)skip, (float*)y, n, c, d, h, w);
   }
   return check_launch("up_fwd_kernel");
+}
+
+static bool up_stats_ok(int n, int c, int d, int h, int w) {
+  const int chn = c / 8;
+  return c % 16 == 0 && (c / 16 == 2 || c / 16 == 4 || c / 16 == 8 || c / 16 == 16) && 256 % chn == 0 &&
+         (long long)n * 2 * d < 65536 && h < 65536;
+}
+
+extern "C" long long u3d_upsample2x_stats_ws_floats(int n, int c, int d, int h, int w) {
+  if (!up_stats_ok(n, c, d, h, w)) return 0;
+  return (long long)n * cdiv(w * (c / 8), 256) * h * 2 * d * 32;
+}
+
+extern "C" int u3d_upsample2x_add_stats(const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
+                                        float* spart, float* stats, u3d_stream_t stream) {
+  U3D_REQUIRE(x && y && spart && stats && n > 0 && c > 0 && d > 0 && h > 0 && w > 0, "upsample_stats: bad args");
+  U3D_REQUIRE(up_stats_ok(n, c, d, h, w), "upsample_stats: unsupported shape (c = %d)", c);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 gr(cdiv(w * (c / 8), 256), h, n * 2 * d), bl(256);
+  switch (c / 16) {
+    case 2: hipLaunchKernelGGL(up_fwd_quad_kernel<2>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w, spart); break;
+    case 4: hipLaunchKernelGGL(up_fwd_quad_kernel<4>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w, spart); break;
+    case 8: hipLaunchKernelGGL(up_fwd_quad_kernel<8>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w, spart); break;
+    default: hipLaunchKernelGGL(up_fwd_quad_kernel<16>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w, spart); break;
+  }
+  if (check_launch("up_fwd_quad_kernel<stats>")) return U3D_EHIP;
+  const int wps = (int)((long long)gr.x * gr.y * 2 * d);
+  return launch_gn16_finalize(spart, n, wps, (double)(c / 16) * 8.0 * d * h * w, stats, s);
 }
 
 extern "C" int u3d_upsample2x_bwd(int dtype, const void* dy, int n, int c, int d, int h, int w, void* dx, int accumulate,

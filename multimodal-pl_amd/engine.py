@@ -39,6 +39,9 @@ class Engine(object):
             if use_cuda:
                 torch.cuda.set_device(self.local_rank % max(1, torch.cuda.device_count()))
             if not dist.is_initialized():
+                # no cached process-group events: the step may be captured into a hipGraph with its all-reduces
+                # (u3d.graph.GraphedStep), and a cached event recorded inside the capture must not reach the watchdog
+                os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
                 dist.init_process_group(backend="nccl" if use_cuda else "gloo", init_method="env://")
             self.devices = list(range(self.world_size))
         else:

@@ -37,6 +37,9 @@ _SIGS = {
     "u3d_conv_dgrad_s2": [P, I, I, P, I, I, I, I, P, P],
     "u3d_conv1x1": [P, I, I, I, I, I, P, I, I, I, P, P, P, I, P, P],
     "u3d_conv_small": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P],
+    "u3d_conv_small_cnt_bytes": [I, I, I, I, I],
+    "u3d_conv_small_spart_floats": [I, I, I, I],
+    "u3d_conv_small2": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P, P, P, P, P],
     "u3d_conv32_brick": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring_stats_ws_floats": [I],
@@ -63,6 +66,10 @@ _SIGS = {
     "u3d_conv_wgrad1": [P, P, I, I, I, I, I, I, I, P, P, P, I, P, I, P],
     "u3d_stem_fwd": [I, P, I, I, I, I, I, P, I, I, P, P, P],
     "u3d_stem_fwd_ws_bytes": [],
+    "u3d_stem1_stats_ws_floats": [I, I, I, I],
+    "u3d_upsample2x_stats_ws_floats": [I, I, I, I, I],
+    "u3d_upsample2x_add_stats": [P, I, I, I, I, I, P, P, P, P, P],
+    "u3d_stem1_fwd_stats": [P, I, I, I, I, P, P, P, P, P, P],
     "u3d_stem_wgrad_splits": [I, I, I, I, I],
     "u3d_stem_wgrad_splits2": [I, I, I, I, I, I, I, I],
     "u3d_stem_wgrad": [I, P, P, I, I, I, I, I, I, I, P, I, P],
@@ -114,7 +121,7 @@ _SIGS = {
     "u3d_aug_affine": [P, L, F, F, P],
     "u3d_aug_contrast": [P, L, F, P, I, P],
 }
-_RESTYPE = {"u3d_stem_fwd_ws_bytes": L, "u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
+_RESTYPE = {"u3d_stem_fwd_ws_bytes": L, "u3d_stem1_stats_ws_floats": L, "u3d_conv_small_cnt_bytes": L, "u3d_conv_small_spart_floats": L, "u3d_upsample2x_stats_ws_floats": L, "u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
             "u3d_eam_attn_bwd_part_floats": L, "u3d_upsample_trilinear_bwd_ws_floats": L, "u3d_renew_token_ws_bytes": L,
             "u3d_consistency_ws_bytes": L, "u3d_volume_stats_ws_bytes": L, "u3d_convg_brick_stats_ws_floats": L}
 

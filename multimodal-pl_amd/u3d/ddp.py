@@ -4,8 +4,10 @@ a bucket's last gradient is written, so the all-reduce of the decoder/bottleneck
 remaining encoder backward. This is the data-parallel wrapper the reference reached through
 engine.data_parallel (engine.py:30-32; original run: torch.distributed.launch + DDP, run_amos_atlas_final.sh:2).
 
-Per step every rank writes its parameter gradients straight into fresh flat bucket buffers (no copy); the
-bucket is averaged in place; the trunk's autograd Function returns the bucket views as parameter grads.
+Per step every rank writes its parameter gradients straight into flat bucket buffers allocated once (no copy,
+fixed addresses, so the whole data-parallel step can be captured as one hipGraph with its RCCL all-reduces); the
+bucket is averaged in place and each parameter's .grad is its bucket slice. Which kernel forms the backward runs
+never depends on a device poll (ops.DDP_TOLERANT): the same data gives the same bits on every run.
 """
 import contextlib
 import threading
@@ -17,6 +19,11 @@ import torch.distributed as dist
 from . import ops
 
 _local = threading.local()
+
+
+def capturing():
+    """True inside a hipGraph capture on this thread's current stream."""
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
 
 def current_sink():
@@ -34,7 +41,13 @@ def use_sink(sink):
 
 
 class GradBucketer:
-    def __init__(self, named_params, bucket_mb=25.0, group=None):
+    def __init__(self, named_params, bucket_mb=40.0, group=None, tail_mb=2.0):
+        """Buckets follow reverse registration order (~ the order the native backward produces gradients), greedy up
+        to ``bucket_mb``, except the LAST bucket, which holds only the last-produced parameters up to ``tail_mb``
+        (the stem and the shallow encoder levels of the U-Net: ~1.5 MB): it is the one all-reduce that cannot overlap
+        the backward (it is launched at its end), and the weight-gradient flush in front of it stays short. Every
+        other bucket completes inside the backward and its all-reduce runs beside the encoder's backward kernels.
+        The 16-organ trunk (66 MB of fp32 gradients) gets 3 buckets: 34.5 + 29.7 + 1.5 MB."""
         params = [(n, p) for n, p in named_params if p.requires_grad]
         self.params = dict(params)
         self.assigned = set()   # names whose .grad finish() set to the bucket view (the tape returns None for them)
@@ -42,50 +55,74 @@ class GradBucketer:
         self.world = dist.get_world_size(group)
         self.avg_native = dist.get_backend(group) == "nccl"
         cap = int(bucket_mb * 1024 * 1024 / 4)
-        self.buckets = []       # list of [names, numel]
-        self.where = {}         # name -> (bucket index, offset, shape)
+        tcap = int(min(tail_mb, bucket_mb) * 1024 * 1024 / 4)
+        order = list(reversed(params))
+        cut, tn = len(order), 0
+        while cut > 1 and tn + order[cut - 1][1].numel() <= tcap:
+            cut -= 1
+            tn += order[cut][1].numel()
+        groups = []
         cur, cur_n = [], 0
-        for n, p in reversed(params):  # reverse registration order ~= order the native backward produces grads
+        for n, p in order[:cut]:
             if cur and cur_n + p.numel() > cap:
-                self.buckets.append((cur, cur_n))
+                groups.append(cur)
                 cur, cur_n = [], 0
-            self.where[n] = (len(self.buckets), cur_n, tuple(p.shape))
-            cur.append(n)
+            cur.append((n, p))
             cur_n += p.numel()
         if cur:
-            self.buckets.append((cur, cur_n))
+            groups.append(cur)
+        if cut < len(order):
+            groups.append(order[cut:])
+        self.buckets = []       # list of [names, numel]
+        self.where = {}         # name -> (bucket index, offset, shape)
+        for grp in groups:
+            off = 0
+            for n, p in grp:
+                self.where[n] = (len(self.buckets), off, tuple(p.shape))
+                off += p.numel()
+            self.buckets.append(([n for n, _ in grp], off))
         self.device = params[0][1].device if params else None
         self.active = False
         self.synced = set()
         self.on_finish = None   # set by U3DDataParallel: queues its end-of-backward callback on every rank
+        self.sets = []          # at most two sets of flat bucket buffers, allocated once and reused every step
+        self.bufs = None
+        self._deferred = None
+
+    def _aliased(self, bufs):
+        """Whether a parameter's .grad still is a slice of ``bufs`` (the user kept the gradients: accumulation across
+        backward passes, or zero_grad(set_to_none=False))."""
+        ptrs = {b.untyped_storage().data_ptr() for b in bufs}
+        for p in self.params.values():
+            g = p.grad
+            if g is not None and g.untyped_storage().data_ptr() in ptrs:
+                return True
+        return False
 
     def begin(self):
+        """Start of a backward's bucket bookkeeping. The bucket buffers are allocated once (gradient as bucket view,
+        fixed addresses: a captured hipGraph replays into them) and every slice is overwritten by its gradient (or
+        zeroed, _zero_missing) before its bucket is launched, so they need no clearing. Where the previous step's
+        gradients still alias the current set, the other set is used and finish() adds into the kept gradients."""
         ops.COLLECTIVE_IN_FLIGHT[0] = False  # a backward that raised before finish() must not leave it set
-        ops.COLLECTIVE_POLL[0] = self.in_flight
-        self.bufs = [torch.empty(nel, dtype=torch.float32, device=self.device) for _, nel in self.buckets]
+        if not self.sets:
+            self.sets.append([torch.empty(nel, dtype=torch.float32, device=self.device) for _, nel in self.buckets])
+        cur = self.sets[0] if self.bufs is None else self.bufs
+        if self._aliased(cur):
+            other = [s for s in self.sets if s is not cur]
+            if not other:
+                other = [[torch.empty(nel, dtype=torch.float32, device=self.device) for _, nel in self.buckets]]
+                self.sets.append(other[0])
+            cur = other[0]
+        self.bufs = cur
         self.left = [len(names) for names, _ in self.buckets]
         self.done_names = set()
         self.synced = set()
         self.works = [None] * len(self.buckets)
-        self.completed = set()  # buckets whose all-reduce has finished on the device
         self.pend = [0] * len(self.buckets)  # parameters of each bucket whose gradient is written but parked
         self.pend_names = set()
         self.flush_due = False  # the parked gradients complete a bucket: the tape flushes them after its current op
         self.active = True
-
-    def in_flight(self):
-        """True while a launched bucket's all-reduce has not completed on the device (``work.is_completed()``, a
-        non-blocking event query). ops asks this before each launch that has a collective-tolerant form, so the slower
-        work-stealing / short-range kernels run only while a collective can actually hold CUs, not from the first
-        bucket to the end of the backward."""
-        live = False
-        for b, w in enumerate(self.works):
-            if w is not None and b not in self.completed:
-                if w.is_completed():
-                    self.completed.add(b)
-                else:
-                    live = True
-        return live
 
     def out(self, name):
         if not self.active or name not in self.where:
@@ -102,7 +139,8 @@ class GradBucketer:
     def _launch(self, b):
         op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
         self.works[b] = dist.all_reduce(self.bufs[b], op=op, group=self.group, async_op=True)
-        ops.COLLECTIVE_IN_FLIGHT[0] = True  # ops polls in_flight() from here on and clears it when all have completed
+        if ops.DDP_TOLERANT[0]:
+            ops.COLLECTIVE_IN_FLIGHT[0] = True  # static latch (tape order), cleared in finish(): see ops.DDP_TOLERANT
 
     def note_pending(self, name):
         """The tape parked ``name``'s gradient (a weight gradient waiting for the batched slab sum + standardisation
@@ -146,21 +184,24 @@ class GradBucketer:
                 self.bufs[b].div_(self.world)
         self.synced = set(self.done_names)  # averaged here: the post-accumulate hooks skip these
         # gradient as bucket view: .grad becomes the averaged bucket slice itself (autograd's AccumulateGrad would
-        # copy a view: +69 MB of device copies per step, r04 trace); the tape then returns None for these parameters
+        # copy a view: +69 MB of device copies per step, r04 trace); the tape then returns None for these parameters.
+        # A parameter this rank's tapes never produced still gets the averaged slice (the other ranks' contributions,
+        # DDP's semantics for a parameter unused on one rank) unless a plain-autograd path already gave it a gradient;
+        # one that plain autograd produces later accumulates into the slice and is averaged by the fallback path.
         self.assigned = set()
-        for n in self.done_names:
-            p = self.params.get(n)
-            if p is None:
+        for n, p in self.params.items():
+            produced = n in self.done_names
+            if not produced and p.grad is not None:
                 continue
             v = self.view(n)
             if p.grad is None:
                 p.grad = v
-            else:  # accumulation across backward passes without zero_grad
+            else:  # accumulation across backward passes without zero_grad (begin() picked the other buffer set)
                 p.grad.add_(v)
-            self.assigned.add(n)
+            if produced:
+                self.assigned.add(n)
         self.active = False
         ops.COLLECTIVE_IN_FLIGHT[0] = False
-        ops.COLLECTIVE_POLL[0] = None
         if self.on_finish is not None:
             self.on_finish()
 
@@ -203,7 +244,11 @@ class GradBucketer:
         all-gathers always pair. A rank with gradients to average compares at once (it needs the values before its
         all-reduce); an empty rank with a device key defers the comparison to its next forward (a pinned copy and an
         event: no host sync in the backward) and raises there."""
-        self.verify_pending()
+        if capturing():
+            # hipGraph capture: the set of gradients a replay produces is fixed by the capture, and the eager warm-up
+            # steps before it ran this check on every rank; host-side pinned copies cannot be replayed
+            return
+        self.verify_pending(block=True)  # the previous backward's check: its event completed long ago
         kv = (len(names), zlib.crc32("\0".join(names).encode()))
         key = torch.tensor(kv, dtype=torch.int64)
         if self.avg_native:  # RCCL gathers device tensors (a pinned staging copy: no blocking H2D copy)
@@ -219,13 +264,19 @@ class GradBucketer:
             return
         self._compare([tuple(g.tolist()) for g in got], kv, names)
 
-    def verify_pending(self):
-        """Finish a deferred consistency check (see check_same)."""
-        d, self._deferred = getattr(self, "_deferred", None), None
-        if d is not None:
-            host, ev, key, names = d
-            ev.synchronize()
-            self._compare([tuple(r) for r in host.tolist()], tuple(key), names)
+    def verify_pending(self, block=False):
+        """Finish a deferred consistency check (see check_same). Non-blocking by default (the next forward polls the
+        event and defers again while the copy is still queued, so the host keeps running ahead of the device); the
+        end of the next backward finishes it with ``block=True``."""
+        d = self._deferred
+        if d is None:
+            return
+        host, ev, key, names = d
+        if not block and not ev.query():
+            return
+        self._deferred = None
+        ev.synchronize()
+        self._compare([tuple(r) for r in host.tolist()], tuple(key), names)
 
     @staticmethod
     def _compare(got, key, names):
@@ -243,14 +294,14 @@ class U3DDataParallel(torch.nn.Module):
     gradients are checked to be the same set on every rank (fail loudly otherwise), flattened into ONE buffer,
     averaged by one all-reduce and copied back, so no rank is ever left with an unsynchronised gradient."""
 
-    def __init__(self, module, group=None, bucket_mb=25.0, force_buckets=False):
+    def __init__(self, module, group=None, bucket_mb=40.0, force_buckets=False, tail_mb=2.0):
         """``force_buckets``: run the bucketed all-reduce machinery even at world size 1 (tests of the RCCL branch
         on a one-GPU box; at world 1 the average is the identity)."""
         super().__init__()
         self.module = module
         self.distributed = dist.is_available() and dist.is_initialized() and (
             dist.get_world_size(group) > 1 or force_buckets)
-        self.bucketer = GradBucketer(module.named_parameters(), bucket_mb, group) if self.distributed else None
+        self.bucketer = GradBucketer(module.named_parameters(), bucket_mb, group, tail_mb) if self.distributed else None
         self.fallback_names = []  # parameters averaged by the hook in the last backward (tests / diagnostics)
         self._pending = []        # (name, param) collected by the hooks of the running backward
         self._cb_queued = False   # the end-of-backward callback is queued for the running backward
@@ -301,7 +352,8 @@ class U3DDataParallel(torch.nn.Module):
     def forward(self, *args, **kwargs):
         if self.bucketer is None or not torch.is_grad_enabled():
             return self.module(*args, **kwargs)
-        self.bucketer.verify_pending()  # a deferred rank-consistency check of the previous backward raises here
+        if not capturing():
+            self.bucketer.verify_pending()  # a deferred rank-consistency check of the previous backward raises here
         self.fallback_names = []
         self.bucketer.synced = set()  # exemptions of a previous step whose accumulation never fired do not carry over
         self._pending = []            # a backward that raised left its collected hooks (and its callback) behind

@@ -8,7 +8,9 @@ the step runs on every replay — nothing is cached — so replay does exactly t
 Requirements the native path meets: no host syncs (no .item()), every libu3d call is asynchronous on torch's
 current stream (the capture stream during capture), scratch buffers are grow-only and reach their steady
 size in the warm-up steps, parameter gradients are written into fresh tensors (set_to_none=True) that the
-capture pool keeps at fixed addresses.
+capture pool keeps at fixed addresses, or (data parallel, u3d.ddp) into bucket buffers allocated once. The kernel
+forms of a data-parallel backward are chosen statically (ops.DDP_TOLERANT), never by polling a collective, so the
+captured step is the step every eager run would take.
 
 The reference has no train-step function (train_amos_atlas_final.py:209-399 runs it inline); this is the
 additive helper Engine.graphed_train_step / bench.py use.
@@ -23,9 +25,16 @@ class GraphedStep:
     (on the stream, inside the caller's timing) so each replay sees the new batch.
     """
 
-    def __init__(self, step_fn, static_inputs=(), warmup=3, optimizer=None):
+    def __init__(self, step_fn, static_inputs=(), warmup=3, optimizer=None, capture_error_mode=None):
+        """``capture_error_mode``: torch.cuda.graph's; default "thread_local" when torch.distributed is initialised
+        (the process group's watchdog thread queries events of earlier collectives while this thread captures; the
+        step's own all-reduces are captured as graph nodes on RCCL's stream, joined back by ``work.wait()``), else
+        torch's "global"."""
         self.static_inputs = tuple(static_inputs)
         self.optimizer = optimizer
+        if capture_error_mode is None:
+            import torch.distributed as dist
+            capture_error_mode = "thread_local" if dist.is_available() and dist.is_initialized() else "global"
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -34,9 +43,12 @@ class GraphedStep:
                 step_fn()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        if capture_error_mode == "thread_local":
+            import time
+            time.sleep(0.3)  # let the process group's watchdog retire the warm-up steps' works before the capture
         self.graph = torch.cuda.CUDAGraph()
         self._zero()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
             self.out = step_fn()
         torch.cuda.synchronize()
 

@@ -239,9 +239,7 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
                 2.0 * n * d * h * w_ * 27 * 32 * 32, n * d * h * w_)
         return y
     if _use_small(x.dtype, cin, cout, k, stride, (n, d, h, w_)) and not out_f32 and bias is None:
-        ws = WS.get(SPLITK_WS_BYTES, x.device, slot=4)
-        call("u3d_conv_small", 0, x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be),
-             G, _ptr(residual), y.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        conv_small(0, x, cin, wpk, cout, (st, ga, be, G), residual, y)
         return y
     if _use_gen_brick(x.dtype, cin, cout, k, stride, (n, d, h, w_)) and not out_f32 and bias is None:
         call("u3d_convg_brick", 0, x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be),
@@ -258,6 +256,34 @@ def conv_fwd(x, wpk, cout, k, stride, gn=None, residual=None, bias=None, out_f32
          _ptr(ga), _ptr(be), G, _ptr(residual), _ptr(bias), y.data_ptr(), int(out_f32), ws.data_ptr(), ws.numel(),
          _stream())
     return y
+
+
+# conv_small's split-K slabs combined inside its launch by each output tile's last-arriving workgroup (round 5,
+# u3d_conv_small2: no small_reduce_kernel launch); U3D_SMALL_FUSE=0: the two-kernel form
+SMALL_FUSE = os.environ.get("U3D_SMALL_FUSE", "1") != "0"
+SMALL_CNT_SLOT, SMALL_SPART_SLOT = 16, 17
+
+
+def conv_small(flip, x, cin, wpk, cout, gn, residual, y, want_stats=False):
+    """u3d_conv_small(2) into y; returns the output's GroupNorm(16) statistics [n,16,2] when want_stats and the launch
+    produced them (in-kernel combine with the contraction split), else None."""
+    n, d, h, w_ = x.shape[:4]
+    st, ga, be, G = gn if gn is not None else (None, None, None, 0)
+    ws = WS.get(SPLITK_WS_BYTES, x.device, slot=4)
+    if not SMALL_FUSE:
+        call("u3d_conv_small", flip, x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga),
+             _ptr(be), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        return None
+    cnt = WS.get(query("u3d_conv_small_cnt_bytes", n, d, h, w_, cout), x.device, slot=SMALL_CNT_SLOT)
+    stats = sp = None
+    if want_stats:
+        stats = torch.empty((n, 16, 2), dtype=torch.float32, device=x.device)
+        sp = WS.get(4 * query("u3d_conv_small_spart_floats", n, d, h, w_), x.device, slot=SMALL_SPART_SLOT)
+    made = ctypes.c_int(0)
+    call("u3d_conv_small2", flip, x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga), _ptr(be),
+         G, _ptr(residual), y.data_ptr(), ws.data_ptr(), ws.numel(), cnt.data_ptr(), _ptr(sp), _ptr(stats),
+         ctypes.addressof(made), _stream())
+    return stats if made.value else None
 
 
 def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
@@ -284,6 +310,13 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
         fin = "u3d_conv32_ring_q_stats_finalize" if q else "u3d_conv32_ring_stats_finalize"
         call(fin, ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
         return y, stats
+    if (SMALL_FUSE and SMALL_STATS and cout in (64, 128, 256) and _use_small(x.dtype, cin, cout, k, stride, (n, d, h, w_))
+            and not _use_conv1x1(x.dtype, cin, cout, k, n) and not _use_conv32(x.dtype, cin, cout, k, stride, n, w_)):
+        y = torch.empty((n, d, h, w_, cout), dtype=x.dtype, device=x.device)
+        stats = conv_small(0, x, cin, wpk, cout, gn, residual, y, want_stats=True)
+        if stats is not None:
+            return y, stats
+        return y, None
     if (BRICK_STATS and cout % 32 == 0 and cin <= 256 and k == 3 and stride == 1
             and _use_gen_brick(x.dtype, cin, cout, k, stride, (n, d, h, w_))
             and not _use_conv1x1(x.dtype, cin, cout, k, n) and not _use_conv32(x.dtype, cin, cout, k, stride, n, w_)
@@ -303,18 +336,22 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
 
 # Work-stealing ring (u3d_conv32_ring_q): robust to a concurrent kernel holding CUs (a late workgroup's range is
 # taken over by the others instead of doubling the launch), but 10-25% slower alone (tools/concurrency.py,
-# profiles/r02_concurrency.json). Used for the data-gradient ring while a gradient all-reduce is running
-# (collective_in_flight()); U3D_RING_QUEUE=1 forces it for every ring launch.
+# profiles/r02_concurrency.json), and its GroupNorm backward takes the separate partial pass (another fp32 order
+# than the fused static ring). Used for the data-gradient ring only while COLLECTIVE_IN_FLIGHT is set;
+# U3D_RING_QUEUE=1 forces it for every ring launch.
 RING_QUEUE = os.environ.get("U3D_RING_QUEUE", "0") != "0"
-COLLECTIVE_IN_FLIGHT = [False]  # set by u3d.ddp at a bucket launch (tests may set it to force the collective forms)
-COLLECTIVE_POLL = [None]        # u3d.ddp: callable, True while a launched bucket all-reduce has not completed
+# The collective-tolerant forms (work-stealing data-gradient ring, short-range weight-gradient ring) are chosen
+# STATICALLY, never from a device poll, so a data-parallel step runs the same kernels and produces the same bits
+# every time. Default (DDP_TOLERANT off): the data-parallel backward runs exactly the plain step's forms, so an N-rank
+# step is bitwise the 1-rank step up to the all-reduce itself. U3D_DDP_TOLERANT=1: the tolerant forms from the first
+# bucket launch of a backward to its end (a latch in tape order: deterministic, but other fp32 sums than the plain
+# step's GroupNorm backward).
+DDP_TOLERANT = [os.environ.get("U3D_DDP_TOLERANT", "0") != "0"]
+COLLECTIVE_IN_FLIGHT = [False]  # the latch: set by u3d.ddp at a bucket launch when DDP_TOLERANT (tests may set it)
 
 
 def collective_in_flight():
-    """Whether a gradient all-reduce may hold CUs now: the flag, cleared as soon as the poll (work.is_completed() of
-    every launched bucket) reports them all done, so the collective-tolerant kernel forms run only meanwhile."""
-    if COLLECTIVE_IN_FLIGHT[0] and COLLECTIVE_POLL[0] is not None and not COLLECTIVE_POLL[0]():
-        COLLECTIVE_IN_FLIGHT[0] = False
+    """Whether the collective-tolerant kernel forms run now (a static latch, see DDP_TOLERANT)."""
     return COLLECTIVE_IN_FLIGHT[0]
 
 
@@ -331,6 +368,7 @@ def _queue(device, shape):
     return WS.get(query("u3d_conv32_ring_q_queue_bytes", *shape), device, slot=QUEUE_SLOT).data_ptr()
 
 
+SMALL_STATS = os.environ.get("U3D_SMALL_STATS", "1") != "0"  # GN(16) stats of conv_small outputs from its combine
 BRICK_STATS = os.environ.get("U3D_BRICK_STATS", "1") != "0"  # GN statistics from the persistent brick's epilogue
 RING_STATS = os.environ.get("U3D_RING_STATS", "1") != "0"  # GroupNorm statistics from the ring conv epilogue (False: separate u3d_gn_stats pass)
 SPLITK_WS_BYTES = 64 << 20
@@ -471,9 +509,7 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
              _stream())
         return dx
     if _use_small(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
-        ws = WS.get(SPLITK_WS_BYTES, dy.device, slot=4)
-        call("u3d_conv_small", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None, 0,
-             None, dx.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        conv_small(1, dy, cout, wpk_dgrad, cin, None, None, dx)
         return dx
     if _use_gen_brick(dy.dtype, cout, cin, k, stride, (n, d, h, w_)):
         call("u3d_convg_brick", 1, dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, None, None, None, 0,
@@ -613,6 +649,30 @@ def stem_fwd(x_ncdhw, wpk, cout, stride, dtype):
     return y
 
 
+STEM_STATS = os.environ.get("U3D_STEM_STATS", "1") != "0"  # conv1's GroupNorm(16) statistics from its epilogue
+
+
+def stem_fwd_stats(x_ncdhw, wpk, cout, stride, dtype):
+    """stem_fwd that also returns the output's GroupNorm(16) statistics [n,16,2] when the bf16 conv1 kernel runs with
+    its epilogue statistics (u3d_stem1_fwd_stats); otherwise (stem_fwd(...), None)."""
+    n, cin, d, h, w_ = x_ncdhw.shape
+    if STEM_STATS and dtype == torch.bfloat16 and cin == 1 and cout == 32 and stride == 1 and get_option("STEM1") != 0:
+        nws = query("u3d_stem1_stats_ws_floats", n, d, h, w_)
+        if nws > 0:
+            require_device(x_ncdhw)
+            y = torch.empty((n, d, h, w_, cout), dtype=dtype, device=x_ncdhw.device)
+            stats = torch.empty((n, 16, 2), dtype=torch.float32, device=x_ncdhw.device)
+            sp = WS.get(4 * nws, x_ncdhw.device, slot=STEM_STATS_SLOT)
+            ws = WS.get(STEM_WS_BYTES, x_ncdhw.device, slot=STEM_SLOT)
+            call("u3d_stem1_fwd_stats", x_ncdhw.data_ptr(), n, d, h, w_, wpk.data_ptr(), y.data_ptr(), ws.data_ptr(),
+                 sp.data_ptr(), stats.data_ptr(), _stream())
+            return y, stats
+    return stem_fwd(x_ncdhw, wpk, cout, stride, dtype), None
+
+
+STEM_STATS_SLOT = 14
+
+
 def stem_wgrad(dy, x_ncdhw, stride):
     n, cin, d, h, w_ = x_ncdhw.shape
     cout = dy.shape[-1]
@@ -710,6 +770,28 @@ def upsample2x_add(x, skip=None):
     y = torch.empty((n, 2 * d, 2 * h, 2 * w_, c), dtype=x.dtype, device=x.device)
     call("u3d_upsample2x_add", dt_code(x.dtype), x.data_ptr(), n, c, d, h, w_, _ptr(skip), y.data_ptr(), _stream())
     return y
+
+
+UP_STATS = os.environ.get("U3D_UP_STATS", "1") != "0"  # decoder upsample + skip: GroupNorm(16) stats in the epilogue
+
+
+def upsample2x_add_stats(x, skip=None):
+    """upsample2x_add that also returns the output's GroupNorm(16) statistics [n,16,2] from its epilogue (bf16,
+    u3d_upsample2x_add_stats); otherwise (upsample2x_add(...), None)."""
+    n, d, h, w_, c = x.shape
+    if UP_STATS and x.dtype == torch.bfloat16 and get_option("UP_QUAD") != 0:
+        nws = query("u3d_upsample2x_stats_ws_floats", n, c, d, h, w_)
+        if nws > 0:
+            y = torch.empty((n, 2 * d, 2 * h, 2 * w_, c), dtype=x.dtype, device=x.device)
+            stats = torch.empty((n, 16, 2), dtype=torch.float32, device=x.device)
+            sp = WS.get(4 * nws, x.device, slot=UP_STATS_SLOT)
+            call("u3d_upsample2x_add_stats", x.data_ptr(), n, c, d, h, w_, _ptr(skip), y.data_ptr(), sp.data_ptr(),
+                 stats.data_ptr(), _stream())
+            return y, stats
+    return upsample2x_add(x, skip), None
+
+
+UP_STATS_SLOT = 15
 
 
 def upsample2x_bwd(dy, in_shape, dx=None, accumulate=False):

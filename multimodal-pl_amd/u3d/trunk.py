@@ -120,7 +120,10 @@ class Tape:
         """conv with cin <= 4 from the fp32 NCDHW input volume (unet3D.py:1632 / :1514)."""
         W = self.P[key + ".weight"]
         pf, _, st = self.packed(key, self.std, need_dgrad=False)
-        out = Act(ops.stem_fwd(x, pf, W.shape[0], stride, self.dtype))
+        y, st16 = ops.stem_fwd_stats(x, pf, W.shape[0], stride, self.dtype)
+        out = Act(y)
+        if st16 is not None:
+            out.stats[16] = st16  # GroupNorm(16) statistics from the conv1 epilogue (layer0's gn1 / gn2 read them)
         if self.record:
             def bwd():
                 if out.grad is None:
@@ -219,9 +222,16 @@ class Tape:
         self.grad_done(gn_key + ".weight")
         self.grad_done(gn_key + ".bias")
 
-    def up_add(self, x, skip):
-        """upsamplex2 (trilinear, align_corners=False) + skip, unet3D.py:1646 / :1764-1783."""
-        out = Act(ops.upsample2x_add(x.t, skip.t if skip is not None else None))
+    def up_add(self, x, skip, stats=False):
+        """upsamplex2 (trilinear, align_corners=False) + skip, unet3D.py:1646 / :1764-1783. ``stats``: the output feeds
+        GroupNorm(16)s (a decoder block): take its statistics from the upsample's epilogue."""
+        if stats:
+            y, st16 = ops.upsample2x_add_stats(x.t, skip.t if skip is not None else None)
+            out = Act(y)
+            if st16 is not None:
+                out.stats[16] = st16
+        else:
+            out = Act(ops.upsample2x_add(x.t, skip.t if skip is not None else None))
         if self.record:
             def bwd():
                 dy = out.grad
@@ -265,7 +275,7 @@ class Tape:
         bott = f
         self.dec = []  # decoder features after x8/x4/x2/x1_resb (unet3D_with_feam3 heads read the first three)
         for name, s in zip(["x8_resb", "x4_resb", "x2_resb", "x1_resb"], [skips[3], skips[2], skips[1], skips[0]]):
-            u = self.up_add(f, s)
+            u = self.up_add(f, s, stats=cfg.groups == 16)
             f = self.block(u, name + ".0.", 1, cfg.groups)
             self.dec.append(f)
         return f, bott

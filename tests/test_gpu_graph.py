@@ -64,3 +64,4 @@ def test_graphed_step_matches_eager(gpu, amp):
     assert lossA == pytest.approx(lossB, rel=1e-6, abs=1e-7)
     for (n, pa), (_, pb) in zip(mA.named_parameters(), mB.named_parameters()):
         torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-7, msg=n)
+

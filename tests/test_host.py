@@ -418,7 +418,8 @@ def test_bench_gpus_flag_launches_ranks():
 
 
 def test_bench_launch_mode_defaults():
-    """bench.py times hipGraph replays at N=1 and launches eagerly where the step holds collectives."""
+    """bench.py times hipGraph replays by default, also where the step holds its bucketed all-reduces (N>1,
+    --force-buckets: the kernel forms are static, ops.DDP_TOLERANT); --eager launches kernel by kernel."""
     import argparse
     import sys
     sys.path.insert(0, REPO)
@@ -430,9 +431,9 @@ def test_bench_launch_mode_defaults():
         return argparse.Namespace(**d)
     assert bench.launch_mode(ns(), 1) == "graph"
     assert bench.launch_mode(ns(eager=True), 1) == "eager"
-    assert bench.launch_mode(ns(force_buckets=True), 1) == "eager"
-    assert bench.launch_mode(ns(), 8) == "eager"
-    assert bench.launch_mode(ns(graph=True), 8) == "graph"
+    assert bench.launch_mode(ns(force_buckets=True), 1) == "graph"
+    assert bench.launch_mode(ns(), 8) == "graph"
+    assert bench.launch_mode(ns(eager=True), 8) == "eager"
 
 
 # ------------------------------------------------------------- f1: sliding-window tiles sharded over ranks

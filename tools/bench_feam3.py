@@ -25,12 +25,11 @@ def main():
     a = p.parse_args()
     import unet3D
     from loss_functions.losses import get_loss
-    from oracle.weights_recipe import apply_recipe
     from u3d.optim import SGD
     dev = torch.device("cuda:0")
     nc = 14
+    torch.manual_seed(0)  # random-init weights (the module's own init; nothing from oracle/)
     m = unet3D.unet3D_with_feam3([1, 2, 2, 2, 2], num_classes=nc, weight_std=True, deep_up=True)
-    apply_recipe(m, seed=0)
     m = m.to(dev).train()
     m.compute_dtype = torch.bfloat16
     opt = SGD(m.parameters(), lr=5e-4, momentum=0.9, weight_decay=1e-4)

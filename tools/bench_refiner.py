@@ -21,11 +21,10 @@ def main():
     a = p.parse_args()
     import unet3D
     from loss_functions.losses import get_loss_refine
-    from oracle.weights_recipe import apply_recipe
     from u3d.optim import SGD
     dev = torch.device("cuda:0")
+    torch.manual_seed(0)  # random-init weights (the module's own init; nothing from oracle/)
     m = unet3D.unet3D_g([1, 1, 1, 1, 1], num_classes=2, weight_std=True, init_filter=24, in_channel=2)
-    apply_recipe(m, seed=0)
     m = m.to(dev).train()
     m.compute_dtype = torch.bfloat16
     opt = SGD(m.parameters(), lr=5e-4, momentum=0.9, weight_decay=1e-4)

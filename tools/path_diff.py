@@ -1,5 +1,5 @@
 """Diagnostic: the sequence of native calls (ops.call names) of the plain bf16 step vs the U3DDataParallel step
-(RCCL world 1, forced buckets, completion poll pinned to 'running'), and the gradient differences."""
+(RCCL world 1, forced buckets; PD_HOLD=1: the DDP_TOLERANT latch), and the gradient differences."""
 import os
 import socket
 import sys
@@ -15,7 +15,7 @@ def main():
     from loss_functions.loss_partial import EDiceLoss_partial
     from oracle.weights_recipe import input_volume, label_volume
     from u3d import _lib, ops
-    from u3d.ddp import GradBucketer, U3DDataParallel
+    from u3d.ddp import U3DDataParallel
     dev = torch.device("cuda:0")
     x = torch.from_numpy(input_volume((2, 1, 64, 64, 64), seed=61, kind="ct")).to(dev)
     lab = torch.from_numpy(label_volume((2, 64, 64, 64), 16, seed=62)).to(dev)
@@ -38,7 +38,7 @@ def main():
     c0 = list(calls)
     calls.clear()
     if os.environ.get("PD_HOLD", "1") == "1":
-        GradBucketer.in_flight = lambda self: True
+        ops.DDP_TOLERANT[0] = True
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
