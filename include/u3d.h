@@ -184,6 +184,12 @@ int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, const void*
                           float* stats_ws, u3d_stream_t stream);
 int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
                                    u3d_stream_t stream);
+/* Round 5: u3d_conv32_ring_stats with the statistics finalized by the launch's last-arriving workgroup straight into
+ * stats_out[n][16][2] (no u3d_conv32_ring_stats_finalize launch; fixed-order fp64 combine, agent-scope arrival counter
+ * cnt: one ZEROED unsigned, left zeroed by every launch). */
+int u3d_conv32_ring_stats_fused(const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
+                                const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual,
+                                void* y, float* stats_ws, float* stats_out, unsigned* cnt, u3d_stream_t stream);
 /* Work-stealing form of u3d_conv32_ring / u3d_conv32_ring_stats (same operation, same outputs bitwise): each
  * workgroup claims the sub-chunks of its static range of output planes front to back and, once done, steals
  * sub-chunks from the back of other ranges (64-bit compare-and-swap per claim), so workgroups that start late (CUs
@@ -239,6 +245,12 @@ int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h, int w, co
                           const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                           const void* residual, void* y, float* stats_ws, long long ws_floats, float* stats_out,
                           u3d_stream_t stream);
+/* Round 5: u3d_convg_brick_stats with the statistics finalized by the launch's last-arriving workgroup (no separate
+ * finalize launch); cnt: one ZEROED unsigned, left zeroed. */
+int u3d_convg_brick_stats_fused(const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                                const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                                const void* residual, void* y, float* stats_ws, long long ws_floats, float* stats_out,
+                                unsigned* cnt, u3d_stream_t stream);
 
 /* Data gradient of conv(relu(gn(x))) for the persistent brick (48^3 / 24^3 levels) with the GroupNorm backward's
  * partial pass (per channel sum g and sum g*xhat, g = relu-mask * dA) taken in its epilogue: dx = dA as

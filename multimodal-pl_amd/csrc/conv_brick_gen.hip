@@ -33,6 +33,8 @@ struct GBGeom {
   int nbd, nbh, nbw;
   int gn_groups;
   int nct;
+  float* fstats;   // round 5: forward output statistics finalized in-kernel (with fcnt), else nullptr
+  unsigned* fcnt;  // zeroed arrival counter (left zeroed)
 };
 
 // MFMA row r (0..31) -> (segment = which of the 2 h-rows, position = w): the 16 lanes of each ds_read_b128
@@ -774,11 +776,67 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
           t1 += sst[w][h_][(tn * 2 + v) * 4 + q][1];
         }
         typedef __attribute__((ext_vector_type(2))) double f64x2;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, (f64x2){t0, t1}), prs, (u * CO + c) * 8, 0,
-                                               0);
+        if (g.fcnt)  // (write-through: the finalizing workgroup reads them in this launch)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, (f64x2){t0, t1}), prs, (u * CO + c) * 8, 0,
+                                                 16);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, (f64x2){t0, t1}), prs, (u * CO + c) * 8, 0,
+                                                 0);
       }
     }
     cu = nu;
+  }
+  if constexpr (!GB) {
+    if (spart != nullptr && g.fcnt != nullptr) {
+      // Round 5: the GroupNorm(16) finalize (pbrick_gn_finalize_kernel's sums, one launch less) by the workgroup that
+      // arrives last: every wave drains its sc1 partial stores, one lane per workgroup adds to the arrival counter
+      // (agent scope), the last arriver reads the partials with sc1 loads (MI355X_MICROARCH.md visibility, counter
+      // row). 16 lanes per (sample, group), strided over the sample's bricks, the pairs in order, then an xor tree
+      // over the 16 lanes in fixed order: deterministic.
+      __shared__ unsigned s_last;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(g.fcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == gridDim.x - 1;
+        if (s_last) __hip_atomic_store(g.fcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (s_last) {
+        const int bps = g.nbd * g.nbh * g.nbw, cpg = g.cout / 16, l16 = tid & 15;
+        const double m = (double)cpg * g.d * g.h * g.w;
+        for (int p0 = 0; p0 < g.n * 16; p0 += GB_NT / 16) {
+          const int p = p0 + (tid >> 4);
+          double s1 = 0, s2 = 0;
+          if (p < g.n * 16) {
+            const int nn = p >> 4, gr = p & 15;
+            for (int b = l16; b < bps; b += 16) {
+              const long long brick = (long long)nn * bps + b;
+              for (int c = gr * cpg; c < (gr + 1) * cpg; c += 2) {
+                const int ct = c / CO, cl = c - ct * CO;
+                typedef __attribute__((ext_vector_type(2))) double f64x2;
+                const f64x2 q = __builtin_bit_cast(
+                    f64x2, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(((brick * g.nct + ct) * CO + cl) * 8), 0, 16));
+                s1 += q[0];
+                s2 += q[1];
+              }
+            }
+          }
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) {
+            s1 += __shfl_xor(s1, o);
+            s2 += __shfl_xor(s2, o);
+          }
+          if (p < g.n * 16 && l16 == 0) {
+            const double mean = s1 / m;
+            double var = s2 / m - mean * mean;
+            if (var < 0) var = 0;
+            g.fstats[p * 2] = (float)mean;
+            g.fstats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+          }
+        }
+      }
+    }
   }
 }
 
@@ -837,7 +895,7 @@ static bool pbrick_bw8(int w) {
 static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                       const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                       const void* residual, void* y, float* spart, float* stats_out, u3d_stream_t stream,
-                      const void* gbx = nullptr, float* gbparts = nullptr) {
+                      const void* gbx = nullptr, float* gbparts = nullptr, unsigned* fcnt = nullptr) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && n <= GB_MAXN, "convg_brick: bad args");
   U3D_REQUIRE(!gbparts || (flip && gbx && gn_stats && !residual && !spart && cout % gn_groups == 0),
               "convg_brick_dgrad_gn: bad args");
@@ -875,6 +933,10 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
   if (pers) {
     const bool bw8 = pbrick_bw8(w);
     GBGeom gp = g;
+    if (spart && fcnt) {
+      gp.fstats = stats_out;
+      gp.fcnt = fcnt;
+    }
     if (bw8) {
       gp.nbw = cdiv(w, 8);
       const long long nb8 = (long long)n * gp.nbd * gp.nbh * gp.nbw;
@@ -914,7 +976,7 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
 #undef U3D_PB
     int rc = check_launch("convg_pbrick_kernel");
     if (rc) return rc;
-    if (!spart) return rc;
+    if (!spart || fcnt) return rc;  // (fcnt: finalized by the kernel's last-arriving workgroup)
     hipLaunchKernelGGL(pbrick_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, (const double*)spart, co64 ? 64 : 32, gp.nct,
                        gp.nbd * gp.nbh * gp.nbw, cout, (double)(cout / 16) * d * h * w, stats_out);
     return check_launch("pbrick_gn_finalize_kernel");
@@ -978,4 +1040,16 @@ extern "C" int u3d_convg_brick_stats(const void* x, int n, int cin, int d, int h
   U3D_REQUIRE(ws_floats >= u3d_convg_brick_stats_ws_floats(n, d, h, w, cout), "convg_brick_stats: workspace too small");
   return convg_impl(0, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
                     stats_out, stream);
+}
+
+// Round 5: u3d_convg_brick_stats with the statistics finalized inside the conv launch by its last-arriving workgroup
+// (no pbrick_gn_finalize_kernel launch). cnt: one ZEROED unsigned (left zeroed by every launch).
+extern "C" int u3d_convg_brick_stats_fused(const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
+                                           const float* gn_stats, const float* gn_gamma, const float* gn_beta,
+                                           int gn_groups, const void* residual, void* y, float* stats_ws,
+                                           long long ws_floats, float* stats_out, unsigned* cnt, u3d_stream_t stream) {
+  U3D_REQUIRE(stats_ws && stats_out && cnt, "convg_brick_stats_fused: null statistics buffers");
+  U3D_REQUIRE(ws_floats >= u3d_convg_brick_stats_ws_floats(n, d, h, w, cout), "convg_brick_stats: workspace too small");
+  return convg_impl(0, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
+                    stats_out, stream, nullptr, nullptr, cnt);
 }

@@ -53,6 +53,8 @@ struct RGGeom {
   long long pps;     // output planes per sample; workgroups never straddle samples (per-sample GN statistics)
   int wps;           // workgroups per sample
   int sc, rmax;      // work-stealing mode: output planes per sub-chunk, sub-chunks per (full) range
+  float* fstats;     // round 5: output GroupNorm(16) statistics finalized in-kernel (with fcnt; static forward only)
+  unsigned* fcnt;    // zeroed arrival counter (left zeroed)
 };
 
 // One staged input plane: column (n, h0, w0), input depth zin (-1 / d = zero padding), and whether it is the
@@ -727,7 +729,52 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       float t = 0.f;
 #pragma unroll
       for (int wv = 0; wv < RG_NT / 64; ++wv) t += red[wv * 32 + tid];
-      spart[(long long)bid * 32 + tid] = t;  // [sample][wps][group][2]: bid = sample * wps + jw
+      if (g.fcnt)  // write-through: the finalizing workgroup reads it in this launch
+        __hip_atomic_store(spart + (long long)bid * 32 + tid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        spart[(long long)bid * 32 + tid] = t;  // [sample][wps][group][2]: bid = sample * wps + jw
+    }
+    if (g.fcnt) {
+      // Round 5: ring_gn_finalize_kernel's combine by the workgroup that arrives last (one launch less): every wave
+      // drains, one lane per workgroup adds to the arrival counter (agent scope), the last arriver reads the partial
+      // rows with sc1 loads; 16 lanes per (sample, group) strided over the sample's workgroups, xor tree in fixed order.
+      __shared__ unsigned s_last;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(g.fcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == gridDim.x - 1;
+        if (s_last) __hip_atomic_store(g.fcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (s_last) {
+        const int l16 = tid & 15;
+        const double m = 2.0 * g.d * g.h * g.w;
+        for (int p0 = 0; p0 < g.n * 16; p0 += RG_NT / 16) {
+          const int p = p0 + (tid >> 4);
+          double s1 = 0, s2 = 0;
+          if (p < g.n * 16) {
+            const int nn = p >> 4, gr = p & 15;
+            for (int wk = l16; wk < g.wps; wk += 16) {
+              const float* q = spart + ((long long)nn * g.wps + wk) * 32 + gr * 2;
+              s1 += __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              s2 += __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) {
+            s1 += __shfl_xor(s1, o);
+            s2 += __shfl_xor(s2, o);
+          }
+          if (p < g.n * 16 && l16 == 0) {
+            const double mean = s1 / m;
+            double var = s2 / m - mean * mean;
+            if (var < 0) var = 0;
+            g.fstats[p * 2] = (float)mean;
+            g.fstats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+          }
+        }
+      }
     }
   }
 }
@@ -776,7 +823,8 @@ static int ring_kr(int dflt) {  // RING_KR = 0: no weight steps in registers (ex
 static int ring_wgs() { return std::max(1, opt(OPT_RING_WGS)); }  // persistent grid target: one workgroup per CU
 static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
                             const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
-                            const void* residual, void* y, float* stats_out, float* stats_ws, u3d_stream_t stream) {
+                            const void* residual, void* y, float* stats_out, float* stats_ws, u3d_stream_t stream,
+                            float* fstats = nullptr, unsigned* fcnt = nullptr) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv32_ring: bad args");
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0), "conv32_ring: bad GN");
   U3D_REQUIRE(!stats_out || (gn_stats && stats_ws), "conv32_ring: output statistics need the GN prologue + ws");
@@ -794,6 +842,10 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
   g.wps = (int)((g.pps + g.per - 1) / g.per);
   const long long grid = (long long)n * g.wps;
   g.gn_groups = gn_groups;
+  if (stats_out && fcnt && fstats) {
+    g.fstats = fstats;
+    g.fcnt = fcnt;
+  }
   hipStream_t s = (hipStream_t)stream;
   float* sp = stats_out ? stats_ws : nullptr;
 #define RG_LAUNCH(F, G, R, K)                                                                                  \
@@ -1009,4 +1061,16 @@ extern "C" int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int 
   hipLaunchKernelGGL(ring_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, (hipStream_t)stream, stats_ws, n, wps,
                      2.0 * d * h * w, stats_out);
   return check_launch("ring_gn_finalize_kernel");
+}
+
+// Round 5: u3d_conv32_ring_stats with the statistics finalized by the launch's last-arriving workgroup into stats_out
+// (no u3d_conv32_ring_stats_finalize launch). cnt: one ZEROED unsigned, left zeroed.
+extern "C" int u3d_conv32_ring_stats_fused(const void* x, int n, int d, int h, int w, const void* wpk,
+                                           const float* gn_stats, const float* gn_gamma, const float* gn_beta,
+                                           int gn_groups, const void* residual, void* y, float* stats_ws,
+                                           float* stats_out, unsigned* cnt, u3d_stream_t stream) {
+  U3D_REQUIRE(stats_ws && stats_out && cnt, "conv32_ring_stats_fused: null statistics buffers");
+  U3D_REQUIRE(n * 16 <= 4096, "conv32_ring_stats_fused: n too large");
+  return conv32_ring_impl(0, x, n, d, h, w, wpk, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
+                          stats_ws, stream, stats_out, cnt);
 }

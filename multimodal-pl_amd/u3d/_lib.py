@@ -44,6 +44,7 @@ _SIGS = {
     "u3d_conv32_ring": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring_stats_ws_floats": [I],
     "u3d_conv32_ring_stats": [P, I, I, I, I, P, P, P, P, I, P, P, P, P],
+    "u3d_conv32_ring_stats_fused": [P, I, I, I, I, P, P, P, P, I, P, P, P, P, P, P],
     "u3d_conv32_ring_wps": [I, I, I, I],
     "u3d_conv32_ring_dgrad_gn": [P, I, I, I, I, P, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring_stats_finalize": [P, I, I, I, I, P, P],
@@ -58,6 +59,7 @@ _SIGS = {
     "u3d_convg_brick": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P],
     "u3d_convg_brick_stats_ws_floats": [I, I, I, I, I],
     "u3d_convg_brick_stats": [P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P, P],
+    "u3d_convg_brick_stats_fused": [P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P, P, P],
     "u3d_convg_brick_gn_nparts": [I, I, I, I, I, I],
     "u3d_convg_brick_dgrad_gn": [P, I, I, I, I, I, P, I, P, P, P, P, I, P, P, I, P],
     "u3d_conv_wgrad_brick_splits": [I, I, I, I, I, I, I],

@@ -302,13 +302,18 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
         if q:
             call("u3d_conv32_ring_q", 0, x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
                  be.data_ptr(), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), _queue(x.device, (n, d, h, w_)), _stream())
+        elif FUSED_FINALIZE:  # the statistics finalized by the launch's last-arriving workgroup (round 5)
+            call("u3d_conv32_ring_stats_fused", x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
+                 be.data_ptr(), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), stats.data_ptr(),
+                 WS.get(256, x.device, slot=RING_CNT_SLOT).data_ptr(), _stream())
         else:
             call("u3d_conv32_ring_stats", x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
                  be.data_ptr(), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), _stream())
         _probe1(pr, "conv32_ring fwd GN" + (" +res" if residual is not None else "") + " +stats",
                 2.0 * n * d * h * w_ * 27 * 32 * 32, n * d * h * w_)
-        fin = "u3d_conv32_ring_q_stats_finalize" if q else "u3d_conv32_ring_stats_finalize"
-        call(fin, ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
+        if q or not FUSED_FINALIZE:
+            fin = "u3d_conv32_ring_q_stats_finalize" if q else "u3d_conv32_ring_stats_finalize"
+            call(fin, ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
         return y, stats
     if (SMALL_FUSE and SMALL_STATS and cout in (64, 128, 256) and _use_small(x.dtype, cin, cout, k, stride, (n, d, h, w_))
             and not _use_conv1x1(x.dtype, cin, cout, k, n) and not _use_conv32(x.dtype, cin, cout, k, stride, n, w_)):
@@ -328,8 +333,13 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
         stats = torch.empty((n, 16, 2), dtype=torch.float32, device=x.device)
         nws = query("u3d_convg_brick_stats_ws_floats", n, d, h, w_, cout)
         ws = WS.get(4 * nws, x.device, slot=9)
-        call("u3d_convg_brick_stats", x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga),
-             _ptr(be), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), nws, stats.data_ptr(), _stream())
+        if FUSED_FINALIZE:
+            call("u3d_convg_brick_stats_fused", x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga),
+                 _ptr(be), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), nws, stats.data_ptr(),
+                 WS.get(256, x.device, slot=BRICK_CNT_SLOT).data_ptr(), _stream())
+        else:
+            call("u3d_convg_brick_stats", x.data_ptr(), n, cin, d, h, w_, wpk.data_ptr(), cout, _ptr(st), _ptr(ga),
+                 _ptr(be), G, _ptr(residual), y.data_ptr(), ws.data_ptr(), nws, stats.data_ptr(), _stream())
         return y, stats
     return conv_fwd(x, wpk, cout, k, stride, gn, residual), None
 
@@ -368,6 +378,10 @@ def _queue(device, shape):
     return WS.get(query("u3d_conv32_ring_q_queue_bytes", *shape), device, slot=QUEUE_SLOT).data_ptr()
 
 
+# the ring / persistent-brick conv epilogue statistics finalized by the conv launch's last-arriving workgroup (round 5:
+# no ring_gn_finalize / pbrick_gn_finalize launch); U3D_FUSED_FINALIZE=0: the separate finalize kernels
+FUSED_FINALIZE = os.environ.get("U3D_FUSED_FINALIZE", "1") != "0"
+RING_CNT_SLOT, BRICK_CNT_SLOT = 18, 19
 SMALL_STATS = os.environ.get("U3D_SMALL_STATS", "1") != "0"  # GN(16) stats of conv_small outputs from its combine
 BRICK_STATS = os.environ.get("U3D_BRICK_STATS", "1") != "0"  # GN statistics from the persistent brick's epilogue
 RING_STATS = os.environ.get("U3D_RING_STATS", "1") != "0"  # GroupNorm statistics from the ring conv epilogue (False: separate u3d_gn_stats pass)
@@ -524,6 +538,15 @@ def conv_dgrad(dy, wpk_dgrad, cin, in_shape, k, stride):
 # the downsample branch's stride-2 1^3 data gradient kept at the conv's output resolution when its GroupNorm backward
 # runs paired with gn1 (gn_bwd2(..., da2_s2=True)): no zero-filled full-resolution tensor (U3D_S2_COMPACT=0: off)
 S2_COMPACT = os.environ.get("U3D_S2_COMPACT", "1") != "0"
+
+
+def s2_compact_ok(in_shape, cin, elsize):
+    """Limits of the paired GroupNorm backward that reads a compact stride-2 1^3 data gradient (u3d_gn_bwd2_s2,
+    groupnorm.hip: the voxel -> (z, y, x) split by an fp32 reciprocal needs < 2^24 voxels per sample; the compact
+    operand is read with 32-bit buffer offsets, < 2 GiB). Outside them the caller takes conv_dgrad + gn_bwd2."""
+    n, d, h, w_ = in_shape[:4]
+    cv = out_dim(d, 1, 2) * out_dim(h, 1, 2) * out_dim(w_, 1, 2)
+    return d * h * w_ < (1 << 24) and n * cv * cin * elsize < (1 << 31)
 
 
 def conv_dgrad_1x1s2_compact(dy, wpk_dgrad, cin):

@@ -178,7 +178,8 @@ class Tape:
                 part, ns = ops.conv_wgrad(dyT, x.t, k, stride, gn)
                 self.pend_wgrad(part, ns, W, st, std, key + ".weight")
                 s2c = (gn is not None and pair == "park" and k == 1 and stride == 2 and ops.S2_COMPACT
-                       and ops._use_conv1x1(dyT.dtype, dyT.shape[-1], cin, 1, dyT.shape[0]))
+                       and ops._use_conv1x1(dyT.dtype, dyT.shape[-1], cin, 1, dyT.shape[0])
+                       and ops.s2_compact_ok(x.t.shape, cin, dyT.element_size()))
                 parts = None
                 if gn is not None and not head and pair != "park" and not (pair == "finish" and x.gn_pend):
                     fused = ops.conv_dgrad_gn(dyT, pd, cin, x.t, k, stride, gn)  # GN-bwd partials in the epilogue

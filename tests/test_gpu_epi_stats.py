@@ -105,3 +105,40 @@ def test_conv_small_in_kernel_combine(gpu, n, cin, cout, dims, res, flip):
         assert outs[0][1] is None and outs[1][1] is not None
         assert torch.equal(outs[1][1], outs[2][1])
         _close(outs[1][1], ops.gn_stats(outs[1][0], 16), outs[1][0])
+
+
+@pytest.mark.parametrize("kind,n,c,dims,res", [
+    ("ring", 2, 32, (24, 24, 24), True),    # 32 -> 32 ring conv (the 96^3 level's kernel), 2 samples
+    ("ring", 1, 32, (10, 16, 40), False),
+    ("ring", 3, 32, (9, 12, 16), True),
+    ("brick", 2, 64, (24, 24, 24), True),   # persistent brick (48^3 / 24^3 levels)
+    ("brick", 2, 128, (12, 16, 24), False),
+    ("brick", 3, 64, (8, 16, 32), True),
+])
+def test_fused_finalize_matches_finalize_kernel(gpu, monkeypatch, kind, n, c, dims, res):
+    """The ring / persistent-brick epilogue statistics finalized by the conv launch's last-arriving workgroup
+    (ops.FUSED_FINALIZE, round 5) against the separate finalize kernel on the same partials: outputs bitwise equal,
+    statistics equal up to the fp64 combine order (<= 1e-6 relative), and two fused launches in a row bitwise equal
+    (the arrival counter is left at zero)."""
+    from u3d import ops
+    torch.manual_seed(17)
+    x = (torch.randn((n,) + dims + (c,), device=gpu) + 0.4).to(torch.bfloat16)
+    w = torch.randn(c, c, 3, 3, 3, device=gpu) * 0.1
+    pf, _, _ = ops.wstd_fwd(w, torch.bfloat16, True, need_dgrad=False)
+    gn = (ops.gn_stats(x, 16), 1 + 0.1 * torch.randn(c, device=gpu), 0.1 * torch.randn(c, device=gpu), 16)
+    r = (torch.randn((n,) + dims + (c,), device=gpu) + 1).to(torch.bfloat16) if res else None
+    if kind == "ring":
+        assert ops._use_conv32(torch.bfloat16, c, c, 3, 1, n, dims[2])
+    else:
+        assert ops._use_gen_brick(torch.bfloat16, c, c, 3, 1, (n,) + dims)
+    outs = []
+    for fused in (False, True, True):
+        monkeypatch.setattr(ops, "FUSED_FINALIZE", fused)
+        y, st = ops.conv_fwd_stats(x, pf, c, 3, 1, gn, residual=r)
+        assert st is not None
+        outs.append((y, st))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[1][0], outs[2][0]) and torch.equal(outs[1][1], outs[2][1])
+    rel = ((outs[1][1] - outs[0][1]).abs() / outs[0][1].abs().clamp_min(1e-6)).max().item()
+    assert rel <= 1e-6, rel

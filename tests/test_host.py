@@ -601,3 +601,13 @@ def test_dgrad_gn_routing_brick_levels(monkeypatch):
     assert run(12, 256) is None and calls == []         # small-volume kernel level: no fused form
     monkeypatch.setattr(ops, "GN_BWD_FUSED_BRICK", False)
     assert run(24, 128) is None and calls == []
+
+
+def test_compact_stride2_gn_backward_limits():
+    """the paired GroupNorm backward reading the compact stride-2 1^3 data gradient (u3d_gn_bwd2_s2) needs
+    < 2^24 voxels per sample and a compact operand < 2 GiB; outside them the trunk takes conv_dgrad + gn_bwd2."""
+    from u3d import ops
+    assert ops.s2_compact_ok((2, 96, 96, 96), 32, 2)
+    assert ops.s2_compact_ok((2, 192, 192, 192), 32, 2)              # 7.1M voxels per sample
+    assert not ops.s2_compact_ok((1, 256, 256, 256), 32, 2)          # 2^24 voxels per sample
+    assert not ops.s2_compact_ok((16, 240, 240, 240), 64, 2)         # compact operand 2.8 GB
