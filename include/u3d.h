@@ -147,6 +147,33 @@ int u3d_conv_small2(int flip, const void* x, int n, int cin, int d, int h, int w
                     const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                     const void* residual, void* y, float* ws, long long ws_bytes, unsigned* cnt, float* spart,
                     float* stats_out, int* stats_made, u3d_stream_t stream);
+/* Round 5: data gradient of conv(relu(gn(x))) on the small-volume kernel with the GroupNorm backward's partial sums and
+ * its coefficient finalize inside the launch (the split-K combine reads x at dA's addresses; the workgroup completing
+ * the last tile writes coef[n][5][cin] and dgamma / dbeta[cin] as gn_bwd_parts_finalize would). cin / cout are the
+ * FORWARD conv's channels (dy: cout; x, dx: cin), wpk_dgrad the data-gradient pack. cnt: u3d_conv_small_cnt_bytes(n,
+ * d, h, w, cin) ZEROED bytes; parts: u3d_conv_small_gb_parts_floats floats. *made = 0: nothing launched (the launch
+ * would not split its contraction); the caller then takes u3d_conv_small + u3d_gn_bwd. Follow with
+ * u3d_gn_bwd_apply_coef. Reference: autograd of NoBottleneck's relu(gn(x)) -> conv3x3x3 (unet3D.py:44-73). */
+long long u3d_conv_small_gb_parts_floats(int n, int d, int h, int w, int cin);
+int u3d_conv_small_dgrad_gn(const void* dy, int n, int cout, int d, int h, int w, const void* wpk_dgrad, int cin,
+                            const void* x, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
+                            int gn_groups, void* dx, float* ws, long long ws_bytes, unsigned* cnt, float* parts,
+                            float* coef, float* dgamma, float* dbeta, int* made, u3d_stream_t stream);
+/* the apply pass of the GroupNorm backward from precomputed coefficients coef[n][5][c] (bf16 dA, x, dx) */
+int u3d_gn_bwd_apply_coef(const void* da, const void* x, int n, int c, long long v, int groups, const float* coef,
+                          void* dx, int accumulate, u3d_stream_t stream);
+
+/* Round 5: 3^3 stride-2 forward conv of relu(gn(x)), bf16, cin 32 -> cout 64 (layer1.0.conv1 at 96^3; reference
+ * unet3D.py:45, :56-73) as a persistent walk over input planes: each input plane of a column's halo staged once with the
+ * GroupNorm + ReLU applied once per element, both contributions of an odd plane (kd = 2 of output z, kd = 0 of z + 1)
+ * from one fragment. wpk = forward pack [27][64][32]. With stats_out the output's GroupNorm(16) statistics [n][16][2]
+ * from the epilogue, finalized by the last-arriving workgroup (spart: u3d_conv_s2_ring_ws_floats floats; cnt: one
+ * ZEROED unsigned, left zeroed). u3d_conv_s2_ring_ok: 1 where the shape is served (x < 2 GiB, n <= 32). */
+int u3d_conv_s2_ring_ok(int n, int cin, int d, int h, int w, int cout);
+long long u3d_conv_s2_ring_ws_floats(int n, int d, int h, int w);
+int u3d_conv_s2_ring(const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
+                     const float* gn_gamma, const float* gn_beta, int gn_groups, void* y, float* spart, float* stats_out,
+                     unsigned* cnt, u3d_stream_t stream);
 
 /* Classifier head precls_conv (unet3D.py:1653-1657): GN+ReLU + 1^3 conv cin (16..64, %16) -> cout (<= 32) + bias,
  * bf16 NDHWC input, fp32 NDHWC logits [n*v][cout]; wpk = forward pack [1][cout_p][cin_p]. Streaming MFMA kernel

@@ -54,6 +54,14 @@ struct SCGeom {
   float* spart;            // [n][nbd*nbh*nbw][16][2] fp32 partials of the output statistics (stats != nullptr)
   float* stats;            // [n][16][2] (mean, rstd) of the output, or nullptr
   int cpg;                 // output channels per GroupNorm group (cout / 16; 4, 8 or 16)
+  // round 5, data gradient (flip) through the combine: the backward of the GroupNorm + ReLU on x (the forward's input,
+  // channels = this launch's cout) — per (sample, brick, channel) (sum g, sum g*xhat) of g = relu-mask * dA, then the
+  // apply coefficients coef[n][5][cout] and dgamma / dbeta by the workgroup completing the last tile
+  const bf16* gbx;
+  const float *gbstat, *gbgamma, *gbbeta;
+  int gbgroups;
+  float* gbparts;          // [n][bricks][cout][2]
+  float *coef, *dgamma, *dbeta;
 };
 
 template <bool FLIP>
@@ -248,6 +256,20 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
 #pragma unroll
     for (int k = 0; k < 8; ++k) ls[k] = lq[k] = 0.f;
     const int cpg = g.stats ? g.cpg : 32;
+    // GroupNorm-backward partials (flip with gbx): this thread's 4 channels are fixed (part = tid & 7)
+    float bsc[4], bsh[4], bmu[4], brs[4], b1[4], b2[4];
+    if (g.gbx) {
+      const int gcpg = g.cout / g.gbgroups;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = min(co0 + (tid & 7) * 4 + e, g.cout - 1), gr = c / gcpg;
+        bmu[e] = g.gbstat[(nn * g.gbgroups + gr) * 2];
+        brs[e] = g.gbstat[(nn * g.gbgroups + gr) * 2 + 1];
+        bsc[e] = brs[e] * g.gbgamma[c];
+        bsh[e] = g.gbbeta[c] - bmu[e] * bsc[e];
+        b1[e] = b2[e] = 0.f;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int q = tid + SC_NT * k, vv = q >> 3, part = q & 7;
@@ -279,6 +301,20 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
       o.x = (uint32_t)from_f<bf16>(v[0]) | ((uint32_t)from_f<bf16>(v[1]) << 16);
       o.y = (uint32_t)from_f<bf16>(v[2]) | ((uint32_t)from_f<bf16>(v[3]) << 16);
       *reinterpret_cast<uint2*>(y + vo) = o;
+      if (g.gbx) {  // exactly gn_bwd_partial's per-element terms on the stored bf16 dA and x
+        const uint2 xq = *reinterpret_cast<const uint2*>(g.gbx + vo);
+        const float xv[4] = {__uint_as_float(xq.x << 16), __uint_as_float(xq.x & 0xffff0000u),
+                             __uint_as_float(xq.y << 16), __uint_as_float(xq.y & 0xffff0000u)};
+        const float dv[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
+                             __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (xv[e] - bmu[e]) * brs[e];
+          const float gd = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? dv[e] : 0.f;
+          b1[e] += gd;
+          b2[e] = fmaf(gd, xh, b2[e]);
+        }
+      }
       if (g.stats) {  // the stored values' group sums (4 channels of one group: cpg >= 4)
         const float a0 = __uint_as_float(o.x << 16), a1 = __uint_as_float(o.x & 0xffff0000u);
         const float a2 = __uint_as_float(o.y << 16), a3 = __uint_as_float(o.y & 0xffff0000u);
@@ -290,6 +326,87 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
           lq[k2] += gi == k2 ? qq : 0.f;
         }
       }
+    }
+    if (g.gbx) {
+      // per channel of the tile over the workgroup: lanes with the same tid & 7 (xor 8, 16, 32), then the waves in order
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int o2 = 8; o2 < 64; o2 <<= 1) {
+          b1[e] += __shfl_xor(b1[e], o2);
+          b2[e] += __shfl_xor(b2[e], o2);
+        }
+      float* const red = reinterpret_cast<float*>(smem);  // [wave][32 channels][2]
+      __syncthreads();
+      if (lane < 8)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          red[(wave * 32 + lane * 4 + e) * 2] = b1[e];
+          red[(wave * 32 + lane * 4 + e) * 2 + 1] = b2[e];
+        }
+      __syncthreads();
+      const int nbr = g.nbd * g.nbh * g.nbw, brick = (bd_ * g.nbh + bh_) * g.nbw + bw_;
+      if (tid < 64 && co0 + (tid >> 1) < g.cout) {
+        float t2 = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < SC_NT / 64; ++wv) t2 += red[wv * 64 + tid];
+        __hip_atomic_store(g.gbparts + (((long long)nn * nbr + brick) * g.cout + co0) * 2 + tid, t2, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);  // sc1
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int ntiles = (int)(gridDim.x / g.nks);
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(g.cnt + ntiles, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == (unsigned)(ntiles - 1);
+        if (s_last) __hip_atomic_store(g.cnt + ntiles, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (!s_last) return;
+      // gn_bwd_parts_finalize + gn_bwd_coefs: per (n, c) fp64 sums over the bricks in order, then the coefficients
+      double* const cs = reinterpret_cast<double*>(smem);  // [n * cout][2] (<= 8192 doubles: host-checked)
+      for (int p = tid; p < g.n * g.cout; p += SC_NT) {
+        const int n2 = p / g.cout, c = p - n2 * g.cout;
+        double s1 = 0, s2 = 0;
+        for (int b2_ = 0; b2_ < nbr; ++b2_) {
+          const float* pp = g.gbparts + (((long long)n2 * nbr + b2_) * g.cout + c) * 2;
+          s1 += __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s2 += __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        cs[2 * p] = s1;
+        cs[2 * p + 1] = s2;
+      }
+      __syncthreads();
+      const int gcpg = g.cout / g.gbgroups;
+      const double M = (double)g.d * g.h * g.w * gcpg;
+      for (int p = tid; p < g.n * g.cout; p += SC_NT) {
+        const int n2 = p / g.cout, c = p - n2 * g.cout, gr = c / gcpg;
+        double a = 0, bb = 0;
+        for (int k2 = 0; k2 < gcpg; ++k2) {
+          const int cc = gr * gcpg + k2;
+          a += (double)g.gbgamma[cc] * cs[2 * (n2 * g.cout + cc)];
+          bb += (double)g.gbgamma[cc] * cs[2 * (n2 * g.cout + cc) + 1];
+        }
+        const float ca = (float)(a / M), cb = (float)(bb / M);
+        const float mu = g.gbstat[(n2 * g.gbgroups + gr) * 2], rs = g.gbstat[(n2 * g.gbgroups + gr) * 2 + 1];
+        const float scv = rs * g.gbgamma[c];
+        float* oc = g.coef + (long long)n2 * 5 * g.cout;
+        oc[c] = scv;
+        oc[g.cout + c] = g.gbbeta[c] - mu * scv;
+        oc[2 * g.cout + c] = rs * g.gbgamma[c];
+        oc[3 * g.cout + c] = -rs * rs * cb;
+        oc[4 * g.cout + c] = -rs * ca + rs * rs * cb * mu;
+      }
+      for (int c = tid; c < g.cout; c += SC_NT) {
+        double tg = 0, tb = 0;
+        for (int n2 = 0; n2 < g.n; ++n2) {
+          tb += cs[2 * (n2 * g.cout + c)];
+          tg += cs[2 * (n2 * g.cout + c) + 1];
+        }
+        if (g.dgamma) g.dgamma[c] = (float)tg;
+        if (g.dbeta) g.dbeta[c] = (float)tb;
+      }
+      return;
     }
     if (!g.stats) return;
     // ---- output GroupNorm(16) statistics: this tile's groups reduced over the workgroup (fixed order), one partial
@@ -401,10 +518,17 @@ __global__ __launch_bounds__(256) void small_reduce_kernel(const float* __restri
 
 using namespace u3d;
 
+struct SCGb {  // the GroupNorm-backward partials of the data gradient (u3d_conv_small_dgrad_gn)
+  const void* x;
+  const float *stats, *gamma, *beta;
+  int groups;
+  float *parts, *coef, *dgamma, *dbeta;
+};
 static int conv_small_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                            const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                            const void* residual, void* y, float* ws, long long ws_bytes, unsigned* cnt,
-                           float* spart, float* stats_out, int* nks_out, u3d_stream_t stream);
+                           float* spart, float* stats_out, int* nks_out, u3d_stream_t stream,
+                           const SCGb* gb = nullptr, bool plan_only = false);
 
 extern "C" int u3d_conv_small(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                               const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
@@ -440,7 +564,8 @@ extern "C" int u3d_conv_small2(int flip, const void* x, int n, int cin, int d, i
 static int conv_small_impl(int flip, const void* x, int n, int cin, int d, int h, int w, const void* wpk, int cout,
                            const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                            const void* residual, void* y, float* ws, long long ws_bytes, unsigned* cnt,
-                           float* spart, float* stats_out, int* nks_out, u3d_stream_t stream) {
+                           float* spart, float* stats_out, int* nks_out, u3d_stream_t stream,
+                           const SCGb* gb, bool plan_only) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv_small: bad args");
   U3D_REQUIRE(cin % 8 == 0 && cout % 8 == 0, "conv_small: channels must be multiples of 8");
   U3D_REQUIRE(!gn_stats || (!flip && gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0),
@@ -479,6 +604,15 @@ static int conv_small_impl(int flip, const void* x, int n, int cin, int d, int h
   g.stats = g.cnt ? stats_out : nullptr;
   g.spart = g.stats ? spart : nullptr;
   g.cpg = cout / 16;
+  if (plan_only) return 0;
+  if (gb && g.cnt) {
+    U3D_REQUIRE(flip && !residual && gb->groups > 0 && cout % gb->groups == 0 && (long long)n * cout * 2 <= 8192,
+                "conv_small_dgrad_gn: bad GroupNorm-backward args");
+    g.gbx = (const bf16*)gb->x;
+    g.gbstat = gb->stats; g.gbgamma = gb->gamma; g.gbbeta = gb->beta; g.gbgroups = gb->groups;
+    g.gbparts = gb->parts; g.coef = gb->coef; g.dgamma = gb->dgamma; g.dbeta = gb->dbeta;
+    g.stats = nullptr;
+  }
   U3D_REQUIRE(!g.stats || (n * 16 <= SC_NT && g.nks * (long long)n * d * h * w * cout * 4 < (1LL << 31)),
               "conv_small2: statistics form limits");
   const long long nwg = tiles * g.nks;
@@ -498,4 +632,35 @@ static int conv_small_impl(int flip, const void* x, int n, int cin, int d, int h
   hipLaunchKernelGGL(small_reduce_kernel, dim3((unsigned)std::min<long long>(4096, (per4 + 255) / 256)), dim3(256), 0,
                      s, ws, g.nks, per4, (const bf16*)residual, (bf16*)y);
   return check_launch("small_reduce_kernel");
+}
+
+// Round 5: data gradient of conv(relu(gn(x))) for the small deep-level volumes with the GroupNorm backward's partial
+// pass AND its coefficient finalize inside the launch (the split-K combine computes the bf16 dA, reads x at the same
+// addresses, sums g = relu-mask * dA and g * xhat per (sample, brick, channel); the workgroup completing the last tile
+// forms the apply coefficients coef[n][5][cin] and dgamma / dbeta as gn_bwd_parts_finalize does). Then only
+// u3d_gn_bwd_apply_coef runs. cin / cout are the FORWARD conv's: dy has cout, dx / x have cin; wpk = the dgrad pack.
+// parts: u3d_conv_small_gb_parts_floats floats; cnt: u3d_conv_small_cnt_bytes(n, d, h, w, cin) zeroed bytes.
+// *made = 0 (nothing launched; the caller takes the separate passes) where the launch would not split its
+// contraction over 2..8 workgroups.
+extern "C" long long u3d_conv_small_gb_parts_floats(int n, int d, int h, int w, int cin) {
+  return 2LL * n * d * h * w * cin;  // >= n * bricks * cin * 2
+}
+extern "C" int u3d_conv_small_dgrad_gn(const void* dy, int n, int cout, int d, int h, int w, const void* wpk_dgrad,
+                                       int cin, const void* x, const float* gn_stats, const float* gn_gamma,
+                                       const float* gn_beta, int gn_groups, void* dx, float* ws, long long ws_bytes,
+                                       unsigned* cnt, float* parts, float* coef, float* dgamma, float* dbeta,
+                                       int* made, u3d_stream_t stream) {
+  U3D_REQUIRE(dy && x && dx && cnt && parts && coef && made && gn_stats && gn_gamma && gn_beta,
+              "conv_small_dgrad_gn: bad args");
+  *made = 0;
+  int nks = 0;
+  int rc = conv_small_impl(1, dy, n, cout, d, h, w, wpk_dgrad, cin, nullptr, nullptr, nullptr, 0, nullptr, dx, ws,
+                           ws_bytes, cnt, nullptr, nullptr, &nks, stream, nullptr, true);
+  if (rc) return rc;
+  if (nks < 2 || nks > 8 || (long long)n * cin * 2 > 8192) return 0;
+  const SCGb gb{x, gn_stats, gn_gamma, gn_beta, gn_groups, parts, coef, dgamma, dbeta};
+  rc = conv_small_impl(1, dy, n, cout, d, h, w, wpk_dgrad, cin, nullptr, nullptr, nullptr, 0, nullptr, dx, ws,
+                       ws_bytes, cnt, nullptr, nullptr, &nks, stream, &gb);
+  if (rc == 0) *made = 1;
+  return rc;
 }

@@ -738,6 +738,21 @@ extern "C" int u3d_gn_bwd_parts(const void* da, const void* x, int n, int c, lon
   return check_launch("gn_bwd_parts");
 }
 
+// Round 5: the apply pass of the GroupNorm backward alone, from apply coefficients coef[n][5][c] a producer already
+// formed (u3d_conv_small_dgrad_gn: partials and finalize inside the data-gradient launch). bf16.
+extern "C" int u3d_gn_bwd_apply_coef(const void* da, const void* x, int n, int c, long long v, int groups,
+                                     const float* coef, void* dx, int accumulate, u3d_stream_t stream) {
+  U3D_REQUIRE(da && x && coef && dx && n >= 1 && groups > 0 && c % groups == 0, "gn_bwd_apply_coef: bad args");
+  U3D_REQUIRE(c % 8 == 0 && c <= 256, "gn_bwd_apply_coef: channels %d unsupported", c);
+  RedGeom g = make_geom(n, c, v, groups, 8);
+  const long long nvec = v * g.chn;
+  const int athr = GT / g.chn * g.chn;
+  const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + athr - 1) / athr);
+  hipLaunchKernelGGL(gn_bwd_apply<bf16>, dim3(ablk, n), dim3(athr), 0, (hipStream_t)stream, (const bf16*)da,
+                     (const bf16*)x, g, coef, (bf16*)dx, accumulate);
+  return check_launch("gn_bwd_apply_coef");
+}
+
 extern "C" int u3d_gn_apply(int dtype, const void* x, int n, int c, long long v, int groups, const float* stats,
                             const float* gamma, const float* beta, void* y, u3d_stream_t stream) {
   U3D_REQUIRE(dtype == U3D_F32 || dtype == U3D_BF16, "gn_apply: bad dtype");

@@ -55,6 +55,13 @@ class Engine(object):
         from u3d.ddp import U3DDataParallel
         return U3DDataParallel(model)
 
+    def graphed_train_step(self, step_fn, static_inputs=(), optimizer=None, warmup=3):
+        """Additive helper (the reference runs its step inline, train_amos_atlas_final.py:209-399): capture
+        ``step_fn`` (forward, loss, backward, optimizer step on the tensors in ``static_inputs``) once as a hipGraph,
+        data-parallel all-reduces included; calling the result with new batches replays it (u3d.graph.GraphedStep)."""
+        from u3d.graph import GraphedStep
+        return GraphedStep(step_fn, static_inputs, warmup=warmup, optimizer=optimizer)
+
     def get_train_loader(self, train_dataset, collate_fn=None):
         train_sampler = None
         is_shuffle = True

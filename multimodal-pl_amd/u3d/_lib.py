@@ -40,6 +40,12 @@ _SIGS = {
     "u3d_conv_small_cnt_bytes": [I, I, I, I, I],
     "u3d_conv_small_spart_floats": [I, I, I, I],
     "u3d_conv_small2": [I, P, I, I, I, I, I, P, I, P, P, P, I, P, P, P, L, P, P, P, P, P],
+    "u3d_conv_small_gb_parts_floats": [I, I, I, I, I],
+    "u3d_conv_small_dgrad_gn": [P, I, I, I, I, I, P, I, P, P, P, P, I, P, P, L, P, P, P, P, P, P, P],
+    "u3d_gn_bwd_apply_coef": [P, P, I, I, L, I, P, P, I, P],
+    "u3d_conv_s2_ring_ok": [I, I, I, I, I, I],
+    "u3d_conv_s2_ring_ws_floats": [I, I, I, I],
+    "u3d_conv_s2_ring": [P, I, I, I, I, P, P, P, P, I, P, P, P, P, P],
     "u3d_conv32_brick": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring_stats_ws_floats": [I],
@@ -123,7 +129,7 @@ _SIGS = {
     "u3d_aug_affine": [P, L, F, F, P],
     "u3d_aug_contrast": [P, L, F, P, I, P],
 }
-_RESTYPE = {"u3d_stem_fwd_ws_bytes": L, "u3d_stem1_stats_ws_floats": L, "u3d_conv_small_cnt_bytes": L, "u3d_conv_small_spart_floats": L, "u3d_upsample2x_stats_ws_floats": L, "u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
+_RESTYPE = {"u3d_stem_fwd_ws_bytes": L, "u3d_stem1_stats_ws_floats": L, "u3d_conv_small_cnt_bytes": L, "u3d_conv_small_spart_floats": L, "u3d_conv_small_gb_parts_floats": L, "u3d_conv_s2_ring_ws_floats": L, "u3d_upsample2x_stats_ws_floats": L, "u3d_wstd_bwd_scratch_bytes": L, "u3d_gn_workspace_bytes": L, "u3d_channel_sum_workspace_bytes": L, "u3d_loss_workspace_bytes": L,
             "u3d_eam_attn_bwd_part_floats": L, "u3d_upsample_trilinear_bwd_ws_floats": L, "u3d_renew_token_ws_bytes": L,
             "u3d_consistency_ws_bytes": L, "u3d_volume_stats_ws_bytes": L, "u3d_convg_brick_stats_ws_floats": L}
 

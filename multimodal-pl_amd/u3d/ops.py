@@ -315,6 +315,18 @@ def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
             fin = "u3d_conv32_ring_q_stats_finalize" if q else "u3d_conv32_ring_stats_finalize"
             call(fin, ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
         return y, stats
+    if (S2_RING and gn is not None and residual is None and k == 3 and stride == 2 and x.dtype == torch.bfloat16
+            and cin == 32 and cout == 64 and query("u3d_conv_s2_ring_ok", n, cin, d, h, w_, cout)):
+        # stride-2 forward as an input-plane walk, GN applied once per staged element, output statistics in-kernel
+        st, ga, be, G = gn
+        od, oh, ow = out_dim(d, 3, 2), out_dim(h, 3, 2), out_dim(w_, 3, 2)
+        y = torch.empty((n, od, oh, ow, cout), dtype=x.dtype, device=x.device)
+        stats = torch.empty((n, 16, 2), dtype=torch.float32, device=x.device)
+        sp = WS.get(4 * query("u3d_conv_s2_ring_ws_floats", n, d, h, w_), x.device, slot=S2_SPART_SLOT)
+        call("u3d_conv_s2_ring", x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(), be.data_ptr(),
+             G, y.data_ptr(), sp.data_ptr(), stats.data_ptr(), WS.get(256, x.device, slot=S2_CNT_SLOT).data_ptr(),
+             _stream())
+        return y, stats
     if (SMALL_FUSE and SMALL_STATS and cout in (64, 128, 256) and _use_small(x.dtype, cin, cout, k, stride, (n, d, h, w_))
             and not _use_conv1x1(x.dtype, cin, cout, k, n) and not _use_conv32(x.dtype, cin, cout, k, stride, n, w_)):
         y = torch.empty((n, d, h, w_, cout), dtype=x.dtype, device=x.device)
@@ -382,6 +394,10 @@ def _queue(device, shape):
 # no ring_gn_finalize / pbrick_gn_finalize launch); U3D_FUSED_FINALIZE=0: the separate finalize kernels
 FUSED_FINALIZE = os.environ.get("U3D_FUSED_FINALIZE", "1") != "0"
 RING_CNT_SLOT, BRICK_CNT_SLOT = 18, 19
+# the 96^3 stride-2 3^3 forward (cin 32 -> cout 64, GN prologue) as an input-plane walk (conv_s2.hip, round 5);
+# U3D_S2_RING=0: the implicit GEMM + a statistics pass
+S2_RING = os.environ.get("U3D_S2_RING", "1") != "0"
+S2_SPART_SLOT, S2_CNT_SLOT = 21, 22
 SMALL_STATS = os.environ.get("U3D_SMALL_STATS", "1") != "0"  # GN(16) stats of conv_small outputs from its combine
 BRICK_STATS = os.environ.get("U3D_BRICK_STATS", "1") != "0"  # GN statistics from the persistent brick's epilogue
 RING_STATS = os.environ.get("U3D_RING_STATS", "1") != "0"  # GroupNorm statistics from the ring conv epilogue (False: separate u3d_gn_stats pass)
@@ -445,13 +461,19 @@ def _use_gen_brick(dtype, cin, cout, k, stride, shape):
 GN_BWD_FUSED = os.environ.get("U3D_GN_BWD_FUSED", "1") != "0"  # GroupNorm-backward partials in the ring dgrad epilogue
 
 
-def conv_dgrad_gn(dy, wpk_dgrad, cin, x, k, stride, gn):
+def conv_dgrad_gn(dy, wpk_dgrad, cin, x, k, stride, gn, dgb=None):
     """Data gradient of conv(relu(gn(x))) with the GroupNorm backward's partial pass fused into the ring epilogue
     (u3d_conv32_ring_dgrad_gn): returns (dA, parts) for gn_bwd_parts, or None where the static 32-channel ring does
-    not run this conv (the caller then takes conv_dgrad + gn_bwd)."""
+    not run this conv (the caller then takes conv_dgrad + gn_bwd). On the small-volume kernel (and with ``dgb``, a
+    callable returning the (dgamma, dbeta) destinations) the finalize runs inside the launch too: parts is then
+    ("coef", coef) for gn_bwd_apply_coef, dgamma / dbeta already written."""
     n, d, h, w_ = x.shape[:4]
     if not (GN_BWD_FUSED and gn is not None and dy.shape[-1] == 32 and _use_conv32(dy.dtype, cin, 32, k, stride, n, w_)
             and CONV32_FN == "u3d_conv32_ring" and _conv32_fits(dy) and not _ring_queue(dgrad=True)):
+        if dgb is not None:
+            r = _conv_dgrad_gn_small(dy, wpk_dgrad, cin, x, k, stride, gn, dgb)
+            if r is not None:
+                return r
         return _conv_dgrad_gn_brick(dy, wpk_dgrad, cin, x, k, stride, gn)
     st, ga, be, G = gn
     wps = query("u3d_conv32_ring_wps", n, d, h, w_)
@@ -469,6 +491,50 @@ GN_BWD_FUSED_BRICK = os.environ.get("U3D_GN_BWD_FUSED_BRICK", "1") != "0"  # the
 # A/B (tools/kbench.py gnb*, gpurun_out/r04_g): 2x24^3 x 128 ch 51.4 -> 47.9 us for the data gradient + GN backward,
 # 2x48^3 x 64 ch 89.7 -> 92.5 us (the x loads and the epilogue sums outweigh the 56 MB partial pass there)
 GN_BWD_FUSED_BRICK_MAX_VOX = int(os.environ.get("U3D_GN_BWD_FUSED_BRICK_MAX_VOX", str(2 * 32 ** 3)))
+
+
+SMALL_GB = os.environ.get("U3D_SMALL_GB", "1") != "0"  # GN-backward partials + finalize in the small-volume dgrad
+
+
+def _conv_dgrad_gn_small(dy, wpk_dgrad, cin, x, k, stride, gn, dgb):
+    """conv_dgrad_gn where conv_dgrad would run the small-volume kernel (u3d_conv_small_dgrad_gn): the partial pass and
+    the coefficient finalize inside the data-gradient launch; returns (dA, ("coef", coef)) or None."""
+    shape = tuple(x.shape[:4])
+    n, d, h, w_ = shape
+    cout = dy.shape[-1]
+    if not (GN_BWD_FUSED and SMALL_GB and SMALL_FUSE and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+            and k == 3 and stride == 1 and _use_small(dy.dtype, cout, cin, k, stride, shape) and cin % 8 == 0
+            and n * cin * 2 <= 8192):
+        return None
+    st, ga, be, G = gn
+    dg, db = dgb()
+    da = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
+    coef = torch.empty((n, 5, cin), dtype=torch.float32, device=dy.device)
+    ws = WS.get(SPLITK_WS_BYTES, dy.device, slot=4)
+    cnt = WS.get(query("u3d_conv_small_cnt_bytes", n, d, h, w_, cin), dy.device, slot=SMALL_CNT_SLOT)
+    parts = WS.get(4 * query("u3d_conv_small_gb_parts_floats", n, d, h, w_, cin), dy.device, slot=SMALL_GB_SLOT)
+    made = ctypes.c_int(0)
+    call("u3d_conv_small_dgrad_gn", dy.data_ptr(), n, cout, d, h, w_, wpk_dgrad.data_ptr(), cin, x.data_ptr(),
+         st.data_ptr(), ga.data_ptr(), be.data_ptr(), G, da.data_ptr(), ws.data_ptr(), ws.numel(), cnt.data_ptr(),
+         parts.data_ptr(), coef.data_ptr(), _ptr(dg), _ptr(db), ctypes.addressof(made), _stream())
+    if not made.value:
+        return None
+    return da, ("coef", coef)
+
+
+SMALL_GB_SLOT = 20
+
+
+def gn_bwd_apply_coef(da, x, coef, groups, dx=None, accumulate=False):
+    """The apply pass of the GroupNorm backward from precomputed coefficients (u3d_conv_small_dgrad_gn)."""
+    n, c = x.shape[0], x.shape[-1]
+    v = x.numel() // (n * c)
+    if dx is None:
+        dx = torch.empty_like(x)
+        accumulate = False
+    call("u3d_gn_bwd_apply_coef", da.data_ptr(), x.data_ptr(), n, c, v, groups, coef.data_ptr(), dx.data_ptr(),
+         int(accumulate), _stream())
+    return dx
 
 
 def _conv_dgrad_gn_brick(dy, wpk_dgrad, cin, x, k, stride, gn):

@@ -182,7 +182,9 @@ class Tape:
                        and ops.s2_compact_ok(x.t.shape, cin, dyT.element_size()))
                 parts = None
                 if gn is not None and not head and pair != "park" and not (pair == "finish" and x.gn_pend):
-                    fused = ops.conv_dgrad_gn(dyT, pd, cin, x.t, k, stride, gn)  # GN-bwd partials in the epilogue
+                    fused = ops.conv_dgrad_gn(dyT, pd, cin, x.t, k, stride, gn,  # GN-bwd partials in the epilogue
+                                              dgb=lambda: (self.grad_out(gn_key + ".weight", gn[1]),
+                                                           self.grad_out(gn_key + ".bias", gn[2])))
                     if fused is not None:
                         dA, parts = fused
                 if parts is not None:
@@ -212,6 +214,11 @@ class Tape:
         return out
 
     def gn_bwd_one(self, x, dA, gn, gn_key, G, parts=None):
+        if isinstance(parts, tuple) and parts[0] == "coef":  # partials, finalize and dgamma / dbeta done in the dgrad
+            x.grad = ops.gn_bwd_apply_coef(dA, x.t, parts[1], G, dx=x.grad, accumulate=x.grad is not None)
+            self.grad_done(gn_key + ".weight")
+            self.grad_done(gn_key + ".bias")
+            return
         dg = self.grad_out(gn_key + ".weight", gn[1])
         db = self.grad_out(gn_key + ".bias", gn[2])
         if parts is not None:  # partial sums already taken by the data-gradient ring (ops.conv_dgrad_gn)

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 5: stride-2 ring forward + small-level GN-backward fusion: tests, step A/B, kernel trace of the default line.
+TAG=${1:-r05_c}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests/test_gpu_s2ring.py tests/test_gpu_gnfused_small.py tests/test_gpu_epi_stats.py tests/test_gpu_graph.py -x -v -s --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
+grep -E "PASS|FAIL|err" $O/pytest.log | cut -c1-200
+run() {  # run TAG ENV ARGS
+  local t=$1; shift; local e=$1; shift
+  env $e timeout -k 10 300 python bench.py --no-cpu --no-infer --no-roofline --no-mixed --steps 30 --warmup 5 "$@" > $O/bench_$t.log 2>&1 || { echo "bench $t failed"; grep -v "^frame" $O/bench_$t.log | tail -20; exit 1; }
+  grep '^{' $O/bench_$t.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$t', d['ms_per_step'], d['launch'], d.get('graph_error'))"
+}
+for i in 1 2 3; do
+  run s2off$i "U3D_S2_RING=0 U3D_SMALL_GB=0" || exit 1
+  run s2on$i "U3D_S2_RING=1 U3D_SMALL_GB=1" || exit 1
+done
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu --no-roofline --no-infer --no-mixed > $O/bench_kt.log 2>&1) || { echo "prof failed"; tail -20 $O/bench_kt.log; exit 1; }
+f=$(find $O/kt -name '*kernel_trace.csv' | head -1); [ -n "$f" ] && cp $(dirname $f)/*.csv $O/
+python3 tools/prof_summary.py $O 16 > $O/kernel_summary.txt 2>&1 || true
+head -30 $O/kernel_summary.txt
