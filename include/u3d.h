@@ -242,6 +242,13 @@ int u3d_conv32_ring_wps(int n, int d, int h, int w);
 int u3d_conv32_ring_dgrad_gn(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad, const void* x,
                              const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                              void* da, float* parts, u3d_stream_t stream);
+/* Round 5: u3d_conv32_ring_dgrad_gn with the GroupNorm-backward finalize inside the launch: its last-arriving workgroup
+ * writes the apply coefficients coef[n][5][32] and dgamma / dbeta[32] (as u3d_gn_bwd_parts' finalize would; fixed
+ * fp64 order); follow with u3d_gn_bwd_apply_coef. cnt: one ZEROED unsigned, left zeroed. */
+int u3d_conv32_ring_dgrad_gn_fused(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad, const void* x,
+                                   const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                                   void* da, float* parts, float* coef, float* dgamma, float* dbeta, unsigned* cnt,
+                                   u3d_stream_t stream);
 /* Stride-1 3^3 weight gradient, depth-streaming ring schedule (wgrad_ring.hip): same partial-slab contract as
  * u3d_conv_wgrad_brick ([nsplit][27][cout_p][cin_p] fp32, summed by the caller in fixed order); a split is a
  * contiguous range of 16x16-voxel output planes walked down d. */

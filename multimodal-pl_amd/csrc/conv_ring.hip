@@ -55,6 +55,7 @@ struct RGGeom {
   int sc, rmax;      // work-stealing mode: output planes per sub-chunk, sub-chunks per (full) range
   float* fstats;     // round 5: output GroupNorm(16) statistics finalized in-kernel (with fcnt; static forward only)
   unsigned* fcnt;    // zeroed arrival counter (left zeroed)
+  float *coef, *dgamma, *dbeta;  // round 5, data gradient + GN partials: the finalize in-kernel (with fcnt)
 };
 
 // One staged input plane: column (n, h0, w0), input depth zin (-1 / d = zero padding), and whether it is the
@@ -702,7 +703,79 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       float t = 0.f;
 #pragma unroll
       for (int wv = 0; wv < RG_NT / 64; ++wv) t += red[wv * 64 + tid];
-      spart[(long long)bid * 64 + tid] = t;  // [sample][wps][channel][2]: bid = sample * wps + jw
+      if (g.fcnt)  // write-through: the finalizing workgroup reads it in this launch
+        __hip_atomic_store(spart + (long long)bid * 64 + tid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        spart[(long long)bid * 64 + tid] = t;  // [sample][wps][channel][2]: bid = sample * wps + jw
+    }
+    if (g.fcnt) {
+      // Round 5: gn_bwd_parts_finalize by the workgroup that arrives last (one launch less): every wave drains, one lane
+      // per workgroup adds to the arrival counter, the last arriver sums the partial rows per (sample, channel) in fp64
+      // (8 lanes per pair strided over the sample's workgroups, then an xor tree in fixed order: deterministic) and
+      // forms the apply coefficients coef[n][5][32] and dgamma / dbeta exactly as gn_bwd_coefs does.
+      __shared__ unsigned s_last;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(g.fcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == gridDim.x - 1;
+        if (s_last) __hip_atomic_store(g.fcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (!s_last) return;
+      double* const cs = reinterpret_cast<double*>(ring);  // [n * 32][2]
+      const int l8 = tid & 7;
+      for (int p0 = 0; p0 < g.n * 32; p0 += RG_NT / 8) {
+        const int pr = p0 + (tid >> 3);
+        double s1 = 0, s2 = 0;
+        if (pr < g.n * 32) {
+          const int nn = pr >> 5, c = pr & 31;
+          for (int wk = l8; wk < g.wps; wk += 8) {
+            const float* qq = spart + ((long long)nn * g.wps + wk) * 64 + c * 2;
+            s1 += __hip_atomic_load(qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s2 += __hip_atomic_load(qq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+#pragma unroll
+        for (int o = 4; o > 0; o >>= 1) {
+          s1 += __shfl_xor(s1, o);
+          s2 += __shfl_xor(s2, o);
+        }
+        if (pr < g.n * 32 && l8 == 0) {
+          cs[2 * pr] = s1;
+          cs[2 * pr + 1] = s2;
+        }
+      }
+      __syncthreads();
+      const int gcpg = 32 / g.gn_groups;
+      const double M = (double)g.d * g.h * g.w * gcpg;
+      for (int pr = tid; pr < g.n * 32; pr += RG_NT) {
+        const int nn = pr >> 5, c = pr & 31, gr = c / gcpg;
+        double a = 0, bb = 0;
+        for (int k2 = 0; k2 < gcpg; ++k2) {
+          const int cc = gr * gcpg + k2;
+          a += (double)gamma[cc] * cs[2 * (nn * 32 + cc)];
+          bb += (double)gamma[cc] * cs[2 * (nn * 32 + cc) + 1];
+        }
+        const float ca = (float)(a / M), cb = (float)(bb / M);
+        const float mu = gstat[(nn * g.gn_groups + gr) * 2], rs = gstat[(nn * g.gn_groups + gr) * 2 + 1];
+        const float scv = rs * gamma[c];
+        float* oc = g.coef + (long long)nn * 5 * 32;
+        oc[c] = scv;
+        oc[32 + c] = beta[c] - mu * scv;
+        oc[64 + c] = rs * gamma[c];
+        oc[96 + c] = -rs * rs * cb;
+        oc[128 + c] = -rs * ca + rs * rs * cb * mu;
+      }
+      if (tid < 32) {
+        double tg = 0, tb = 0;
+        for (int nn = 0; nn < g.n; ++nn) {
+          tb += cs[2 * (nn * 32 + tid)];
+          tg += cs[2 * (nn * 32 + tid) + 1];
+        }
+        if (g.dgamma) g.dgamma[tid] = (float)tg;
+        if (g.dbeta) g.dbeta[tid] = (float)tb;
+      }
     }
   } else if constexpr (GN) {
     if (spart == nullptr) return;
@@ -1010,10 +1083,35 @@ extern "C" int u3d_conv32_ring_wps(int n, int d, int h, int w) {
   return (int)((pps + per - 1) / per);
 }
 
+static int ring_dgrad_gn_impl(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad, const void* x,
+                              const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                              void* da, float* parts, float* coef, float* dgamma, float* dbeta, unsigned* cnt,
+                              u3d_stream_t stream);
+
 extern "C" int u3d_conv32_ring_dgrad_gn(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad,
                                         const void* x, const float* gn_stats, const float* gn_gamma,
                                         const float* gn_beta, int gn_groups, void* da, float* parts,
                                         u3d_stream_t stream) {
+  return ring_dgrad_gn_impl(dy, n, d, h, w, wpk_dgrad, x, gn_stats, gn_gamma, gn_beta, gn_groups, da, parts, nullptr,
+                            nullptr, nullptr, nullptr, stream);
+}
+
+// Round 5: u3d_conv32_ring_dgrad_gn with the GroupNorm-backward finalize inside the launch (its last-arriving workgroup
+// writes coef[n][5][32] and dgamma / dbeta[32] as u3d_gn_bwd_parts' finalize would); follow with u3d_gn_bwd_apply_coef.
+// cnt: one ZEROED unsigned, left zeroed.
+extern "C" int u3d_conv32_ring_dgrad_gn_fused(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad,
+                                              const void* x, const float* gn_stats, const float* gn_gamma,
+                                              const float* gn_beta, int gn_groups, void* da, float* parts, float* coef,
+                                              float* dgamma, float* dbeta, unsigned* cnt, u3d_stream_t stream) {
+  U3D_REQUIRE(coef && cnt && n * 32 * 2 * 8 <= 4 * RG_SS, "conv32_ring_dgrad_gn_fused: bad args");
+  return ring_dgrad_gn_impl(dy, n, d, h, w, wpk_dgrad, x, gn_stats, gn_gamma, gn_beta, gn_groups, da, parts, coef,
+                            dgamma, dbeta, cnt, stream);
+}
+
+static int ring_dgrad_gn_impl(const void* dy, int n, int d, int h, int w, const void* wpk_dgrad, const void* x,
+                              const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
+                              void* da, float* parts, float* coef, float* dgamma, float* dbeta, unsigned* cnt,
+                              u3d_stream_t stream) {
   U3D_REQUIRE(dy && wpk_dgrad && x && da && parts && n >= 1 && d >= 1 && h >= 1 && w >= 1,
               "conv32_ring_dgrad_gn: bad args");
   U3D_REQUIRE(gn_stats && gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0, "conv32_ring_dgrad_gn: bad GN");
@@ -1029,6 +1127,12 @@ extern "C" int u3d_conv32_ring_dgrad_gn(const void* dy, int n, int d, int h, int
   g.per = (int)((g.pps + wps0 - 1) / wps0);
   g.wps = (int)((g.pps + g.per - 1) / g.per);
   g.gn_groups = gn_groups;
+  if (cnt) {
+    g.fcnt = cnt;
+    g.coef = coef;
+    g.dgamma = dgamma;
+    g.dbeta = dbeta;
+  }
   const long long grid = (long long)n * g.wps;
   const bool kr = ring_kr(1) != 0;
 #define RG_GB(K)                                                                                               \

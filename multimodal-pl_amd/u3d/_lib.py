@@ -44,6 +44,7 @@ _SIGS = {
     "u3d_conv_small_dgrad_gn": [P, I, I, I, I, I, P, I, P, P, P, P, I, P, P, L, P, P, P, P, P, P, P],
     "u3d_gn_bwd_apply_coef": [P, P, I, I, L, I, P, P, I, P],
     "u3d_conv_s2_ring_ok": [I, I, I, I, I, I],
+    "u3d_conv32_ring_dgrad_gn_fused": [P, I, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, P],
     "u3d_conv_s2_ring_ws_floats": [I, I, I, I],
     "u3d_conv_s2_ring": [P, I, I, I, I, P, P, P, P, I, P, P, P, P, P],
     "u3d_conv32_brick": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],

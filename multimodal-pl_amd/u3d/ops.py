@@ -393,7 +393,7 @@ def _queue(device, shape):
 # the ring / persistent-brick conv epilogue statistics finalized by the conv launch's last-arriving workgroup (round 5:
 # no ring_gn_finalize / pbrick_gn_finalize launch); U3D_FUSED_FINALIZE=0: the separate finalize kernels
 FUSED_FINALIZE = os.environ.get("U3D_FUSED_FINALIZE", "1") != "0"
-RING_CNT_SLOT, BRICK_CNT_SLOT = 18, 19
+RING_CNT_SLOT, BRICK_CNT_SLOT, RING_GB_CNT_SLOT = 18, 19, 23
 # the 96^3 stride-2 3^3 forward (cin 32 -> cout 64, GN prologue) as an input-plane walk (conv_s2.hip, round 5);
 # U3D_S2_RING=0: the implicit GEMM + a statistics pass
 S2_RING = os.environ.get("U3D_S2_RING", "1") != "0"
@@ -480,6 +480,14 @@ def conv_dgrad_gn(dy, wpk_dgrad, cin, x, k, stride, gn, dgb=None):
     da = torch.empty((n, d, h, w_, cin), dtype=dy.dtype, device=dy.device)
     parts = torch.empty((n, wps, 32, 2), dtype=torch.float32, device=dy.device)
     pr = _probe0()
+    if FUSED_FINALIZE and dgb is not None:  # the finalize by the launch's last-arriving workgroup (round 5)
+        dg, db = dgb()
+        coef = torch.empty((n, 5, 32), dtype=torch.float32, device=dy.device)
+        call("u3d_conv32_ring_dgrad_gn_fused", dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), x.data_ptr(),
+             st.data_ptr(), ga.data_ptr(), be.data_ptr(), G, da.data_ptr(), parts.data_ptr(), coef.data_ptr(), _ptr(dg),
+             _ptr(db), WS.get(256, dy.device, slot=RING_GB_CNT_SLOT).data_ptr(), _stream())
+        _probe1(pr, "conv32_ring dgrad +GN-bwd partials", 2.0 * n * d * h * w_ * 27 * 32 * 32, n * d * h * w_)
+        return da, ("coef", coef)
     call("u3d_conv32_ring_dgrad_gn", dy.data_ptr(), n, d, h, w_, wpk_dgrad.data_ptr(), x.data_ptr(), st.data_ptr(),
          ga.data_ptr(), be.data_ptr(), G, da.data_ptr(), parts.data_ptr(), _stream())
     _probe1(pr, "conv32_ring dgrad +GN-bwd partials", 2.0 * n * d * h * w_ * 27 * 32 * 32, n * d * h * w_)

@@ -86,3 +86,32 @@ def test_fused_path_not_taken_under_collective(gpu):
         assert ops.conv_dgrad_gn(dy, pd, 32, x, 3, 1, gn) is None
     finally:
         ops.COLLECTIVE_IN_FLIGHT[0] = False
+
+
+@pytest.mark.parametrize("case", CASES[:3] + [(2, 96, 96, 96, 16)], ids=lambda c: "x".join(map(str, c[:4])) + f"_g{c[4]}")
+def test_fused_finalize_in_ring(gpu, case):
+    """Round 5: the finalize in the ring launch (its last-arriving workgroup writes coef / dgamma / dbeta;
+    u3d_conv32_ring_dgrad_gn_fused + u3d_gn_bwd_apply_coef) against the separate form: dA bitwise, dgamma / dbeta
+    rel <= 2e-5, dx rel <= 2e-3; two runs bitwise equal (and the arrival counter left at zero)."""
+    from u3d import ops
+    if not ops.FUSED_FINALIZE:
+        pytest.skip("U3D_FUSED_FINALIZE=0")
+    x, dy, pd, gn = _setup(gpu, *case)
+    a_da, a_dx, a_dg, a_db = _separate(x, dy, pd, gn)
+    outs = []
+    for _ in range(2):
+        dg, db = torch.full((32,), 5.0, device=gpu), torch.full((32,), 5.0, device=gpu)  # overwritten
+        r = ops.conv_dgrad_gn(dy, pd, 32, x, 3, 1, gn, dgb=lambda: (dg, db))
+        assert r is not None and isinstance(r[1], tuple) and r[1][0] == "coef", "the fused ring finalize did not run"
+        dx = ops.gn_bwd_apply_coef(r[0], x, r[1][1], gn[3])
+        outs.append((r[0], dx, dg, db, r[1][1]))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], a_da)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    _, dx, dg, db, _ = outs[0]
+    for a, b in ((a_dg, dg), (a_db, db)):
+        err = ((a - b).norm() / a.norm().clamp_min(1e-12)).item()
+        assert err < 2e-5, err
+    err = ((a_dx.float() - dx.float()).norm() / a_dx.float().norm()).item()
+    assert err < 2e-3, err
