@@ -82,7 +82,7 @@ def synthetic(batch, patch, device, seed, modality="ct"):
 # the ring kernels the bench probes at the full patch, their committed-profile tag (profiles/rNN_pmc_<tag>.json) and the
 # substring of their rocprofv3 kernel name + grid in profiles/rNN_kernel_summary.txt (tools/prof_summary.py)
 RING_TAGS = {
-    "wgrad_ring 32->32 GN": ("wgrad96", ("wgrad_ring_dma_kernel<true>', 1, '1', '256'",  # U3D_WR_DMA=1 (default)
+    "wgrad_ring 32->32 GN": ("wgrad96", ("wgrad_ring_dma_kernel<true>', 1, '1', '256'",  # the 16 x 16-tile ring (LDS-DMA staging)
                                          "wgrad_ring_kernel<true, 16, 16>', 1, '1', '256'")),
     "conv32_ring dgrad +GN-bwd partials": ("dgrad96gn", "conv32_ring_kernel<true, true, false, 8, false>', 256"),
     "conv32_ring fwd GN +res +stats": ("fwd96", "conv32_ring_kernel<false, true, true, 12, false>', 256"),

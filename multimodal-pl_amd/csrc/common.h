@@ -40,7 +40,6 @@ enum Opt : int {
   OPT_WR_TILE16,      // 1: 16 x 16 weight-gradient ring tiles everywhere
   OPT_WR_WGS,         // weight-gradient ring workgroups aimed at
   OPT_WB_S2CO64,      // stride-2 brick weight gradient: two co tiles per workgroup (0: one)
-  OPT_WR_DMA,         // 16 x 16-tile weight-gradient ring with LDS-DMA staging (0: register staging)
   OPT_IGEMM_BM,       // bf16 implicit GEMM M tile: 0 auto (256 for large unsplit BN 64 launches), 128 / 256 force
   OPT_WSTD_ROW,       // weight-standardisation backward: one row per block from registers (0: chunked LDS kernel)
   OPT_UP_QUAD,        // bf16 trilinear x2 upsample: 2 x 2 outputs per thread from 18 loads (0: one output, 8 loads)
@@ -286,21 +285,6 @@ __device__ __forceinline__ TileSplit xcd_tile_split() {
   const int tile = N % nt;
   return TileSplit{tile % (int)gridDim.x, tile / (int)gridDim.x, N / nt};
 }
-
-// ------------------------------------------------------------------ diagnostic in-kernel stamps (never in the product)
-// A -DU3D_STAMPS build (tools/build_variant.sh) lets a kernel record s_memtime / s_memrealtime stamps and per-phase cycle
-// sums into a buffer of its own (a __device__ array of its translation unit, read back with u3d_diag_*_stamps): the
-// clock the chip holds inside the kernel (MI355X_MICROARCH.md, DVFS item 6) and where a persistent walk spends its
-// cycles. Nothing else reads the buffer and no output depends on it.
-#ifdef U3D_STAMPS
-__device__ __forceinline__ unsigned long long stamp_clk() {
-  __builtin_amdgcn_sched_barrier(0);
-  const unsigned long long t = __builtin_amdgcn_s_memtime();
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-__device__ __forceinline__ unsigned long long stamp_real() { return __builtin_amdgcn_s_memrealtime(); }
-#endif
 
 __host__ __device__ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 __host__ __device__ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }

@@ -19,6 +19,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "diag.h"
 
 namespace u3d {
 
@@ -37,11 +38,9 @@ constexpr int RG_NWR = 27 * 32;                      // weight rows (t, co)
 #ifndef RG_HOIST
 #define RG_HOIST 1
 #endif
-#ifdef U3D_STAMPS
-// [workgroup][wave][8]: t0, t1 (s_memtime), r0, r1 (s_memrealtime), cycles in the compute steps (MFMAs + the staging
-// side work between them), in steps without compute, in the barriers, steps | compute steps << 32
-__device__ unsigned long long rg_stamps[2048 * 8 * 8];
-#endif
+// -DU3D_STAMPS phases (diag.h): 0 compute steps (MFMAs + the staging side work between them), 1 steps without compute,
+// 2 the barriers
+U3D_STAMP_BUFFER(rg_stamps, 2048, u3d_diag_ring_stamps)
 
 struct RGGeom {
   int n, d, h, w;
@@ -131,10 +130,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   char* const wts = smem + 4 * RG_SS;
   char* const junk = wts + 4 * RG_NWR * 16;  // target of the staging lanes past the plane's last row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#ifdef U3D_PRIO
-  // diagnostic: static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
+  diag_prio_second_half(wave);
   // staging: fixed 8-channel chunk (plane) per thread, 8 threads = 8 consecutive rows of one plane (a wave covers 16
   // whole rows = 1 KB of contiguous voxels per load)
   const int ch = (tid >> 3) & 3;
@@ -574,10 +570,8 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
     return p;
   };
-#ifdef U3D_STAMPS
-  const unsigned long long st_t0 = stamp_clk(), st_r0 = stamp_real();
-  unsigned long long st_c = 0, st_s = 0, st_b = 0, st_n = 0;
-#endif
+  PhaseStamps ps;
+  ps.begin();
   RGPlane pw = next_plane();  // plane 0
   load_plane(pw, va, ma);
   __syncthreads();            // weights visible
@@ -626,26 +620,16 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         }
       }
     };
-#ifdef U3D_STAMPS
-    const unsigned long long a0 = stamp_clk();
-#endif
+    ps.mark_now();
     if (pc.valid && pc.out) {
       compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 0>{}, side);
     } else {
       static_for<0, 2 * RG_LD>(side);
     }
-#ifdef U3D_STAMPS
-    const unsigned long long a1 = stamp_clk();
-    if (pc.valid && pc.out)
-      st_c += a1 - a0;
-    else
-      st_s += a1 - a0;
-    st_n += 1ull + ((pc.valid && pc.out) ? (1ull << 32) : 0ull);
-#endif
+    ps.lap((pc.valid && pc.out) ? 0 : 1);
+    ps.step(pc.valid && pc.out);
     __syncthreads();
-#ifdef U3D_STAMPS
-    st_b += stamp_clk() - a1;
-#endif
+    ps.lap(2);
     pc = pw;
     pw = pl;
     ++s;
@@ -656,15 +640,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     step(vb, mb, va, ma);
   }
   epilogue(pend);  // the last computed plane (ok = false if none)
-#ifdef U3D_STAMPS
-  if (!Q) {
-    const unsigned long long t1 = stamp_clk(), r1 = stamp_real();
-    if (lane == 0) {
-      unsigned long long* o = rg_stamps + ((long long)(blockIdx.x & 2047) * 8 + wave) * 8;
-      o[0] = st_t0; o[1] = t1; o[2] = st_r0; o[3] = r1; o[4] = st_c; o[5] = st_s; o[6] = st_b; o[7] = st_n;
-    }
-  }
-#endif
+  if (!Q) ps.end(rg_stamps, blockIdx.x & 2047, wave, lane);
   if constexpr (Q) {
     if constexpr (PRO) {
       if (spart != nullptr && acc_chunk >= 0) flush(acc_chunk);
@@ -965,12 +941,6 @@ static void ring_q_geom(int n, int d, int h, int w, RGGeom& g, bool stats = fals
   g.rmax = (g.per + g.sc - 1) / g.sc;
 }
 
-#ifdef U3D_STAMPS
-extern "C" int u3d_diag_ring_stamps(void* out, long long nbytes) {
-  U3D_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(u3d::rg_stamps), std::min<long long>(nbytes, sizeof(u3d::rg_stamps))));
-  return 0;
-}
-#endif
 
 extern "C" int u3d_conv32_ring_q_stats_ws_floats(int n, int d, int h, int w) {
   RGGeom g;

@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "diag.h"
 
 namespace u3d {
 namespace {
@@ -117,11 +118,8 @@ struct WRWalk {
   }
 };
 
-#ifdef U3D_STAMPS
-// [workgroup][wave][8]: t0, t1 (s_memtime), r0, r1 (s_memrealtime), cycles in write (incl. the staged loads' wait),
-// in compute, in the barrier, steps | compute steps << 32
-__device__ unsigned long long wr_stamps[4096 * 8 * 8];
-#endif
+// -DU3D_STAMPS phases (diag.h): 0 the staged plane's write (incl. its loads' wait), 1 compute, 2 the barrier
+U3D_STAMP_BUFFER(wr_stamps, 4096, u3d_diag_wgrad_stamps)
 }  // namespace
 
 template <bool GN, int PH = 16, int PW = 16>
@@ -140,9 +138,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
   char* const junk = dyr + 2 * WR_DSLOT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = tid & 3;
-#ifdef U3D_PRIO
-  if (__builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);  // diagnostic (see conv_ring.hip)
-#endif
+  diag_prio_second_half(wave);
   const TileSplit ts = xcd_tile_split();  // XCD-aware: the channel tiles of neighbouring plane ranges share an L2
   const int ci0 = ts.tx * 32, co0 = ts.ty * 32, split = ts.split;
   WRWalk walk{};
@@ -378,47 +374,31 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
 
   u32x4 xa[WR_LX], xb[WR_LX], ya[WR_LY], yb[WR_LY];
   unsigned ma = 0, mb = 0;
-#ifdef U3D_STAMPS
-  const unsigned long long st_t0 = stamp_clk(), st_r0 = stamp_real();
-  unsigned long long st_w = 0, st_c = 0, st_b = 0, st_n = 0;
-#endif
+  PhaseStamps ps;
+  ps.begin();
   WRPlane pw = walk.next(g);
   load_plane(pw, xa, ya, ma);
   WRPlane pc{};
   int s = 0;
   auto step = [&](u32x4 (&cx)[WR_LX], u32x4 (&cy)[WR_LY], unsigned& mc, u32x4 (&nx)[WR_LX], u32x4 (&ny)[WR_LY],
                   unsigned& mn) {
-#ifdef U3D_STAMPS
-    const unsigned long long a0 = stamp_clk();
-#endif
+    ps.mark_now();
     if (pw.valid) write_plane(pw, cx, cy, mc, s & 3, s & 1);
-#ifdef U3D_STAMPS
-    if (pw.valid) {  // the staged loads' wait (vmcnt) lands before the ds_writes
-      __builtin_amdgcn_s_waitcnt(0);
-    }
-    const unsigned long long a1 = stamp_clk();
-    st_w += a1 - a0;
-#endif
+    ps.settle(pw.valid);  // the staged loads' wait (vmcnt) lands before the ds_writes
+    ps.lap(0);
     const WRPlane pl = walk.next(g);
     load_plane(pl, nx, ny, mn);
-#ifdef U3D_STAMPS
-    const unsigned long long a2 = stamp_clk();
-    st_n += 1ull + ((pc.valid && pc.out) ? (1ull << 32) : 0ull);
-#endif
+    ps.mark_now();
+    ps.step(pc.valid && pc.out);
     if (pc.valid && pc.out) {
       if (ntap == 4)
         compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 4>{});
       else
         compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 3>{});
     }
-#ifdef U3D_STAMPS
-    const unsigned long long a3 = stamp_clk();
-    st_c += a3 - a2;
-#endif
+    ps.lap(1);
     __syncthreads();
-#ifdef U3D_STAMPS
-    st_b += stamp_clk() - a3;
-#endif
+    ps.lap(2);
     pc = pw;
     pw = pl;
     ++s;
@@ -428,16 +408,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     if (!(pw.valid || (pc.valid && pc.out))) break;
     step(xb, yb, mb, xa, ya, ma);
   }
-#ifdef U3D_STAMPS
-  {
-    const unsigned long long t1 = stamp_clk(), r1 = stamp_real();
-    const int wg = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & 4095;
-    if (lane == 0) {
-      unsigned long long* o = wr_stamps + ((long long)wg * 8 + wave) * 8;
-      o[0] = st_t0; o[1] = t1; o[2] = st_r0; o[3] = r1; o[4] = st_w; o[5] = st_c; o[6] = st_b; o[7] = st_n;
-    }
-  }
-#endif
+  ps.end(wr_stamps, (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & 4095, wave, lane);
   // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h. Buffer stores with 32-bit
   // offsets computed here (the host keeps the slabs below 2 GiB): no 64-bit addresses held across the walk.
   int t0 = tid;
@@ -708,10 +679,8 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
     });
   };
 
-#ifdef U3D_STAMPS
-  const unsigned long long st_t0 = stamp_clk(), st_r0 = stamp_real();
-  unsigned long long st_w = 0, st_c = 0, st_b = 0, st_n = 0;
-#endif
+  PhaseStamps ps;
+  ps.begin();
   // plane counter s: plane s sits in x slot s % 5 / dy slot s % 3 (DMA'd during step s-1, transformed at step s)
   unsigned ma = 0, mb = 0;  // row masks of the planes in flight (rotating)
   WRPlane pw = walk.next(g);  // plane 0
@@ -743,10 +712,8 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
         if constexpr (GN) xform_x(u - 6, x5, mcur);
       }
     };
-#ifdef U3D_STAMPS
-    const unsigned long long a2 = stamp_clk();
-    st_n += 1ull + ((pc.valid && pc.out) ? (1ull << 32) : 0ull);
-#endif
+    ps.mark_now();
+    ps.step(pc.valid && pc.out);
     if (pc.valid && pc.out) {
       const int s0 = x5 >= 3 ? x5 - 3 : x5 + 2, dsc = d3 == 0 ? 2 : d3 - 1;  // planes s-3.. / dy of plane s-1
       if (ntap == 4)
@@ -756,14 +723,9 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
     } else {
       sfor<0, 2 * KS2>([&](auto uc) { side(uc); });
     }
-#ifdef U3D_STAMPS
-    const unsigned long long a3 = stamp_clk();
-    st_c += a3 - a2;
-#endif
+    ps.lap(1);
     bar();
-#ifdef U3D_STAMPS
-    st_b += stamp_clk() - a3;
-#endif
+    ps.lap(2);
     pc = pw;
     pw = pl;
     x5 = xn;
@@ -775,16 +737,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
     step(mb, ma);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup's LDS is released
-#ifdef U3D_STAMPS
-  {
-    const unsigned long long t1 = stamp_clk(), r1 = stamp_real();
-    const int wg = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & 4095;
-    if (lane == 0) {
-      unsigned long long* o = wr_stamps + ((long long)wg * 8 + wave) * 8;
-      o[0] = st_t0; o[1] = t1; o[2] = st_r0; o[3] = r1; o[4] = st_w; o[5] = st_c; o[6] = st_b; o[7] = st_n;
-    }
-  }
-#endif
+  ps.end(wr_stamps, (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & 4095, wave, lane);
   int t0 = tid;
   asm volatile("" : "+v"(t0));
   const int w8 = t0 >> 6;
@@ -828,12 +781,6 @@ static void wr_geom(int n, int cin, int d, int h, int w, int cout, WRGeom& g) {
   g.ybytes = (long long)n * d * h * w * cout * 2;
 }
 
-#ifdef U3D_STAMPS
-extern "C" int u3d_diag_wgrad_stamps(void* out, long long nbytes) {
-  U3D_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(wr_stamps), std::min<long long>(nbytes, sizeof(wr_stamps))));
-  return 0;
-}
-#endif
 
 extern "C" int u3d_conv_wgrad_ring_splits_target(int n, int cin, int d, int h, int w, int cout, int wgs) {
   WRGeom g;
@@ -876,15 +823,13 @@ extern "C" int u3d_conv_wgrad_ring(const void* dy, const void* x, int n, int cin
     if (gn) U3D_WR(true, 12, 24); else U3D_WR(false, 12, 24);
   } else if (g.pw == 12) {
     if (gn) U3D_WR(true, 12, 12); else U3D_WR(false, 12, 12);
-  } else if (opt(OPT_WR_DMA) != 0) {  // 16 x 16 tiles: LDS-DMA staging (round 4)
+  } else {  // 16 x 16 tiles: LDS-DMA staging (round 4; the register-staged 16 x 16 form was dropped in round 5)
     if (gn)
       hipLaunchKernelGGL((wgrad_ring_dma_kernel<true>), grid, dim3(WR_NT), 0, s, (const bf16*)dy, (const bf16*)x,
                          gn_stats, gn_gamma, gn_beta, partials, g);
     else
       hipLaunchKernelGGL((wgrad_ring_dma_kernel<false>), grid, dim3(WR_NT), 0, s, (const bf16*)dy, (const bf16*)x,
                          gn_stats, gn_gamma, gn_beta, partials, g);
-  } else {
-    if (gn) U3D_WR(true, 16, 16); else U3D_WR(false, 16, 16);
   }
 #undef U3D_WR
   return check_launch("wgrad_ring_kernel");

@@ -1,10 +1,10 @@
-"""The 16 x 16-tile weight-gradient ring with LDS-DMA staging (wgrad_ring.hip, wgrad_ring_dma_kernel; option WR_DMA) against
-the register-staged ring it replaces (WR_DMA = 0) and against fp64. Same walk, same tap assignment, same MFMA order:
-the partial slabs must be BITWISE equal; the summed gradient is checked against fp64 on the same bf16 operands.
-Cases: the bench levels (2 x 96^3 x 32, 2 x 48^3 x 64), partial plane tiles (h, w not multiples of 16: rows past the
-volume come from out-of-range DMAs), several channel tiles, odd depths and sample counts, GroupNorm prologue on and off
-(the off form has no in-place transform; its padding rows are the DMA's zero fill). Reference: autograd of F.conv3d in
-Conv3d.forward (unet3D.py:27)."""
+"""The 16 x 16-tile weight-gradient ring with LDS-DMA staging (wgrad_ring.hip, wgrad_ring_dma_kernel — since round 5
+the only 16 x 16 form) against the halo-brick weight gradient (the other stride-1 kernel, a different tiling and
+summation order: fp32 sums of the same bf16 products) and against fp64 on the same bf16 operands; two runs bitwise
+equal. Cases: the bench levels (2 x 96^3 x 32, 2 x 48^3 x 64), partial plane tiles (h, w not multiples of 16: rows
+past the volume come from out-of-range DMAs), several channel tiles, odd depths and sample counts, GroupNorm prologue
+on and off (the off form has no in-place transform; its padding rows are the DMA's zero fill). Reference: autograd of
+F.conv3d in Conv3d.forward (unet3D.py:27)."""
 import pytest
 import torch
 
@@ -18,24 +18,23 @@ CASES = [(2, 32, 32, (96, 96, 96), True), (2, 64, 64, (48, 48, 48), True), (1, 3
 
 
 @pytest.mark.parametrize("n,cin,cout,dims,use_gn", CASES, ids=lambda v: str(v))
-def test_wgrad_dma_ring_bitwise_vs_register_ring(gpu, n, cin, cout, dims, use_gn):
+def test_wgrad_dma_ring_vs_brick_and_fp64(gpu, n, cin, cout, dims, use_gn):
     from u3d import ops
     x, _, gn = _operands(gpu, n, cin, cout, dims, 41)
     gn = gn if use_gn else None
     dy = (torch.randn((n,) + dims + (cout,), device=gpu) * 0.7).to(torch.bfloat16)
     with ops.option("WR_TILE16", 1):
-        with ops.option("WR_DMA", 0):
-            p_reg, ns_reg = ops.conv_wgrad(dy, x, 3, 1, gn, brick="ring")
-        with ops.option("WR_DMA", 1):
-            p_dma, ns_dma = ops.conv_wgrad(dy, x, 3, 1, gn, brick="ring")
-            p_dma2, _ = ops.conv_wgrad(dy, x, 3, 1, gn, brick="ring")
+        p_dma, _ = ops.conv_wgrad(dy, x, 3, 1, gn, brick="ring")
+        p_dma2, _ = ops.conv_wgrad(dy, x, 3, 1, gn, brick="ring")
+    p_brk, _ = ops.conv_wgrad(dy, x, 3, 1, gn, brick=True)
     torch.cuda.synchronize()
-    assert ns_reg == ns_dma
     assert torch.equal(p_dma, p_dma2), "DMA ring not deterministic"
-    assert torch.equal(p_dma, p_reg), f"max |diff| {(p_dma - p_reg).abs().max().item():.3e}"
+    dw = p_dma.sum(0).double()[:, :cout, :cin]
+    db = p_brk.sum(0).double()[:, :cout, :cin]
+    err = ((dw - db).norm() / db.norm()).item()
+    assert err <= 5e-4, err  # fp32 reassociation (and the GN prologue's bf16 roundings, computed in another order)
     if max(dims) <= 48:
-        dw = p_dma.sum(0).cpu().double()[:, :cout, :cin]
         a = _act(x, gn, torch.float64) if gn is not None else _bf(x.cpu()).permute(0, 4, 1, 2, 3)
         ref = torch.nn.grad.conv3d_weight(a, (cout, cin, 3, 3, 3), _bf(dy.cpu()).permute(0, 4, 1, 2, 3), padding=1)
         ref = ref.reshape(cout, cin, 27).permute(2, 0, 1)
-        assert ((dw - ref).norm() / ref.norm()).item() <= 1e-3
+        assert ((dw.cpu() - ref).norm() / ref.norm()).item() <= 1e-3

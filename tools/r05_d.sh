@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-timeout -k 10 500 python -u -m pytest tests/test_gpu_epi_stats.py tests/test_gpu_gnfused_small.py tests/test_gpu_s2ring.py tests/test_gpu_graph.py tests/test_gpu_ddp.py tests/test_gpu_gnfused_brick.py tests/test_gpu_gnfused.py -v -s --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_epi_stats.py tests/test_gpu_gnfused_small.py tests/test_gpu_s2ring.py tests/test_gpu_graph.py tests/test_gpu_ddp.py tests/test_gpu_gnfused_brick.py tests/test_gpu_gnfused.py tests/test_gpu_wgrad_dma.py -v -s --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|ERROR|err |bitwise" $O/pytest.log | cut -c1-220
 [ $rc -eq 0 ] || { grep -E "^E |Error" $O/pytest.log | head -40; exit 1; }
