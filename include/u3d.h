@@ -85,6 +85,10 @@ int u3d_wstd_fwd_batch(int dtype, const u3d_wstd_desc* descs, int count, u3d_str
 /* scratch: device fp32 buffer of u3d_wstd_bwd_scratch_bytes(descs, count) bytes (per-row sums) */
 long long u3d_wstd_bwd_scratch_bytes(const u3d_wstd_desc* descs, int count);
 int u3d_wstd_bwd_batch(const u3d_wstd_desc* descs, int count, float* scratch, u3d_stream_t stream);
+/* Round 5: slab 0 <- the sum of slabs 0..nsplit-1 of ONE weight gradient's partials [nsplit][k3][cout_p][cin_p]
+ * (the sum u3d_wstd_bwd_batch runs, same order, bitwise equal), launched right after the weight-gradient kernel so the
+ * slabs are re-read from cache; pass nsplit = 1 to the standardisation backward afterwards. */
+int u3d_wgrad_sum_slabs(float* part, int nsplit, int k3, int cout, int cin, u3d_stream_t stream);
 
 /* ---------------------------------------------------------------- 3-D convolution (A1-A3, A7)
  * F.conv3d(relu(group_norm(x)), W_hat, bias, stride, pad=k//2) (unet3D.py:27, 44-53, 1640-1657) as one

@@ -547,3 +547,18 @@ extern "C" int u3d_wstd_bwd_batch(const u3d_wstd_desc* descs, int count, float* 
   hipLaunchKernelGGL(wstd_grad_kernel, dim3(ablocks), dim3(WG_T), 0, st, ab);
   return check_launch("wstd_grad_kernel");
 }
+
+// Round 5: the slab sum of ONE weight gradient right after the launch that wrote its slabs (they then sit in L2 / the
+// Infinity Cache instead of being re-read from HBM by the batched sum at the end of the backward). Same kernel, same
+// slab groups, same order: slab 0 ends bitwise equal to the batched form's.
+extern "C" int u3d_wgrad_sum_slabs(float* part, int nsplit, int k3, int cout, int cin, u3d_stream_t stream) {
+  U3D_REQUIRE(part && nsplit >= 1 && (k3 == 1 || k3 == 27) && cout > 0 && cin > 0, "wgrad_sum_slabs: bad args");
+  if (nsplit == 1) return U3D_OK;
+  const long long per4 = (long long)k3 * round_up(cout, 32) * round_up(cin, 32) / 4;
+  int sg = 1;
+  while (sg < 32 && nsplit > 16 * sg) sg *= 2;  // as u3d_wstd_bwd_batch
+  WBatch<WSum> sb{};
+  sb.d[sb.count++] = WSum{part, nsplit, (int)per4, sg, 0};
+  hipLaunchKernelGGL(wstd_sum_slabs_kernel, dim3(cdiv(per4, WB_T / sg)), dim3(WB_T), 0, (hipStream_t)stream, sb);
+  return check_launch("wstd_sum_slabs_kernel");
+}

@@ -22,6 +22,7 @@ _SIGS = {
     "u3d_wstd_bwd": [P, I, P, P, I, I, I, I, P, I, P],
     "u3d_wstd_fwd_batch": [I, P, I, P],
     "u3d_wstd_bwd_batch": [P, I, P, P],
+    "u3d_wgrad_sum_slabs": [P, I, I, I, I, P],
     "u3d_wstd_bwd_scratch_bytes": [P, I],
     "u3d_conv_fwd": [I, P, I, I, I, I, I, P, I, I, I, P, P, P, I, P, P, P, I, P, L, P],
     "u3d_conv_dgrad": [I, P, I, I, P, I, I, I, I, I, I, P, P, L, P],

@@ -693,6 +693,19 @@ def conv_wgrad(dy, x, k, stride, gn=None, brick=None):
     return part, ns
 
 
+# sum each weight gradient's slabs right after the launch that wrote them (round 5, cache-resident) instead of in the
+# batched standardisation backward at the end: conv_wgrad then returns (partials, 1)
+EAGER_SLAB_SUM = os.environ.get("U3D_EAGER_SLAB_SUM", "0") != "0"
+EAGER_SLAB_MIN = int(os.environ.get("U3D_EAGER_SLAB_MIN", "2"))  # fewest slabs summed eagerly
+
+
+def sum_slabs(part, ns, cout, cin):
+    """slab 0 of ``part`` [ns, k^3, cout_p, cin_p] <- the sum over slabs (u3d_wgrad_sum_slabs). Returns (part, 1)."""
+    if ns > 1:
+        call("u3d_wgrad_sum_slabs", part.data_ptr(), ns, part.shape[1], cout, cin, _stream())
+    return part, 1
+
+
 def use_head(dtype, cin, cout, k, stride):
     """The streaming MFMA head kernel (head.hip) serves GN+ReLU + 1^3 conv with cout <= 32 (precls_conv)."""
     return USE_HEAD and dtype == torch.bfloat16 and k == 1 and stride == 1 and cout <= 32 and cin % 16 == 0 \

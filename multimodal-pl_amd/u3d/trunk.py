@@ -176,6 +176,8 @@ class Tape:
                         self.acc_grad(residual, dy)
                     dyT = ops.cast(dy, self.dtype, pad_to=8)  # GEMM operand: channels padded to 8 (2-class head)
                 part, ns = ops.conv_wgrad(dyT, x.t, k, stride, gn)
+                if ops.EAGER_SLAB_SUM and ns >= ops.EAGER_SLAB_MIN:
+                    part, ns = ops.sum_slabs(part, ns, cout, cin)
                 self.pend_wgrad(part, ns, W, st, std, key + ".weight")
                 s2c = (gn is not None and pair == "park" and k == 1 and stride == 2 and ops.S2_COMPACT
                        and ops._use_conv1x1(dyT.dtype, dyT.shape[-1], cin, 1, dyT.shape[0])

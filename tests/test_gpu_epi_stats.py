@@ -112,8 +112,8 @@ def test_conv_small_in_kernel_combine(gpu, n, cin, cout, dims, res, flip):
     ("ring", 1, 32, (10, 16, 40), False),
     ("ring", 3, 32, (9, 12, 16), True),
     ("brick", 2, 64, (24, 24, 24), True),   # persistent brick (48^3 / 24^3 levels)
-    ("brick", 2, 128, (12, 16, 24), False),
-    ("brick", 3, 64, (8, 16, 32), True),
+    ("brick", 2, 128, (16, 24, 32), False),
+    ("brick", 3, 64, (16, 32, 32), True),
 ])
 def test_fused_finalize_matches_finalize_kernel(gpu, monkeypatch, kind, n, c, dims, res):
     """The ring / persistent-brick epilogue statistics finalized by the conv launch's last-arriving workgroup

@@ -25,10 +25,10 @@ CASES = [  # n, d, h, w, cin (x, dA), cout (dy), groups, x offset
     (2, 24, 24, 24, 64, 128, 8, 0.0),     # cin != cout, 8 channels per group
     (2, 24, 24, 24, 64, 64, 16, 40.0),    # |mean| / std ~ 50: the (x - mean) form of the sums
     # the epilogue's two-slot GroupNorm table (indexed by sample parity) and the padded-channel masks
-    (1, 24, 24, 24, 64, 64, 16, 0.0),     # n = 1
+    (1, 32, 32, 32, 64, 64, 16, 0.0),     # n = 1
     (3, 16, 24, 24, 64, 64, 16, 0.0),     # n = 3: workgroups whose brick runs cross sample boundaries
     (2, 24, 24, 24, 48, 64, 8, 0.0),      # dA channels 48: a partially padded 32-channel tile, 6 per group
-    (2, 16, 16, 32, 40, 64, 8, 3.0),      # dA channels 40, 5 per group
+    (2, 16, 32, 32, 40, 64, 8, 3.0),      # dA channels 40, 5 per group
 ]
 
 

@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-timeout -k 10 500 python -u -m pytest tests/test_gpu_epi_stats.py tests/test_gpu_gnfused_small.py tests/test_gpu_s2ring.py tests/test_gpu_graph.py tests/test_gpu_ddp.py tests/test_gpu_gnfused_brick.py tests/test_gpu_gnfused.py tests/test_gpu_wgrad_dma.py -v -s --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_epi_stats.py tests/test_gpu_gnfused_small.py tests/test_gpu_s2ring.py tests/test_gpu_graph.py tests/test_gpu_ddp.py tests/test_gpu_gnfused_brick.py tests/test_gpu_gnfused.py tests/test_gpu_wgrad_dma.py tests/test_gpu_slabsum.py -v -s --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|ERROR|err |bitwise" $O/pytest.log | cut -c1-220
 [ $rc -eq 0 ] || { grep -E "^E |Error" $O/pytest.log | head -40; exit 1; }
@@ -19,6 +19,7 @@ OFF="U3D_STEM_STATS=0 U3D_UP_STATS=0 U3D_SMALL_FUSE=0 U3D_FUSED_FINALIZE=0 U3D_S
 for i in 1 2 3; do
   run off$i "$OFF" || exit 1
   run on$i "A=1" || exit 1
+  run slab$i "U3D_EAGER_SLAB_SUM=1" || exit 1
 done
 run s2off "U3D_S2_RING=0" || exit 1
 run fb25_25 "A=1" --force-buckets --bucket-mb 25 --tail-mb 25 || exit 1
