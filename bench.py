@@ -54,8 +54,8 @@ def parse():
                    help="N=1 only: RCCL (nccl backend) at world size 1 with U3DDataParallel(force_buckets=True), i.e. "
                         "the bucketed all-reduces launched from inside the backward and the collective-tolerant kernel "
                         "forms while they run (what N>1 pays for the overlap, measured on one GPU)")
-    p.add_argument("--bucket-mb", type=float, default=40.0, help="gradient bucket cap (MB of fp32 gradients)")
-    p.add_argument("--tail-mb", type=float, default=2.0, help="cap of the last bucket (launched at the backward's end)")
+    p.add_argument("--bucket-mb", type=float, default=25.0, help="gradient bucket cap (MB of fp32 gradients)")
+    p.add_argument("--tail-mb", type=float, default=25.0, help="cap of the last bucket (launched at the backward's end)")
     p.add_argument("--print-rank-env", action="store_true", help=argparse.SUPPRESS)  # launcher test (no GPU)
     p.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph (the default, also at "
                    "N>1 and with --force-buckets; the ring kernels' live timing comes from an eager pass of the same "

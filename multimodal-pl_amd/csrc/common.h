@@ -163,6 +163,60 @@ __device__ __forceinline__ float wave_sum_transposed(float (&v)[N], int lane) {
   return v[0];
 }
 
+// The combine of a launch's last-arriving workgroup over the partial rows the launch's workgroups wrote (sc1 stores):
+// out[r * K + k] (fp64, LDS) = sum over w < nw of rows[(r * nw + w) * K + k], for r < nr, k < K (K % 4 == 0).
+// L lanes per (row r, column quad), L the largest power of two <= 64 with all items in one pass of NT threads; lane l
+// sums w = l, l + L, ... in order with 8 sc1 16-B loads in flight (r05: the first form, one dependent load pair per
+// iteration, cost its conv launch 8-11 us), then an xor tree over the L lanes. Fixed order: deterministic.
+// Every thread of the workgroup must call it (shuffles); `out` is read after the caller's barrier.
+template <int NT>
+__device__ __forceinline__ void lastarriver_rowsum(const float* rows, int nr, int nw, int K, double* out) {
+  const int nq = K >> 2, items = nr * nq;
+  int L = 64;
+  while (L > 1 && items * L > NT) L >>= 1;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)rows, 0, 0x7FFFFFFF, 0x00020000);
+  const int tid = threadIdx.x, l = tid & (L - 1);
+  for (int i0 = 0; i0 < items; i0 += NT / L) {
+    const int it = i0 + tid / L;
+    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    if (it < items) {
+      const int r = it / nq, q = it - r * nq;
+      const int base = (r * nw * K + 4 * q) * 4;
+      for (int w0 = l; w0 < nw; w0 += 8 * L) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int w = w0 + u * L;
+          v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rs, w < nw ? base + w * K * 4 : (int)0xFFFFFFF0u, 0, 16));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (w0 + u * L < nw) {
+            a0 += v[u][0];
+            a1 += v[u][1];
+            a2 += v[u][2];
+            a3 += v[u][3];
+          }
+      }
+    }
+    for (int o = L >> 1; o > 0; o >>= 1) {
+      a0 += __shfl_xor(a0, o);
+      a1 += __shfl_xor(a1, o);
+      a2 += __shfl_xor(a2, o);
+      a3 += __shfl_xor(a3, o);
+    }
+    if (it < items && l == 0) {
+      const int r = it / nq, q = it - r * nq;
+      double* o4 = out + r * K + 4 * q;
+      o4[0] = a0;
+      o4[1] = a1;
+      o4[2] = a2;
+      o4[3] = a3;
+    }
+  }
+}
+
 // GroupNorm(16) statistics from per-workgroup partials [sample][wps][16][2] (fp32 sums of values and squares): one
 // wave per (sample, group), fixed-order fp64 combine (conv_ring.hip). m = values per group and sample.
 int launch_gn16_finalize(const float* spart, int n, int wps, double m, float* stats, hipStream_t s);

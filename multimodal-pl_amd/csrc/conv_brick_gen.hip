@@ -809,17 +809,26 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
           const int p = p0 + (tid >> 4);
           double s1 = 0, s2 = 0;
           if (p < g.n * 16) {
-            const int nn = p >> 4, gr = p & 15;
-            for (int b = l16; b < bps; b += 16) {
-              const long long brick = (long long)nn * bps + b;
-              for (int c = gr * cpg; c < (gr + 1) * cpg; c += 2) {
-                const int ct = c / CO, cl = c - ct * CO;
-                typedef __attribute__((ext_vector_type(2))) double f64x2;
-                const f64x2 q = __builtin_bit_cast(
-                    f64x2, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(((brick * g.nct + ct) * CO + cl) * 8), 0, 16));
-                s1 += q[0];
-                s2 += q[1];
+            // this lane's (brick, channel pair) items in the order b = l16, l16 + 16, ..., pairs inner; 8 sc1 loads
+            // in flight (a dependent load per item cost the launch ~10 us)
+            typedef __attribute__((ext_vector_type(2))) double f64x2;
+            const int nn = p >> 4, gr = p & 15, ncp = cpg >> 1, nk = (bps - l16 + 15) / 16 * ncp;
+            for (int k0 = 0; k0 < nk; k0 += 8) {
+              f64x2 q[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int k = k0 + u, bi = k / ncp, c = gr * cpg + 2 * (k - bi * ncp), ct = c / CO, cl = c - ct * CO;
+                const long long brick = (long long)nn * bps + l16 + 16 * bi;
+                q[u] = __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     prs, k < nk ? (int)(((brick * g.nct + ct) * CO + cl) * 8)
+                                                                 : (int)0xFFFFFFF0u, 0, 16));
               }
+#pragma unroll
+              for (int u = 0; u < 8; ++u)
+                if (k0 + u < nk) {
+                  s1 += q[u][0];
+                  s2 += q[u][1];
+                }
             }
           }
 #pragma unroll

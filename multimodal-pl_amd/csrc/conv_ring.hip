@@ -700,28 +700,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       __syncthreads();
       if (!s_last) return;
       double* const cs = reinterpret_cast<double*>(ring);  // [n * 32][2]
-      const int l8 = tid & 7;
-      for (int p0 = 0; p0 < g.n * 32; p0 += RG_NT / 8) {
-        const int pr = p0 + (tid >> 3);
-        double s1 = 0, s2 = 0;
-        if (pr < g.n * 32) {
-          const int nn = pr >> 5, c = pr & 31;
-          for (int wk = l8; wk < g.wps; wk += 8) {
-            const float* qq = spart + ((long long)nn * g.wps + wk) * 64 + c * 2;
-            s1 += __hip_atomic_load(qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s2 += __hip_atomic_load(qq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-#pragma unroll
-        for (int o = 4; o > 0; o >>= 1) {
-          s1 += __shfl_xor(s1, o);
-          s2 += __shfl_xor(s2, o);
-        }
-        if (pr < g.n * 32 && l8 == 0) {
-          cs[2 * pr] = s1;
-          cs[2 * pr + 1] = s2;
-        }
-      }
+      lastarriver_rowsum<RG_NT>(spart, g.n, g.wps, 64, cs);
       __syncthreads();
       const int gcpg = 32 / g.gn_groups;
       const double M = (double)g.d * g.h * g.w * gcpg;
@@ -797,54 +776,59 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       }
       __syncthreads();
       if (s_last) {
-        const int l16 = tid & 15;
+        double* const cs = reinterpret_cast<double*>(ring) + 2048;  // [n * 16][2] (past the stats rows in `red`)
+        lastarriver_rowsum<RG_NT>(spart, g.n, g.wps, 32, cs);
+        __syncthreads();
         const double m = 2.0 * g.d * g.h * g.w;
-        for (int p0 = 0; p0 < g.n * 16; p0 += RG_NT / 16) {
-          const int p = p0 + (tid >> 4);
-          double s1 = 0, s2 = 0;
-          if (p < g.n * 16) {
-            const int nn = p >> 4, gr = p & 15;
-            for (int wk = l16; wk < g.wps; wk += 16) {
-              const float* q = spart + ((long long)nn * g.wps + wk) * 32 + gr * 2;
-              s1 += __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              s2 += __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-          }
-#pragma unroll
-          for (int o = 8; o > 0; o >>= 1) {
-            s1 += __shfl_xor(s1, o);
-            s2 += __shfl_xor(s2, o);
-          }
-          if (p < g.n * 16 && l16 == 0) {
-            const double mean = s1 / m;
-            double var = s2 / m - mean * mean;
-            if (var < 0) var = 0;
-            g.fstats[p * 2] = (float)mean;
-            g.fstats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
-          }
+        for (int p = tid; p < g.n * 16; p += RG_NT) {
+          const double mean = cs[2 * p] / m;
+          double var = cs[2 * p + 1] / m - mean * mean;
+          if (var < 0) var = 0;
+          g.fstats[p * 2] = (float)mean;
+          g.fstats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
         }
       }
     }
   }
 }
 
-// stats[n][16] = (mean, rstd) of GroupNorm(16, 32) from the ring kernel's per-workgroup partials: one wave per
-// (n, group), lanes strided over the workgroups, fp64 butterfly in fixed order (deterministic)
-__global__ __launch_bounds__(64) void ring_gn_finalize_kernel(const float* __restrict__ spart, int n, int wps, double m,
-                                                             float* __restrict__ stats) {
-  const int p = blockIdx.x, nn = p / 16, gr = p % 16;
+// stats[n][16] = (mean, rstd) of GroupNorm(16, 32) from per-workgroup partial rows [n][wps][16][2] (ring, stem,
+// upsample): one 256-thread block per (n, group), threads strided over the rows with 8 loads in flight (r05: one wave
+// with a dependent load per row took 12.5 us at the stem's 3456 rows per sample), then the wave butterflies and the
+// 4 waves in order (fixed order: deterministic)
+__global__ __launch_bounds__(256) void ring_gn_finalize_kernel(const float* __restrict__ spart, int n, int wps, double m,
+                                                              float* __restrict__ stats) {
+  __shared__ double red[4][2];
+  const int p = blockIdx.x, nn = p / 16, gr = p % 16, tid = threadIdx.x;
+  const float2* rows = reinterpret_cast<const float2*>(spart + (long long)nn * wps * 32 + gr * 2);
   double s1 = 0, s2 = 0;
-  for (int w = threadIdx.x; w < wps; w += 64) {
-    s1 += spart[((long long)nn * wps + w) * 32 + gr * 2];
-    s2 += spart[((long long)nn * wps + w) * 32 + gr * 2 + 1];
+  for (int w0 = tid; w0 < wps; w0 += 8 * 256) {
+    float2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int w = w0 + u * 256;
+      v[u] = w < wps ? rows[(long long)w * 16] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s1 += v[u].x;
+      s2 += v[u].y;
+    }
   }
   for (int o = 32; o > 0; o >>= 1) {
     s1 += __shfl_xor(s1, o);
     s2 += __shfl_xor(s2, o);
   }
-  if (threadIdx.x == 0) {
-    const double mean = s1 / m;
-    double var = s2 / m - mean * mean;
+  if ((tid & 63) == 0) {
+    red[tid >> 6][0] = s1;
+    red[tid >> 6][1] = s2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double t1 = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
+    const double t2 = ((red[0][1] + red[1][1]) + red[2][1]) + red[3][1];
+    const double mean = t1 / m;
+    double var = t2 / m - mean * mean;
     if (var < 0) var = 0;
     stats[p * 2] = (float)mean;
     stats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
@@ -852,7 +836,7 @@ __global__ __launch_bounds__(64) void ring_gn_finalize_kernel(const float* __res
 }
 
 int launch_gn16_finalize(const float* spart, int n, int wps, double m, float* stats, hipStream_t s) {
-  hipLaunchKernelGGL(ring_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, spart, n, wps, m, stats);
+  hipLaunchKernelGGL(ring_gn_finalize_kernel, dim3(n * 16), dim3(256), 0, s, spart, n, wps, m, stats);
   return check_launch("ring_gn_finalize_kernel");
 }
 
@@ -1132,7 +1116,7 @@ extern "C" int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int 
   const long long wps0 = std::max<long long>(1, std::min<long long>(pps, ring_wgs() / n));
   const long long per = (pps + wps0 - 1) / wps0;
   const int wps = (int)((pps + per - 1) / per);
-  hipLaunchKernelGGL(ring_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, (hipStream_t)stream, stats_ws, n, wps,
+  hipLaunchKernelGGL(ring_gn_finalize_kernel, dim3(n * 16), dim3(256), 0, (hipStream_t)stream, stats_ws, n, wps,
                      2.0 * d * h * w, stats_out);
   return check_launch("ring_gn_finalize_kernel");
 }

@@ -306,31 +306,16 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
   }
   __syncthreads();
   if (!s_last) return;
-  const int lq = tid & 15;
+  double* const cs = reinterpret_cast<double*>(smem) + 64;  // [n * 16][2] (past the wave rows in `red`)
+  lastarriver_rowsum<S2_NT>(g.spart, g.n, g.wps, 32, cs);
+  __syncthreads();
   const double m = 4.0 * g.od * g.oh * g.ow;  // values per group and sample: 4 channels
-  for (int p0 = 0; p0 < g.n * 16; p0 += S2_NT / 16) {
-    const int pr = p0 + (tid >> 4);
-    double s1 = 0, s2 = 0;
-    if (pr < g.n * 16) {
-      const int nn = pr >> 4, gr = pr & 15;
-      for (int wk = lq; wk < g.wps; wk += 16) {
-        const float* qq = g.spart + ((long long)nn * g.wps + wk) * 32 + gr * 2;
-        s1 += __hip_atomic_load(qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s2 += __hip_atomic_load(qq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
-      s1 += __shfl_xor(s1, o);
-      s2 += __shfl_xor(s2, o);
-    }
-    if (pr < g.n * 16 && lq == 0) {
-      const double mean = s1 / m;
-      double var = s2 / m - mean * mean;
-      if (var < 0) var = 0;
-      g.stats[pr * 2] = (float)mean;
-      g.stats[pr * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
-    }
+  for (int pr = tid; pr < g.n * 16; pr += S2_NT) {
+    const double mean = cs[2 * pr] / m;
+    double var = cs[2 * pr + 1] / m - mean * mean;
+    if (var < 0) var = 0;
+    g.stats[pr * 2] = (float)mean;
+    g.stats[pr * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
   }
 }
 

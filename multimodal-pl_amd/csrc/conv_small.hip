@@ -365,17 +365,7 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
       if (!s_last) return;
       // gn_bwd_parts_finalize + gn_bwd_coefs: per (n, c) fp64 sums over the bricks in order, then the coefficients
       double* const cs = reinterpret_cast<double*>(smem);  // [n * cout][2] (<= 8192 doubles: host-checked)
-      for (int p = tid; p < g.n * g.cout; p += SC_NT) {
-        const int n2 = p / g.cout, c = p - n2 * g.cout;
-        double s1 = 0, s2 = 0;
-        for (int b2_ = 0; b2_ < nbr; ++b2_) {
-          const float* pp = g.gbparts + (((long long)n2 * nbr + b2_) * g.cout + c) * 2;
-          s1 += __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s2 += __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        cs[2 * p] = s1;
-        cs[2 * p + 1] = s2;
-      }
+      lastarriver_rowsum<SC_NT>(g.gbparts, g.n, nbr, 2 * g.cout, cs);
       __syncthreads();
       const int gcpg = g.cout / g.gbgroups;
       const double M = (double)g.d * g.h * g.w * gcpg;
@@ -441,20 +431,16 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
     }
     __syncthreads();
     if (!s_last) return;
-    if (tid < g.n * 16) {
-      const int n2 = tid >> 4, gr = tid & 15;
-      double s1 = 0, s2 = 0;
-      for (int b2 = 0; b2 < nbr; ++b2) {
-        const float* pp = g.spart + ((long long)n2 * nbr + b2) * 32 + gr * 2;
-        s1 += __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s2 += __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    double* const cs = reinterpret_cast<double*>(smem) + 64;  // [n * 16][2] (past the wave rows in `red`)
+    lastarriver_rowsum<SC_NT>(g.spart, g.n, nbr, 32, cs);
+    __syncthreads();
+    for (int p = tid; p < g.n * 16; p += SC_NT) {
       const double m = (double)g.cpg * g.d * g.h * g.w;
-      const double mean = s1 / m;
-      double var = s2 / m - mean * mean;
+      const double mean = cs[2 * p] / m;
+      double var = cs[2 * p + 1] / m - mean * mean;
       if (var < 0) var = 0;
-      g.stats[tid * 2] = (float)mean;
-      g.stats[tid * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+      g.stats[p * 2] = (float)mean;
+      g.stats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
     }
     return;
   }
