@@ -18,6 +18,7 @@
 //     the 64-channel output, whose (sum, sum of squares) the epilogue accumulates for the next GroupNorm's statistics,
 //     finalized by the workgroup that arrives last (no statistics pass).
 #include "common.h"
+#include "diag.h"
 
 namespace u3d {
 namespace {
@@ -92,6 +93,9 @@ struct S2Walk {
 };
 
 }  // namespace
+
+// -DU3D_STAMPS phases (diag.h): 0 the staged plane's GN + LDS write (incl. its loads' wait), 1 compute, 2 the barrier
+U3D_STAMP_BUFFER(s2_stamps, 1024, u3d_diag_s2_stamps)
 
 __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                                bf16* __restrict__ y, const float* __restrict__ gstat,
@@ -265,16 +269,25 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
   load_plane(pw);
   S2Plane pc{};
   int s = 0;
+  PhaseStamps ps;
+  ps.begin();
   while (pw.valid || pc.valid) {
+    ps.mark_now();
     if (pw.valid) write_plane(pw, s & 1);
+    ps.lap(0);
     const S2Plane pl = walk.next(g);
     load_plane(pl);
+    ps.mark_now();
+    ps.step(pc.valid);
     if (pc.valid) compute(pc, (s - 1) & 1);
+    ps.lap(1);
     __syncthreads();
+    ps.lap(2);
     pc = pw;
     pw = pl;
     ++s;
   }
+  ps.end(s2_stamps, blockIdx.x & 1023, wave, lane);
 
   if (g.spart == nullptr) return;
   // ---- GroupNorm(16) statistics of the output: lanes with the same q4 hold the same group (xor over l16), the two

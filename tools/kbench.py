@@ -158,6 +158,15 @@ CASES["dgrad1_s2_96"] = lambda: _dgrad(2, 32, 64, 96, 1, 2)
 CASES["dgrad1_s2_48"] = lambda: _dgrad(2, 64, 128, 48, 1, 2)
 CASES["fwd1_s2_96"] = lambda: _fwd(2, 32, 64, 96, 1, 2, True, False)
 CASES["fwd96_nores"] = lambda: _fwd(2, 32, 32, 96, 3, 1, True, False)
+
+
+def _fwd_s2_ring(n=2, s=96):
+    """the production stride-2 forward (layer1.0.conv1, 32 -> 64 with GN prologue + output stats: conv_s2.hip)"""
+    x, pf, pd, g, r, dy, flop = conv_case(n, 32, 64, s, 3, 2, True)
+    return t_(lambda: ops.conv_fwd_stats(x, pf, 64, 3, 2, g)), flop
+
+
+CASES["fwds2ring"] = _fwd_s2_ring
 CASES["wgrad1_96"] = lambda: _wgrad(2, 32, 16, 96, 1, 1)      # the head's 1^3 weight gradient
 CASES["wgrad1_s2_96"] = lambda: _wgrad(2, 32, 64, 96, 1, 2)   # layer1 downsample
 CASES["fwd96_nogn"] = lambda: _fwd(2, 32, 32, 96, 3, 1, False, True)

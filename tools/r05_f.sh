@@ -11,3 +11,5 @@ cat $O/fin.log
 f=$(find $O/kt -name '*kernel_trace.csv' | head -1); [ -n "$f" ] && cp $(dirname $f)/*.csv $O/
 python3 tools/prof_summary.py $O 16 > $O/kernel_summary.txt 2>&1 || true
 head -45 $O/kernel_summary.txt
+timeout -k 10 120 python tools/kbench.py fwds2ring > $O/kb_s2.log 2>&1 && cat $O/kb_s2.log
+U3D_LIB=$R/multimodal-pl_amd/u3d/libu3d_stamps.so timeout -k 10 120 python tools/stamps.py s2ring96 > $O/stamps_s2.log 2>&1; cat $O/stamps_s2.log | tail -12
