@@ -109,6 +109,8 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
   char* const wts = smem + 2 * S2_SS;
   char* const junk = wts + 4 * WPL;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  PhaseStamps ps;  // (from kernel entry: "other" = the weight prologue, the load issue and the walk)
+  ps.begin();
   const int l16 = lane & 15, q4 = lane >> 4;
   const int rg = wave >> 2, cb = wave & 3;  // output rows 4 rg .. 4 rg + 3 of the tile, channels 16 cb .. 16 cb + 15
   const int ch = (tid >> 3) & 3, srow = (tid & 7) + 8 * (tid >> 5);  // staging: 8 consecutive rows of one chunk plane
@@ -269,8 +271,6 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
   load_plane(pw);
   S2Plane pc{};
   int s = 0;
-  PhaseStamps ps;
-  ps.begin();
   while (pw.valid || pc.valid) {
     ps.mark_now();
     if (pw.valid) write_plane(pw, s & 1);

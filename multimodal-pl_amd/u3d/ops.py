@@ -390,9 +390,11 @@ def _queue(device, shape):
     return WS.get(query("u3d_conv32_ring_q_queue_bytes", *shape), device, slot=QUEUE_SLOT).data_ptr()
 
 
-# the ring / persistent-brick conv epilogue statistics finalized by the conv launch's last-arriving workgroup (round 5:
-# no ring_gn_finalize / pbrick_gn_finalize launch); U3D_FUSED_FINALIZE=0: the separate finalize kernels
-FUSED_FINALIZE = os.environ.get("U3D_FUSED_FINALIZE", "1") != "0"
+# the ring / persistent-brick conv epilogue statistics (and the ring data gradient's GroupNorm-backward coefficients)
+# finalized by the conv launch's last-arriving workgroup instead of a separate finalize launch (round 5, U3D_FUSED_FINALIZE=1).
+# Off by default: measured no cheaper than the launch it replaces (step A/B r05_e 5.671 / 5.672 off vs 5.687 / 5.678 on;
+# the in-step ring / brick launches grow 4-8 us each by the last arriver's drain + atomic + cross-XCD loads, r05_f trace)
+FUSED_FINALIZE = os.environ.get("U3D_FUSED_FINALIZE", "0") != "0"
 RING_CNT_SLOT, BRICK_CNT_SLOT, RING_GB_CNT_SLOT = 18, 19, 23
 # the 96^3 stride-2 3^3 forward (cin 32 -> cout 64, GN prologue) as an input-plane walk (conv_s2.hip, round 5);
 # U3D_S2_RING=0: the implicit GEMM + a statistics pass

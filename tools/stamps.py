@@ -62,6 +62,8 @@ else:
     nwg = _lib.query("u3d_conv_wgrad_ring_splits", 2, c, s, s, s, c) * (ops.round32(c) // 32) ** 2
     names = ("write+load-wait", "compute", "barrier")
 b = buf.reshape(4096, 8, 8)[:nwg].astype(np.float64)
+b = b[(b[:, :, 1] - b[:, :, 0]).min(axis=1) > 0]  # workgroups that ran (the grid may be smaller than nwg)
+nwg = len(b)
 clk = (b[:, 0, 1] - b[:, 0, 0]) / np.maximum(1, b[:, 0, 3] - b[:, 0, 2]) * 100.0  # MHz
 wall = b[:, :, 1] - b[:, :, 0]
 print(f"{case}: {n} launches, last 20 avg {us:.1f} us/launch, workgroups {nwg}")
