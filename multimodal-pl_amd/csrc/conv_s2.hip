@@ -160,7 +160,7 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
   int col_h0 = -1, col_w0 = -1;
   u32x4 v[S2_LD];
   unsigned vm = 0;
-  auto load_plane = [&](const S2Plane& p) {
+  auto load_column = [&](const S2Plane& p) {
     if (p.valid && (p.oh0 != col_h0 || p.ow0 != col_w0)) {  // uniform: once per run
       col_h0 = p.oh0;
       col_w0 = p.ow0;
@@ -173,32 +173,35 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
         pin |= (ok ? 1u : 0u) << i;
       }
     }
+  };
+  // piece i of plane p into v[i] (its previous content already written to LDS); bit i of vm = inside the volume
+  auto load_piece = [&](const S2Plane& p, int i) {
     const bool pv = p.valid && (unsigned)p.p < (unsigned)g.d;  // (p = -1 / d: zero padding)
     const int base = (((p.n * g.d + p.p) * g.h + 2 * p.oh0 - 1) * g.w + 2 * p.ow0 - 1) * 64;
-    vm = 0;
+    const bool ok = pv && ((pin >> i) & 1u);
+    const unsigned off = ok ? (unsigned)(base + plo[i]) : 0xFFFFFFF0u;
+    v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    vm = (vm & ~(1u << i)) | ((ok ? 1u : 0u) << i);
+  };
+  auto load_plane = [&](const S2Plane& p) {
+    load_column(p);
 #pragma unroll
-    for (int i = 0; i < S2_LD; ++i) {
-      const bool ok = pv && ((pin >> i) & 1u);
-      const unsigned off = ok ? (unsigned)(base + plo[i]) : 0xFFFFFFF0u;
-      v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-      vm |= (ok ? 1u : 0u) << i;
-    }
+    for (int i = 0; i < S2_LD; ++i) load_piece(p, i);
   };
   f32x2 sc[4], sh[4];
   int gn_n = -1;
-  auto write_plane = [&](const S2Plane& p, int slot) {
+  auto gn_table = [&](const S2Plane& p) {
     if (p.n != gn_n) {  // uniform
       gn_n = p.n;
       gn_coef8(gstat, gamma, beta, g.gn_groups, 32, p.n, ch * 8, sc, sh);
     }
-#pragma unroll
-    for (int i = 0; i < S2_LD; ++i) {
-      const int row = srow + i * (S2_NT / 4);
-      u32x4 val = gn_relu8(v[i], sc, sh);
-      if (!((vm >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
-      char* dst = row < S2_NR ? ring + slot * S2_SS + ch * S2_PS + row * 16 : junk + lane * 16;
-      *reinterpret_cast<u32x4*>(dst) = val;
-    }
+  };
+  auto write_piece = [&](int i, int slot) {
+    const int row = srow + i * (S2_NT / 4);
+    u32x4 val = gn_relu8(v[i], sc, sh);
+    if (!((vm >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
+    char* dst = row < S2_NR ? ring + slot * S2_SS + ch * S2_PS + row * 16 : junk + lane * 16;
+    *reinterpret_cast<u32x4*>(dst) = val;
   };
 
   f32x4 accA[4], accB[4];  // output finishing next (accA) / the one after it (accB), per voxel block
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
 
   // everything staged input plane p (LDS slot `slot`) contributes; B fragment of tap (kh, kw) and voxel block vb:
   // row (2 (4 rg + vb) + kh) * 33 + (kw = 0: 0, 1: 17, 2: 1) + l16 of chunk plane q4
-  auto compute = [&](const S2Plane& p, int slot) {
+  auto compute = [&](const S2Plane& p, int slot, auto&& side) {
     const bool odd = (p.p & 1) != 0;
     const int zlo = odd ? (p.p - 1) >> 1 : p.p >> 1;  // odd: finishing output (kd = 2); even: output p / 2 (kd = 1)
     const bool has2 = odd && zlo >= p.zf, has0 = odd && zlo + 1 < p.zl;
@@ -243,6 +246,7 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
         for (int vb = 0; vb < 4; ++vb)
           bf[vb] = *reinterpret_cast<const bf16x8*>(bb + ((2 * vb + kh) * S2_RPH + cofs) * 16);
         const int t = kh * 3 + kw;
+        side(t);
         if (odd) {
           if (has2)
 #pragma unroll
@@ -266,20 +270,34 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
     }
   };
 
-  // step s: write plane s (loaded during step s-1) into slot s & 1, load plane s+1, compute plane s-1 (slot (s-1) & 1)
+  // step s: compute plane s-1 (slot (s-1) & 1) and, between its taps, write plane s (loaded during step s-1) piece by
+  // piece into slot s & 1, each piece's register then reloaded with the piece of plane s+1 (r05: as a separate phase
+  // before the MFMAs the writes and the load issue took 40% of the step, stamps); one barrier per step
   S2Plane pw = walk.next(g);
   load_plane(pw);
   S2Plane pc{};
   int s = 0;
   while (pw.valid || pc.valid) {
     ps.mark_now();
-    if (pw.valid) write_plane(pw, s & 1);
-    ps.lap(0);
+    if (pw.valid) gn_table(pw);
     const S2Plane pl = walk.next(g);
-    load_plane(pl);
-    ps.mark_now();
+    load_column(pl);
+    const int wslot = s & 1;
+    const bool wv = pw.valid;
+    auto side = [&](int t) __attribute__((always_inline)) {
+      if (t < S2_LD) {
+        if (wv) write_piece(t, wslot);
+        load_piece(pl, t);
+      }
+    };
+    ps.lap(0);
     ps.step(pc.valid);
-    if (pc.valid) compute(pc, (s - 1) & 1);
+    if (pc.valid) {
+      compute(pc, (s - 1) & 1, side);
+    } else {
+#pragma unroll
+      for (int t = 0; t < S2_LD; ++t) side(t);
+    }
     ps.lap(1);
     __syncthreads();
     ps.lap(2);

@@ -69,6 +69,9 @@ wall = b[:, :, 1] - b[:, :, 0]
 print(f"{case}: {n} launches, last 20 avg {us:.1f} us/launch, workgroups {nwg}")
 print(f"  in-kernel clock: median {np.median(clk):.0f} MHz (p10 {np.percentile(clk, 10):.0f}, p90 {np.percentile(clk, 90):.0f})")
 print(f"  workgroup span: median {np.median(wall[:, 0]) / np.median(clk):.1f} us, max {wall[:, 0].max() / np.median(clk):.1f} us")
+r0, r1 = b[:, 0, 2], b[:, 0, 3]  # s_memrealtime (100 MHz) at the workgroup's first / last stamp
+print(f"  starts spread over {(r0.max() - r0.min()) / 100:.1f} us (p90 {(np.percentile(r0, 90) - r0.min()) / 100:.1f}), "
+      f"ends over {(r1.max() - r1.min()) / 100:.1f} us; first start to last end {(r1.max() - r0.min()) / 100:.1f} us")
 steps = b[:, :, 7].astype(np.uint64)
 for w in range(8):
     tot = wall[:, w]
