@@ -192,77 +192,72 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
   };
   // (hoisted only for the 16 x 16 tiles: the 12 x 24 tile's register budget has no room for the six offsets)
   constexpr bool HOIST = PW == 16;
-  auto load_plane = [&](const WRPlane& p, u32x4 (&vx)[WR_LX], u32x4 (&vy)[WR_LY], unsigned& m) {
-    m = 0;
+  // Staging, one 16-B piece at a time (round 5): piece i of plane p into vx[i] / vy[i]; bit i of m = the x row is
+  // inside the volume. The step writes the staged plane's pieces between its MFMA sub-steps and reloads each piece's
+  // register with the next plane right after (one register set: as a separate phase before the MFMAs the staging took
+  // 40% of the step, r04 stamps of the 16 x 16 form).
+  auto load_x = [&](const WRPlane& p, int i, u32x4 (&vx)[WR_LX], unsigned& m) {
+    bool ok;
+    unsigned off;
     if constexpr (!HOIST) {
-#pragma unroll
-      for (int i = 0; i < WR_LX; ++i) {
-        const int row = (tid >> 2) + i * (WR_NT / 4);
-        const int hw = row % WR_HW, hh = row / WR_HW;
-        const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
-        const bool ok = p.valid && cok && row < WR_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
-                        (unsigned)zw < (unsigned)g.w;
-        const unsigned off =
-            ok ? (unsigned)(((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * g.cin + ci0 + ch * 8) * 2) : 0xFFFFFFF0u;
-        vx[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-        m |= (ok ? 1u : 0u) << i;
-      }
-#pragma unroll
-      for (int i = 0; i < WR_LY; ++i) {
-        const int v = (tid >> 2) + i * (WR_NT / 4);
-        const int zh = p.h0 + v / WR_PW, zw = p.w0 + v % WR_PW, zo = p.zin - 1;
-        const bool ok = p.valid && p.out && dok && v < WR_NV && zh < g.h && zw < g.w;
-        const unsigned off =
-            ok ? (unsigned)(((((p.n * g.d + zo) * g.h + zh) * g.w + zw) * g.cout + co0 + ch * 8) * 2) : 0xFFFFFFF0u;
-        vy[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0));
-      }
-      return;
+      const int row = (tid >> 2) + i * (WR_NT / 4);
+      const int hw = row % WR_HW, hh = row / WR_HW;
+      const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
+      ok = p.valid && cok && row < WR_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
+           (unsigned)zw < (unsigned)g.w;
+      off = ok ? (unsigned)(((((p.n * g.d + p.zin) * g.h + zh) * g.w + zw) * g.cin + ci0 + ch * 8) * 2) : 0xFFFFFFF0u;
+    } else {
+      const bool pv = p.valid && (unsigned)p.zin < (unsigned)g.d;
+      const int xb = (((p.n * g.d + p.zin) * g.h + p.h0 - 1) * g.w + p.w0 - 1) * g.cin * 2;
+      ok = pv && ((xin >> i) & 1u);
+      off = ok ? (unsigned)(xb + xlo[i]) : 0xFFFFFFF0u;
     }
-    column(p);
-    const bool pv = p.valid && (unsigned)p.zin < (unsigned)g.d;
-    const int xb = (((p.n * g.d + p.zin) * g.h + p.h0 - 1) * g.w + p.w0 - 1) * g.cin * 2;
-#pragma unroll
-    for (int i = 0; i < WR_LX; ++i) {
-      const bool ok = pv && ((xin >> i) & 1u);
-      const unsigned off = ok ? (unsigned)(xb + xlo[i]) : 0xFFFFFFF0u;
-      vx[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-      m |= (ok ? 1u : 0u) << i;
-    }
-    const bool po = p.valid && p.out;
-    const int yb = (((p.n * g.d + p.zin - 1) * g.h + p.h0) * g.w + p.w0) * g.cout * 2;
-#pragma unroll
-    for (int i = 0; i < WR_LY; ++i) {
-      const unsigned off = po && ((yin >> i) & 1u) ? (unsigned)(yb + ylo[i]) : 0xFFFFFFF0u;
-      vy[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0));
-    }
+    vx[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    m = (m & ~(1u << i)) | ((ok ? 1u : 0u) << i);
   };
-  auto write_plane = [&](const WRPlane& p, const u32x4 (&vx)[WR_LX], const u32x4 (&vy)[WR_LY], unsigned m, int slot,
-                         int dslot) {
-    if (GN && p.n != gn_n) {
+  auto load_y = [&](const WRPlane& p, int i, u32x4 (&vy)[WR_LY]) {
+    unsigned off;
+    if constexpr (!HOIST) {
+      const int v = (tid >> 2) + i * (WR_NT / 4);
+      const int zh = p.h0 + v / WR_PW, zw = p.w0 + v % WR_PW, zo = p.zin - 1;
+      const bool ok = p.valid && p.out && dok && v < WR_NV && zh < g.h && zw < g.w;
+      off = ok ? (unsigned)(((((p.n * g.d + zo) * g.h + zh) * g.w + zw) * g.cout + co0 + ch * 8) * 2) : 0xFFFFFFF0u;
+    } else {
+      const bool po = p.valid && p.out;
+      const int yb = (((p.n * g.d + p.zin - 1) * g.h + p.h0) * g.w + p.w0) * g.cout * 2;
+      off = po && ((yin >> i) & 1u) ? (unsigned)(yb + ylo[i]) : 0xFFFFFFF0u;
+    }
+    vy[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(yrs, off, 0, 0));
+  };
+  auto load_plane = [&](const WRPlane& p, u32x4 (&vx)[WR_LX], u32x4 (&vy)[WR_LY], unsigned& m) {
+    if constexpr (HOIST) column(p);
+#pragma unroll
+    for (int i = 0; i < WR_LX; ++i) load_x(p, i, vx, m);
+#pragma unroll
+    for (int i = 0; i < WR_LY; ++i) load_y(p, i, vy);
+  };
+  auto gn_refresh = [&](const WRPlane& p) {
+    if (GN && p.valid && p.n != gn_n) {
       gn_n = p.n;
       gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, p.n, ci0 + ch * 8, sc, sh);
     }
-#pragma unroll
-    for (int i = 0; i < WR_LX; ++i) {
-      const int row = (tid >> 2) + i * (WR_NT / 4);
-      u32x4 val = vx[i];
-      if constexpr (GN) {
-        val = gn_relu8(val, sc, sh);
-        if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
-      }
-      const int lo = T::M16 ? (ch >> 1) * T::HP + row * 32 + (ch & 1) * 16 : row * WR_ROWB + ch * 16;
-      char* dst = row < WR_NR ? ring + slot * WR_SLOT + lo : junk + (tid & 63) * 16;
-      *reinterpret_cast<u32x4*>(dst) = val;
+  };
+  auto write_x = [&](int i, const u32x4 (&vx)[WR_LX], unsigned m, int slot) {
+    const int row = (tid >> 2) + i * (WR_NT / 4);
+    u32x4 val = vx[i];
+    if constexpr (GN) {
+      val = gn_relu8(val, sc, sh);
+      if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
     }
-    if (p.out) {
-#pragma unroll
-      for (int i = 0; i < WR_LY; ++i) {
-        const int v = (tid >> 2) + i * (WR_NT / 4);
-        if (WR_NV % (WR_NT / 4) == 0 || v < WR_NV)
-          *reinterpret_cast<u32x4*>(dyr + dslot * WR_DSLOT +
-                                    (T::M16 ? (ch >> 1) * T::DHP + v * 32 + (ch & 1) * 16 : v * WR_ROWB + ch * 16)) = vy[i];
-      }
-    }
+    const int lo = T::M16 ? (ch >> 1) * T::HP + row * 32 + (ch & 1) * 16 : row * WR_ROWB + ch * 16;
+    char* dst = row < WR_NR ? ring + slot * WR_SLOT + lo : junk + (tid & 63) * 16;
+    *reinterpret_cast<u32x4*>(dst) = val;
+  };
+  auto write_y = [&](int i, const u32x4 (&vy)[WR_LY], int dslot) {
+    const int v = (tid >> 2) + i * (WR_NT / 4);
+    if (WR_NV % (WR_NT / 4) == 0 || v < WR_NV)
+      *reinterpret_cast<u32x4*>(dyr + dslot * WR_DSLOT +
+                                (T::M16 ? (ch >> 1) * T::DHP + v * 32 + (ch & 1) * 16 : v * WR_ROWB + ch * 16)) = vy[i];
   };
 
   constexpr int MAXT = 4;  // taps per wave: t = wave + 8j
@@ -298,7 +293,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     return (a * WR_HW + b + lrow[m] + (lrow[m] >= WR_PW - b ? 2 : 0)) * WR_ROWB + colb;
   };
 
-  auto compute = [&](int dslot, int s0, int s1, int s2, auto ntc) {
+  auto compute = [&](int dslot, int s0, int s1, int s2, auto ntc, auto&& side) {
     constexpr int NTP = decltype(ntc)::value;
     (void)s1;
     (void)s2;
@@ -339,6 +334,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
           if constexpr (((u + 1) & 1) == 0) rdA((u + 1) >> 1);
           rdB(u + 1);
         }
+        side(uc);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < NTP; ++j)
@@ -364,6 +360,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     sfor<0, T::KS>([&](auto kc) {
       constexpr int ks = decltype(kc)::value;
       if constexpr (ks + LA < T::KS) rd(ks + LA, (ks + LA) % (LA + 1));
+      side(kc);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NTP; ++j)
@@ -372,29 +369,43 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     });
   };
 
-  u32x4 xa[WR_LX], xb[WR_LX], ya[WR_LY], yb[WR_LY];
-  unsigned ma = 0, mb = 0;
+  u32x4 vx[WR_LX], vy[WR_LY];
+  unsigned vm = 0;
+  constexpr int NSUB = T::M16 ? 2 * (T::NV / 32) : T::KS;  // MFMA sub-steps per computed plane
+  static_assert(WR_LX + WR_LY <= NSUB, "one staging piece per sub-step at most");
   PhaseStamps ps;
   ps.begin();
   WRPlane pw = walk.next(g);
-  load_plane(pw, xa, ya, ma);
+  load_plane(pw, vx, vy, vm);
   WRPlane pc{};
   int s = 0;
-  auto step = [&](u32x4 (&cx)[WR_LX], u32x4 (&cy)[WR_LY], unsigned& mc, u32x4 (&nx)[WR_LX], u32x4 (&ny)[WR_LY],
-                  unsigned& mn) {
+  while (pw.valid || (pc.valid && pc.out)) {
     ps.mark_now();
-    if (pw.valid) write_plane(pw, cx, cy, mc, s & 3, s & 1);
-    ps.settle(pw.valid);  // the staged loads' wait (vmcnt) lands before the ds_writes
-    ps.lap(0);
+    gn_refresh(pw);
     const WRPlane pl = walk.next(g);
-    load_plane(pl, nx, ny, mn);
-    ps.mark_now();
+    if constexpr (HOIST) column(pl);
+    const int xs = s & 3, ds = s & 1;
+    const bool wv = pw.valid, wo = pw.valid && pw.out;
+    // sub-step u: piece u (x pieces first, then dy) of plane s written, its register reloaded with plane s+1's
+    auto side = [&](auto uc) __attribute__((always_inline)) {
+      constexpr int u = decltype(uc)::value;
+      if constexpr (u < WR_LX) {
+        if (wv) write_x(u, vx, vm, xs);
+        load_x(pl, u, vx, vm);
+      } else if constexpr (u < WR_LX + WR_LY) {
+        if (wo) write_y(u - WR_LX, vy, ds);
+        load_y(pl, u - WR_LX, vy);
+      }
+    };
+    ps.lap(0);
     ps.step(pc.valid && pc.out);
     if (pc.valid && pc.out) {
       if (ntap == 4)
-        compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 4>{});
+        compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 4>{}, side);
       else
-        compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 3>{});
+        compute((s - 1) & 1, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 3>{}, side);
+    } else {
+      sfor<0, WR_LX + WR_LY>([&](auto uc) { side(uc); });
     }
     ps.lap(1);
     __syncthreads();
@@ -402,11 +413,6 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_kernel(const bf16* __rest
     pc = pw;
     pw = pl;
     ++s;
-  };
-  while (pw.valid || (pc.valid && pc.out)) {
-    step(xa, ya, ma, xb, yb, mb);
-    if (!(pw.valid || (pc.valid && pc.out))) break;
-    step(xb, yb, mb, xa, ya, ma);
   }
   ps.end(wr_stamps, (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & 4095, wave, lane);
   // D[row = co][col = ci]: lane col ci0 + (lane&31), rows co0 + (i&3) + 8(i>>2) + 4h. Buffer stores with 32-bit
