@@ -158,8 +158,6 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
   }
   unsigned pin = 0;
   int col_h0 = -1, col_w0 = -1;
-  u32x4 v[S2_LD];
-  unsigned vm = 0;
   auto load_column = [&](const S2Plane& p) {
     if (p.valid && (p.oh0 != col_h0 || p.ow0 != col_w0)) {  // uniform: once per run
       col_h0 = p.oh0;
@@ -175,7 +173,7 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
     }
   };
   // piece i of plane p into v[i] (its previous content already written to LDS); bit i of vm = inside the volume
-  auto load_piece = [&](const S2Plane& p, int i) {
+  auto load_piece = [&](const S2Plane& p, int i, u32x4 (&v)[S2_LD], unsigned& vm) {
     const bool pv = p.valid && (unsigned)p.p < (unsigned)g.d;  // (p = -1 / d: zero padding)
     const int base = (((p.n * g.d + p.p) * g.h + 2 * p.oh0 - 1) * g.w + 2 * p.ow0 - 1) * 64;
     const bool ok = pv && ((pin >> i) & 1u);
@@ -183,10 +181,10 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
     v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     vm = (vm & ~(1u << i)) | ((ok ? 1u : 0u) << i);
   };
-  auto load_plane = [&](const S2Plane& p) {
+  auto load_plane = [&](const S2Plane& p, u32x4 (&v)[S2_LD], unsigned& vm) {
     load_column(p);
 #pragma unroll
-    for (int i = 0; i < S2_LD; ++i) load_piece(p, i);
+    for (int i = 0; i < S2_LD; ++i) load_piece(p, i, v, vm);
   };
   f32x2 sc[4], sh[4];
   int gn_n = -1;
@@ -196,7 +194,7 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
       gn_coef8(gstat, gamma, beta, g.gn_groups, 32, p.n, ch * 8, sc, sh);
     }
   };
-  auto write_piece = [&](int i, int slot) {
+  auto write_piece = [&](int i, int slot, const u32x4 (&v)[S2_LD], unsigned vm) {
     const int row = srow + i * (S2_NT / 4);
     u32x4 val = gn_relu8(v[i], sc, sh);
     if (!((vm >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
@@ -270,24 +268,29 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
     }
   };
 
-  // step s: compute plane s-1 (slot (s-1) & 1) and, between its taps, write plane s (loaded during step s-1) piece by
-  // piece into slot s & 1, each piece's register then reloaded with the piece of plane s+1 (r05: as a separate phase
-  // before the MFMAs the writes and the load issue took 40% of the step, stamps); one barrier per step
-  S2Plane pw = walk.next(g);
-  load_plane(pw);
+  // step s: compute plane s-1 (slot (s-1) & 1) and, between its taps, write plane s (loaded during step s-2) piece by
+  // piece into slot s & 1, each piece's register then reloaded with the piece of plane s+2: two staged planes in flight
+  // per workgroup (r05 stamps: with one, the writes waited on their loads — the kernel streams 125 MB at 2-3 TB/s);
+  // one barrier per step, unrolled by two so the register sets alternate statically
+  u32x4 va[S2_LD], vb[S2_LD];
+  unsigned ma = 0, mb = 0;
+  S2Plane pw = walk.next(g);  // plane s   (in va)
+  load_plane(pw, va, ma);
+  S2Plane pn = walk.next(g);  // plane s+1 (in vb)
+  load_plane(pn, vb, mb);
   S2Plane pc{};
   int s = 0;
-  while (pw.valid || pc.valid) {
+  auto step = [&](u32x4 (&vc)[S2_LD], unsigned& mc) __attribute__((always_inline)) {
     ps.mark_now();
     if (pw.valid) gn_table(pw);
-    const S2Plane pl = walk.next(g);
+    const S2Plane pl = walk.next(g);  // plane s+2
     load_column(pl);
     const int wslot = s & 1;
     const bool wv = pw.valid;
     auto side = [&](int t) __attribute__((always_inline)) {
       if (t < S2_LD) {
-        if (wv) write_piece(t, wslot);
-        load_piece(pl, t);
+        if (wv) write_piece(t, wslot, vc, mc);
+        load_piece(pl, t, vc, mc);
       }
     };
     ps.lap(0);
@@ -302,8 +305,14 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
     __syncthreads();
     ps.lap(2);
     pc = pw;
-    pw = pl;
+    pw = pn;
+    pn = pl;
     ++s;
+  };
+  while (pw.valid || pc.valid) {
+    step(va, ma);
+    if (!(pw.valid || pc.valid)) break;
+    step(vb, mb);
   }
   ps.end(s2_stamps, blockIdx.x & 1023, wave, lane);
 
