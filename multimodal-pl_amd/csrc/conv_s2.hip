@@ -158,7 +158,9 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
   }
   unsigned pin = 0;
   int col_h0 = -1, col_w0 = -1;
-  auto load_column = [&](const S2Plane& p) {
+  u32x4 v[S2_LD];
+  unsigned vm = 0;
+  auto load_plane = [&](const S2Plane& p) {
     if (p.valid && (p.oh0 != col_h0 || p.ow0 != col_w0)) {  // uniform: once per run
       col_h0 = p.oh0;
       col_w0 = p.ow0;
@@ -171,35 +173,32 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
         pin |= (ok ? 1u : 0u) << i;
       }
     }
-  };
-  // piece i of plane p into v[i] (its previous content already written to LDS); bit i of vm = inside the volume
-  auto load_piece = [&](const S2Plane& p, int i, u32x4 (&v)[S2_LD], unsigned& vm) {
     const bool pv = p.valid && (unsigned)p.p < (unsigned)g.d;  // (p = -1 / d: zero padding)
     const int base = (((p.n * g.d + p.p) * g.h + 2 * p.oh0 - 1) * g.w + 2 * p.ow0 - 1) * 64;
-    const bool ok = pv && ((pin >> i) & 1u);
-    const unsigned off = ok ? (unsigned)(base + plo[i]) : 0xFFFFFFF0u;
-    v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-    vm = (vm & ~(1u << i)) | ((ok ? 1u : 0u) << i);
-  };
-  auto load_plane = [&](const S2Plane& p, u32x4 (&v)[S2_LD], unsigned& vm) {
-    load_column(p);
+    vm = 0;
 #pragma unroll
-    for (int i = 0; i < S2_LD; ++i) load_piece(p, i, v, vm);
+    for (int i = 0; i < S2_LD; ++i) {
+      const bool ok = pv && ((pin >> i) & 1u);
+      const unsigned off = ok ? (unsigned)(base + plo[i]) : 0xFFFFFFF0u;
+      v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      vm |= (ok ? 1u : 0u) << i;
+    }
   };
   f32x2 sc[4], sh[4];
   int gn_n = -1;
-  auto gn_table = [&](const S2Plane& p) {
+  auto write_plane = [&](const S2Plane& p, int slot) {
     if (p.n != gn_n) {  // uniform
       gn_n = p.n;
       gn_coef8(gstat, gamma, beta, g.gn_groups, 32, p.n, ch * 8, sc, sh);
     }
-  };
-  auto write_piece = [&](int i, int slot, const u32x4 (&v)[S2_LD], unsigned vm) {
-    const int row = srow + i * (S2_NT / 4);
-    u32x4 val = gn_relu8(v[i], sc, sh);
-    if (!((vm >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
-    char* dst = row < S2_NR ? ring + slot * S2_SS + ch * S2_PS + row * 16 : junk + lane * 16;
-    *reinterpret_cast<u32x4*>(dst) = val;
+#pragma unroll
+    for (int i = 0; i < S2_LD; ++i) {
+      const int row = srow + i * (S2_NT / 4);
+      u32x4 val = gn_relu8(v[i], sc, sh);
+      if (!((vm >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
+      char* dst = row < S2_NR ? ring + slot * S2_SS + ch * S2_PS + row * 16 : junk + lane * 16;
+      *reinterpret_cast<u32x4*>(dst) = val;
+    }
   };
 
   f32x4 accA[4], accB[4];  // output finishing next (accA) / the one after it (accB), per voxel block
@@ -229,7 +228,7 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
 
   // everything staged input plane p (LDS slot `slot`) contributes; B fragment of tap (kh, kw) and voxel block vb:
   // row (2 (4 rg + vb) + kh) * 33 + (kw = 0: 0, 1: 17, 2: 1) + l16 of chunk plane q4
-  auto compute = [&](const S2Plane& p, int slot, auto&& side) {
+  auto compute = [&](const S2Plane& p, int slot) {
     const bool odd = (p.p & 1) != 0;
     const int zlo = odd ? (p.p - 1) >> 1 : p.p >> 1;  // odd: finishing output (kd = 2); even: output p / 2 (kd = 1)
     const bool has2 = odd && zlo >= p.zf, has0 = odd && zlo + 1 < p.zl;
@@ -244,7 +243,6 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
         for (int vb = 0; vb < 4; ++vb)
           bf[vb] = *reinterpret_cast<const bf16x8*>(bb + ((2 * vb + kh) * S2_RPH + cofs) * 16);
         const int t = kh * 3 + kw;
-        side(t);
         if (odd) {
           if (has2)
 #pragma unroll
@@ -268,51 +266,26 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
     }
   };
 
-  // step s: compute plane s-1 (slot (s-1) & 1) and, between its taps, write plane s (loaded during step s-2) piece by
-  // piece into slot s & 1, each piece's register then reloaded with the piece of plane s+2: two staged planes in flight
-  // per workgroup (r05 stamps: with one, the writes waited on their loads — the kernel streams 125 MB at 2-3 TB/s);
-  // one barrier per step, unrolled by two so the register sets alternate statically
-  u32x4 va[S2_LD], vb[S2_LD];
-  unsigned ma = 0, mb = 0;
-  S2Plane pw = walk.next(g);  // plane s   (in va)
-  load_plane(pw, va, ma);
-  S2Plane pn = walk.next(g);  // plane s+1 (in vb)
-  load_plane(pn, vb, mb);
+  // step s: write plane s (loaded during step s-1) into slot s & 1, load plane s+1, compute plane s-1 (slot (s-1) & 1)
+  S2Plane pw = walk.next(g);
+  load_plane(pw);
   S2Plane pc{};
   int s = 0;
-  auto step = [&](u32x4 (&vc)[S2_LD], unsigned& mc) __attribute__((always_inline)) {
+  while (pw.valid || pc.valid) {
     ps.mark_now();
-    if (pw.valid) gn_table(pw);
-    const S2Plane pl = walk.next(g);  // plane s+2
-    load_column(pl);
-    const int wslot = s & 1;
-    const bool wv = pw.valid;
-    auto side = [&](int t) __attribute__((always_inline)) {
-      if (t < S2_LD) {
-        if (wv) write_piece(t, wslot, vc, mc);
-        load_piece(pl, t, vc, mc);
-      }
-    };
+    if (pw.valid) write_plane(pw, s & 1);
     ps.lap(0);
+    const S2Plane pl = walk.next(g);
+    load_plane(pl);
+    ps.mark_now();
     ps.step(pc.valid);
-    if (pc.valid) {
-      compute(pc, (s - 1) & 1, side);
-    } else {
-#pragma unroll
-      for (int t = 0; t < S2_LD; ++t) side(t);
-    }
+    if (pc.valid) compute(pc, (s - 1) & 1);
     ps.lap(1);
     __syncthreads();
     ps.lap(2);
     pc = pw;
-    pw = pn;
-    pn = pl;
+    pw = pl;
     ++s;
-  };
-  while (pw.valid || pc.valid) {
-    step(va, ma);
-    if (!(pw.valid || pc.valid)) break;
-    step(vb, mb);
   }
   ps.end(s2_stamps, blockIdx.x & 1023, wave, lane);
 
