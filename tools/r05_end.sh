@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 closing measurements on one box (committed under profiles/r04_*): whole GPU suite, smoke(), the default bench
+# Round-5 closing measurements on one box (committed under profiles/r05_*): whole GPU suite, smoke(), the default bench
 # line (with the CPU baseline and the configs[4] leg, before any counter pass), the forced-bucket line, a kernel-trace
 # profile of the bench + summary (the roofline's trace check reads it), PMC traffic and an SQ pass of the three 96^3
 # ring kernels.
@@ -7,10 +7,14 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r05_end
 mkdir -p $O
 cd $R
-timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+PART=${1:-all}
+if [ "$PART" = all ] || [ "$PART" = tests ]; then
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
+fi
+[ "$PART" = tests ] && exit 0
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { echo "bench failed"; tail -5 $O/bench.log; exit 1; }
 grep '^{' $O/bench.log | tail -1 > $O/bench.json; cut -c1-300 $O/bench.json
 timeout -k 10 300 python bench.py --no-cpu --no-infer --no-roofline --force-buckets > $O/bench_fb.log 2>&1 || { echo "fb failed"; exit 1; }
