@@ -43,7 +43,6 @@ enum Opt : int {
   OPT_IGEMM_BM,       // bf16 implicit GEMM M tile: 0 auto (256 for large unsplit BN 64 launches), 128 / 256 force
   OPT_WSTD_ROW,       // weight-standardisation backward: one row per block from registers (0: chunked LDS kernel)
   OPT_UP_QUAD,        // bf16 trilinear x2 upsample: 2 x 2 outputs per thread from 18 loads (0: one output, 8 loads)
-  OPT_RING_NW,        // 4: the static GN forward / GN data-gradient 96^3 rings as 4-wave workgroups (default 8)
   OPT_COUNT
 };
 int opt(Opt o);

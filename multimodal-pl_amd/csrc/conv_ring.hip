@@ -113,8 +113,8 @@ struct RGWalk {
 // The MFMA is v_mfma_f32_16x16x32_bf16 (round 3: the same cycles per flop as 32x32x16, but the chip holds a higher
 // clock under it, MI355X_MICROARCH.md DVFS item 7): per tap (K = its 32 input channels) 4 MFMAs per wave = 2 voxel
 // blocks x 2 output-channel blocks. KR = weight fragments (tap, co block) held in registers.
-template <bool FLIP, bool GN, bool RES, int KR, bool Q = false, int NW = 8>
-__global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
+template <bool FLIP, bool GN, bool RES, int KR, bool Q = false>
+__global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                               bf16* __restrict__ y, const bf16* __restrict__ res,
                                                               const float* __restrict__ gstat,
                                                               const float* __restrict__ gamma,
@@ -124,10 +124,6 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
   // backward of that prologue's GroupNorm starts in the epilogue — res = x (the forward's pre-GroupNorm input), and
   // per channel (sum g, sum g*xhat) of g = relu-mask * dA go to spart[workgroup][32][2] (u3d_gn_bwd_parts finishes)
   constexpr bool PRO = GN && !FLIP, GB = GN && FLIP, LDR = RES || GB;
-  // NW = 4 (round 5): one wave per SIMD, each wave two h-rows of the 8-row tile — every weight fragment read from
-  // LDS serves 8 MFMAs instead of 4 (4 + 2 fragment reads per 8 MFMAs instead of 2 + 2 per 4)
-  constexpr int NT = NW * 64, LD = (RG_NR * 4 + NT - 1) / NT, R = 8 / NW;
-  static_assert(NW == 8 || (NW == 4 && !Q), "NW = 4: static schedule only");
   static_assert(!(GB && (Q || RES)), "the fused GroupNorm backward runs on the static data-gradient ring only");
   __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024 + 512 + (GB ? 576 : 0)];
   char* const ring = smem;
@@ -209,7 +205,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     walk.zlast = 0;  // forces start_run on the first next()
   }
 
-  for (int i = tid; i < RG_NWR * 4; i += NT) {  // weights: plane c, row t*32 + co
+  for (int i = tid; i < RG_NWR * 4; i += RG_NT) {  // weights: plane c, row t*32 + co
     const int c = i / RG_NWR, row = i % RG_NWR;
     *reinterpret_cast<u32x4*>(wts + (c * RG_NWR + row) * 16) = *reinterpret_cast<const u32x4*>(wpk + row * 32 + c * 8);
   }
@@ -233,24 +229,24 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
   // plus a wave-uniform plane base, and its in-volume test changes only with the column — per piece and plane one add
   // and one select instead of the integer address math (r04 stamps / ISA: issue slots the MFMA chain needs)
 #if RG_HOIST
-  int plo[LD];
+  int plo[RG_LD];
 #pragma unroll
-  for (int i = 0; i < LD; ++i) {
-    const int row = srow + i * (NT / 4);
+  for (int i = 0; i < RG_LD; ++i) {
+    const int row = srow + i * (RG_NT / 4);
     plo[i] = (((row / RG_HW) * g.w + row % RG_HW) * 64 + ch * 16);
   }
   unsigned pin = 0;
   int col_h0 = -1, col_w0 = -1;
 #endif
-  auto load_piece = [&](const RGPlane& p, int i, u32x4 (&v)[LD], unsigned& m) {
+  auto load_piece = [&](const RGPlane& p, int i, u32x4 (&v)[RG_LD], unsigned& m) {
 #if RG_HOIST
     if (i == 0 && p.valid && (p.h0 != col_h0 || p.w0 != col_w0)) {  // uniform: once per run of the walk
       col_h0 = p.h0;
       col_w0 = p.w0;
       pin = 0;
 #pragma unroll
-      for (int j = 0; j < LD; ++j) {
-        const int row = srow + j * (NT / 4);
+      for (int j = 0; j < RG_LD; ++j) {
+        const int row = srow + j * (RG_NT / 4);
         const bool ok = row < RG_NR && (unsigned)(p.h0 - 1 + row / RG_HW) < (unsigned)g.h &&
                         (unsigned)(p.w0 - 1 + row % RG_HW) < (unsigned)g.w;
         pin |= (ok ? 1u : 0u) << j;
@@ -260,7 +256,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     const bool ok = p.valid && (unsigned)p.zin < (unsigned)g.d && ((pin >> i) & 1u);
     const unsigned off = ok ? (unsigned)(base + plo[i]) : 0xFFFFFFF0u;
 #else
-    const int row = srow + i * (NT / 4);
+    const int row = srow + i * (RG_NT / 4);
     const int hw = row % RG_HW, hh = row / RG_HW;
     const int zh = p.h0 - 1 + hh, zw = p.w0 - 1 + hw;
     const bool ok = p.valid && row < RG_NR && (unsigned)p.zin < (unsigned)g.d && (unsigned)zh < (unsigned)g.h &&
@@ -270,9 +266,9 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     m = (i == 0 ? 0u : m) | ((ok ? 1u : 0u) << i);
   };
-  auto load_plane = [&](const RGPlane& p, u32x4 (&v)[LD], unsigned& m) {
+  auto load_plane = [&](const RGPlane& p, u32x4 (&v)[RG_LD], unsigned& m) {
 #pragma unroll
-    for (int i = 0; i < LD; ++i) load_piece(p, i, v, m);
+    for (int i = 0; i < RG_LD; ++i) load_piece(p, i, v, m);
   };
   auto gn_table = [&](const RGPlane& p) {
     if (PRO && p.valid && p.n != gn_n) {
@@ -281,7 +277,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     }
   };
   auto write_piece = [&](int i, const u32x4& v, unsigned m, int slot) {
-    const int row = srow + i * (NT / 4);
+    const int row = srow + i * (RG_NT / 4);
     u32x4 val = v;
     if constexpr (PRO) val = gn_relu8(v, sc, sh);
     if constexpr (PRO) if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
@@ -292,20 +288,17 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
   // A computed output plane waiting for its epilogue: the epilogue (bf16 pack, permlane swap, residual add,
   // stores) of plane k runs between the MFMAs of plane k+1, so it is off the per-plane critical path.
   struct Pending {
-    f32x4 a4[4 * R];  // [(row r * 2 + voxel block vb) * 2 + co block cb]
-    u32x4 rv[2 * R];  // residual of (row r, voxel block vb)
-    long long vox;    // row 0, voxel block 0 (row r: + r w)
-    bool ok[2 * R];   // (r, vb) inside the volume
+    f32x4 a4[4];   // [voxel block vb * 2 + co block cb]
+    u32x4 rv[2];   // residual of voxel blocks 0, 1
+    long long vox;
+    bool ok, ok1;  // voxel blocks 0 and 1 inside the volume
     int chunk;
   };
   Pending pend;
-#pragma unroll
-  for (int i = 0; i < 2 * R; ++i) {
-    pend.ok[i] = false;
-    pend.rv[i] = u32x4{0u, 0u, 0u, 0u};  // (GB reads them before the first computed plane)
-  }
+  pend.ok = pend.ok1 = false;
   pend.vox = 0;
   pend.chunk = -1;
+  pend.rv[0] = pend.rv[1] = u32x4{0u, 0u, 0u, 0u};  // (GB reads them before the first computed plane)
   // GroupNorm(16, 32) statistics of the output (GN variants = the forward convs whose outputs feed the next
   // GroupNorm), from the fp32 values just before the final bf16 rounding (no unpack; the voxel's in-volume flag
   // selects): 4 (sum, sum of squares) pairs per lane, fp32 over the lane's voxels, reduced per workgroup at the end.
@@ -351,8 +344,8 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
 #pragma unroll
       for (int j = 0; j < NSL; ++j) {
         const int grp = slot_group(j);
-        spart[((long long)c * (NT / 64) + wave) * 32 + grp * 2] = gs[j];
-        spart[((long long)c * (NT / 64) + wave) * 32 + grp * 2 + 1] = gq[j];
+        spart[((long long)c * (RG_NT / 64) + wave) * 32 + grp * 2] = gs[j];
+        spart[((long long)c * (RG_NT / 64) + wave) * 32 + grp * 2 + 1] = gq[j];
       }
     }
 #pragma unroll
@@ -371,15 +364,14 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     // voxel -> one 16-B store per voxel block.
     const int cbase = 16 * (q4 & 1) + 8 * (q4 >> 1);
 #pragma unroll
-    for (int i = 0; i < 2 * R; ++i) {
-      const int vb = i & 1, r = i >> 1;
-      const bool okv = p.ok[i];
+    for (int vb = 0; vb < 2; ++vb) {
+      const bool okv = vb ? p.ok1 : p.ok;
       if constexpr (PRO && !RES) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const float t = okv ? p.a4[i * 2 + cb][k] : 0.f;  // select: rows past the volume may be non-finite
+            const float t = okv ? p.a4[vb * 2 + cb][k] : 0.f;  // select: rows past the volume may be non-finite
             gs[2 * cb + (k >> 1)] += t;
             gq[2 * cb + (k >> 1)] = fmaf(t, t, gq[2 * cb + (k >> 1)]);
           }
@@ -388,7 +380,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-        for (int e = 0; e < 2; ++e) pk[cb][e] = pack_bf16x2(p.a4[i * 2 + cb][2 * e], p.a4[i * 2 + cb][2 * e + 1]);
+        for (int e = 0; e < 2; ++e) pk[cb][e] = pack_bf16x2(p.a4[vb * 2 + cb][2 * e], p.a4[vb * 2 + cb][2 * e + 1]);
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const auto sw = __builtin_amdgcn_permlane16_swap(pk[0][e], pk[1][e], false, false);
@@ -399,7 +391,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
       if constexpr (RES) {
         float a[8], c[8];
         load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
-        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[i]), c);
+        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[vb]), c);
 #pragma unroll
         for (int e = 0; e < 8; ++e) a[e] += c[e];
         if constexpr (GN) {
@@ -415,7 +407,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
       if constexpr (GB) {  // from the stored bf16 dA, as u3d_gn_bwd's partial pass reads it
         float a[8], xv[8];
         load16<bf16>(reinterpret_cast<const bf16*>(&v), a);
-        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[i]), xv);
+        load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[vb]), xv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const f32x4 t = gtab[cbase + (cbase >> 3) + e];
@@ -424,7 +416,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
           bs2[e] = fmaf(m ? a[e] : 0.f, m ? (xv[e] - t[3]) * t[2] : 0.f, bs2[e]);
         }
       }
-      if (okv) *reinterpret_cast<u32x4*>(y + (p.vox + (long long)r * g.w + 16 * vb) * 32 + cbase) = v;
+      if (okv) *reinterpret_cast<u32x4*>(y + (p.vox + 16 * vb) * 32 + cbase) = v;
     }
   };
 
@@ -439,28 +431,22 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     // consecutive channels of one voxel per (vb, cb). Fragments: lane (l16, q4) reads 16 B of chunk plane q4
     // (channels 8 q4 ..) of row l16 of the block: the 4 chunk planes of one row are one tap's K.
     const int zo = pc.zin - 1;
-    const int zh = pc.h0 + wave * R, zw = pc.w0 + l16;
+    const int zh = pc.h0 + wave, zw = pc.w0 + l16;
     Pending nw;
     nw.chunk = pc.chunk;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      nw.ok[2 * r] = zh + r < g.h && zw < g.w;
-      nw.ok[2 * r + 1] = zh + r < g.h && zw + 16 < g.w;
-    }
+    nw.ok = zh < g.h && zw < g.w;
+    nw.ok1 = zh < g.h && zw + 16 < g.w;
     nw.vox = (((long long)pc.n * g.d + zo) * g.h + zh) * g.w + zw;
-#pragma unroll
-    for (int i = 0; i < 2 * R; ++i) nw.rv[i] = u32x4{0u, 0u, 0u, 0u};
-    if constexpr (LDR) {  // the 16 B this lane stores after the swap, per (row, voxel block) (residual, or GB's x)
+    nw.rv[0] = nw.rv[1] = u32x4{0u, 0u, 0u, 0u};
+    if constexpr (LDR) {  // the 16 B this lane stores after the swap, per voxel block (residual, or GB's x)
       const int cb2 = 2 * (16 * (q4 & 1) + 8 * (q4 >> 1));
-#pragma unroll
-      for (int i = 0; i < 2 * R; ++i) {
-        const unsigned ro = nw.ok[i] ? (unsigned)((nw.vox + (long long)(i >> 1) * g.w + 16 * (i & 1)) * 64 + cb2)
-                                     : 0xFFFFFFC0u;
-        nw.rv[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, ro, 0, 0));
-      }
+      const unsigned r0 = nw.ok ? (unsigned)(nw.vox * 64 + cb2) : 0xFFFFFFC0u;
+      const unsigned r1 = nw.ok1 ? (unsigned)((nw.vox + 16) * 64 + cb2) : 0xFFFFFFC0u;
+      nw.rv[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, r0, 0, 0));
+      nw.rv[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rrs, r1, 0, 0));
     }
     const int sl[3] = {FLIP ? s2 : s0, s1, FLIP ? s0 : s2};
-    const char* ibase = ring + q4 * RG_PS + (wave * R * RG_HW + l16) * 16;
+    const char* ibase = ring + q4 * RG_PS + (wave * RG_HW + l16) * 16;
     const char* wbase = wts + (q4 * RG_NWR + l16) * 16;
     auto ioff = [&](int t) {
       const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
@@ -468,16 +454,13 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
       return sl[td] * RG_SS + (oh * RG_HW + ow) * 16;
     };
 #pragma unroll
-    for (int i = 0; i < 4 * R; ++i) nw.a4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) nw.a4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     constexpr int LA = 2;  // taps of fragments in flight
-    bf16x8 fi[LA + 1][2 * R], fw[LA + 1][2];
+    bf16x8 fi[LA + 1][2], fw[LA + 1][2];
     auto rd = [&](int t, int k) {
       const int o = ioff(t);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        fi[k][2 * r] = *reinterpret_cast<const bf16x8*>(ibase + o + r * RG_HW * 16);
-        fi[k][2 * r + 1] = *reinterpret_cast<const bf16x8*>(ibase + o + (r * RG_HW + 16) * 16);
-      }
+      fi[k][0] = *reinterpret_cast<const bf16x8*>(ibase + o);
+      fi[k][1] = *reinterpret_cast<const bf16x8*>(ibase + o + 16 * 16);
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int st = 2 * t + cb;
@@ -496,11 +479,11 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
       if constexpr (t == 15) epilogue(pend);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 2 * R; ++i)
+      for (int vb = 0; vb < 2; ++vb)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
-          nw.a4[i * 2 + cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t % (LA + 1)][cb], fi[t % (LA + 1)][i],
-                                                                      nw.a4[i * 2 + cb], 0, 0, 0);
+          nw.a4[vb * 2 + cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t % (LA + 1)][cb], fi[t % (LA + 1)][vb],
+                                                                       nw.a4[vb * 2 + cb], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     };
     __builtin_amdgcn_sched_barrier(0);
@@ -510,7 +493,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
 
   // step s: load plane s+1 into registers, write plane s (loaded during step s-1) into slot s&3, compute the
   // output whose triple ends at plane s-1, barrier. Unrolled by two so the register sets swap statically.
-  u32x4 va[LD], vb[LD];
+  u32x4 va[RG_LD], vb[RG_LD];
   unsigned ma = 0, mb = 0;
   auto set_range = [&](long long o0, long long o1) {
     walk.o_next = o0;
@@ -596,7 +579,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
   int s = 0;
   // The staged plane is written at the start of the step, BEFORE the next plane's loads are issued: its loads
   // (a full step old) are then the oldest in flight, so no wait inside the MFMA chain can fall on a young load.
-  auto step = [&](u32x4 (&vcur)[LD], unsigned& mcur, u32x4 (&vnxt)[LD], unsigned& mnxt) {
+  auto step = [&](u32x4 (&vcur)[RG_LD], unsigned& mcur, u32x4 (&vnxt)[RG_LD], unsigned& mnxt) {
     if constexpr (Q) {
       if (nxt == -2) nxt = qslot[2];
       if (check >= 0) {  // verdict of the claim issued two steps ago; its first plane is pc now
@@ -625,11 +608,11 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     gn_table(pw);
     const int slot = s & 3;
     const RGPlane pl = next_plane();  // plane s+1
-    // side work of the step, k = 0 .. 2 LD - 1: even k writes staged piece k/2 of plane s into slot s & 3 (its
+    // side work of the step, k = 0 .. 2 RG_LD - 1: even k writes staged piece k/2 of plane s into slot s & 3 (its
     // loads were issued a full step ago), odd k issues the load of piece k/2 of plane s + 1
     auto side = [&](auto kc) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value;
-      if constexpr (k >= 0 && k < 2 * LD) {
+      if constexpr (k >= 0 && k < 2 * RG_LD) {
         if constexpr ((k & 1) == 0) {
           if (pw.valid) write_piece(k >> 1, vcur[k >> 1], mcur, slot);
         } else {
@@ -641,7 +624,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     if (pc.valid && pc.out) {
       compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 0>{}, side);
     } else {
-      static_for<0, 2 * LD>(side);
+      static_for<0, 2 * RG_LD>(side);
     }
     ps.lap((pc.valid && pc.out) ? 0 : 1);
     ps.step(pc.valid && pc.out);
@@ -695,7 +678,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     if (tid < 64) {
       float t = 0.f;
 #pragma unroll
-      for (int wv = 0; wv < NT / 64; ++wv) t += red[wv * 64 + tid];
+      for (int wv = 0; wv < RG_NT / 64; ++wv) t += red[wv * 64 + tid];
       if (g.fcnt)  // write-through: the finalizing workgroup reads it in this launch
         __hip_atomic_store(spart + (long long)bid * 64 + tid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
@@ -717,11 +700,11 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
       __syncthreads();
       if (!s_last) return;
       double* const cs = reinterpret_cast<double*>(ring);  // [n * 32][2]
-      lastarriver_rowsum<NT>(spart, g.n, g.wps, 64, cs);
+      lastarriver_rowsum<RG_NT>(spart, g.n, g.wps, 64, cs);
       __syncthreads();
       const int gcpg = 32 / g.gn_groups;
       const double M = (double)g.d * g.h * g.w * gcpg;
-      for (int pr = tid; pr < g.n * 32; pr += NT) {
+      for (int pr = tid; pr < g.n * 32; pr += RG_NT) {
         const int nn = pr >> 5, c = pr & 31, gr = c / gcpg;
         double a = 0, bb = 0;
         for (int k2 = 0; k2 < gcpg; ++k2) {
@@ -773,7 +756,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
     if (tid < 32) {
       float t = 0.f;
 #pragma unroll
-      for (int wv = 0; wv < NT / 64; ++wv) t += red[wv * 32 + tid];
+      for (int wv = 0; wv < RG_NT / 64; ++wv) t += red[wv * 32 + tid];
       if (g.fcnt)  // write-through: the finalizing workgroup reads it in this launch
         __hip_atomic_store(spart + (long long)bid * 32 + tid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
@@ -794,10 +777,10 @@ __global__ __launch_bounds__(NW * 64, 1) void conv32_ring_kernel(const bf16* __r
       __syncthreads();
       if (s_last) {
         double* const cs = reinterpret_cast<double*>(ring) + 2048;  // [n * 16][2] (past the stats rows in `red`)
-        lastarriver_rowsum<NT>(spart, g.n, g.wps, 32, cs);
+        lastarriver_rowsum<RG_NT>(spart, g.n, g.wps, 32, cs);
         __syncthreads();
         const double m = 2.0 * g.d * g.h * g.w;
-        for (int p = tid; p < g.n * 16; p += NT) {
+        for (int p = tid; p < g.n * 16; p += RG_NT) {
           const double mean = cs[2 * p] / m;
           double var = cs[2 * p + 1] / m - mean * mean;
           if (var < 0) var = 0;
@@ -871,18 +854,6 @@ static int ring_kr(int dflt) {  // RING_KR = 0: no weight steps in registers (ex
 }
 
 static int ring_wgs() { return std::max(1, opt(OPT_RING_WGS)); }  // persistent grid target: one workgroup per CU
-// RING_NW = 4 (round 5): the static GN forward / GN data-gradient rings as 4-wave workgroups (one wave per SIMD, two
-// h-rows per wave); weight fragments held in registers: RG4_KR_* (of 54)
-static int ring_nw() { return opt(OPT_RING_NW) == 4 ? 4 : 8; }
-#ifndef RG4_KR_FWD
-#define RG4_KR_FWD 54
-#endif
-#ifndef RG4_KR_RES
-#define RG4_KR_RES 54
-#endif
-#ifndef RG4_KR_GB
-#define RG4_KR_GB 32
-#endif
 static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
                             const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                             const void* residual, void* y, float* stats_out, float* stats_ws, u3d_stream_t stream,
@@ -921,16 +892,6 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
   U3D_REQUIRE(!(flip && (gn_stats || residual)), "conv32_ring: the data gradient takes no prologue / residual");
   // register budget (2 waves per SIMD): GN + residual holds 12 weight steps, GN 16, the others 27
   const bool kr = ring_kr(1) != 0;
-  if (!flip && gn_stats && ring_nw() == 4) {
-#define RG4_LAUNCH(R, K)                                                                                             \
-  hipLaunchKernelGGL((conv32_ring_kernel<false, true, R, K, false, 4>), dim3((unsigned)grid), dim3(256), 0, s,      \
-                     (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, \
-                     sp, g)
-    if (residual) RG4_LAUNCH(true, RG4_KR_RES);
-    else RG4_LAUNCH(false, RG4_KR_FWD);
-#undef RG4_LAUNCH
-    return check_launch("conv32_ring_kernel");
-  }
   if (flip) RG_KR(true, false, false, 27);
   else if (gn_stats && residual) RG_KR(false, true, true, 12);  // + the statistics accumulators: 12 steps
   else if (gn_stats) RG_KR(false, true, false, 16);  // (12 measured equal: 124.6 vs 124.8 us)
@@ -1132,11 +1093,7 @@ static int ring_dgrad_gn_impl(const void* dy, int n, int d, int h, int w, const 
   hipLaunchKernelGGL((conv32_ring_kernel<true, true, false, K>), dim3((unsigned)grid), dim3(RG_NT), 0,         \
                      (hipStream_t)stream, (const bf16*)dy, (const bf16*)wpk_dgrad, (bf16*)da, (const bf16*)x,  \
                      gn_stats, gn_gamma, gn_beta, parts, g)
-  if (ring_nw() == 4)
-    hipLaunchKernelGGL((conv32_ring_kernel<true, true, false, RG4_KR_GB, false, 4>), dim3((unsigned)grid), dim3(256),
-                       0, (hipStream_t)stream, (const bf16*)dy, (const bf16*)wpk_dgrad, (bf16*)da, (const bf16*)x,
-                       gn_stats, gn_gamma, gn_beta, parts, g);
-  else if (kr) RG_GB(U3D_RING_GB_KR);
+  if (kr) RG_GB(U3D_RING_GB_KR);
   else RG_GB(0);
 #undef RG_GB
   return check_launch("conv32_ring_dgrad_gn");
