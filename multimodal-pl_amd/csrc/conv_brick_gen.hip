@@ -850,29 +850,48 @@ __global__ __launch_bounds__(GB_NT, 1) void convg_pbrick_kernel(const bf16* __re
 }
 
 // GroupNorm(16) (mean, rstd) of the persistent brick conv's output from its per-unit channel-pair partials
-// spart[unit][CO / 2][2] (unit = brick * nct + co tile): one wave per (sample, group), lanes strided over the
-// sample's bricks, pairs summed in order, fp64 butterfly in fixed order (deterministic)
-__global__ __launch_bounds__(64) void pbrick_gn_finalize_kernel(const double* __restrict__ spart, int co_tile, int nct,
-                                                               int bricks_per_sample, int cout, double m,
-                                                               float* __restrict__ stats) {
-  const int p = blockIdx.x, nn = p / 16, gr = p % 16, cpg = cout / 16;
+// spart[unit][CO / 2][2] (unit = brick * nct + co tile): one 256-thread block per (sample, group), item k = (brick
+// k / npg, pair k % npg) of the sample, threads strided over the items with 8 loads in flight (r05: one wave with a
+// dependent load per item), the wave butterflies, then the 4 waves in order (fixed order: deterministic)
+__global__ __launch_bounds__(256) void pbrick_gn_finalize_kernel(const double* __restrict__ spart, int co_tile, int nct,
+                                                                int bricks_per_sample, int cout, double m,
+                                                                float* __restrict__ stats) {
+  __shared__ double red[4][2];
+  const int p = blockIdx.x, nn = p / 16, gr = p % 16, cpg = cout / 16, npg = cpg / 2, tid = threadIdx.x;
+  const int nk = bricks_per_sample * npg;
   double s1 = 0, s2 = 0;
-  for (int b = threadIdx.x; b < bricks_per_sample; b += 64) {
-    const long long brick = (long long)nn * bricks_per_sample + b;
-    for (int c = gr * cpg; c < (gr + 1) * cpg; c += 2) {
-      const int ct = c / co_tile, cl = c - ct * co_tile;
-      const double* q = spart + ((brick * nct + ct) * co_tile + cl);
-      s1 += q[0];
-      s2 += q[1];
+  for (int k0 = tid; k0 < nk; k0 += 8 * 256) {
+    double2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u * 256;
+      if (k < nk) {
+        const int b = k / npg, c = gr * cpg + 2 * (k - b * npg), ct = c / co_tile, cl = c - ct * co_tile;
+        v[u] = *reinterpret_cast<const double2*>(spart + ((((long long)nn * bricks_per_sample + b) * nct + ct) * co_tile + cl));
+      } else {
+        v[u] = make_double2(0.0, 0.0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s1 += v[u].x;
+      s2 += v[u].y;
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
     s1 += __shfl_xor(s1, o);
     s2 += __shfl_xor(s2, o);
   }
-  if (threadIdx.x == 0) {
-    const double mean = s1 / m;
-    double var = s2 / m - mean * mean;
+  if ((tid & 63) == 0) {
+    red[tid >> 6][0] = s1;
+    red[tid >> 6][1] = s2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double t1 = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
+    const double t2 = ((red[0][1] + red[1][1]) + red[2][1]) + red[3][1];
+    const double mean = t1 / m;
+    double var = t2 / m - mean * mean;
     if (var < 0) var = 0;
     stats[p * 2] = (float)mean;
     stats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
@@ -986,7 +1005,7 @@ static int convg_impl(int flip, const void* x, int n, int cin, int d, int h, int
     int rc = check_launch("convg_pbrick_kernel");
     if (rc) return rc;
     if (!spart || fcnt) return rc;  // (fcnt: finalized by the kernel's last-arriving workgroup)
-    hipLaunchKernelGGL(pbrick_gn_finalize_kernel, dim3(n * 16), dim3(64), 0, s, (const double*)spart, co64 ? 64 : 32, gp.nct,
+    hipLaunchKernelGGL(pbrick_gn_finalize_kernel, dim3(n * 16), dim3(256), 0, s, (const double*)spart, co64 ? 64 : 32, gp.nct,
                        gp.nbd * gp.nbh * gp.nbw, cout, (double)(cout / 16) * d * h * w, stats_out);
     return check_launch("pbrick_gn_finalize_kernel");
   }

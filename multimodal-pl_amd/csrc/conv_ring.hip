@@ -205,9 +205,20 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     walk.zlast = 0;  // forces start_run on the first next()
   }
 
-  for (int i = tid; i < RG_NWR * 4; i += RG_NT) {  // weights: plane c, row t*32 + co
-    const int c = i / RG_NWR, row = i % RG_NWR;
-    *reinterpret_cast<u32x4*>(wts + (c * RG_NWR + row) * 16) = *reinterpret_cast<const u32x4*>(wpk + row * 32 + c * 8);
+  {  // weights: plane c, row t*32 + co. Every load of a thread is issued before its first LDS store (r05 stamps: the
+     // rolled loop waited on each of its 7 loads in turn, ~10 us of every launch's prologue)
+    constexpr int NWL = (RG_NWR * 4 + RG_NT - 1) / RG_NT;
+    u32x4 wl[NWL];
+#pragma unroll
+    for (int k = 0; k < NWL; ++k) {
+      const int i = tid + k * RG_NT, c = i / RG_NWR, row = i % RG_NWR;
+      if (i < RG_NWR * 4) wl[k] = *reinterpret_cast<const u32x4*>(wpk + row * 32 + c * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < NWL; ++k) {
+      const int i = tid + k * RG_NT;
+      if (i < RG_NWR * 4) *reinterpret_cast<u32x4*>(wts + i * 16) = wl[k];  // (c * RG_NWR + row = i)
+    }
   }
   // k16 step st = (tap t = st >> 1, half s = st & 1): this lane's weight fragment is W[t][co = r][16s + 8h ..]
   // weight fragment st = (tap st >> 1, co block st & 1): W[t][co = 16 (st & 1) + l16][8 q4 ..] (whole taps only)
@@ -474,6 +485,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     for (int k = 0; k < LA; ++k) rd(k, k);
     auto tstep = [&](auto tc) {
       constexpr int t = decltype(tc)::value;
+      progress_prio<t, 27>();
       if constexpr (t + LA < 27) rd(t + LA, (t + LA) % (LA + 1));
       side(std::integral_constant<int, t - 1>{});
       if constexpr (t == 15) epilogue(pend);

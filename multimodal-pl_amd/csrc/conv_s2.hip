@@ -137,10 +137,19 @@ __global__ __launch_bounds__(S2_NT, 1) void conv_s2_ring_kernel(const bf16* __re
     const int t = j < 9 ? j : j + 9;
     wreg[j] = *reinterpret_cast<const bf16x8*>(wpk + ((t * 64 + 16 * cb + l16) * 32 + 8 * q4));
   }
-  for (int i = tid; i < 9 * 64 * 4; i += S2_NT) {  // kd = 1 taps: row (t - 9) * 64 + co, chunk plane c
-    const int c = i & 3, row = i >> 2;
-    *reinterpret_cast<u32x4*>(wts + c * WPL + row * 16) =
-        *reinterpret_cast<const u32x4*>(wpk + ((9 * 64 + row) * 32 + c * 8));
+  {  // kd = 1 taps: row (t - 9) * 64 + co, chunk plane c; all of a thread's loads issued before its stores
+    constexpr int NWL = (9 * 64 * 4 + S2_NT - 1) / S2_NT;
+    u32x4 wl[NWL];
+#pragma unroll
+    for (int k = 0; k < NWL; ++k) {
+      const int i = tid + k * S2_NT;
+      if (i < 9 * 64 * 4) wl[k] = *reinterpret_cast<const u32x4*>(wpk + ((9 * 64 + (i >> 2)) * 32 + (i & 3) * 8));
+    }
+#pragma unroll
+    for (int k = 0; k < NWL; ++k) {
+      const int i = tid + k * S2_NT;
+      if (i < 9 * 64 * 4) *reinterpret_cast<u32x4*>(wts + (i & 3) * WPL + (i >> 2) * 16) = wl[k];
+    }
   }
   const char* const wb1 = wts + q4 * WPL + (16 * cb + l16) * 16;  // + (t - 9) * 64 * 16
 
