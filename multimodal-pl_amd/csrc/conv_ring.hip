@@ -38,8 +38,8 @@ constexpr int RG_NWR = 27 * 32;                      // weight rows (t, co)
 #ifndef RG_HOIST
 #define RG_HOIST 1
 #endif
-// -DU3D_STAMPS phases (diag.h): 0 compute steps (MFMAs + the staging side work between them), 1 steps without compute,
-// 2 the barriers
+// -DU3D_STAMPS phases (diag.h): 0 the steps' MFMAs + the staging side work between them, 1 the steps' heads (claims,
+// GN table, walk), 2 the barriers
 U3D_STAMP_BUFFER(rg_stamps, 2048, u3d_diag_ring_stamps)
 
 struct RGGeom {
@@ -632,13 +632,13 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         }
       }
     };
-    ps.mark_now();
+    ps.lap(1);  // phase 1: the step's head (claims, GN table, walk) since the previous barrier
     if (pc.valid && pc.out) {
       compute(pc, (s - 3) & 3, (s - 2) & 3, (s - 1) & 3, std::integral_constant<int, 0>{}, side);
     } else {
       static_for<0, 2 * RG_LD>(side);
     }
-    ps.lap((pc.valid && pc.out) ? 0 : 1);
+    ps.lap(0);  // phase 0: the step's MFMAs and staging (compute-less steps included)
     ps.step(pc.valid && pc.out);
     __syncthreads();
     ps.lap(2);

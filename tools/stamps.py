@@ -56,7 +56,7 @@ if s2:
 elif ring:
     assert h.u3d_diag_ring_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_longlong(buf.nbytes)) == 0
     nwg = 256
-    names = ("compute steps", "no-compute steps", "barrier")
+    names = ("steps", "step heads", "barrier")
 else:
     assert h.u3d_diag_wgrad_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_longlong(buf.nbytes)) == 0
     nwg = _lib.query("u3d_conv_wgrad_ring_splits", 2, c, s, s, s, c) * (ops.round32(c) // 32) ** 2
