@@ -130,6 +130,8 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   char* const wts = smem + 4 * RG_SS;
   char* const junk = wts + 4 * RG_NWR * 16;  // target of the staging lanes past the plane's last row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  PhaseStamps ps;  // (from kernel entry: "other" = the weight prologue and the last plane's epilogue)
+  ps.begin();
   diag_prio_second_half(wave);
   // staging: fixed 8-channel chunk (plane) per thread, 8 threads = 8 consecutive rows of one plane (a wave covers 16
   // whole rows = 1 KB of contiguous voxels per load)
@@ -485,7 +487,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     for (int k = 0; k < LA; ++k) rd(k, k);
     auto tstep = [&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      progress_prio<t, 27>();
       if constexpr (t + LA < 27) rd(t + LA, (t + LA) % (LA + 1));
       side(std::integral_constant<int, t - 1>{});
       if constexpr (t == 15) epilogue(pend);
@@ -582,8 +583,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
     return p;
   };
-  PhaseStamps ps;
-  ps.begin();
   RGPlane pw = next_plane();  // plane 0
   load_plane(pw, va, ma);
   __syncthreads();            // weights visible

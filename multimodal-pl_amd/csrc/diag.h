@@ -69,21 +69,6 @@ struct PhaseStamps {
 #define U3D_STAMP_BUFFER(NAME, WGS, READER) static constexpr unsigned long long* NAME = nullptr;
 #endif
 
-// Progress priority (round 5): at step position POS of N, a wave sets its issue priority to 3 - 4 POS / N, so of
-// the two waves sharing a SIMD the one further behind in the step issues first. Without it the older wave runs ahead
-// and then waits at the step barrier for ~30% of its time while the younger one runs alone (stamps, r05_k). Compiled
-// in unless -DU3D_PPRIO=0.
-#ifndef U3D_PPRIO
-#define U3D_PPRIO 1
-#endif
-template <int POS, int N>
-__device__ __forceinline__ void progress_prio() {
-#if U3D_PPRIO
-  constexpr int q = 4 * POS / N, pq = POS == 0 ? -1 : 4 * (POS - 1) / N;
-  if constexpr (q != pq) __builtin_amdgcn_s_setprio(3 - q);
-#endif
-}
-
 // static priority 1 for waves 4..7 of an 8-wave workgroup (-DU3D_PRIO builds)
 __device__ __forceinline__ void diag_prio_second_half(int wave) {
 #ifdef U3D_PRIO

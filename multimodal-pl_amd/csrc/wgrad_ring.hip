@@ -669,7 +669,6 @@ __global__ __launch_bounds__(WR_NT, 1) void wgrad_ring_dma_kernel(const bf16* __
     __builtin_amdgcn_sched_barrier(0);
     sfor<0, 2 * KS2>([&](auto uc) {
       constexpr int u = decltype(uc)::value, ks = u >> 1, cib = u & 1;
-      progress_prio<u, 2 * KS2>();
       if constexpr (u + WD_LA < 2 * KS2) {
         if constexpr (((u + WD_LA) & 1) == 0) rdA((u + WD_LA) >> 1);
         rdB(u + WD_LA);
