@@ -45,11 +45,17 @@ struct WBatch {
   D d[U3D_WSTD_BATCH_MAX];
 };
 
+// the descriptor whose block range holds blk (b0 ascending): binary search over the kernel-argument batch (the linear
+// walk was up to 48 dependent scalar loads at the start of every block)
 template <typename B>
 __device__ __forceinline__ int find_desc(const B& bt, int blk) {
-  int i = 0;
-  while (i + 1 < bt.count && bt.d[i + 1].b0 <= blk) ++i;
-  return i;
+  int lo = 0, hi = bt.count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (bt.d[mid].b0 <= blk) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
 }
 
 template <typename T>
@@ -383,10 +389,14 @@ __global__ __launch_bounds__(WG_T) void wstd_grad_kernel(WBatch<WPack> bt) {
 // row sums (fp32 per thread in a fixed order, fp64 across the block in a fixed order) and dW from the same registers.
 // One load round-trip per row instead of the chunk stage / barrier chain of wstd_grad_kernel, whose 64-block launch
 // of a 256x256 layer took 44 us (latency-bound, r04 trace); wstd_grad_kernel stays for rows longer than 56 x 256.
+// (round 5) the row of g is read coalesced in its [t][ci] order into LDS and re-read per thread in parameter order
+// [ci][t] (the per-element gather read one float per 4 KB+ stride: the kernel ran at ~2.5 TB/s of useful bytes)
+constexpr int WROW_MAXK = 56 * 256;  // the largest row the row kernel takes (NPT <= 56)
 template <int NPT>
 __global__ __launch_bounds__(WB_T) void wstd_grad_row_kernel(WBatch<WPack> bt) {
   __shared__ double red[WB_T / 64][2];
   __shared__ float fs[2];
+  __shared__ float gl[NPT * WB_T];
   const WPack& D = bt.d[find_desc(bt, blockIdx.x)];
   const int co = blockIdx.x - D.b0, tid = threadIdx.x;
   const int K3 = D.k3, K = D.cin * K3, cout_p = round_up(D.cout, 32), cin_p = round_up(D.cin, 32);
@@ -395,13 +405,31 @@ __global__ __launch_bounds__(WB_T) void wstd_grad_row_kernel(WBatch<WPack> bt) {
   const float rsg = std_ ? 1.f / D.st[co * 2 + 1] : 1.f;
   const float* wr = D.w + (long long)co * K;
   float wv[NPT], gv[NPT];
+  {  // g[t][co][ci], element j = t * cin + ci -> LDS slot ci * K3 + t (parameter order)
+    float gt[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int j = tid + i * WB_T;
+      const int t = j / D.cin, ci = j - t * D.cin;
+      gt[i] = j < K ? D.g[((long long)t * cout_p + co) * cin_p + ci] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int j = tid + i * WB_T;
+      const int t = j / D.cin, ci = j - t * D.cin;
+      if (j < K) gl[ci * K3 + t] = gt[i];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
     const int e = tid + i * WB_T;
-    const int ci = K3 == 27 ? e / 27 : e, t = e - ci * K3;
-    const bool in = e < K;
-    wv[i] = in && std_ ? wr[e] : 0.f;
-    gv[i] = in ? D.g[((long long)t * cout_p + co) * cin_p + ci] : 0.f;
+    wv[i] = e < K && std_ ? wr[e] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int e = tid + i * WB_T;
+    gv[i] = e < K ? gl[e] : 0.f;
   }
   float f1 = 0.f, f2 = 0.f;
   if (std_) {
