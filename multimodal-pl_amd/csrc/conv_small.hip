@@ -17,6 +17,7 @@
 //   * epilogue through LDS: coalesced 64-B voxel rows, residual added on the way out.
 // FLIP = data gradient: flipped tap offsets with the [t][ci][co] pack, no prologue.
 #include "common.h"
+#include "diag.h"
 
 namespace u3d {
 
@@ -64,6 +65,10 @@ struct SCGeom {
   float *coef, *dgamma, *dbeta;
 };
 
+// -DU3D_STAMPS phases (diag.h): 0 a chunk's MFMAs, 1 the next chunk's commit (GN + LDS writes) and its barrier, 2 the
+// barrier after the MFMAs; "other" = the first chunk's loads and commit (the epilogue is after the last stamp)
+U3D_STAMP_BUFFER(sc_stamps, 1024, u3d_diag_small_stamps)
+
 template <bool FLIP>
 __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                              bf16* __restrict__ y, const bf16* __restrict__ res,
@@ -74,6 +79,8 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
   char* const hal = smem;
   char* const wts = smem + 4 * SC_PS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  PhaseStamps ps;
+  ps.begin();
   const int r = lane & 31, hh = lane >> 5;
 
   int bid;  // XCD-aware: each XCD owns a contiguous range of (brick, co tile)
@@ -187,6 +194,8 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
       w_load(c + 1);
       stg_c = c + 1;
     }
+    ps.mark_now();
+    ps.step(true);
     if (active) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -203,12 +212,16 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
         }
       }
     }
+    ps.lap(0);
     __syncthreads();
+    ps.lap(2);
     if (more) {
       commit();
       __syncthreads();
+      ps.lap(1);
     }
   }
+  ps.end(sc_stamps, blockIdx.x & 1023, wave, lane);
   if (g.nks > 1) {  // fp32 partial through the wave's LDS tile: 128-B rows, coalesced
     float* const ept = reinterpret_cast<float*>(smem + wave * 4096);
     if (active) {

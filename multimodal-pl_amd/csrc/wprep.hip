@@ -391,7 +391,6 @@ __global__ __launch_bounds__(WG_T) void wstd_grad_kernel(WBatch<WPack> bt) {
 // of a 256x256 layer took 44 us (latency-bound, r04 trace); wstd_grad_kernel stays for rows longer than 56 x 256.
 // (round 5) the row of g is read coalesced in its [t][ci] order into LDS and re-read per thread in parameter order
 // [ci][t] (the per-element gather read one float per 4 KB+ stride: the kernel ran at ~2.5 TB/s of useful bytes)
-constexpr int WROW_MAXK = 56 * 256;  // the largest row the row kernel takes (NPT <= 56)
 template <int NPT>
 __global__ __launch_bounds__(WB_T) void wstd_grad_row_kernel(WBatch<WPack> bt) {
   __shared__ double red[WB_T / 64][2];

@@ -19,7 +19,8 @@ case = sys.argv[1] if len(sys.argv) > 1 else "wgrad96"
 secs = float(sys.argv[2]) if len(sys.argv) > 2 else 2.5
 ring = not case.startswith("wgrad")
 s2 = case.startswith("s2ring")
-s, c = {"96": (96, 32), "48": (48, 64), "24": (24, 128), "12": (12, 256)}[case[-2:]]
+small = case.startswith("small")
+s, c = {"96": (96, 32), "48": (48, 64), "24": (24, 128), "12": (12, 256), "06": (6, 256)}[case[-2:]]
 x = torch.randn((2, s, s, s, c), device=dev).to(torch.bfloat16)
 dy = torch.randn_like(x)
 gn = (ops.gn_stats(x, 16), torch.ones(c, device=dev), torch.zeros(c, device=dev), 16)
@@ -30,6 +31,13 @@ fn = {"wgrad": lambda: ops.conv_wgrad(dy, x, 3, 1, gn, brick="ring"),
       "fwdnores": lambda: ops.conv_fwd_stats(x, pf, c, 3, 1, gn),
       "dgradgn": lambda: ops.conv_dgrad_gn(dy, pd, c, x, 3, 1, gn),
       "dgrad": lambda: ops.conv_dgrad(dy, pd, c, x.shape[:4], 3, 1)}.get(case[:-2])
+if small:  # the small-volume conv (conv_small.hip) at 12^3 / 6^3, 256 -> 256 with the GN prologue
+    c = 256
+    x = torch.randn((2, s, s, s, c), device=dev).to(torch.bfloat16)
+    gn = (ops.gn_stats(x, 16), torch.ones(c, device=dev), torch.zeros(c, device=dev), 16)
+    w3 = torch.randn(c, c, 3, 3, 3, device=dev)
+    pf3, _, _ = ops.wstd_fwd(w3, torch.bfloat16, True, need_dgrad=False)
+    fn = lambda: ops.conv_fwd(x, pf3, c, 3, 1, gn)  # noqa: E731
 if s2:  # the stride-2 forward ring (conv_s2.hip): 32 -> 64
     w2 = torch.randn(64, 32, 3, 3, 3, device=dev)
     pf2, _, _ = ops.wstd_fwd(w2, torch.bfloat16, True, need_dgrad=False)
@@ -49,7 +57,11 @@ while time.time() - t0 < secs:
 us = e0.elapsed_time(e1) / 20 * 1e3
 buf = np.zeros(4096 * 8 * 8, dtype=np.uint64)
 h = _lib.lib()
-if s2:
+if small:
+    assert h.u3d_diag_small_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_longlong(buf.nbytes)) == 0
+    nwg = 1024
+    names = ("chunk MFMAs", "commit+barrier", "barrier")
+elif s2:
     assert h.u3d_diag_s2_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_longlong(buf.nbytes)) == 0
     nwg = 256
     names = ("write+load-wait", "compute", "barrier")
