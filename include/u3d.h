@@ -191,6 +191,15 @@ int u3d_head_fwd(const void* x, int n, long long v, int cin, const void* wpk, in
 int u3d_head_bwd_blocks(long long rows);
 int u3d_head_bwd(const float* dy, long long rows, int cout, const void* wpk_dgrad, int cin, void* dA, void* dy_bf16,
                  float* dbias_partials, u3d_stream_t stream);
+/* u3d_partial_loss_bwd (softmax, uce 1, C = 16 classes, fp32) fused into u3d_head_bwd on its result (round 5): the
+ * loss gradient is formed per voxel in registers and never stored; dA, dy_bf16 and dbias_partials equal the two calls'
+ * bit for bit. rows = S * V (the loss's voxel count); logits / labels / weights / sums / grad_out as for
+ * u3d_partial_loss_bwd, wpk_dgrad / cin / outputs as for u3d_head_bwd with cout = C.
+ * Replaces the pair EDiceLoss_partial.backward (loss_partial.py:59-99 through autograd) -> precls_conv backward
+ * (unet3D.py:1653-1657) for the bench's loss. */
+int u3d_head_loss_bwd(const float* logits, const float* labels, long long rows, int C, const float* weights,
+                      const double* sums, const float* grad_out, const void* wpk_dgrad, int cin, void* dA,
+                      void* dy_bf16, float* dbias_partials, u3d_stream_t stream);
 
 /* bf16 32->32 3^3 stride-1 conv (cin = cout = 32; the full-resolution layers) in halo-brick form with the
  * weights held in registers: flip=0 forward (wpk = forward pack, optional GN+ReLU prologue and residual),

@@ -22,6 +22,7 @@
 namespace u3d {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 
 // U3D_SC_NT = 512: one 8-wave workgroup of up to 256 output voxels per CU (105 KB of LDS); 256: 4-wave workgroups
 // of up to 128 voxels, two per CU (<= 80 KB each: smaller halo, GN table for cin <= 640)
@@ -68,6 +69,7 @@ struct SCGeom {
 // -DU3D_STAMPS phases (diag.h): 0 a chunk's MFMAs, 1 the next chunk's commit (GN + LDS writes) and its barrier, 2 the
 // barrier after the MFMAs; "other" = the first chunk's loads and commit (the epilogue is after the last stamp)
 U3D_STAMP_BUFFER(sc_stamps, 1024, u3d_diag_small_stamps)
+U3D_STAMP_BUFFER(sc_tail, 256, u3d_diag_small_tail)  // TailStamps: 16 per workgroup
 
 template <bool FLIP>
 __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
@@ -222,6 +224,7 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
     }
   }
   ps.end(sc_stamps, blockIdx.x & 1023, wave, lane);
+  TailStamps ts(sc_tail, blockIdx.x & 1023, tid == 0);
   if (g.nks > 1) {  // fp32 partial through the wave's LDS tile: 128-B rows, coalesced
     float* const ept = reinterpret_cast<float*>(smem + wave * 4096);
     if (active) {
@@ -251,12 +254,14 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
         }
       }
     }
+    ts.mark<1>();
     if (!g.cnt) return;  // the separate small_reduce_kernel sums the slabs
     // ---- in-kernel split-K combine (round 5): the workgroup that completes its output tile last sums the tile's
     // nks slabs in slab order (bitwise the small_reduce_kernel sums), adds the residual and stores y
     __shared__ unsigned s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
+    ts.mark<2>();
     const int tile = bid / g.nks;
     if (tid == 0) {
       const unsigned old = __hip_atomic_fetch_add(g.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -264,6 +269,7 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
       if (s_last) __hip_atomic_store(g.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    ts.mark<3>();
     if (!s_last) return;
     float ls[8], lq[8];
 #pragma unroll
@@ -283,63 +289,104 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
         b1[e] = b2[e] = 0.f;
       }
     }
+    // every load of the thread's 4 output pieces (nks slabs, residual, x) in flight before the first add: one memory
+    // round trip; then the adds in slab order
+    const int ypb = g.n * g.d * g.h * g.w * g.cout * 2;  // bytes of y / residual / x (host: < 2 GiB)
+    const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, res ? ypb : 0, 0x00020000);
+    const auto xrs2 = __builtin_amdgcn_make_buffer_rsrc((void*)g.gbx, 0, g.gbx ? ypb : 0, 0x00020000);
+    // with a second hand-off (statistics / GroupNorm-backward partials) the y stores wait until this workgroup's
+    // partials are published: its vmcnt(0) drain then covers only the partial store, not the tile's y stores
+    const bool defer_y = g.stats || g.gbx;
+    uint2 yv[4];
+    long long yoff[4];
+    bool yok[4];
+    auto store_y = [&]() {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int q = tid + SC_NT * k, vv = q >> 3, part = q & 7;
-      if (vv >= SC_MAXV) break;
-      const int uw = vv % g.bw, uh = (vv / g.bw) % g.bh, ud = vv / (g.bw * g.bh);
-      const int zd = o0d + ud, zh = o0h + uh, zw = o0w + uw, co = co0 + part * 4;
-      const bool ok = vv < g.nv && zd < g.d && zh < g.h && zw < g.w && co < g.cout;
-      const long long vo = ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cout + co;
-      f32x4 t[8];
+      for (int k = 0; k < 4; ++k)
+        if (yok[k]) *reinterpret_cast<uint2*>(y + yoff[k]) = yv[k];
+    };
+    auto combine = [&](auto nsc) {
+      constexpr int NS = decltype(nsc)::value;
+      static_assert(4 * SC_NT / 8 == SC_MAXV, "4 pieces of 4 channels per thread cover the brick's 32-channel tile");
+      f32x4 t[4][NS];
+      u32x2 rq[4], xq[4];
+      long long vo[4];
+      bool ok[4];
 #pragma unroll
-      for (int s_ = 0; s_ < 8; ++s_) {  // all slab loads in flight, then the adds in slab order
-        const bool in = ok && s_ < g.nks;
-        t[s_] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              srs, in ? (int)((s_ * per + vo) * 4) : (int)0xFFFFFFF0u, 0, 16));
+      for (int k = 0; k < 4; ++k) {
+        const int q = tid + SC_NT * k, vv = q >> 3, part = q & 7;
+        const int uw = vv % g.bw, uh = (vv / g.bw) % g.bh, ud = vv / (g.bw * g.bh);
+        const int zd = o0d + ud, zh = o0h + uh, zw = o0w + uw, co = co0 + part * 4;
+        ok[k] = vv < g.nv && zd < g.d && zh < g.h && zw < g.w && co < g.cout;
+        vo[k] = ok[k] ? ((((long long)nn * g.d + zd) * g.h + zh) * g.w + zw) * g.cout + co : 0;
+#pragma unroll
+        for (int s_ = 0; s_ < NS; ++s_) {
+          const bool in = ok[k] && s_ < g.nks;
+          t[k][s_] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   srs, in ? (int)((s_ * per + vo[k]) * 4) : (int)0xFFFFFFF0u, 0, 16));
+        }
+        const int yo = ok[k] ? (int)(vo[k] * 2) : (int)0xFFFFFFF0u;
+        if (res) rq[k] = __builtin_amdgcn_raw_buffer_load_b64(rrs, yo, 0, 0);
+        if (g.gbx) xq[k] = __builtin_amdgcn_raw_buffer_load_b64(xrs2, yo, 0, 0);
       }
-      if (!ok) continue;
-      f32x4 v = t[0];
 #pragma unroll
-      for (int s_ = 1; s_ < 8; ++s_)
-        if (s_ < g.nks) v += t[s_];
-      if (res) {
-        const uint2 rq = *reinterpret_cast<const uint2*>(res + vo);
-        v[0] += __uint_as_float(rq.x << 16);
-        v[1] += __uint_as_float(rq.x & 0xffff0000u);
-        v[2] += __uint_as_float(rq.y << 16);
-        v[3] += __uint_as_float(rq.y & 0xffff0000u);
-      }
-      uint2 o;
-      o.x = (uint32_t)from_f<bf16>(v[0]) | ((uint32_t)from_f<bf16>(v[1]) << 16);
-      o.y = (uint32_t)from_f<bf16>(v[2]) | ((uint32_t)from_f<bf16>(v[3]) << 16);
-      *reinterpret_cast<uint2*>(y + vo) = o;
-      if (g.gbx) {  // exactly gn_bwd_partial's per-element terms on the stored bf16 dA and x
-        const uint2 xq = *reinterpret_cast<const uint2*>(g.gbx + vo);
-        const float xv[4] = {__uint_as_float(xq.x << 16), __uint_as_float(xq.x & 0xffff0000u),
-                             __uint_as_float(xq.y << 16), __uint_as_float(xq.y & 0xffff0000u)};
-        const float dv[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
-                             __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
+      for (int k = 0; k < 4; ++k) {
+        yok[k] = false;
+        if (!ok[k]) continue;
+        const int part = (tid + SC_NT * k) & 7;
+        f32x4 v = t[k][0];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float xh = (xv[e] - bmu[e]) * brs[e];
-          const float gd = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? dv[e] : 0.f;
-          b1[e] += gd;
-          b2[e] = fmaf(gd, xh, b2[e]);
+        for (int s_ = 1; s_ < NS; ++s_)
+          if (s_ < g.nks) v += t[k][s_];
+        if (res) {
+          v[0] += __uint_as_float(rq[k][0] << 16);
+          v[1] += __uint_as_float(rq[k][0] & 0xffff0000u);
+          v[2] += __uint_as_float(rq[k][1] << 16);
+          v[3] += __uint_as_float(rq[k][1] & 0xffff0000u);
+        }
+        uint2 o;
+        o.x = (uint32_t)from_f<bf16>(v[0]) | ((uint32_t)from_f<bf16>(v[1]) << 16);
+        o.y = (uint32_t)from_f<bf16>(v[2]) | ((uint32_t)from_f<bf16>(v[3]) << 16);
+        if (defer_y) {
+          yv[k] = o;
+          yoff[k] = vo[k];
+          yok[k] = true;
+        } else {
+          *reinterpret_cast<uint2*>(y + vo[k]) = o;
+        }
+        if (g.gbx) {  // exactly gn_bwd_partial's per-element terms on the stored bf16 dA and x
+          const float xv[4] = {__uint_as_float(xq[k][0] << 16), __uint_as_float(xq[k][0] & 0xffff0000u),
+                               __uint_as_float(xq[k][1] << 16), __uint_as_float(xq[k][1] & 0xffff0000u)};
+          const float dv[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
+                               __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float xh = (xv[e] - bmu[e]) * brs[e];
+            const float gd = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? dv[e] : 0.f;
+            b1[e] += gd;
+            b2[e] = fmaf(gd, xh, b2[e]);
+          }
+        }
+        if (g.stats) {  // the stored values' group sums (4 channels of one group: cpg >= 4)
+          const float a0 = __uint_as_float(o.x << 16), a1 = __uint_as_float(o.x & 0xffff0000u);
+          const float a2 = __uint_as_float(o.y << 16), a3 = __uint_as_float(o.y & 0xffff0000u);
+          const float ss = (a0 + a1) + (a2 + a3), qq = (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+          const int gi = (part * 4) / cpg;
+#pragma unroll
+          for (int k2 = 0; k2 < 8; ++k2) {
+            ls[k2] += gi == k2 ? ss : 0.f;
+            lq[k2] += gi == k2 ? qq : 0.f;
+          }
         }
       }
-      if (g.stats) {  // the stored values' group sums (4 channels of one group: cpg >= 4)
-        const float a0 = __uint_as_float(o.x << 16), a1 = __uint_as_float(o.x & 0xffff0000u);
-        const float a2 = __uint_as_float(o.y << 16), a3 = __uint_as_float(o.y & 0xffff0000u);
-        const float ss = (a0 + a1) + (a2 + a3), qq = (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
-        const int gi = (part * 4) / cpg;
-#pragma unroll
-        for (int k2 = 0; k2 < 8; ++k2) {
-          ls[k2] += gi == k2 ? ss : 0.f;
-          lq[k2] += gi == k2 ? qq : 0.f;
-        }
-      }
-    }
+    };
+    if (g.nks <= 2)
+      combine(std::integral_constant<int, 2>{});
+    else if (g.nks <= 4)
+      combine(std::integral_constant<int, 4>{});
+    else
+      combine(std::integral_constant<int, 8>{});
+    ts.mark<4>();
     if (g.gbx) {
       // per channel of the tile over the workgroup: lanes with the same tid & 7 (xor 8, 16, 32), then the waves in order
 #pragma unroll
@@ -368,6 +415,7 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      ts.mark<5>();
       const int ntiles = (int)(gridDim.x / g.nks);
       if (tid == 0) {
         const unsigned old = __hip_atomic_fetch_add(g.cnt + ntiles, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -375,6 +423,8 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
         if (s_last) __hip_atomic_store(g.cnt + ntiles, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
+      ts.mark<6>();
+      store_y();
       if (!s_last) return;
       // gn_bwd_parts_finalize + gn_bwd_coefs: per (n, c) fp64 sums over the bricks in order, then the coefficients
       double* const cs = reinterpret_cast<double*>(smem);  // [n * cout][2] (<= 8192 doubles: host-checked)
@@ -409,6 +459,7 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
         if (g.dgamma) g.dgamma[c] = (float)tg;
         if (g.dbeta) g.dbeta[c] = (float)tb;
       }
+      ts.mark<7>();
       return;
     }
     if (!g.stats) return;
@@ -436,6 +487,7 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    ts.mark<5>();
     const int ntiles = (int)(gridDim.x / g.nks);
     if (tid == 0) {
       const unsigned old = __hip_atomic_fetch_add(g.cnt + ntiles, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -443,6 +495,8 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
       if (s_last) __hip_atomic_store(g.cnt + ntiles, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    ts.mark<6>();
+    store_y();
     if (!s_last) return;
     double* const cs = reinterpret_cast<double*>(smem) + 64;  // [n * 16][2] (past the wave rows in `red`)
     lastarriver_rowsum<SC_NT>(g.spart, g.n, nbr, 32, cs);
@@ -455,6 +509,7 @@ __global__ __launch_bounds__(SC_NT, 512 / SC_NT) void conv_small_kernel(const bf
       g.stats[p * 2] = (float)mean;
       g.stats[p * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
     }
+    ts.mark<7>();
     return;
   }
 
@@ -616,7 +671,7 @@ static int conv_small_impl(int flip, const void* x, int n, int cin, int d, int h
               "conv_small2: statistics form limits");
   const long long nwg = tiles * g.nks;
   U3D_REQUIRE(nwg < (1LL << 31), "conv_small: grid too large");
-  U3D_REQUIRE((long long)n * d * h * w * cin * 2 < (1LL << 31) - 64 && 27LL * g.cout_p * g.cin_p * 2 < (1LL << 31) - 64,
+  U3D_REQUIRE((long long)n * d * h * w * std::max(cin, cout) * 2 < (1LL << 31) - 64 && 27LL * g.cout_p * g.cin_p * 2 < (1LL << 31) - 64,
               "conv_small: operands beyond the 2 GiB buffer-offset range");
   hipStream_t s = (hipStream_t)stream;
   if (flip)

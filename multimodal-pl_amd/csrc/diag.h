@@ -50,6 +50,30 @@ struct PhaseStamps {
     }
   }
 };
+// Up to 8 s_memtime marks of one workgroup's tail (after its main loop), written by thread 0 when the object leaves
+// scope (any return path), with the s_memrealtime at that point: buf[wg * 16 + 0..7] marks (0 = not reached),
+// buf[wg * 16 + 8] the real time at exit.
+struct TailStamps {
+  unsigned long long t[8];
+  unsigned long long* buf;
+  int wg;
+  bool writer;
+  __device__ __forceinline__ TailStamps(unsigned long long* b, int w, bool wr) : buf(b), wg(w), writer(wr) {
+#pragma unroll
+    for (int i = 1; i < 8; ++i) t[i] = 0;
+    t[0] = stamp_clk();
+  }
+  template <int K>
+  __device__ __forceinline__ void mark() { t[K] = stamp_clk(); }
+  __device__ __forceinline__ ~TailStamps() {
+    const unsigned long long re = stamp_real();
+    if (writer) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) buf[(long long)wg * 16 + i] = t[i];
+      buf[(long long)wg * 16 + 8] = re;
+    }
+  }
+};
 // the buffer of WGS workgroups x 8 waves and its host reader
 #define U3D_STAMP_BUFFER(NAME, WGS, READER)                                                                   \
   __device__ unsigned long long NAME[(WGS) * 8 * 8];                                                          \
@@ -65,6 +89,11 @@ struct PhaseStamps {
   __device__ __forceinline__ void step(bool) {}
   __device__ __forceinline__ void settle(bool) {}
   __device__ __forceinline__ void end(unsigned long long*, int, int, int) {}
+};
+struct TailStamps {
+  __device__ __forceinline__ TailStamps(unsigned long long*, int, bool) {}
+  template <int K>
+  __device__ __forceinline__ void mark() {}
 };
 #define U3D_STAMP_BUFFER(NAME, WGS, READER) static constexpr unsigned long long* NAME = nullptr;
 #endif

@@ -9,6 +9,7 @@
 //   backward: dA[v][ci] = sum_co dy[v][co] W[co][ci] (bf16), plus dy in bf16 for the weight gradient and the
 //             per-block column sums of dy (bias gradient partials) — the fp32 dy is read once.
 #include "common.h"
+#include "loss_grad.h"
 
 namespace u3d {
 
@@ -275,6 +276,133 @@ __global__ __launch_bounds__(HD_T) void head_bwd_kernel(const float* __restrict_
   }
 }
 
+// The head's data gradient with the partial-label loss gradient formed in registers (the bench's loss: softmax over
+// 16 classes + per-class BCE): dlogits never reaches HBM (-2 x 113 MB per step at 2 x 96^3). Every lane loads its
+// voxel's 16 logits (lanes r and r + 32 the same 64 B: one request per line), forms the 16 gradients exactly as
+// loss_bwd_kernel (dice_bce_softmax_grad16) and keeps its 8; the rest is head_bwd_kernel's transposed path with the
+// same grid, so dA, the bf16 dy and the bias partials equal the two-kernel form's bit for bit. The next tile's logits
+// and label are loaded before this tile's math.
+__global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
+                                                            long long rows, const float* __restrict__ wt,
+                                                            const double* __restrict__ sums,
+                                                            const float* __restrict__ gout, const bf16* __restrict__ wpd,
+                                                            int cin, bf16* __restrict__ dA, bf16* __restrict__ dyb,
+                                                            float* __restrict__ dbp) {
+  constexpr int cout = 16, cout_p = 32;
+  __shared__ float red[HD_T / 64][32];
+  __shared__ float kd_a[16], kd_b[16], kb[16];
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  if (threadIdx.x < 16) {
+    float a, b, e;
+    dice_bce_coefs(threadIdx.x, 16, sums, wt, gout, 1, (double)rows, a, b, e);
+    kd_a[threadIdx.x] = a;
+    kd_b[threadIdx.x] = b;
+    kb[threadIdx.x] = e;
+  }
+  bf16x8 bw[2][2];  // [k-step][n-tile of 32 ci]
+  const int ntn = (cin + 31) / 32;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      const int ci = tn * 32 + r, co = 16 * s + 8 * h;
+      bw[s][tn] = (tn < ntn && co < cout_p)
+                      ? as_frag(*reinterpret_cast<const u32x4*>(wpd + (long long)ci * cout_p + co))
+                      : as_frag(u32x4{0u, 0u, 0u, 0u});
+    }
+  float colsum[2][8];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) colsum[s][e] = 0.f;
+  __syncthreads();
+  const long long tiles = (rows + 31) / 32;
+  const long long wid = (long long)blockIdx.x * (HD_T / 64) + wave;
+  const long long nw = (long long)gridDim.x * (HD_T / 64);
+  auto load = [&](long long tile, f32x4 (&q)[4], float& t) {  // clamped row, no branch around the loads
+    long long row = tile * 32 + r;
+    row = row < rows ? row : rows - 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + row * 16 + 4 * k);
+    t = lab[row];
+  };
+  f32x4 cur[4], nxt[4];
+  float tcur = 0.f, tnxt = 0.f;
+  load(wid, cur, tcur);
+  for (long long tile = wid; tile < tiles; tile += nw) {
+    load(tile + nw, nxt, tnxt);
+    const long long row = tile * 32 + r;
+    const bool ok = row < rows;
+    float gr[16];
+    dice_bce_softmax_grad16(cur, tcur, kd_a, kd_b, kb, gr);
+    u32x4 a[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = ok && s == 0 ? (h ? gr[8 + e] : gr[e]) : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) colsum[s][e] += f[e];
+      store16<bf16>(reinterpret_cast<bf16*>(&a[s]), f);
+      if (ok && s == 0) *reinterpret_cast<u32x4*>(dyb + row * cout + 8 * h) = a[s];
+    }
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      if (tn >= ntn) break;
+      f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[0][tn], as_frag(a[0]), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[1][tn], as_frag(a[1]), acc, 0, 0, 0);
+      uint32_t pk[4][2];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) pk[q][e] = pack_bf16x2(acc[4 * q + 2 * e], acc[4 * q + 2 * e + 1]);
+#pragma unroll
+      for (int q = 0; q < 4; q += 2)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(pk[q][e], pk[q + 1][e], false, false);
+          pk[q][e] = sw[0];
+          pk[q + 1][e] = sw[1];
+        }
+      if (ok) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int ci = tn * 32 + 16 * u + 8 * h;
+          if (ci < cin)
+            *reinterpret_cast<u32x4*>(dA + row * cin + ci) =
+                u32x4{pk[2 * u][0], pk[2 * u][1], pk[2 * u + 1][0], pk[2 * u + 1][1]};
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    tcur = tnxt;
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = colsum[s][e];
+      for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o, 32);
+      colsum[s][e] = t;
+    }
+  if (r == 0) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wave][16 * s + 8 * h + e] = colsum[s][e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float t = 0.f;
+    for (int w = 0; w < HD_T / 64; ++w) t += red[w][threadIdx.x];
+    if (threadIdx.x < cout) dbp[(long long)blockIdx.x * cout + threadIdx.x] = t;
+  }
+}
+
 // grid cap: 768 = three 4-wave blocks per CU, resident at once at the backward's 148 VGPRs (2048 ran it in 2.7
 // rounds). 2 x 96^3 x 32 -> 16 (tools/kbench.py headf96 / headb96, gpurun_out/r04_hd): forward 37.3 -> 36.0 us,
 // backward 62.2 -> 57.3 us; 1024 / 1280 blocks: backward 66-70 us
@@ -333,4 +461,20 @@ extern "C" int u3d_head_bwd(const float* dy, long long rows, int cout, const voi
   hipLaunchKernelGGL(head_bwd_kernel, dim3(head_blocks(rows)), dim3(HD_T), 0, (hipStream_t)stream, dy, rows, cout,
                      (const bf16*)wpk_dgrad, cout_p, cin, (bf16*)dA, (bf16*)dy_bf16, cout8, dbias_partials, tr);
   return check_launch("head_bwd_kernel");
+}
+
+// Fused form of u3d_partial_loss_bwd (softmax, uce 1, C = 16, fp32 dlogits) followed by u3d_head_bwd on the result
+// (cout = C): the same dA, bf16 dy and bias partials without the dlogits tensor. rows = S * V voxels (the loss's
+// count), logits / labels as u3d_partial_loss_bwd takes them (NDHWC fp32 logits, fp32 labels).
+extern "C" int u3d_head_loss_bwd(const float* logits, const float* labels, long long rows, int C, const float* weights,
+                                 const double* sums, const float* grad_out, const void* wpk_dgrad, int cin, void* dA,
+                                 void* dy_bf16, float* dbias_partials, u3d_stream_t stream) {
+  U3D_REQUIRE(logits && labels && weights && sums && grad_out && wpk_dgrad && dA && dy_bf16 && dbias_partials &&
+                  rows >= 1,
+              "head_loss_bwd: bad args");
+  U3D_REQUIRE(C == 16 && cin % 8 == 0 && cin >= 8 && cin <= 64, "head_loss_bwd: C %d (16 only) / cin %d", C, cin);
+  hipLaunchKernelGGL(head_loss_bwd_kernel, dim3(head_blocks(rows)), dim3(HD_T), 0, (hipStream_t)stream, logits, labels,
+                     rows, weights, sums, grad_out, (const bf16*)wpk_dgrad, cin, (bf16*)dA, (bf16*)dy_bf16,
+                     dbias_partials);
+  return check_launch("head_loss_bwd_kernel");
 }

@@ -7,6 +7,7 @@
 // Backward is one elementwise pass: dL/dp from the sums, then the softmax (or sigmoid) Jacobian.
 // Class counts the models use (2, 8, 14, 16) are compile-time so every per-voxel array stays in registers.
 #include "common.h"
+#include "loss_grad.h"
 
 namespace u3d {
 
@@ -244,16 +245,8 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
   __shared__ float kd_a[NC], kd_b[NC], kb[NC];
   if (threadIdx.x < NC) {
     const int c = threadIdx.x;
-    float a = 0.f, b = 0.f, e = 0.f;
-    if (c < C) {
-      const double I = sums[c * 4], Z = sums[c * 4 + 1], Y = sums[c * 4 + 2];
-      const double num = 2.0 * I + 1e-5, den = Z + Y + 1e-5;
-      const double scale = (double)wt[c] / C * gout[0];
-      // d(1 - num/den)/dp = -(2 t den - num * 2 p) / den^2  =  t * a + p * b
-      a = (float)(-2.0 / den * scale);
-      b = (float)(2.0 * num / (den * den) * scale);
-      e = uce == 1 ? (float)((double)wt[c] / count * gout[0]) : uce == 2 ? (float)(1.0 / count * gout[0]) : 0.f;
-    }
+    float a, b, e;
+    dice_bce_coefs(c, C, sums, wt, gout, uce, count, a, b, e);
     kd_a[c] = a;
     kd_b[c] = b;
     kb[c] = e;
@@ -276,36 +269,11 @@ __global__ __launch_bounds__(LT) void loss_bwd_kernel(const float* __restrict__ 
       load(v, cur, tcur);
       for (; v < nvox; v += stride) {
         load(v + stride, nxt, tnxt);
-        float x[16], p[16];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) x[4 * k + j] = cur[k][j];
-        float m = x[0];
-#pragma unroll
-        for (int c = 1; c < 16; ++c) m = fmaxf(m, x[c]);
-        float s = 0.f;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          p[c] = __builtin_amdgcn_exp2f((x[c] - m) * LOG2E);
-          s += p[c];
-        }
-        const float inv = __builtin_amdgcn_rcpf(s);
-#pragma unroll
-        for (int c = 0; c < 16; ++c) p[c] *= inv;
-        float g[16], dot = 0.f;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          const float tc = (tcur == (float)c) ? 1.f : 0.f;
-          float gc = fmaf(tc, kd_a[c], p[c] * kd_b[c]);
-          gc += kb[c] * (p[c] - tc) * __builtin_amdgcn_rcpf(fmaxf((1.f - p[c]) * p[c], 1e-12f));
-          g[c] = gc;
-          dot = fmaf(gc, p[c], dot);
-        }
+        float r[16];
+        dice_bce_softmax_grad16(cur, tcur, kd_a, kd_b, kb, r);
 #pragma unroll
         for (int c = 0; c < 16; c += 4)
-          *reinterpret_cast<f32x4*>(dl + v * 16 + c) = f32x4{p[c] * (g[c] - dot), p[c + 1] * (g[c + 1] - dot),
-                                                             p[c + 2] * (g[c + 2] - dot), p[c + 3] * (g[c + 3] - dot)};
+          *reinterpret_cast<f32x4*>(dl + v * 16 + c) = f32x4{r[c], r[c + 1], r[c + 2], r[c + 3]};
 #pragma unroll
         for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
         tcur = tnxt;

@@ -1,5 +1,6 @@
 """Autograd Function for the fused partial-label Dice + BCE loss (reference loss_partial.py:59-99)."""
 import torch
+from torch.utils import _pytree as pytree
 
 from . import ops
 
@@ -25,6 +26,42 @@ def class_weights(mask, C, device):
     return w.reshape(-1)[:C].to(device=device, dtype=torch.float32)
 
 
+class DeferredLossGrad(torch.Tensor):
+    """The partial loss's gradient w.r.t. the trunk's logits, handed back unformed when the logits came straight from
+    the streaming head (trunk._TrunkFn tags them): the trunk's backward passes it to the head, whose backward forms the
+    loss gradient in registers (ops.head_loss_bwd) — the fp32 dlogits tensor (113 MB at 2 x 96^3 x 16) is never
+    written or read. Anything else that touches it (a hook, torch.autograd.grad on the logits, a sum with another
+    gradient) goes through __torch_dispatch__, which forms the real gradient first (ops.partial_loss_bwd): every
+    reader sees the same values as without the hand-off."""
+
+    @staticmethod
+    def __new__(cls, like, make, payload, link):
+        shape, stride, dtype, device = like
+        r = torch.Tensor._make_wrapper_subclass(cls, shape, strides=stride, dtype=dtype, device=device)
+        r._make, r.payload, r.link, r._real = make, payload, link, None
+        return r
+
+    def unformed(self):
+        return self._real is None
+
+    def materialize(self):
+        if self._real is None:
+            self._real = self._make()
+            self.payload = None
+        return self._real
+
+    __torch_function__ = torch._C._disabled_torch_function_impl
+
+    @classmethod
+    def __torch_dispatch__(cls, func, types, args=(), kwargs=None):
+        def real(t):
+            return t.materialize() if isinstance(t, DeferredLossGrad) else t
+        return func(*pytree.tree_map(real, args), **pytree.tree_map(real, kwargs or {}))
+
+    def __repr__(self):
+        return f"DeferredLossGrad(shape={tuple(self.shape)}, formed={self._real is not None})"
+
+
 class _PartialLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, weights, mode, uce):
@@ -33,14 +70,23 @@ class _PartialLossFn(torch.autograd.Function):
         loss, sums = ops.partial_loss_fwd(lg, lab, weights, mode, uce)
         ctx.save_for_backward(lg, lab, weights, sums)
         ctx.mode, ctx.uce = mode, uce
+        link = getattr(logits, "_u3d_head_link", None)
+        ctx.link = (link if ops.HEAD_LOSS_FUSED and link is not None and mode == MODE_SOFTMAX and int(uce) == 1
+                    and lg.shape[-1] == 16 and lg.dtype == torch.float32 else None)
+        ctx.like = (tuple(logits.shape), tuple(logits.stride()), logits.dtype, logits.device)
         return loss.reshape(())
 
     @staticmethod
     def backward(ctx, g):
         lg, lab, weights, sums = ctx.saved_tensors
         go = g.reshape(1).float().contiguous()
-        dl = ops.partial_loss_bwd(lg, lab, weights, sums, go, ctx.mode, ctx.uce)
-        return dl.permute(0, 4, 1, 2, 3), None, None, None, None
+        mode, uce = ctx.mode, ctx.uce
+
+        def form():
+            return ops.partial_loss_bwd(lg, lab, weights, sums, go, mode, uce).permute(0, 4, 1, 2, 3)
+        if ctx.link is not None:
+            return DeferredLossGrad(ctx.like, form, (lg, lab, weights, sums, go), ctx.link), None, None, None, None
+        return form(), None, None, None, None
 
 
 def partial_loss(logits, target, weights, mode=MODE_SOFTMAX, uce=True):

@@ -746,6 +746,28 @@ def head_bwd(dy, wpk_dgrad, cin, dbias=None):
     return dA, dyb
 
 
+# the partial-label loss hands its gradient to the streaming head unformed (loss.DeferredLossGrad) and the head's
+# backward forms it in registers (u3d_head_loss_bwd): no fp32 dlogits tensor
+HEAD_LOSS_FUSED = os.environ.get("U3D_HEAD_LOSS_FUSED", "1") != "0"
+
+
+def head_loss_bwd(lg, lab, weights, sums, grad_out, wpk_dgrad, cin, dbias=None):
+    """head_bwd(partial_loss_bwd(lg, lab, weights, sums, grad_out)) for the softmax + BCE loss over 16 classes in one
+    pass (u3d_head_loss_bwd): lg fp32 NDHWC [S, ..., 16], lab fp32 [S, ...]; the same (dA, dy bf16) and bias gradient
+    bitwise, without the fp32 dlogits tensor."""
+    C = lg.shape[-1]
+    rows = lg.numel() // C
+    dA = torch.empty(tuple(lg.shape[:-1]) + (cin,), dtype=torch.bfloat16, device=lg.device)
+    dyb = torch.empty(tuple(lg.shape[:-1]) + (C,), dtype=torch.bfloat16, device=lg.device)
+    nb = query("u3d_head_bwd_blocks", rows)
+    dbp = torch.empty((nb, C), dtype=torch.float32, device=lg.device)
+    call("u3d_head_loss_bwd", lg.data_ptr(), lab.data_ptr(), rows, C, weights.data_ptr(), sums.data_ptr(),
+         grad_out.data_ptr(), wpk_dgrad.data_ptr(), cin, dA.data_ptr(), dyb.data_ptr(), dbp.data_ptr(), _stream())
+    if dbias is not None:
+        channel_sum(dbp, out=dbias)
+    return dA, dyb
+
+
 STEM_SLOT = 13  # the conv1 kernel's fp32 weight table
 STEM_WS_BYTES = 27 * 32 * 4  # = u3d_stem_fwd_ws_bytes() (tests/test_host.py); a constant so A/B runs load older builds
 

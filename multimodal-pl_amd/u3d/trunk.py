@@ -12,6 +12,7 @@ from dataclasses import dataclass
 import torch
 
 from . import ops
+from .loss import DeferredLossGrad
 
 
 @dataclass(frozen=True)
@@ -153,6 +154,8 @@ class Tape:
         else:
             y = ops.conv_fwd(x.t, pf, cout, k, stride, gn, residual.t if residual is not None else None, b, out_f32)
         out = Act(y)
+        if head and cout == 16:
+            self.head_out = out  # the partial loss may hand its gradient to this head unformed (_TrunkFn)
         if st16 is not None:
             out.stats[16] = st16  # GroupNorm(16) statistics from the conv epilogue (consumed by the next GN)
         if self.record:
@@ -165,7 +168,12 @@ class Tape:
                     return
                 if head:  # dA, bf16 dy and the bias gradient in one pass over the fp32 dlogits
                     db = self.grad_out(key + ".bias", b) if bias else None
-                    dA, dyT = ops.head_bwd(dy, pd, cin, dbias=db)
+                    if isinstance(dy, DeferredLossGrad):  # the loss gradient formed inside the head's pass
+                        lg_, lab_, wt_, sums_, go_ = dy.payload
+                        assert lg_.data_ptr() == y.data_ptr() and lg_.shape == y.shape, "deferred loss gradient: not this head's logits"
+                        dA, dyT = ops.head_loss_bwd(lg_, lab_, wt_, sums_, go_, pd, cin, dbias=db)
+                    else:
+                        dA, dyT = ops.head_bwd(dy, pd, cin, dbias=db)
                     if bias:
                         self.grad_done(key + ".bias")
                 else:
@@ -329,15 +337,25 @@ class _TrunkFn(torch.autograd.Function):
         f, _ = tape.trunk(x, cfg)
         lg = tape.head(f, cfg)
         ctx.tape, ctx.out, ctx.names = tape, lg, names
-        return lg.t.permute(0, 4, 1, 2, 3)
+        out = lg.t.permute(0, 4, 1, 2, 3)
+        ctx.link = None
+        if getattr(tape, "head_out", None) is lg:  # logits straight from the streaming head (no final upsample)
+            ctx.link = object()
+            out._u3d_head_link = ctx.link  # the partial loss hands its gradient back unformed (loss.DeferredLossGrad)
+        return out
 
     @staticmethod
     def backward(ctx, g):
-        g = g.permute(0, 2, 3, 4, 1)
-        if not g.is_contiguous():
-            g = g.contiguous()
         tape = ctx.tape
-        tape.backward(ctx.out, g.float())
+        if isinstance(g, DeferredLossGrad) and ctx.link is not None and g.link is ctx.link and g.unformed():
+            tape.backward(ctx.out, g)  # to the head's backward as is (ops.head_loss_bwd)
+        else:
+            if isinstance(g, DeferredLossGrad):
+                g = g.materialize()
+            g = g.permute(0, 2, 3, 4, 1)
+            if not g.is_contiguous():
+                g = g.contiguous()
+            tape.backward(ctx.out, g.float())
         if tape.sink is not None:
             tape.sink.finish()
         grads = [tape.pgrad.get(n) for n in ctx.names]

@@ -1,0 +1,93 @@
+"""The partial loss's gradient formed inside the head's backward (u3d_head_loss_bwd, loss.DeferredLossGrad): the same
+dA, bf16 dy and bias gradient as partial_loss_bwd + head_bwd bit for bit, the same parameter gradients for the whole
+step, and every other reader of the logits' gradient (a second loss term, a hook, autograd.grad) sees the formed
+tensor."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cin,dims", [(32, (2, 7, 9, 11)), (32, (2, 16, 16, 16)), (64, (1, 5, 6, 7)),
+                                      (16, (3, 4, 4, 5)), (32, (1, 1, 1, 3))])
+def test_head_loss_bwd_bitwise(gpu, cin, dims):
+    from u3d import ops
+    g = torch.Generator().manual_seed(3)
+    lg = (torch.randn(dims + (16,), generator=g) * 3).to(gpu)
+    lab = torch.randint(0, 16, dims, generator=g).float().to(gpu)
+    wt = (torch.rand(16, generator=g) < 0.7).float().to(gpu)
+    _, sums = ops.partial_loss_fwd(lg, lab, wt, True, True)
+    go = torch.tensor([0.73], device=gpu)
+    w = torch.randn(16, cin, 1, 1, 1, generator=g).to(gpu)
+    _, pd, _ = ops.wstd_fwd(w, torch.bfloat16, False)
+    db0, db1 = torch.empty(16, device=gpu), torch.empty(16, device=gpu)
+    dl = ops.partial_loss_bwd(lg, lab, wt, sums, go, True, True)
+    dA0, dy0 = ops.head_bwd(dl, pd, cin, dbias=db0)
+    dA1, dy1 = ops.head_loss_bwd(lg, lab, wt, sums, go, pd, cin, dbias=db1)
+    assert torch.equal(dA0, dA1)
+    assert torch.equal(dy0, dy1)
+    assert torch.equal(db0, db1)
+
+
+def _step_grads(dev, fused, extra, monkeypatch, calls):
+    import unet3D
+    from loss_functions.loss_partial import EDiceLoss_partial
+    from u3d import ops
+    monkeypatch.setattr(ops, "HEAD_LOSS_FUSED", fused)
+    torch.manual_seed(0)
+    m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=16, weight_std=True).to(dev).train()
+    crit = EDiceLoss_partial(16)
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand((2, 1, 32, 32, 32), generator=g) * 2 - 1).to(dev)
+    lab = torch.randint(0, 16, (2, 32, 32, 32), generator=g).float().to(dev)
+    mask = (torch.rand(16, generator=g) < 0.7).long().to(dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lg, _, _ = m(x)
+    loss = crit(lg, lab, mask=[mask])
+    seen = []
+    if extra == "sum":  # a second consumer of the logits: autograd sums the two gradients
+        loss = loss + 0.05 * lg.square().mean()
+    elif extra == "hook":
+        lg.register_hook(lambda t: seen.append(t.double().abs().sum().item()))
+    n0 = calls[0]
+    loss.backward()
+    torch.cuda.synchronize()
+    return {n: p.grad.clone() for n, p in m.named_parameters()}, calls[0] - n0, seen
+
+
+@pytest.mark.parametrize("extra", [None, "sum", "hook"])
+def test_step_gradients_bitwise(gpu, monkeypatch, extra):
+    from u3d import ops
+    calls = [0]
+    real = ops.head_loss_bwd
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return real(*a, **k)
+    monkeypatch.setattr(ops, "head_loss_bwd", counted)
+    a, na, sa = _step_grads(gpu, False, extra, monkeypatch, calls)
+    b, nb, sb = _step_grads(gpu, True, extra, monkeypatch, calls)
+    assert na == 0
+    assert nb == (1 if extra is None else 0)  # any other reader forms the gradient first: the two-pass path runs
+    assert sa == sb
+    for n in a:
+        assert torch.equal(a[n], b[n]), n
+
+
+def test_autograd_grad_on_logits_is_formed(gpu):
+    import unet3D
+    from loss_functions.loss_partial import EDiceLoss_partial
+    from u3d import ops
+    from u3d.loss import ndhwc_view
+    torch.manual_seed(1)
+    m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=16, weight_std=True).to(gpu).train()
+    g = torch.Generator().manual_seed(9)
+    x = (torch.rand((1, 1, 16, 16, 16), generator=g) * 2 - 1).to(gpu)
+    lab = torch.randint(0, 16, (1, 16, 16, 16), generator=g).float().to(gpu)
+    lg, _, _ = m(x)
+    loss = EDiceLoss_partial(16)(lg, lab, mask=[torch.ones(16, dtype=torch.long, device=gpu)])
+    (gl,) = torch.autograd.grad(loss, lg)
+    lgv = ndhwc_view(lg.detach())
+    _, sums = ops.partial_loss_fwd(lgv, lab, torch.ones(16, device=gpu), True, True)
+    ref = ops.partial_loss_bwd(lgv, lab, torch.ones(16, device=gpu), sums, torch.ones(1, device=gpu), True, True)
+    assert torch.equal(gl.permute(0, 2, 3, 4, 1), ref)

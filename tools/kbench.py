@@ -288,6 +288,22 @@ def _head(bwd, n=2, s=96, cin=32, cout=16):
     return t_(lambda: ops.head_bwd(dyf, pd, cin, dbias=db)), flop
 
 
+def _head_loss(fused, n=2, s=96, cin=32, C=16):
+    """the loss backward + the head's data gradient: partial_loss_bwd then head_bwd, or u3d_head_loss_bwd"""
+    x, pf, pd, g, r, dy, flop = conv_case(n, cin, C, s, 1, 1, True)
+    lg = torch.randn((n, s, s, s, C), device=dev)
+    lab = torch.randint(0, C, (n, s, s, s), device=dev).float()
+    wt = torch.ones(C, device=dev)
+    _, sums = ops.partial_loss_fwd(lg, lab, wt)
+    go = torch.ones(1, device=dev)
+    db = torch.empty(C, device=dev)
+    if fused:
+        return t_(lambda: ops.head_loss_bwd(lg, lab, wt, sums, go, pd, cin, dbias=db)), flop
+    return t_(lambda: ops.head_bwd(ops.partial_loss_bwd(lg, lab, wt, sums, go), pd, cin, dbias=db)), flop
+
+
+CASES["headloss96"] = lambda: _head_loss(True)
+CASES["headloss96_2pass"] = lambda: _head_loss(False)
 CASES["headf96"] = lambda: _head(False)
 CASES["headb96"] = lambda: _head(True)
 CASES["stemw96"] = lambda: _stemw()

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round 5 batch s: the small-volume conv with XCD blocks by fewest L2 fill bytes and the combine's loads in one round
+# trip: GPU tests, tail stamps, kernel and step A/B (U3D_SMALL_XMAP=0; libu3d_prev.so = before both).
+TAG=${1:-r05_s}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_gnfused_small.py tests/test_gpu_epi_stats.py tests/test_gpu_bf16.py tests/test_gpu_gnfused_brick.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for c in small12 small06 smalldg12 smalldg06; do
+  U3D_LIB=$R/multimodal-pl_amd/u3d/libu3d_stamps.so timeout -k 10 120 python tools/stamps.py $c > $O/stamps_$c.log 2>&1 || { cat $O/stamps_$c.log; exit 1; }
+  echo "== $c"; grep -v "amdgpu.ids\|wave [1-7]:" $O/stamps_$c.log
+done
+for v in "A=1" "U3D_SMALL_XMAP=0" "U3D_LIB=$R/multimodal-pl_amd/u3d/libu3d_prev.so"; do
+  env $v timeout -k 10 120 python tools/kbench.py fwd12 dgrad12 fwd6 dgrad6 > $O/kb.log 2>&1 || { cat $O/kb.log; exit 1; }
+  echo "== $v"; grep -v amdgpu.ids $O/kb.log
+done
+run() {  # run TAG ENV
+  local t=$1; shift; local e=$1; shift
+  env $e timeout -k 10 300 python bench.py --no-cpu --no-infer --no-roofline --no-mixed --steps 30 --warmup 5 "$@" > $O/bench_$t.log 2>&1 || { echo "bench $t failed"; grep -v "^frame" $O/bench_$t.log | tail -20; exit 1; }
+  grep '^{' $O/bench_$t.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$t', d['ms_per_step'], d['launch'], d.get('graph_error'))"
+}
+for i in 1 2; do
+  run new$i "A=1" || exit 1
+  run noxmap$i "U3D_SMALL_XMAP=0" || exit 1
+  run prev$i "U3D_LIB=$R/multimodal-pl_amd/u3d/libu3d_prev.so" || exit 1
+done

@@ -20,6 +20,7 @@ secs = float(sys.argv[2]) if len(sys.argv) > 2 else 2.5
 ring = not case.startswith("wgrad")
 s2 = case.startswith("s2ring")
 small = case.startswith("small")
+smalldg = case.startswith("smalldg")
 s, c = {"96": (96, 32), "48": (48, 64), "24": (24, 128), "12": (12, 256), "06": (6, 256)}[case[-2:]]
 x = torch.randn((2, s, s, s, c), device=dev).to(torch.bfloat16)
 dy = torch.randn_like(x)
@@ -37,7 +38,12 @@ if small:  # the small-volume conv (conv_small.hip) at 12^3 / 6^3, 256 -> 256 wi
     gn = (ops.gn_stats(x, 16), torch.ones(c, device=dev), torch.zeros(c, device=dev), 16)
     w3 = torch.randn(c, c, 3, 3, 3, device=dev)
     pf3, _, _ = ops.wstd_fwd(w3, torch.bfloat16, True, need_dgrad=False)
-    fn = lambda: ops.conv_fwd(x, pf3, c, 3, 1, gn)  # noqa: E731
+    fn = lambda: ops.conv_fwd_stats(x, pf3, c, 3, 1, gn)  # noqa: E731 (the step's form: output statistics in the combine)
+    if smalldg:  # the data gradient with the GroupNorm-backward partials + finalize in its combine
+        _, pd3, _ = ops.wstd_fwd(w3, torch.bfloat16, True)
+        dy = torch.randn_like(x)
+        dgam, dbet = torch.empty(c, device=dev), torch.empty(c, device=dev)
+        fn = lambda: ops.conv_dgrad_gn(dy, pd3, c, x, 3, 1, gn, dgb=lambda: (dgam, dbet))  # noqa: E731
 if s2:  # the stride-2 forward ring (conv_s2.hip): 32 -> 64
     w2 = torch.randn(64, 32, 3, 3, 3, device=dev)
     pf2, _, _ = ops.wstd_fwd(w2, torch.bfloat16, True, need_dgrad=False)
@@ -91,3 +97,23 @@ for w in range(8):
     print(f"  wave {w}: " + "  ".join(f"{nm} {np.median(f):.3f}" for nm, f in zip(names, fr)) +
           f"  other {1 - np.median(fr[0] + fr[1] + fr[2]):.3f}  steps {int(np.median(steps[:, w] & np.uint64(0xffffffff)))}"
           f" compute-steps {int(np.median(steps[:, w] >> np.uint64(32)))}")
+if small:  # the tail after the main loop (TailStamps: slab stores, their drain, the tile counter, the combine, ...)
+    tb = np.zeros(256 * 64, dtype=np.uint64)
+    assert h.u3d_diag_small_tail(ctypes.c_void_p(tb.ctypes.data), ctypes.c_longlong(tb.nbytes)) == 0
+    t = tb.reshape(1024, 16)[:nwg].astype(np.float64)
+    mhz = np.median(clk)
+    segs = ("slab stores issued", "stores drained", "tile counter", "combine", "partials stored", "stats counter",
+            "finalize")
+    for lab, sel in (("all", t[:, 3] > 0), ("tile-last", t[:, 4] > 0), ("final", t[:, 7] > 0)):
+        q = t[sel]
+        if not len(q):
+            continue
+        row = []
+        for k, nm in enumerate(segs, start=1):
+            ok = (q[:, k] > 0) & (q[:, k - 1] > 0)
+            if ok.any():
+                row.append(f"{nm} {np.median(q[ok, k] - q[ok, k - 1]) / mhz:.2f}")
+        print(f"  tail ({lab}, {len(q)} wgs, us): " + "  ".join(row))
+    rend = t[:, 8]
+    print(f"  first start to last exit {(rend.max() - r0.min()) / 100:.1f} us; main-loop ends to exits: median "
+          f"{np.median(rend - r1) / 100:.1f} us, max {(rend - r1).max() / 100:.1f} us")
