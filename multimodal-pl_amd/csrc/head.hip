@@ -277,11 +277,11 @@ __global__ __launch_bounds__(HD_T) void head_bwd_kernel(const float* __restrict_
 }
 
 // The head's data gradient with the partial-label loss gradient formed in registers (the bench's loss: softmax over
-// 16 classes + per-class BCE): dlogits never reaches HBM (-2 x 113 MB per step at 2 x 96^3). Every lane loads its
-// voxel's 16 logits (lanes r and r + 32 the same 64 B: one request per line), forms the 16 gradients exactly as
-// loss_bwd_kernel (dice_bce_softmax_grad16) and keeps its 8; the rest is head_bwd_kernel's transposed path with the
-// same grid, so dA, the bf16 dy and the bias partials equal the two-kernel form's bit for bit. The next tile's logits
-// and label are loaded before this tile's math.
+// 16 classes + per-class BCE): dlogits never reaches HBM (-2 x 113 MB per step at 2 x 96^3). Lanes r and r + 32 hold
+// one voxel's classes 0-7 / 8-15 (the 8 channels each feeds the MFMA) and form their gradients as loss_bwd_kernel
+// does (dice_bce_softmax_grad8, bitwise dice_bce_softmax_grad16); the rest is head_bwd_kernel's transposed path with
+// the same grid, so dA, the bf16 dy and the bias partials equal the two-kernel form's bit for bit. The next tile's
+// logits and label are loaded before this tile's math.
 __global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
                                                             long long rows, const float* __restrict__ wt,
                                                             const double* __restrict__ sums,
@@ -319,28 +319,28 @@ __global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __rest
   const long long tiles = (rows + 31) / 32;
   const long long wid = (long long)blockIdx.x * (HD_T / 64) + wave;
   const long long nw = (long long)gridDim.x * (HD_T / 64);
-  auto load = [&](long long tile, f32x4 (&q)[4], float& t) {  // clamped row, no branch around the loads
+  auto load = [&](long long tile, f32x4 (&q)[2], float& t) {  // clamped row, no branch around the loads
     long long row = tile * 32 + r;
     row = row < rows ? row : rows - 1;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + row * 16 + 4 * k);
+    for (int k = 0; k < 2; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + row * 16 + 8 * h + 4 * k);
     t = lab[row];
   };
-  f32x4 cur[4], nxt[4];
+  f32x4 cur[2], nxt[2];
   float tcur = 0.f, tnxt = 0.f;
   load(wid, cur, tcur);
   for (long long tile = wid; tile < tiles; tile += nw) {
     load(tile + nw, nxt, tnxt);
     const long long row = tile * 32 + r;
     const bool ok = row < rows;
-    float gr[16];
-    dice_bce_softmax_grad16(cur, tcur, kd_a, kd_b, kb, gr);
+    float gr[8];
+    dice_bce_softmax_grad8(cur, tcur, h, kd_a, kd_b, kb, gr);
     u32x4 a[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float f[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = ok && s == 0 ? (h ? gr[8 + e] : gr[e]) : 0.f;
+      for (int e = 0; e < 8; ++e) f[e] = ok && s == 0 ? gr[e] : 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) colsum[s][e] += f[e];
       store16<bf16>(reinterpret_cast<bf16*>(&a[s]), f);
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __rest
       }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    for (int k = 0; k < 2; ++k) cur[k] = nxt[k];
     tcur = tnxt;
   }
 #pragma unroll
