@@ -302,6 +302,19 @@ def _head_loss(fused, n=2, s=96, cin=32, C=16):
     return t_(lambda: ops.head_bwd(ops.partial_loss_bwd(lg, lab, wt, sums, go), pd, cin, dbias=db)), flop
 
 
+def _small_step(s, dg, c=256, n=2):
+    """the step's forms of the small-volume conv (12^3 / 6^3): forward + output statistics (+ residual), data gradient
+    + GroupNorm-backward partials and finalize"""
+    x, pf, pd, g, r, dy, flop = conv_case(n, c, c, s, 3, 1, True, not dg)
+    if not dg:
+        return t_(lambda: ops.conv_fwd_stats(x, pf, c, 3, 1, g, r)), flop
+    dgam, dbet = torch.empty(c, device=dev), torch.empty(c, device=dev)
+    return t_(lambda: ops.conv_dgrad_gn(dy, pd, c, x, 3, 1, g, dgb=lambda: (dgam, dbet))), flop
+
+
+for s_ in (12, 6):
+    CASES[f"fwd{s_}st"] = (lambda s_=s_: _small_step(s_, False))
+    CASES[f"dgrad{s_}gb"] = (lambda s_=s_: _small_step(s_, True))
 CASES["headloss96"] = lambda: _head_loss(True)
 CASES["headloss96_2pass"] = lambda: _head_loss(False)
 CASES["headf96"] = lambda: _head(False)
