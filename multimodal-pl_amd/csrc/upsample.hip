@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void up_fwd_kernel(const T* __restrict__ x, co
 // grid: x = (iw, chunk) pairs of one input row, y = ih, z = n * D + od
 // CPG > 0 (round 5; channels per GroupNorm(16) group = c / 16, 2 / 4 / 8 / 16): the output's GroupNorm statistics from
 // the epilogue. Each thread sums the stored bf16 values of its 4 outputs per group its 8-channel chunk covers (and
-// their squares), the block reduces them per (group, sum | square) over its threads in a fixed order (LDS), one
+// their squares), the block reduces them per (group, sum | square) in a fixed order (wave shuffles, then LDS), one
 // [16][2] fp32 row per block into spart ([sample][wps][16][2], wps = blocks per sample: a block never straddles
 // samples), and launch_gn16_finalize combines the rows in fp64: no statistics pass over the output.
 template <int CPG = 0>
@@ -157,23 +157,36 @@ __global__ __launch_bounds__(256) void up_fwd_quad_kernel(const bf16* __restrict
   }
   }  // i < w * chn
   if constexpr (STATS) {
-    __shared__ float red[256][2 * NSL];
+    // per (chunk, slot) over the block: the lanes of a wave that hold the same chunk (lane % chn) by xor shuffles,
+    // then the 4 waves in order through LDS (a serial pass of 32 threads over the block's 256 rows was the tail)
+    constexpr int NV = 2 * NSL;
+    float v[NV];
 #pragma unroll
     for (int k = 0; k < NSL; ++k) {
-      red[threadIdx.x][2 * k] = gs[k];
-      red[threadIdx.x][2 * k + 1] = gq[k];
+      v[2 * k] = gs[k];
+      v[2 * k + 1] = gq[k];
     }
+    for (int o = chn; o < 64; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[k] += __shfl_xor(v[k], o);
+    __shared__ float red[4][32][NV];  // [wave][chunk][value]: chn <= 32
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane < chn)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) red[wave][lane][k] = v[k];
     __syncthreads();
     if (threadIdx.x < 32) {
       const int g = threadIdx.x >> 1, comp = threadIdx.x & 1;
-      const int nact = min(256, w * chn - (int)blockIdx.x * 256);  // 256 % chn == 0: local thread L has chunk L % chn
       float t = 0.f;
-      if constexpr (CPG >= 16) {  // chunks 2g, 2g + 1 (slot 0 each), in order
-        for (int jj = 2 * g; jj < 2 * g + 2; ++jj)
-          for (int L = jj; L < nact; L += chn) t += red[L][comp];
-      } else {
-        const int jj = g / NSL, k = g - jj * NSL;
-        for (int L = jj; L < nact; L += chn) t += red[L][2 * k + comp];
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv) {
+        if constexpr (CPG >= 16) {  // chunks 2g, 2g + 1 (slot 0 each)
+          t += red[wv][2 * g][comp];
+          t += red[wv][2 * g + 1][comp];
+        } else {
+          const int jj = g / NSL, k = g - jj * NSL;
+          t += red[wv][jj][2 * k + comp];
+        }
       }
       const int D_ = 2 * d, od = blockIdx.z % D_, nn = blockIdx.z / D_;
       const long long wps = (long long)gridDim.x * gridDim.y * D_;

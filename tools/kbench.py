@@ -115,6 +115,15 @@ def _upb(n, c, s):
     return t_(lambda: ops.upsample2x_bwd(dy, shape)), 2.0 * (dy.numel() + dy.numel() // 8)
 
 
+def _up_stats(n, c, s):
+    """the decoder's upsample + skip with the output's GroupNorm(16) statistics from its epilogue (the step's form)"""
+    x = torch.randn((n, s // 2, s // 2, s // 2, c), device=dev).to(bf)
+    sk = torch.randn((n, s, s, s, c), device=dev).to(bf)
+    return t_(lambda: ops.upsample2x_add_stats(x, sk)), 2.0 * (x.numel() + 2 * sk.numel())
+
+
+CASES["up96st"] = lambda: _up_stats(2, 32, 96)
+CASES["up48st"] = lambda: _up_stats(2, 64, 48)
 CASES["up96"] = lambda: _up(2, 32, 96)
 CASES["upb96"] = lambda: _upb(2, 32, 96)
 CASES["upb48"] = lambda: _upb(2, 64, 48)
