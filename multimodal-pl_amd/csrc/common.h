@@ -43,6 +43,7 @@ enum Opt : int {
   OPT_IGEMM_BM,       // bf16 implicit GEMM M tile: 0 auto (256 for large unsplit BN 64 launches), 128 / 256 force
   OPT_WSTD_ROW,       // weight-standardisation backward: one row per block from registers (0: chunked LDS kernel)
   OPT_UP_QUAD,        // bf16 trilinear x2 upsample: 2 x 2 outputs per thread from 18 loads (0: one output, 8 loads)
+  OPT_LOSS_PAIR,      // loss forward, 16 classes softmax + BCE: each voxel's classes over a lane pair (0: one lane)
   OPT_COUNT
 };
 int opt(Opt o);

@@ -205,6 +205,86 @@ reduce:
   }
 }
 
+// The 16-class softmax + per-class BCE forward (the bench's loss) with each voxel's classes split over a lane pair
+// (lanes i, i + 32 hold classes 0-7 / 8-15; the max and the softmax sum exchanged once each, as the backward's
+// dice_bce_softmax_grad8): 4 x 8 accumulators per lane instead of 4 x 16, so the grid can keep three times the waves in
+// flight (the one-lane form held 161 VGPRs and ran at 3.2 TB/s, latency-bound). Per-block partials in
+// loss_partial_kernel's layout ([block][k * 16 + c]), summed by loss_combine_kernel.
+constexpr int LP_NB = 1280;  // blocks: five 4-wave blocks per CU resident at once (90 VGPRs)
+__global__ __launch_bounds__(LT) void loss_partial16_pair_kernel(const float* __restrict__ lg,
+                                                                const float* __restrict__ lab, long long nvox,
+                                                                float* __restrict__ ws) {
+  __shared__ float red[LT / 64][64];
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  float acc[4][8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[k][c] = 0.f;
+  const long long stride = (long long)gridDim.x * (LT / 2);
+  long long v = (long long)blockIdx.x * (LT / 2) + wave * 32 + r;  // lanes r and r + 32: the same voxel
+  auto load = [&](long long vv, f32x4 (&q)[2], float& t) {  // clamped index, no branch around the loads
+    vv = vv < nvox ? vv : nvox - 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + vv * 16 + 8 * h + 4 * k);
+    t = lab[vv];
+  };
+  f32x4 cur[2], nxt[2];
+  float tcur = 0.f, tnxt = 0.f;
+  load(v, cur, tcur);
+  for (; v < nvox; v += stride) {  // both lanes of a pair take the same trips (the exchanges need both)
+    load(v + stride, nxt, tnxt);
+    float x[8], e[8];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[4 * k + j] = cur[k][j];
+    float m = x[0];
+#pragma unroll
+    for (int c = 1; c < 8; ++c) m = fmaxf(m, x[c]);
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      x[c] -= m;
+      e[c] = __builtin_amdgcn_exp2f(x[c] * LOG2E);
+      s += e[c];
+    }
+    s += __shfl_xor(s, 32);
+    const float inv = __builtin_amdgcn_rcpf(s), ls = __builtin_amdgcn_logf(s) * LN2;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bool hit = tcur == (float)(8 * h + c);
+      const float tc = hit ? 1.f : 0.f, p = e[c] * inv;
+      acc[0][c] = fmaf(p, tc, acc[0][c]);
+      acc[1][c] = fmaf(p, p, acc[1][c]);
+      acc[2][c] += tc;
+      const float lq = hit ? x[c] - ls : __builtin_amdgcn_logf(s - e[c]) * LN2 - ls;
+      acc[3][c] -= fmaxf(lq, -100.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) cur[k] = nxt[k];
+    tcur = tnxt;
+  }
+  // per class over the wave's 32 voxels (lanes with equal h), then the block's waves in order
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float t = acc[k][c];
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) t += __shfl_xor(t, o, 32);
+      if (r == 0) red[wave][k * 16 + 8 * h + c] = t;
+    }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < LT / 64; ++w) t += red[w][threadIdx.x];
+    ws[(long long)blockIdx.x * 64 + threadIdx.x] = t;
+  }
+}
+
 // one block per (k, c): s = sum over the per-block partials, fixed order (fp64)
 __global__ __launch_bounds__(LT) void loss_combine_kernel(const float* __restrict__ ws, int nblk, int C,
                                                          double* __restrict__ sums) {
@@ -446,8 +526,13 @@ static int loss_blocks(long long nvox) {
 
 using namespace u3d;
 
+static int loss_pair_blocks(long long nvox) {
+  return (int)std::min<long long>(LP_NB, std::max<long long>(1, (nvox + LT / 2 - 1) / (LT / 2)));
+}
+
 extern "C" long long u3d_loss_workspace_bytes(int S, long long V, int C) {
-  return (long long)loss_blocks((long long)S * V) * 4 * C * 4;
+  const long long nvox = (long long)S * V;
+  return (long long)std::max(loss_blocks(nvox), C == 16 ? loss_pair_blocks(nvox) : 0) * 4 * C * 4;
 }
 
 extern "C" int u3d_partial_loss_fwd(const float* logits, const float* labels, int S, long long V, int C, int softmax,
@@ -459,11 +544,16 @@ extern "C" int u3d_partial_loss_fwd(const float* logits, const float* labels, in
               "softmax logits only)", uce);
   hipStream_t s = (hipStream_t)stream;
   const long long nvox = (long long)S * V;
-  const int nb = loss_blocks(nvox);
+  int nb = loss_blocks(nvox);
+  if (C == 16 && softmax == 1 && uce == 1 && opt(OPT_LOSS_PAIR) != 0) {
+    nb = loss_pair_blocks(nvox);
+    hipLaunchKernelGGL(loss_partial16_pair_kernel, dim3(nb), dim3(LT), 0, s, logits, labels, nvox, ws);
+  } else {
 #define LAUNCH(NCV) \
   hipLaunchKernelGGL(loss_partial_kernel<NCV>, dim3(nb), dim3(LT), 0, s, logits, labels, nvox, C, softmax, uce, ws)
-  U3D_NC_DISPATCH(C, LAUNCH)
+    U3D_NC_DISPATCH(C, LAUNCH)
 #undef LAUNCH
+  }
   hipLaunchKernelGGL(loss_combine_kernel, dim3(4 * C), dim3(LT), 0, s, ws, nb, C, sums);
   hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, s, C, weights, uce, (double)nvox, sums, loss);
   return check_launch("partial_loss_fwd");

@@ -91,3 +91,22 @@ def test_autograd_grad_on_logits_is_formed(gpu):
     _, sums = ops.partial_loss_fwd(lgv, lab, torch.ones(16, device=gpu), True, True)
     ref = ops.partial_loss_bwd(lgv, lab, torch.ones(16, device=gpu), sums, torch.ones(1, device=gpu), True, True)
     assert torch.equal(gl.permute(0, 2, 3, 4, 1), ref)
+
+
+@pytest.mark.parametrize("dims", [(2, 7, 9, 11), (1, 16, 16, 16), (2, 1, 1, 5), (2, 40, 40, 40)])
+def test_loss_forward_lane_pair_form(gpu, dims):
+    """The 16-class softmax + BCE forward with each voxel's classes over a lane pair (LOSS_PAIR) against the one-lane
+    form: the same loss and per-class sums up to the fp32 partial-sum order; deterministic."""
+    from u3d import ops
+    g = torch.Generator().manual_seed(11)
+    lg = (torch.randn(dims + (16,), generator=g) * 4).to(gpu)
+    lab = torch.randint(0, 16, dims, generator=g).float().to(gpu)
+    wt = (torch.rand(16, generator=g) < 0.7).float().to(gpu)
+    l1, s1 = ops.partial_loss_fwd(lg, lab, wt, True, True)
+    l1b, s1b = ops.partial_loss_fwd(lg, lab, wt, True, True)
+    assert torch.equal(l1, l1b) and torch.equal(s1, s1b)
+    with ops.option("LOSS_PAIR", 0):
+        l0, s0 = ops.partial_loss_fwd(lg, lab, wt, True, True)
+    # fp32 per-block partials of up to a few thousand terms, summed in a different order: ~1e-6 relative apart
+    torch.testing.assert_close(s1, s0, rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(l1, l0, rtol=2e-5, atol=1e-7)
