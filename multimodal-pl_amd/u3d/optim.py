@@ -5,7 +5,8 @@ per 48 tensors (u3d_sgd_step) instead of torch's 3-5 foreach passes.
 
 The learning rate lives in a one-element device tensor per group, refreshed from param_groups on every step()
 call and by sync_lr() — a hipGraph that captured step() reads the current value on replay
-(GraphedStep calls sync_lr() before each replay).
+(GraphedStep calls sync_lr() before each replay). The tensor is rewritten only when param_groups' lr differs from the
+value last written (an unchanged lr cost a fill launch in front of every replay).
 """
 import ctypes
 
@@ -30,21 +31,28 @@ class SGD(torch.optim.Optimizer):
                         nesterov=nesterov, maximize=maximize)
         super().__init__(params, defaults)
         self._lr_dev = {}
+        self._lr_val = {}  # group -> the lr value last written into its device tensor
+
+    def _write_lr(self, gi, group):
+        lr = float(group["lr"])
+        if self._lr_val.get(gi) != lr:
+            self._lr_dev[gi].fill_(lr)
+            self._lr_val[gi] = lr
 
     def _lr_tensor(self, gi, group, device):
         t = self._lr_dev.get(gi)
         if t is None or t.device != device:
             t = torch.empty((1,), dtype=torch.float32, device=device)
             self._lr_dev[gi] = t
-            t.fill_(float(group["lr"]))
+            self._lr_val.pop(gi, None)
+            self._write_lr(gi, group)
         return t
 
     def sync_lr(self):
-        """Write every group's current lr into its device tensor (outside any graph capture)."""
+        """Write every group's current lr into its device tensor where it changed (outside any graph capture)."""
         for gi, group in enumerate(self.param_groups):
-            t = self._lr_dev.get(gi)
-            if t is not None:
-                t.fill_(float(group["lr"]))
+            if self._lr_dev.get(gi) is not None:
+                self._write_lr(gi, group)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -69,7 +77,7 @@ class SGD(torch.optim.Optimizer):
                     raise _lib.U3DError("u3d SGD: fp32 dense parameters and gradients only")
             lr_t = self._lr_tensor(gi, group, params[0].device)
             if not capturing:
-                lr_t.fill_(float(group["lr"]))
+                self._write_lr(gi, group)
             mom = float(group["momentum"])
             fresh, old = [], []
             for p in params:  # state only with momentum, as torch.optim.SGD keeps it

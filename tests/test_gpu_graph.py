@@ -65,3 +65,48 @@ def test_graphed_step_matches_eager(gpu, amp):
     for (n, pa), (_, pb) in zip(mA.named_parameters(), mB.named_parameters()):
         torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-7, msg=n)
 
+
+
+def test_graphed_step_follows_lr_changes(gpu):
+    """A poly-LR style schedule written into param_groups between replays reaches the captured u3d SGD update."""
+    from u3d.graph import GraphedStep
+    from u3d.optim import SGD
+
+    bs = _batches(gpu)
+    sched = [1e-2, 5e-3, 5e-3, 2e-3]
+
+    def setup():
+        m, _, crit = _setup(gpu)
+        return m, SGD(m.parameters(), lr=1e-2, momentum=0.9, weight_decay=1e-4), crit
+
+    def make_step(m, opt, crit, x, t, mk):
+        def step():
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                lg, _, _ = m(x)
+            loss = crit(lg, t, mask=[mk])
+            loss.backward()
+            opt.step()
+            return loss
+        return step
+
+    mA, oA, cA = setup()
+    xA, tA, kA = (t.clone() for t in bs[0])
+    stepA = make_step(mA, oA, cA, xA, tA, kA)
+    for _ in range(3):
+        stepA()
+    for i, b in enumerate(bs[1:] + bs[:1]):
+        for dst, src in zip((xA, tA, kA), b):
+            dst.copy_(src)
+        oA.param_groups[0]["lr"] = sched[i]
+        stepA()
+
+    mB, oB, cB = setup()
+    xB, tB, kB = (t.clone() for t in bs[0])
+    g = GraphedStep(make_step(mB, oB, cB, xB, tB, kB), (xB, tB, kB), warmup=3, optimizer=oB)
+    for i, b in enumerate(bs[1:] + bs[:1]):
+        oB.param_groups[0]["lr"] = sched[i]
+        g(*b)
+    torch.cuda.synchronize()
+    for (n, pa), (_, pb) in zip(mA.named_parameters(), mB.named_parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-7, msg=n)
