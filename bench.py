@@ -424,6 +424,16 @@ def main():
             print(f"[bench] hipGraph capture failed ({graph_error}); running eager", file=sys.stderr)
             torch.cuda.synchronize()
             a.eager = True
+        if dist.is_initialized():
+            # every rank replays or every rank runs eager: a rank-local fallback would leave the ranks issuing
+            # different collective sequences (captured vs eager all-reduces) and mis-pair or hang them
+            ok = torch.tensor([0 if a.eager else 1], dtype=torch.int32, device=device)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0 and not a.eager:
+                graph_error = "hipGraph capture failed on another rank; every rank runs eager"
+                print(f"[bench] {graph_error}", file=sys.stderr)
+                graphed = None
+                a.eager = True
     if a.eager:
         def run(i):
             x.copy_(batches[i % 2][0], non_blocking=True)

@@ -35,6 +35,9 @@ constexpr int RG_SS = 4 * RG_PS;                     // ring slot stride
 constexpr int RG_NT = 512;
 constexpr int RG_LD = (RG_NR * 4 + RG_NT - 1) / RG_NT;  // 3 staged 16-B pieces per thread and plane
 constexpr int RG_NWR = 27 * 32;                      // weight rows (t, co)
+#ifndef U3D_ABL_RING
+#define U3D_ABL_RING 0
+#endif
 #ifndef RG_HOIST
 #define RG_HOIST 1
 #endif
@@ -292,8 +295,10 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   auto write_piece = [&](int i, const u32x4& v, unsigned m, int slot) {
     const int row = srow + i * (RG_NT / 4);
     u32x4 val = v;
+#if !(U3D_ABL_RING & 1)  // (timing-only ablation builds, tools/build_variant.sh: bit 0 = GroupNorm prologue compiled out)
     if constexpr (PRO) val = gn_relu8(v, sc, sh);
     if constexpr (PRO) if (!((m >> i) & 1u)) val = u32x4{0u, 0u, 0u, 0u};  // padding stays zero after the prologue
+#endif
     char* dst = row < RG_NR ? ring + slot * RG_SS + ch * RG_PS + row * 16 : junk + (tid & 63) * 16;
     *reinterpret_cast<u32x4*>(dst) = val;
   };
@@ -379,7 +384,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
 #pragma unroll
     for (int vb = 0; vb < 2; ++vb) {
       const bool okv = vb ? p.ok1 : p.ok;
-      if constexpr (PRO && !RES) {
+      if constexpr (PRO && !RES && !(U3D_ABL_RING & 2)) {  // (ablation bit 1: output statistics compiled out)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -407,7 +412,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
         load16<bf16>(reinterpret_cast<const bf16*>(&p.rv[vb]), c);
 #pragma unroll
         for (int e = 0; e < 8; ++e) a[e] += c[e];
-        if constexpr (GN) {
+        if constexpr (GN && !(U3D_ABL_RING & 2)) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float t = okv ? a[e] : 0.f;

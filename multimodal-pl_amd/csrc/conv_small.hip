@@ -608,7 +608,11 @@ extern "C" int u3d_conv_small2(int flip, const void* x, int n, int cin, int d, i
                                float* spart, float* stats_out, int* stats_made, u3d_stream_t stream) {
   U3D_REQUIRE(cnt && stats_made, "conv_small2: needs the counter workspace and stats_made");
   int nks = 0;
-  const bool want = stats_out && spart && !flip && cout % 16 == 0 && (cout / 16 == 4 || cout / 16 == 8 || cout / 16 == 16);
+  // the statistics form's own limits (one thread per (sample, group) in the finalize, 31-bit slab offsets): past
+  // them the launch declines with *stats_made = 0 and the caller runs the statistics pass
+  const bool want = stats_out && spart && !flip && cout % 16 == 0 &&
+                    (cout / 16 == 4 || cout / 16 == 8 || cout / 16 == 16) && n * 16 <= SC_NT &&
+                    8LL * n * d * h * w * cout * 4 < (1LL << 31);
   const int rc = conv_small_impl(flip, x, n, cin, d, h, w, wpk, cout, gn_stats, gn_gamma, gn_beta, gn_groups, residual,
                                  y, ws, ws_bytes, cnt, want ? spart : nullptr, want ? stats_out : nullptr, &nks, stream);
   *stats_made = rc == 0 && want && nks > 1 && nks <= 8;

@@ -84,6 +84,17 @@ class GradBucketer:
                 self.where[n] = (len(self.buckets), off, tuple(p.shape))
                 off += p.numel()
             self.buckets.append(([n for n, _ in grp], off))
+        # DDP's local_used_map, without a collective of its own: one fp32 flag per parameter (1 = this rank's native
+        # backward produced it) rides at the end of the LAST bucket, which is therefore launched only by finish(), once
+        # the produced set is final. After the average a flag is > 0 iff some rank produced the parameter.
+        self.order = [n for n, _ in params]
+        self.flag_off = 0
+        if self.buckets:
+            names, nel = self.buckets[-1]
+            self.flag_off = nel
+            self.buckets[-1] = (names, nel + len(self.order))
+        self._flag_src = {}     # produced set -> device flag vector (built once per set)
+        self._used = {}         # produced set -> set of names some rank produced (read from the averaged flags)
         self.device = params[0][1].device if params else None
         self.active = False
         self.synced = set()
@@ -169,32 +180,73 @@ class GradBucketer:
             self.pend[b] -= 1
         self.left[b] -= 1
         if self.left[b] == 0:
-            self._launch(b)
+            if b != len(self.buckets) - 1:  # the last bucket carries the used flags: finish() launches it
+                self._launch(b)
         elif self.pend[b] == self.left[b]:  # what is left of the bucket is parked: write it now
             self.flush_due = True
 
+    def _write_flags(self, produced):
+        """The used flags of this backward into the last bucket's flag region (one device copy; the flag vector of a
+        produced set is built once: by a host copy in eager mode, by slice fills under a hipGraph capture)."""
+        src = self._flag_src.get(produced)
+        if src is None:
+            vals = [1.0 if n in produced else 0.0 for n in self.order]
+            if capturing():
+                src = torch.zeros(len(vals), dtype=torch.float32, device=self.device)
+                for i, v in enumerate(vals):
+                    if v:
+                        src[i:i + 1].fill_(1.0)
+            else:
+                src = torch.tensor(vals, dtype=torch.float32).to(self.device)
+            self._flag_src[produced] = src
+        last = self.bufs[len(self.buckets) - 1]
+        last[self.flag_off:self.flag_off + len(self.order)].copy_(src)
+
+    def _used_names(self, produced):
+        """Names whose gradient some rank produced. Every local name produced: all of them (no read). Otherwise the
+        averaged flags are read back (one small device->host copy after the last bucket, eager mode only); a hipGraph
+        capture reuses what the eager warm-up steps read for the same produced set (a replay's set is fixed)."""
+        if len(produced) == len(self.order):
+            return produced
+        if capturing():
+            got = self._used.get(produced)
+            if got is None:
+                raise RuntimeError("U3DDataParallel: a hipGraph capture reached a produced-parameter set no eager "
+                                   "step has seen; run eager warm-up steps (u3d.graph.GraphedStep does) first")
+            return got
+        last = len(self.buckets) - 1
+        flags = self.bufs[last][self.flag_off:self.flag_off + len(self.order)].cpu()
+        got = frozenset(n for n, f in zip(self.order, flags.tolist()) if f > 0.0)
+        self._used[produced] = got
+        return got
+
     def finish(self):
-        """Zero never-produced grads, launch the rest, wait (stream-level) for every bucket."""
+        """Zero never-produced grads, write the used flags, launch the rest, wait (stream-level) for every bucket."""
         if not self.active:
             return
+        produced = frozenset(self.done_names)
         for b, (names, _) in enumerate(self.buckets):
             if self.works[b] is None:
                 self._zero_missing(b, names)
+                if b == len(self.buckets) - 1:
+                    self._write_flags(produced)
                 self._launch(b)
         for b, w in enumerate(self.works):
             w.wait()
             if not self.avg_native:
                 self.bufs[b].div_(self.world)
+        used = self._used_names(produced)
         self.synced = set(self.done_names)  # averaged here: the post-accumulate hooks skip these
         # gradient as bucket view: .grad becomes the averaged bucket slice itself (autograd's AccumulateGrad would
         # copy a view: +69 MB of device copies per step, r04 trace); the tape then returns None for these parameters.
-        # A parameter this rank's tapes never produced still gets the averaged slice (the other ranks' contributions,
-        # DDP's semantics for a parameter unused on one rank) unless a plain-autograd path already gave it a gradient;
-        # one that plain autograd produces later accumulates into the slice and is averaged by the fallback path.
+        # A parameter this rank's tapes never produced gets the averaged slice when another rank produced it (DDP's
+        # semantics for a parameter unused on one rank) unless a plain-autograd path already gave it a gradient; one
+        # that NO rank produced keeps .grad None, as on one GPU and under torch DDP (SGD then skips it: no weight
+        # decay or momentum on it — ADVICE r5).
         self.assigned = set()
         for n, p in self.params.items():
             produced = n in self.done_names
-            if not produced and p.grad is not None:
+            if not produced and (p.grad is not None or n not in used):
                 continue
             v = self.view(n)
             if p.grad is None:
@@ -322,6 +374,8 @@ class U3DDataParallel(torch.nn.Module):
         def fn(p):
             if name in self.bucketer.synced:  # averaged in its bucket: exempt this one accumulation
                 self.bucketer.synced.discard(name)
+                return
+            if p.grad is None:  # the engine runs the hook for an undefined gradient too (torch 2.10): nothing to average
                 return
             self._queue_flush()
             self._pending.append((name, p))

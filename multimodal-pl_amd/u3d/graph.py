@@ -15,7 +15,37 @@ captured step is the step every eager run would take.
 The reference has no train-step function (train_amos_atlas_final.py:209-399 runs it inline); this is the
 additive helper Engine.graphed_train_step / bench.py use.
 """
+import os
+
 import torch
+
+
+def _rccl_groups():
+    """The initialised torch.distributed process groups whose backend is "nccl" (= RCCL on ROCm)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return []
+    from torch.distributed import distributed_c10d as c10d
+    out = []
+    for pg in list(c10d._world.pg_map.keys()):
+        try:
+            if dist.get_backend(pg) == "nccl":
+                out.append(pg)
+        except (RuntimeError, ValueError):
+            continue
+    return out
+
+
+def _check_event_cache():
+    """ProcessGroupNCCL's event cache hands an event a captured collective recorded (a capture node) back to later
+    works, and the watchdog's completion query of such an event aborts the process (hipErrorCapturedEvent; one abort
+    on record, r05 `bench_fb1.log`). The cache is read when the process group is created, so the setting cannot be
+    fixed here: fail loudly instead of aborting later in the watchdog. ``U3D_GRAPH_ALLOW_EVENT_CACHE=1`` skips the
+    check (diagnostics only)."""
+    if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") == "0" or os.environ.get("U3D_GRAPH_ALLOW_EVENT_CACHE") == "1":
+        return
+    raise RuntimeError("GraphedStep with an RCCL process group needs TORCH_NCCL_CUDA_EVENT_CACHE=0 in the environment "
+                       "before the process group is created (bench.py and engine.py set it)")
 
 
 class GraphedStep:
@@ -32,9 +62,12 @@ class GraphedStep:
         torch's "global"."""
         self.static_inputs = tuple(static_inputs)
         self.optimizer = optimizer
+        rccl_groups = _rccl_groups()
         if capture_error_mode is None:
             import torch.distributed as dist
             capture_error_mode = "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+        if rccl_groups:
+            _check_event_cache()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -43,9 +76,11 @@ class GraphedStep:
                 step_fn()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        if capture_error_mode == "thread_local":
-            import time
-            time.sleep(0.3)  # let the process group's watchdog retire the warm-up steps' works before the capture
+        # Every warm-up collective has completed on the device; wait until each RCCL process group's watchdog has
+        # also retired them (its work list empty), so no watchdog query of a pre-capture work is in flight when the
+        # capture begins. A deterministic condition, not a delay: ProcessGroupNCCL::waitForPendingWorks.
+        for pg in rccl_groups:
+            pg._wait_for_pending_works()
         self.graph = torch.cuda.CUDAGraph()
         self._zero()
         with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):

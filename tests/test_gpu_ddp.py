@@ -271,3 +271,65 @@ def test_rccl_world1_graphed_bucketed_step_is_bitwise_reproducible(gpu):
     for k in g_eager:
         assert torch.equal(reps[0][k], reps[1][k]), f"{k}: two replays differ"
         assert torch.equal(reps[0][k], g_eager[k]), f"{k}: replay differs from the eager bucketed step"
+
+
+def test_rccl_world1_bucketed_feam3_keeps_unproduced_grads_none(gpu):
+    """a parameter no rank's backward produces (unet3D_with_feam3's eamXX.proj; in the logits-only pre-train
+    branch, losses.py:179-182, also the attention and deep-supervision heads) keeps .grad None under the bucketed
+    all-reduce, as on one GPU and under torch DDP, so SGD's weight decay and momentum leave it alone. The used flags
+    ride in the last bucket (u3d/ddp.py GradBucketer); eager steps read them back, a captured step reuses what its eager
+    warm-ups read. Post-SGD weights equal the plain one-GPU step's (fp32, RCCL world 1: the average is the identity)."""
+    import torch.distributed as dist
+    import unet3D
+    from u3d.ddp import U3DDataParallel
+    from u3d.graph import GraphedStep
+    from u3d.optim import SGD
+
+    def build():
+        m = unet3D.unet3D_with_feam3([1, 2, 2, 2, 2], num_classes=14, weight_std=True)
+        apply_recipe(m, seed=0)
+        return m.to(gpu).train()
+
+    from oracle.weights_recipe import apply_recipe, input_volume
+    x = torch.from_numpy(input_volume((1, 1, 32, 32, 32), seed=80, kind="normal")).to(gpu)
+
+    def run(m, net, graphed):
+        opt = SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            logits, _, _, _ = net(x)
+            loss = (logits * 1e-3).square().sum()
+            loss.backward()
+            opt.step()
+            return loss
+        if graphed:
+            gs = GraphedStep(step, (), warmup=2, optimizer=None)
+            gs()
+        else:
+            step()
+        torch.cuda.synchronize()
+        return ({k: (None if p.grad is None else p.grad.detach().clone()) for k, p in m.named_parameters()},
+                {k: p.detach().clone() for k, p in m.named_parameters()})
+
+    m = build()
+    g_ref, w_ref = run(m, m, False)
+    unused = sorted(k for k, g in g_ref.items() if g is None)
+    assert any(k.endswith("proj.weight") for k in unused) and "eam84.kv.weight" in unused, unused
+    del m
+    _init_rccl_world1()
+    try:
+        for graphed in (False, True):
+            m = build()
+            net = U3DDataParallel(m, bucket_mb=1.0, force_buckets=True)
+            g, w = run(m, net, graphed)
+            assert sorted(k for k, v in g.items() if v is None) == unused, graphed
+            for k in w_ref:
+                if graphed:  # three SGD steps (two warm-ups, one replay) vs one: compare the untouched ones only
+                    if k in unused:
+                        assert torch.equal(w[k], w_ref[k]), k
+                    continue
+                assert (w[k] - w_ref[k]).abs().max().item() <= 1e-6 * max(1.0, w_ref[k].abs().max().item()), k
+            del net, m
+    finally:
+        dist.destroy_process_group()

@@ -206,6 +206,54 @@ def test_ddp_bucketer_gloo_world2():
     assert np.allclose(out[0][2], out[1][2])  # init broadcast: identical weights on both ranks
 
 
+def _used_flags_worker(rank, world, port, q):
+    """DDP's unused-parameter semantics through the bucket flags: p2 is produced on rank 0 only (both ranks get the
+    averaged slice), p4 on no rank (.grad stays None on both: no weight decay / momentum on it, as on one GPU)."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-pl_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from u3d.ddp import GradBucketer
+    params = [(f"p{i}", torch.nn.Parameter(torch.randn(n))) for i, n in enumerate([5, 300, 7, 1000, 3])]
+    b = GradBucketer(params, bucket_mb=0.002)
+    out = []
+    for step in range(2):  # the second step reads the flags again (eager: no cached answer)
+        for _, p in params:
+            p.grad = None
+        b.begin()
+        for n, p in reversed(params):
+            if n == "p4" or (n == "p2" and rank == 1):
+                continue
+            b.out(n).fill_(float(rank + 1) * (1 + int(n[1:])))
+            b.done(n)
+        b.finish()
+        out.append({n: (None if p.grad is None else p.grad.tolist()) for n, p in params})
+    q.put((rank, out, sorted(b.assigned)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_used_flags_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_used_flags_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=60) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, steps, assigned in out:
+        assert assigned == (["p0", "p1", "p2", "p3"] if rank == 0 else ["p0", "p1", "p3"])
+        for grads in steps:
+            assert grads["p4"] is None, (rank, "a parameter no rank produced must keep grad None")
+            assert np.allclose(grads["p2"], 0.5 * 1 * 3), (rank, grads["p2"][:3])  # rank 0's (0+1)*3 over 2 ranks
+            for i in (0, 1, 3):
+                assert np.allclose(grads[f"p{i}"], 1.5 * (1 + i)), (rank, i)
+
+
 def _fallback_worker(rank, world, port, q):
     """Plain torch autograd parameters (no native tape) under U3DDataParallel: every gradient reaches the
     post-accumulate hook and is averaged; equals one process on the concatenated batch."""

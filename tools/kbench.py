@@ -92,6 +92,14 @@ for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 
     CASES[f"dgrad{lvl}"] = (lambda s=s, c=c: _dgrad(2, c, c, s, 3, 1))
     CASES[f"wgrad{lvl}"] = (lambda s=s, c=c: _wgrad(2, c, c, s, 3, 1))
 CASES["dgrad96gn"] = lambda: _dgrad_gn(2, 32, 96)
+CASES["fwd96nr"] = lambda: _fwd(2, 32, 32, 96, 3, 1, True, False)   # GN prologue + statistics, no residual
+CASES["wgrad96nogn"] = lambda: _wgrad_plain(2, 32, 96)               # the weight-gradient ring without its GN prologue
+
+
+def _wgrad_plain(n, c, s):
+    x, pf, pd, g, r, dy, flop = conv_case(n, c, c, s, 3, 1, False)
+    us = t_(lambda: ops.conv_wgrad(dy, x, 3, 1, None))
+    return us, flop
 CASES["dgrad48gn"] = lambda: _dgrad_gn(2, 64, 48)   # persistent brick + GN-backward partials (round 4)
 
 
