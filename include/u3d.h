@@ -224,6 +224,14 @@ int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, const void*
                           float* stats_ws, u3d_stream_t stream);
 int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,
                                    u3d_stream_t stream);
+/* Round 6: u3d_conv32_ring_stats that also stores the input after its GroupNorm + ReLU prologue, relu(gn(x)) (bf16
+ * NDHWC, x's shape, caller-owned, not aliasing x), to xn — the operand of the conv's weight gradient
+ * (unet3D.py:27 F.conv3d's backward w.r.t. the weight, fed by NoBottleneck's relu(gn) :56-73): u3d_conv_wgrad_ring
+ * without gn_stats on xn gives bitwise the partials of the GroupNorm form on x, without re-normalising every staged
+ * piece. */
+int u3d_conv32_ring_stats_xn(const void* x, int n, int d, int h, int w, const void* wpk, const float* gn_stats,
+                             const float* gn_gamma, const float* gn_beta, int gn_groups, const void* residual, void* y,
+                             void* xn, float* stats_ws, u3d_stream_t stream);
 /* Round 5: u3d_conv32_ring_stats with the statistics finalized by the launch's last-arriving workgroup straight into
  * stats_out[n][16][2] (no u3d_conv32_ring_stats_finalize launch; fixed-order fp64 combine, agent-scope arrival counter
  * cnt: one ZEROED unsigned, left zeroed by every launch). */

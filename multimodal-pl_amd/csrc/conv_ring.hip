@@ -116,18 +116,23 @@ struct RGWalk {
 // The MFMA is v_mfma_f32_16x16x32_bf16 (round 3: the same cycles per flop as 32x32x16, but the chip holds a higher
 // clock under it, MI355X_MICROARCH.md DVFS item 7): per tap (K = its 32 input channels) 4 MFMAs per wave = 2 voxel
 // blocks x 2 output-channel blocks. KR = weight fragments (tap, co block) held in registers.
-template <bool FLIP, bool GN, bool RES, int KR, bool Q = false>
+// XN (round 6, forward with the GroupNorm prologue only): the staged, normalised input relu(gn(x)) of the tile's own
+// rows (not the halo) is also stored to xno (bf16 NDHWC, x's shape), so the conv's weight gradient reads it as is
+// (wgrad_ring_dma_kernel<false>: no second GroupNorm transform of every staged x piece in the backward).
+template <bool FLIP, bool GN, bool RES, int KR, bool Q = false, bool XN = false>
 __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wpk,
                                                               bf16* __restrict__ y, const bf16* __restrict__ res,
                                                               const float* __restrict__ gstat,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float* __restrict__ spart,
-                                                              RGGeom g, int* __restrict__ queue = nullptr) {
+                                                              RGGeom g, int* __restrict__ queue = nullptr,
+                                                              bf16* __restrict__ xno = nullptr) {
   // GN on the forward (!FLIP): GroupNorm + ReLU prologue on the staged input. GN on the data gradient (FLIP): the
   // backward of that prologue's GroupNorm starts in the epilogue — res = x (the forward's pre-GroupNorm input), and
   // per channel (sum g, sum g*xhat) of g = relu-mask * dA go to spart[workgroup][32][2] (u3d_gn_bwd_parts finishes)
   constexpr bool PRO = GN && !FLIP, GB = GN && FLIP, LDR = RES || GB;
   static_assert(!(GB && (Q || RES)), "the fused GroupNorm backward runs on the static data-gradient ring only");
+  static_assert(!XN || (PRO && !Q && RG_HOIST), "the normalised side output belongs to the static GN forward");
   __shared__ __attribute__((aligned(16))) char smem[4 * RG_SS + 4 * RG_NWR * 16 + 1024 + 512 + (GB ? 576 : 0)];
   char* const ring = smem;
   char* const wts = smem + 4 * RG_SS;
@@ -253,7 +258,16 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   }
   unsigned pin = 0;
   int col_h0 = -1, col_w0 = -1;
+  unsigned pint = 0;  // XN: bit i = piece i's halo row is one of the tile's own rows (stored to xno)
+  if constexpr (XN) {
+#pragma unroll
+    for (int i = 0; i < RG_LD; ++i) {
+      const int row = srow + i * (RG_NT / 4), hh = row / RG_HW, hw = row % RG_HW;
+      pint |= (row < RG_NR && hh >= 1 && hh <= RG_BH && hw >= 1 && hw <= RG_BW ? 1u : 0u) << i;
+    }
+  }
 #endif
+  const auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)xno, 0, XN ? (int)g.xbytes : 0, 0x00020000);
   auto load_piece = [&](const RGPlane& p, int i, u32x4 (&v)[RG_LD], unsigned& m) {
 #if RG_HOIST
     if (i == 0 && p.valid && (p.h0 != col_h0 || p.w0 != col_w0)) {  // uniform: once per run of the walk
@@ -292,7 +306,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       gn_coef8(gstat, gamma, beta, g.gn_groups, 32, p.n, ch * 8, sc, sh);
     }
   };
-  auto write_piece = [&](int i, const u32x4& v, unsigned m, int slot) {
+  auto write_piece = [&](int i, const u32x4& v, unsigned m, int slot, int xbase) {
     const int row = srow + i * (RG_NT / 4);
     u32x4 val = v;
 #if !(U3D_ABL_RING & 1)  // (timing-only ablation builds, tools/build_variant.sh: bit 0 = GroupNorm prologue compiled out)
@@ -301,6 +315,12 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
 #endif
     char* dst = row < RG_NR ? ring + slot * RG_SS + ch * RG_PS + row * 16 : junk + (tid & 63) * 16;
     *reinterpret_cast<u32x4*>(dst) = val;
+#if RG_HOIST
+    if constexpr (XN) {  // the tile's own in-volume rows: an out-of-range offset drops the store (no branch)
+      const unsigned off = ((m & pint) >> i) & 1u ? (unsigned)(xbase + plo[i]) : 0xFFFFFFF0u;
+      __builtin_amdgcn_raw_buffer_store_b128(val, nrs, off, 0, 0);
+    }
+#endif
   };
 
   // A computed output plane waiting for its epilogue: the epilogue (bf16 pack, permlane swap, residual add,
@@ -623,6 +643,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     }
     gn_table(pw);
     const int slot = s & 3;
+    const int xbase = XN ? (((pw.n * g.d + pw.zin) * g.h + pw.h0 - 1) * g.w + pw.w0 - 1) * 64 : 0;
     const RGPlane pl = next_plane();  // plane s+1
     // side work of the step, k = 0 .. 2 RG_LD - 1: even k writes staged piece k/2 of plane s into slot s & 3 (its
     // loads were issued a full step ago), odd k issues the load of piece k/2 of plane s + 1
@@ -630,7 +651,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       constexpr int k = decltype(kc)::value;
       if constexpr (k >= 0 && k < 2 * RG_LD) {
         if constexpr ((k & 1) == 0) {
-          if (pw.valid) write_piece(k >> 1, vcur[k >> 1], mcur, slot);
+          if (pw.valid) write_piece(k >> 1, vcur[k >> 1], mcur, slot, xbase);
         } else {
           load_piece(pl, k >> 1, vnxt, mnxt);
         }
@@ -864,6 +885,13 @@ using namespace u3d;
 #define U3D_RING_GB_KR 8  // weight steps in registers beside the fused GroupNorm-backward state
 #endif
 
+#ifndef U3D_RING_XN_KR
+#define U3D_RING_XN_KR 14
+#endif
+#ifndef U3D_RING_XN_KR_RES
+#define U3D_RING_XN_KR_RES 10
+#endif
+
 static int ring_kr(int dflt) {  // RING_KR = 0: no weight steps in registers (experiments)
   const int kr = opt(OPT_RING_KR);
   return kr < 0 ? dflt : kr;
@@ -873,10 +901,11 @@ static int ring_wgs() { return std::max(1, opt(OPT_RING_WGS)); }  // persistent 
 static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w, const void* wpk,
                             const float* gn_stats, const float* gn_gamma, const float* gn_beta, int gn_groups,
                             const void* residual, void* y, float* stats_out, float* stats_ws, u3d_stream_t stream,
-                            float* fstats = nullptr, unsigned* fcnt = nullptr) {
+                            float* fstats = nullptr, unsigned* fcnt = nullptr, void* xn = nullptr) {
   U3D_REQUIRE(x && wpk && y && n >= 1 && d >= 1 && h >= 1 && w >= 1, "conv32_ring: bad args");
   U3D_REQUIRE(!gn_stats || (gn_gamma && gn_beta && gn_groups > 0 && 32 % gn_groups == 0), "conv32_ring: bad GN");
   U3D_REQUIRE(!stats_out || (gn_stats && stats_ws), "conv32_ring: output statistics need the GN prologue + ws");
+  U3D_REQUIRE(!xn || (gn_stats && !flip && xn != x), "conv32_ring: the normalised side output needs the GN prologue");
   RGGeom g{};
   g.n = n; g.d = d; g.h = h; g.w = w;
   g.nbh = cdiv(h, RG_BH); g.nbw = cdiv(w, RG_BW);
@@ -908,6 +937,16 @@ static int conv32_ring_impl(int flip, const void* x, int n, int d, int h, int w,
   U3D_REQUIRE(!(flip && (gn_stats || residual)), "conv32_ring: the data gradient takes no prologue / residual");
   // register budget (2 waves per SIMD): GN + residual holds 12 weight steps, GN 16, the others 27
   const bool kr = ring_kr(1) != 0;
+  if (xn) {  // (two weight steps fewer: the side store's offsets)
+#define RG_XN(R, K)                                                                                                 \
+  hipLaunchKernelGGL((conv32_ring_kernel<false, true, R, K, false, true>), dim3((unsigned)grid), dim3(RG_NT), 0, s, \
+                     (const bf16*)x, (const bf16*)wpk, (bf16*)y, (const bf16*)residual, gn_stats, gn_gamma, gn_beta, \
+                     sp, g, nullptr, (bf16*)xn)
+    if (residual) RG_XN(true, U3D_RING_XN_KR_RES);
+    else RG_XN(false, U3D_RING_XN_KR);
+#undef RG_XN
+    return check_launch("conv32_ring_kernel (normalised side output)");
+  }
   if (flip) RG_KR(true, false, false, 27);
   else if (gn_stats && residual) RG_KR(false, true, true, 12);  // + the statistics accumulators: 12 steps
   else if (gn_stats) RG_KR(false, true, false, 16);  // (12 measured equal: 124.6 vs 124.8 us)
@@ -1123,6 +1162,17 @@ extern "C" int u3d_conv32_ring_stats(const void* x, int n, int d, int h, int w, 
   U3D_REQUIRE(stats_ws, "conv32_ring_stats: null statistics workspace");
   return conv32_ring_impl(0, x, n, d, h, w, wpk, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
                           stats_ws, stream);
+}
+
+// Round 6: u3d_conv32_ring_stats that also stores the normalised input relu(gn(x)) (bf16 NDHWC, x's shape) to xn,
+// for the conv's weight gradient (u3d_conv_wgrad_ring without gn_stats on xn: bitwise the GN form's partials).
+extern "C" int u3d_conv32_ring_stats_xn(const void* x, int n, int d, int h, int w, const void* wpk,
+                                        const float* gn_stats, const float* gn_gamma, const float* gn_beta,
+                                        int gn_groups, const void* residual, void* y, void* xn, float* stats_ws,
+                                        u3d_stream_t stream) {
+  U3D_REQUIRE(stats_ws && xn && gn_stats, "conv32_ring_stats_xn: null statistics workspace / side output / GN");
+  return conv32_ring_impl(0, x, n, d, h, w, wpk, gn_stats, gn_gamma, gn_beta, gn_groups, residual, y, stats_ws,
+                          stats_ws, stream, nullptr, nullptr, xn);
 }
 
 extern "C" int u3d_conv32_ring_stats_finalize(const float* stats_ws, int n, int d, int h, int w, float* stats_out,

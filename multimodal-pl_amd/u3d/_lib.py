@@ -53,6 +53,7 @@ _SIGS = {
     "u3d_conv32_ring": [I, P, I, I, I, I, P, P, P, P, I, P, P, P],
     "u3d_conv32_ring_stats_ws_floats": [I],
     "u3d_conv32_ring_stats": [P, I, I, I, I, P, P, P, P, I, P, P, P, P],
+    "u3d_conv32_ring_stats_xn": [P, I, I, I, I, P, P, P, P, I, P, P, P, P, P],
     "u3d_conv32_ring_stats_fused": [P, I, I, I, I, P, P, P, P, I, P, P, P, P, P, P],
     "u3d_conv32_ring_wps": [I, I, I, I],
     "u3d_conv32_ring_dgrad_gn": [P, I, I, I, I, P, P, P, P, P, I, P, P, P],

@@ -286,6 +286,36 @@ def conv_small(flip, x, cin, wpk, cout, gn, residual, y, want_stats=False):
     return stats if made.value else None
 
 
+RING_XN = os.environ.get("U3D_RING_XN", "1") != "0"  # the forward ring stores relu(gn(x)) for the weight gradient
+
+
+def ring_xn_ok(x, cout, k, stride, gn):
+    """Whether conv_fwd_stats_xn applies: the static 32->32 ring forward with its GroupNorm prologue (bf16)."""
+    n, d, h, w_, cin = x.shape
+    return (RING_XN and RING_STATS and gn is not None and cout == 32 and CONV32_FN == "u3d_conv32_ring"
+            and not FUSED_FINALIZE and not _ring_queue() and _use_conv32(x.dtype, cin, cout, k, stride, n, w_)
+            and _conv32_fits(x))
+
+
+def conv_fwd_stats_xn(x, wpk, cout, k, stride, gn, residual=None):
+    """conv_fwd_stats on the static ring that also returns xn = relu(gn(x)) (bf16 NDHWC, x's shape), stored by the
+    ring from its staged input: the conv's weight gradient then reads xn without a GroupNorm prologue (bitwise the
+    same partials as conv_wgrad(dy, x, ..., gn)). Caller checks ring_xn_ok. Returns (y, stats, xn)."""
+    n, d, h, w_, cin = x.shape
+    st, ga, be, G = gn
+    y = torch.empty((n, d, h, w_, cout), dtype=x.dtype, device=x.device)
+    xn = torch.empty_like(x)
+    stats = torch.empty((n, 16, 2), dtype=torch.float32, device=x.device)
+    ws = WS.get(4 * query("u3d_conv32_ring_stats_ws_floats", n), x.device, slot=9)
+    pr = _probe0()
+    call("u3d_conv32_ring_stats_xn", x.data_ptr(), n, d, h, w_, wpk.data_ptr(), st.data_ptr(), ga.data_ptr(),
+         be.data_ptr(), G, _ptr(residual), y.data_ptr(), xn.data_ptr(), ws.data_ptr(), _stream())
+    _probe1(pr, "conv32_ring fwd GN" + (" +res" if residual is not None else "") + " +stats",
+            2.0 * n * d * h * w_ * 27 * 32 * 32, n * d * h * w_)
+    call("u3d_conv32_ring_stats_finalize", ws.data_ptr(), n, d, h, w_, stats.data_ptr(), _stream())
+    return y, stats, xn
+
+
 def conv_fwd_stats(x, wpk, cout, k, stride, gn=None, residual=None):
     """conv_fwd that also returns the GroupNorm(16) statistics [n,16,2] of its output when the 32->32 ring kernel
     runs with a GN prologue (epilogue-accumulated); otherwise (conv_fwd(...), None)."""

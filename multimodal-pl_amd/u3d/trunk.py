@@ -147,8 +147,12 @@ class Tape:
         b = self.P[key + ".bias"] if bias else None
         head = out_f32 and residual is None and ops.use_head(x.t.dtype, cin, cout, k, stride)
         st16 = None
+        xn = None  # relu(gn(x)) stored by the forward ring: the weight gradient's operand (no GN prologue there)
         if head:  # precls_conv: streaming MFMA head (head.hip)
             y = ops.head_fwd(x.t, pf, cout, b, gn)
+        elif self.record and b is None and not out_f32 and ops.ring_xn_ok(x.t, cout, k, stride, gn):
+            y, st16, xn = ops.conv_fwd_stats_xn(x.t, pf, cout, k, stride, gn,
+                                                residual.t if residual is not None else None)
         elif gn is not None and b is None and not out_f32 and (cout == 32 or (ops.BRICK_STATS and cout % 32 == 0)):
             y, st16 = ops.conv_fwd_stats(x.t, pf, cout, k, stride, gn, residual.t if residual is not None else None)
         else:
@@ -183,7 +187,10 @@ class Tape:
                     if residual is not None:
                         self.acc_grad(residual, dy)
                     dyT = ops.cast(dy, self.dtype, pad_to=8)  # GEMM operand: channels padded to 8 (2-class head)
-                part, ns = ops.conv_wgrad(dyT, x.t, k, stride, gn)
+                if xn is not None:
+                    part, ns = ops.conv_wgrad(dyT, xn, k, stride, None)
+                else:
+                    part, ns = ops.conv_wgrad(dyT, x.t, k, stride, gn)
                 if ops.EAGER_SLAB_SUM and ns >= ops.EAGER_SLAB_MIN:
                     part, ns = ops.sum_slabs(part, ns, cout, cin)
                 self.pend_wgrad(part, ns, W, st, std, key + ".weight")

@@ -25,6 +25,12 @@ def load(d):
 
 
 rows = load(d)
+if len(sys.argv) > 4 and sys.argv[4].startswith("steady"):  # only the last `steps` complete (timed) steps
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import trace_steps
+    rows, walls, steps = trace_steps.steady(rows, steps)
+    print(f"steady state: the last {steps} complete steps, wall per step {sum(walls) / len(walls) / 1e3:.3f} ms "
+          f"(min {min(walls) / 1e3:.3f}, max {max(walls) / 1e3:.3f})")
 tot = collections.defaultdict(float)
 grp = collections.defaultdict(lambda: [0, 0.0])
 for r in rows:

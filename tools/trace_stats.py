@@ -9,6 +9,11 @@ import sys
 d = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+if len(sys.argv) > 3 and sys.argv[3] == "steady":  # only the last `steps` complete (timed) steps
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import trace_steps
+    rows, _, steps = trace_steps.steady(rows, steps)
 gn = collections.defaultdict(float)
 n_u3d = 0
 for r in rows:
