@@ -38,12 +38,6 @@ constexpr int RG_NWR = 27 * 32;                      // weight rows (t, co)
 #ifndef U3D_ABL_RING
 #define U3D_ABL_RING 0
 #endif
-#ifndef U3D_RING_SPREAD
-#define U3D_RING_SPREAD 0
-#endif
-#ifndef U3D_RING_SPREAD_NV
-#define U3D_RING_SPREAD_NV 6
-#endif
 #ifndef RG_HOIST
 #define RG_HOIST 1
 #endif
@@ -248,7 +242,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
   // merge would make the wait-count insertion pessimistic)
   const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)g.xbytes, 0x00020000);
   const auto rrs = __builtin_amdgcn_make_buffer_rsrc((void*)res, 0, LDR ? (int)g.xbytes : 0, 0x00020000);
-  const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, (int)g.xbytes, 0x00020000);
   f32x2 sc[4], sh[4];
   int gn_n = -1;
   // branch-free staging: out-of-volume rows load a valid dummy address and are zeroed when written
@@ -396,9 +389,8 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
 #pragma unroll
     for (int j = 0; j < NSL; ++j) gs[j] = gq[j] = 0.f;
   };
-  auto epilogue_part = [&](const Pending& p, auto v0c, auto v1c) __attribute__((always_inline)) {
-    constexpr int V0 = decltype(v0c)::value, V1 = decltype(v1c)::value;  // voxel blocks [V0, V1)
-    if constexpr (Q && PRO && V0 == 0) {
+  auto epilogue = [&](const Pending& p) __attribute__((always_inline)) {
+    if constexpr (Q && PRO) {
       if (spart != nullptr && p.chunk != acc_chunk) {
         if (acc_chunk >= 0) flush(acc_chunk);
         acc_chunk = p.chunk;
@@ -410,7 +402,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     // voxel -> one 16-B store per voxel block.
     const int cbase = 16 * (q4 & 1) + 8 * (q4 >> 1);
 #pragma unroll
-    for (int vb = V0; vb < V1; ++vb) {
+    for (int vb = 0; vb < 2; ++vb) {
       const bool okv = vb ? p.ok1 : p.ok;
       if constexpr (PRO && !RES && !(U3D_ABL_RING & 2)) {  // (ablation bit 1: output statistics compiled out)
 #pragma unroll
@@ -462,16 +454,8 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
           bs2[e] = fmaf(m ? a[e] : 0.f, m ? (xv[e] - t[3]) * t[2] : 0.f, bs2[e]);
         }
       }
-#if U3D_RING_SPREAD  // branch-free (an exec-masked store would end the tap's scheduling region)
-      __builtin_amdgcn_raw_buffer_store_b128(v, yrs, okv ? (unsigned)((p.vox + 16 * vb) * 64 + 2 * cbase) : 0xFFFFFFF0u,
-                                             0, 0);
-#else
       if (okv) *reinterpret_cast<u32x4*>(y + (p.vox + 16 * vb) * 32 + cbase) = v;
-#endif
     }
-  };
-  auto epilogue = [&](const Pending& p) __attribute__((always_inline)) {
-    epilogue_part(p, std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
   };
 
   // output plane from the three slots s0 (z-1), s1 (z), s2 (z+1); the staging writes of the staged plane, the
@@ -529,30 +513,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
     auto tstep = [&](auto tc) {
       constexpr int t = decltype(tc)::value;
       if constexpr (t + LA < 27) rd(t + LA, (t + LA) % (LA + 1));
-#if U3D_RING_SPREAD
-      // (round 6) the step's side work spread over the taps — staging pieces at taps 1, 5, ..., 21, the epilogue of
-      // the previous plane in two voxel-block halves at taps 11 and 19 — and, within a tap, the MFMAs interleaved with
-      // that VALU (one MFMA, then up to SP_NV vector instructions), so the vector work issues beside the matrix pipe
-      constexpr bool SIDE = t >= 1 && (t - 1) % 4 == 0 && (t - 1) / 4 < 2 * RG_LD;
-      if constexpr (SIDE) side(std::integral_constant<int, (t - 1) / 4>{});
-      if constexpr (t == 11) epilogue_part(pend, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-      if constexpr (t == 19) epilogue_part(pend, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
-#pragma unroll
-      for (int vb = 0; vb < 2; ++vb)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          nw.a4[vb * 2 + cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t % (LA + 1)][cb], fi[t % (LA + 1)][vb],
-                                                                       nw.a4[vb * 2 + cb], 0, 0, 0);
-      if constexpr (SIDE || t == 11 || t == 19) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);           // 1 MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, U3D_RING_SPREAD_NV, 0);  // then vector ALU
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           // an LDS read
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#else
       side(std::integral_constant<int, t - 1>{});
       if constexpr (t == 15) epilogue(pend);
       __builtin_amdgcn_sched_barrier(0);
@@ -563,7 +523,6 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
           nw.a4[vb * 2 + cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[t % (LA + 1)][cb], fi[t % (LA + 1)][vb],
                                                                        nw.a4[vb * 2 + cb], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-#endif
     };
     __builtin_amdgcn_sched_barrier(0);
     static_for<0, 27>(tstep);
@@ -692,11 +651,7 @@ __global__ __launch_bounds__(RG_NT, 1) void conv32_ring_kernel(const bf16* __res
       constexpr int k = decltype(kc)::value;
       if constexpr (k >= 0 && k < 2 * RG_LD) {
         if constexpr ((k & 1) == 0) {
-#if U3D_RING_SPREAD  // unconditional: a past-the-walk plane stages zeros into the free slot (no branch in the tap)
-          write_piece(k >> 1, vcur[k >> 1], mcur, slot, xbase);
-#else
           if (pw.valid) write_piece(k >> 1, vcur[k >> 1], mcur, slot, xbase);
-#endif
         } else {
           load_piece(pl, k >> 1, vnxt, mnxt);
         }
