@@ -84,9 +84,9 @@ def synthetic(batch, patch, device, seed, modality="ct"):
 RING_TAGS = {
     "wgrad_ring 32->32 GN": ("wgrad96", ("wgrad_ring_dma_kernel<true>', 1, '1', '256'",  # the 16 x 16-tile ring (LDS-DMA staging)
                                          "wgrad_ring_kernel<true, 16, 16>', 1, '1', '256'")),
-    "conv32_ring dgrad +GN-bwd partials": ("dgrad96gn", "conv32_ring_kernel<true, true, false, 8, false>', 256"),
-    "conv32_ring fwd GN +res +stats": ("fwd96", "conv32_ring_kernel<false, true, true, 12, false>', 256"),
-    "conv32_ring fwd GN +stats": ("fwd96_nores", "conv32_ring_kernel<false, true, false, 16, false>', 256"),
+    "conv32_ring dgrad +GN-bwd partials": ("dgrad96gn", "conv32_ring_kernel<true, true, false, 8, false, false>', 256"),
+    "conv32_ring fwd GN +res +stats": ("fwd96", "conv32_ring_kernel<false, true, true, 12, false, false>', 256"),
+    "conv32_ring fwd GN +stats": ("fwd96_nores", "conv32_ring_kernel<false, true, false, 16, false, false>', 256"),
 }
 
 
@@ -348,6 +348,11 @@ def spawn_ranks(n):
     return rc
 
 
+def capturable():
+    """Whether the step's collectives can be captured into a hipGraph: RCCL (backend "nccl") can, gloo cannot."""
+    return not dist.is_initialized() or dist.get_backend() == "nccl"
+
+
 def launch_mode(a, world):
     """'graph' (hipGraph replay of the whole step, its bucketed RCCL all-reduces included at N>1 / --force-buckets)
     unless --eager; a refused capture falls back to eager and says so in the line (`launch`, `graph_error`)."""
@@ -364,10 +369,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # U3D_BENCH_BACKEND=gloo with U3D_BENCH_SHARE_GPU=1: rehearse the N>1 path on a one-GPU box (every rank on device
+    # local % count, gloo collectives on device tensors: the bucketed all-reduce, the ranks' agreement on graph vs eager
+    # — gloo collectives cannot be captured — and the max-over-ranks timing). Not a scaling measurement.
+    backend = os.environ.get("U3D_BENCH_BACKEND", "nccl")
+    if os.environ.get("U3D_BENCH_SHARE_GPU") == "1":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
         assert dist.get_world_size() == world
     elif a.force_buckets:
         import socket
@@ -413,13 +424,15 @@ def main():
     # the step replays as one hipGraph (the Python host launching ~180 library calls per step was measured slower than
     # the GPU runs them: eager 6.03-6.19 vs graph 5.98-6.01 ms/step, gpurun_out/r04_k); at N>1 / --force-buckets the
     # bucketed RCCL all-reduces are captured with it (their kernel forms are static: ops.DDP_TOLERANT)
-    a.eager = launch_mode(a, world) == "eager"
+    a.eager = launch_mode(a, world) == "eager" or not capturable()
     from u3d import ops as _ops
     if not a.eager:
         from u3d.graph import GraphedStep
         try:
             graphed = GraphedStep(step, (x, target, mask), warmup=3, optimizer=opt)
-        except Exception as e:  # capture refused (e.g. a collective backend without graph support): run eager
+        except Exception as e:  # refused before the capture began (e.g. the event-cache check): run eager
+            if getattr(e, "u3d_capture_started", False):
+                raise  # the device's capture stream is left capturing: no eager fallback in this process
             graph_error = f"{type(e).__name__}: {e}"[:300]
             print(f"[bench] hipGraph capture failed ({graph_error}); running eager", file=sys.stderr)
             torch.cuda.synchronize()

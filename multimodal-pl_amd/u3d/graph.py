@@ -83,8 +83,15 @@ class GraphedStep:
             pg._wait_for_pending_works()
         self.graph = torch.cuda.CUDAGraph()
         self._zero()
-        with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
-            self.out = step_fn()
+        try:
+            with torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
+                self.out = step_fn()
+        except Exception as e:
+            # torch.cuda.graph leaves its capture stream current (and capturing) when capture_end raises (e.g. a gloo
+            # collective's unjoined work): nothing on this device can run afterwards, so callers must not fall back to
+            # eager in this process (bench.py decides eager up front for backends that cannot be captured)
+            e.u3d_capture_started = True
+            raise
         torch.cuda.synchronize()
 
     def _zero(self):

@@ -299,6 +299,16 @@ def ring_xn_ok(x, cout, k, stride, gn):
             and _conv32_fits(x))
 
 
+# stride-2 3^3 convs with cin >= 64 (the 48^3 / 24^3 / 12^3 downsampling convs on the implicit GEMM): normalise the
+# input once (round 6, kbench gpurun_out/r06_g: 48^3 forward 65.5 -> 48.4 + 14.1 us, its weight gradient 36.0 -> 30.2)
+S2_NORM_ONCE = os.environ.get("U3D_S2_NORM_ONCE", "1") != "0"
+
+
+def s2_normalise_once(x, cin, cout, k, stride, gn):
+    return (S2_NORM_ONCE and gn is not None and k == 3 and stride == 2 and x.dtype == torch.bfloat16 and cin >= 64
+            and cin % 8 == 0 and not (S2_RING and cin == 32 and cout == 64))
+
+
 def conv_fwd_stats_xn(x, wpk, cout, k, stride, gn, residual=None):
     """conv_fwd_stats on the static ring that also returns xn = relu(gn(x)) (bf16 NDHWC, x's shape), stored by the
     ring from its staged input: the conv's weight gradient then reads xn without a GroupNorm prologue (bitwise the

@@ -153,6 +153,11 @@ class Tape:
         elif self.record and b is None and not out_f32 and ops.ring_xn_ok(x.t, cout, k, stride, gn):
             y, st16, xn = ops.conv_fwd_stats_xn(x.t, pf, cout, k, stride, gn,
                                                 residual.t if residual is not None else None)
+        elif b is None and not out_f32 and residual is None and ops.s2_normalise_once(x.t, cin, cout, k, stride, gn):
+            # stride-2 3^3 conv on the implicit GEMM: relu(gn(x)) materialised once (the GEMM's prologue normalised
+            # every gathered element, 27/8 times per input element) and reused by the weight gradient
+            xn = ops.gn_apply(x.t, *gn)
+            y, st16 = ops.conv_fwd_stats(xn, pf, cout, k, stride, None)
         elif gn is not None and b is None and not out_f32 and (cout == 32 or (ops.BRICK_STATS and cout % 32 == 0)):
             y, st16 = ops.conv_fwd_stats(x.t, pf, cout, k, stride, gn, residual.t if residual is not None else None)
         else:

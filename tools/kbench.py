@@ -166,6 +166,31 @@ CASES["wgrad_s2_96"] = lambda: _wgrad(2, 32, 64, 96, 3, 2)
 CASES["wgrad_s2_48"] = lambda: _wgrad(2, 64, 128, 48, 3, 2)
 CASES["wgrad_s2_24"] = lambda: _wgrad(2, 128, 256, 24, 3, 2)
 CASES["fwd_s2_24"] = lambda: _fwd(2, 128, 256, 24, 3, 2, True, False)
+CASES["fwd_s2_24nogn"] = lambda: _fwd(2, 128, 256, 24, 3, 2, False, False)
+CASES["fwd_s2_48"] = lambda: _fwd(2, 64, 128, 48, 3, 2, True, False)
+CASES["fwd_s2_48nogn"] = lambda: _fwd(2, 64, 128, 48, 3, 2, False, False)
+CASES["fwd_s2_12"] = lambda: _fwd(2, 256, 256, 12, 3, 2, True, False)
+CASES["fwd_s2_12nogn"] = lambda: _fwd(2, 256, 256, 12, 3, 2, False, False)
+CASES["wgrad_s2_48nogn"] = lambda: _wgrad_nogn(2, 64, 128, 48, 2)
+CASES["wgrad_s2_24nogn"] = lambda: _wgrad_nogn(2, 128, 256, 24, 2)
+CASES["wgrad_s2_96nogn"] = lambda: _wgrad_nogn(2, 32, 64, 96, 2)
+CASES["gn_apply48"] = lambda: _gn_apply(2, 64, 48)
+CASES["gn_apply24"] = lambda: _gn_apply(2, 128, 24)
+
+
+def _wgrad_nogn(n, cin, cout, s, stride):
+    x, pf, pd, g, r, dy, flop = conv_case(n, cin, cout, s, 3, stride, False)
+    us = t_(lambda: ops.conv_wgrad(dy, x, 3, stride, None))
+    return us, flop
+
+
+def _gn_apply(n, c, s):
+    """relu(gn(x)) materialised (bf16 NDHWC): the cost of normalising a stride-2 conv's input once"""
+    x = torch.randn((n, s, s, s, c), device=dev).to(bf)
+    st = ops.gn_stats(x, 16)
+    ga, be = torch.ones(c, device=dev), torch.zeros(c, device=dev)
+    us = t_(lambda: ops.gn_apply(x, st, ga, be, 16))
+    return us, 0.0
 CASES["dgrad_s2_24"] = lambda: _dgrad(2, 128, 256, 24, 3, 2)
 CASES["dgrad_s2_96"] = lambda: _dgrad(2, 32, 64, 96, 3, 2)
 CASES["dgrad_s2_48"] = lambda: _dgrad(2, 64, 128, 48, 3, 2)
