@@ -92,6 +92,19 @@ for (lvl, s, c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 
     CASES[f"dgrad{lvl}"] = (lambda s=s, c=c: _dgrad(2, c, c, s, 3, 1))
     CASES[f"wgrad{lvl}"] = (lambda s=s, c=c: _wgrad(2, c, c, s, 3, 1))
 CASES["dgrad96gn"] = lambda: _dgrad_gn(2, 32, 96)
+for (_lvl, _s, _c) in [("96", 96, 32), ("48", 48, 64), ("24", 24, 128), ("12", 12, 256)]:
+    CASES[f"wgsum{_lvl}"] = (lambda s=_s, c=_c: _wgrad_sum(2, c, s))  # weight gradient + its slab sum
+
+
+def _wgrad_sum(n, c, s):
+    """the stride-1 ring weight gradient and the sum of its split slabs (what the step pays per weight, before the
+    standardisation backward)"""
+    x, pf, pd, g, r, dy, flop = conv_case(n, c, c, s, 3, 1, True)
+
+    def f():
+        part, ns = ops.conv_wgrad(dy, x, 3, 1, g)
+        ops.sum_slabs(part, ns, c, c)
+    return t_(f), flop
 CASES["fwd96nr"] = lambda: _fwd(2, 32, 32, 96, 3, 1, True, False)   # GN prologue + statistics, no residual
 CASES["wgrad96nogn"] = lambda: _wgrad_plain(2, 32, 96)               # the weight-gradient ring without its GN prologue
 
