@@ -44,6 +44,8 @@ enum Opt : int {
   OPT_WSTD_ROW,       // weight-standardisation backward: one row per block from registers (0: chunked LDS kernel)
   OPT_UP_QUAD,        // bf16 trilinear x2 upsample: 2 x 2 outputs per thread from 18 loads (0: one output, 8 loads)
   OPT_LOSS_PAIR,      // loss forward, 16 classes softmax + BCE: each voxel's classes over a lane pair (0: one lane)
+  OPT_HEAD_NB,        // classifier head / head backward blocks (at most)
+  OPT_HEAD_GN_NB,     // head backward with the prologue GN's partials: blocks over all samples (at most)
   OPT_COUNT
 };
 int opt(Opt o);

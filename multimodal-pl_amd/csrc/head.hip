@@ -16,6 +16,12 @@ namespace u3d {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 
 constexpr int HD_T = 256;  // 4 waves
+#ifndef HD_ND
+#define HD_ND 2  // head_loss_bwd_kernel: tiles in flight per wave (3, 4: measured equal)
+#endif
+#ifndef HD_ND_GN
+#define HD_ND_GN 2
+#endif
 constexpr int HD_GMAX = 2048;  // TR forward with GN: n * cin <= HD_GMAX (per-block LDS coefficient table)
 
 __device__ __forceinline__ bf16x8 as_frag(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
@@ -282,14 +288,26 @@ __global__ __launch_bounds__(HD_T) void head_bwd_kernel(const float* __restrict_
 // does (dice_bce_softmax_grad8, bitwise dice_bce_softmax_grad16); the rest is head_bwd_kernel's transposed path with
 // the same grid, so dA, the bf16 dy and the bias partials equal the two-kernel form's bit for bit. The next tile's
 // logits and label are loaded before this tile's math.
+// GN (round 6): the head's input x = relu(gn(x0)) prologue's GroupNorm backward starts here, as the data-gradient
+// ring's epilogue does it (u3d_conv32_ring_dgrad_gn): per (sample, block, channel) (sum g, sum g * xhat) of
+// g = relu-mask * dA, from the stored bf16 dA and the bf16 x0 at the same voxel (gn_bwd_partial's per-element terms) —
+// the separate partial pass over dA and x0 goes (2 x 113 MB at 2 x 96^3 -> 1 x 113 MB here). Blocks never straddle
+// samples (grid = n x bps, tiles of 32 voxels inside one sample: v % 32 == 0); parts[n][bps][cin][2].
+template <bool GN>
 __global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __restrict__ lg, const float* __restrict__ lab,
                                                             long long rows, const float* __restrict__ wt,
                                                             const double* __restrict__ sums,
                                                             const float* __restrict__ gout, const bf16* __restrict__ wpd,
                                                             int cin, bf16* __restrict__ dA, bf16* __restrict__ dyb,
-                                                            float* __restrict__ dbp) {
+                                                            float* __restrict__ dbp, const bf16* __restrict__ x0 = nullptr,
+                                                            const float* __restrict__ gst = nullptr,
+                                                            const float* __restrict__ gga = nullptr,
+                                                            const float* __restrict__ gbe = nullptr, int ggroups = 0,
+                                                            long long v = 0, int bps = 1,
+                                                            float* __restrict__ gparts = nullptr) {
   constexpr int cout = 16, cout_p = 32;
   __shared__ float red[HD_T / 64][32];
+  __shared__ f32x4 gtb[GN ? 64 : 1];  // per channel (scale, shift, rstd, mean) of the block's sample
   __shared__ float kd_a[16], kd_b[16], kb[16];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
   if (threadIdx.x < 16) {
@@ -316,23 +334,48 @@ __global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __rest
 #pragma unroll
     for (int e = 0; e < 8; ++e) colsum[s][e] = 0.f;
   __syncthreads();
-  const long long tiles = (rows + 31) / 32;
-  const long long wid = (long long)blockIdx.x * (HD_T / 64) + wave;
-  const long long nw = (long long)gridDim.x * (HD_T / 64);
-  auto load = [&](long long tile, f32x4 (&q)[2], float& t) {  // clamped row, no branch around the loads
-    long long row = tile * 32 + r;
-    row = row < rows ? row : rows - 1;
+  // GN: block b runs tiles of sample b / bps only (row offset row0); otherwise the whole grid strides over all rows
+  const int smp = GN ? (int)(blockIdx.x / bps) : 0;
+  const long long row0 = GN ? (long long)smp * v : 0, rows_b = GN ? row0 + v : rows;
+  const long long tiles = GN ? v / 32 : (rows + 31) / 32;
+  const long long wid = (long long)(GN ? blockIdx.x % bps : blockIdx.x) * (HD_T / 64) + wave;
+  const long long nw = (long long)(GN ? bps : gridDim.x) * (HD_T / 64);
+  float g1[16], g2[16];  // GN: (sum g, sum g * xhat) of this lane's 16 channels 16 u + 8 h + e
+#pragma unroll
+  for (int e = 0; e < 16; ++e) g1[e] = g2[e] = 0.f;
+  if constexpr (GN) {
+    if (threadIdx.x < cin) {
+      const int c = threadIdx.x, gr = c / (cin / ggroups);
+      const float mu = gst[(smp * ggroups + gr) * 2], rs = gst[(smp * ggroups + gr) * 2 + 1];
+      const float scv = rs * gga[c];
+      gtb[c] = f32x4{scv, gbe[c] - mu * scv, rs, mu};
+    }
+    __syncthreads();
+  }
+  // GN: x0 at this lane's two 8-channel runs of its voxel (where the swap below leaves its dA), prefetched with the
+  // logits
+  auto load = [&](long long tile, f32x4 (&q)[2], float& t, u32x4 (&xq)[2]) {  // clamped row, no branch around loads
+    long long row = row0 + tile * 32 + r;
+    row = row < rows_b ? row : rows_b - 1;
 #pragma unroll
     for (int k = 0; k < 2; ++k) q[k] = *reinterpret_cast<const f32x4*>(lg + row * 16 + 8 * h + 4 * k);
     t = lab[row];
+    if constexpr (GN) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) xq[u] = *reinterpret_cast<const u32x4*>(x0 + row * cin + 16 * u + 8 * h);
+    }
   };
-  f32x4 cur[2], nxt[2];
-  float tcur = 0.f, tnxt = 0.f;
-  load(wid, cur, tcur);
-  for (long long tile = wid; tile < tiles; tile += nw) {
-    load(tile + nw, nxt, tnxt);
-    const long long row = tile * 32 + r;
-    const bool ok = row < rows;
+  // ND tiles' loads in flight per wave (register buffers rotated by moves each tile): the kernel is load-latency-bound with one tile of look-ahead (round 6: 64 us at 2 x 96^3 = 4.5 TB/s).
+  // Tiles are still visited in the order tile, tile + nw, ... (the bias partials' summation order is unchanged).
+  constexpr int ND = GN ? HD_ND_GN : HD_ND;
+  f32x4 qb[ND][2];
+  float tb[ND];
+  u32x4 xb[ND][2];
+#pragma unroll
+  for (int k = 0; k < ND; ++k) load(wid + k * nw, qb[k], tb[k], xb[k]);
+  auto body = [&](long long tile, const f32x4 (&cur)[2], float tcur, const u32x4 (&xq)[2]) {
+    const long long row = row0 + tile * 32 + r;
+    const bool ok = row < rows_b;
     float gr[8];
     dice_bce_softmax_grad8(cur, tcur, h, kd_a, kd_b, kb, gr);
     u32x4 a[2];
@@ -376,10 +419,68 @@ __global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __rest
                 u32x4{pk[2 * u][0], pk[2 * u][1], pk[2 * u + 1][0], pk[2 * u + 1][1]};
         }
       }
-    }
+      if constexpr (GN) {
+        if (tn == 0) {  // (cin == 32: one n-tile; the stored bf16 dA and x0, as gn_bwd_partial reads them)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) cur[k] = nxt[k];
-    tcur = tnxt;
+          for (int u = 0; u < 2; ++u) {
+            const u32x4 av = u32x4{pk[2 * u][0], pk[2 * u][1], pk[2 * u + 1][0], pk[2 * u + 1][1]};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t aw = av[e >> 1], xw = xq[u][e >> 1];
+              const float a = __uint_as_float((e & 1) ? (aw & 0xffff0000u) : (aw << 16));
+              const float xv = __uint_as_float((e & 1) ? (xw & 0xffff0000u) : (xw << 16));
+              const f32x4 t = gtb[16 * u + 8 * h + e];
+              const float gd = ok && fmaf(xv, t[0], t[1]) > 0.f ? a : 0.f;  // the forward prologue's relu test
+              g1[8 * u + e] += gd;
+              g2[8 * u + e] = fmaf(gd, (xv - t[3]) * t[2], g2[8 * u + e]);
+            }
+          }
+        }
+      }
+    }
+  };
+  for (long long tile = wid; tile < tiles; tile += nw) {
+    const f32x4 c[2] = {qb[0][0], qb[0][1]};
+    const float tc = tb[0];
+    const u32x4 xc[2] = {xb[0][0], xb[0][1]};
+#pragma unroll
+    for (int k = 0; k + 1 < ND; ++k) {  // rotate (register moves)
+      qb[k][0] = qb[k + 1][0];
+      qb[k][1] = qb[k + 1][1];
+      tb[k] = tb[k + 1];
+      xb[k][0] = xb[k + 1][0];
+      xb[k][1] = xb[k + 1][1];
+    }
+    load(tile + ND * nw, qb[ND - 1], tb[ND - 1], xb[ND - 1]);
+    body(tile, c, tc, xc);
+  }
+  if constexpr (GN) {
+    // per channel over the block: the 32 lanes of a half hold the same channels (xor over r), then the 4 waves in
+    // order; one [cin][2] row per block into parts[sample][block of the sample]
+    __shared__ float gred[HD_T / 64][64][2];
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        g1[e] += __shfl_xor(g1[e], o, 32);
+        g2[e] += __shfl_xor(g2[e], o, 32);
+      }
+    if (r == 0) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int c = 16 * (e >> 3) + 8 * h + (e & 7);
+        gred[wave][c][0] = g1[e];
+        gred[wave][c][1] = g2[e];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * cin) {
+      const int c = threadIdx.x >> 1, k = threadIdx.x & 1;
+      float t = 0.f;
+#pragma unroll
+      for (int w_ = 0; w_ < HD_T / 64; ++w_) t += gred[w_][c][k];
+      gparts[(((long long)smp * bps + blockIdx.x % bps) * cin + c) * 2 + k] = t;
+    }
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s)
@@ -406,11 +507,8 @@ __global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __rest
 // grid cap: 768 = three 4-wave blocks per CU, resident at once at the backward's 148 VGPRs (2048 ran it in 2.7
 // rounds). 2 x 96^3 x 32 -> 16 (tools/kbench.py headf96 / headb96, gpurun_out/r04_hd): forward 37.3 -> 36.0 us,
 // backward 62.2 -> 57.3 us; 1024 / 1280 blocks: backward 66-70 us
-#ifndef U3D_HEAD_NB
-#define U3D_HEAD_NB 768
-#endif
 static int head_blocks(long long rows) {
-  return (int)std::min<long long>(U3D_HEAD_NB, std::max<long long>(1, (rows + 127) / 128));
+  return (int)std::min<long long>(opt(OPT_HEAD_NB), std::max<long long>(1, (rows + 127) / 128));
 }
 
 }  // namespace u3d
@@ -473,8 +571,37 @@ extern "C" int u3d_head_loss_bwd(const float* logits, const float* labels, long 
                   rows >= 1,
               "head_loss_bwd: bad args");
   U3D_REQUIRE(C == 16 && cin % 8 == 0 && cin >= 8 && cin <= 64, "head_loss_bwd: C %d (16 only) / cin %d", C, cin);
-  hipLaunchKernelGGL(head_loss_bwd_kernel, dim3(head_blocks(rows)), dim3(HD_T), 0, (hipStream_t)stream, logits, labels,
-                     rows, weights, sums, grad_out, (const bf16*)wpk_dgrad, cin, (bf16*)dA, (bf16*)dy_bf16,
+  hipLaunchKernelGGL(head_loss_bwd_kernel<false>, dim3(head_blocks(rows)), dim3(HD_T), 0, (hipStream_t)stream, logits,
+                     labels, rows, weights, sums, grad_out, (const bf16*)wpk_dgrad, cin, (bf16*)dA, (bf16*)dy_bf16,
                      dbias_partials);
   return check_launch("head_loss_bwd_kernel");
+}
+
+// Round 6: blocks per sample of u3d_head_loss_bwd_gn (its parts[n][bps][cin][2] and dbias_partials[n * bps][C]); 0 where
+// the GN form does not apply (v % 32 != 0, cin != 32).
+extern "C" int u3d_head_loss_bwd_gn_bps(int n, long long v, int cin) {
+  if (n < 1 || v < 32 || v % 32 != 0 || cin != 32 || (long long)n * v >= (1LL << 31)) return 0;
+  // 2 blocks per CU (the GN form's ~200 VGPRs leave 2 waves per SIMD; the plain form's 768 = 3 per CU would run as
+  // 1.5 rounds of blocks)
+  return std::max(1, (int)std::min<long long>(opt(OPT_HEAD_GN_NB), ((long long)n * v + 127) / 128) / n);
+}
+
+// u3d_head_loss_bwd plus the GroupNorm-backward partials of the head's GN + ReLU prologue (x0 = its input, gn_* = its
+// GroupNorm) into parts[n][bps][cin][2] = (sum g, sum g * xhat) per block of one sample, bps =
+// u3d_head_loss_bwd_gn_bps(n, v, cin); u3d_gn_bwd_parts then finalizes and applies them. dbias_partials holds n * bps
+// rows. dA, dy and the bias partials' total are those of u3d_head_loss_bwd up to the bias partials' summation order.
+extern "C" int u3d_head_loss_bwd_gn(const float* logits, const float* labels, int n, long long v, int C,
+                                    const float* weights, const double* sums, const float* grad_out,
+                                    const void* wpk_dgrad, int cin, void* dA, void* dy_bf16, float* dbias_partials,
+                                    const void* x0, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
+                                    int gn_groups, float* parts, u3d_stream_t stream) {
+  const int bps = u3d_head_loss_bwd_gn_bps(n, v, cin);
+  U3D_REQUIRE(bps > 0 && C == 16, "head_loss_bwd_gn: needs C = 16, cin = 32, v %% 32 == 0");
+  U3D_REQUIRE(logits && labels && weights && sums && grad_out && wpk_dgrad && dA && dy_bf16 && dbias_partials && x0 &&
+                  gn_stats && gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0 && parts,
+              "head_loss_bwd_gn: bad args");
+  hipLaunchKernelGGL(head_loss_bwd_kernel<true>, dim3(n * bps), dim3(HD_T), 0, (hipStream_t)stream, logits, labels,
+                     (long long)n * v, weights, sums, grad_out, (const bf16*)wpk_dgrad, cin, (bf16*)dA, (bf16*)dy_bf16,
+                     dbias_partials, (const bf16*)x0, gn_stats, gn_gamma, gn_beta, gn_groups, v, bps, parts);
+  return check_launch("head_loss_bwd_kernel<GN>");
 }

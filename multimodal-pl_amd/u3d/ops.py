@@ -793,14 +793,46 @@ def head_bwd(dy, wpk_dgrad, cin, dbias=None):
 HEAD_LOSS_FUSED = os.environ.get("U3D_HEAD_LOSS_FUSED", "1") != "0"
 
 
-def head_loss_bwd(lg, lab, weights, sums, grad_out, wpk_dgrad, cin, dbias=None):
+HEAD_GN_PARTS = os.environ.get("U3D_HEAD_GN_PARTS", "1") == "1"
+
+
+def head_gn_parts_ok(lg, x0, cin, gn):
+    """u3d_head_loss_bwd_gn applies: the head's GN + ReLU prologue input x0 bf16 with 32 channels, voxels per sample a
+    multiple of 32 (its blocks never straddle samples)."""
+    if not HEAD_GN_PARTS or gn is None or x0.dtype != torch.bfloat16 or cin != 32 or lg.shape[-1] != 16:
+        return False
+    n = lg.shape[0]
+    return query("u3d_head_loss_bwd_gn_bps", n, lg.numel() // (16 * n), cin) > 0
+
+
+def head_loss_bwd(lg, lab, weights, sums, grad_out, wpk_dgrad, cin, dbias=None, x0=None, gn=None):
     """head_bwd(partial_loss_bwd(lg, lab, weights, sums, grad_out)) for the softmax + BCE loss over 16 classes in one
     pass (u3d_head_loss_bwd): lg fp32 NDHWC [S, ..., 16], lab fp32 [S, ...]; the same (dA, dy bf16) and bias gradient
-    bitwise, without the fp32 dlogits tensor."""
+    bitwise, without the fp32 dlogits tensor.
+
+    ``x0``, ``gn`` = (stats, gamma, beta, groups) of the head's GroupNorm + ReLU prologue (round 6,
+    u3d_head_loss_bwd_gn, when head_gn_parts_ok): the GroupNorm backward's partial sums are taken in the same pass;
+    returns (dA, dy, parts) with parts [n, bps, cin, 2] for gn_bwd_parts."""
     C = lg.shape[-1]
     rows = lg.numel() // C
     dA = torch.empty(tuple(lg.shape[:-1]) + (cin,), dtype=torch.bfloat16, device=lg.device)
     dyb = torch.empty(tuple(lg.shape[:-1]) + (C,), dtype=torch.bfloat16, device=lg.device)
+    if gn is not None:
+        require_device(x0)
+        n = lg.shape[0]
+        v = rows // n
+        assert x0.shape[:-1] == lg.shape[:-1] and x0.shape[-1] == cin and x0.is_contiguous(), "head_loss_bwd: x0 shape"
+        bps = query("u3d_head_loss_bwd_gn_bps", n, v, cin)
+        assert bps > 0, "head_loss_bwd: GN-partials form does not apply (head_gn_parts_ok)"
+        dbp = torch.empty((n * bps, C), dtype=torch.float32, device=lg.device)
+        parts = torch.empty((n, bps, cin, 2), dtype=torch.float32, device=lg.device)
+        st, ga, be, G = gn
+        call("u3d_head_loss_bwd_gn", lg.data_ptr(), lab.data_ptr(), n, v, C, weights.data_ptr(), sums.data_ptr(),
+             grad_out.data_ptr(), wpk_dgrad.data_ptr(), cin, dA.data_ptr(), dyb.data_ptr(), dbp.data_ptr(),
+             x0.data_ptr(), st.data_ptr(), ga.data_ptr(), be.data_ptr(), G, parts.data_ptr(), _stream())
+        if dbias is not None:
+            channel_sum(dbp, out=dbias)
+        return dA, dyb, parts
     nb = query("u3d_head_bwd_blocks", rows)
     dbp = torch.empty((nb, C), dtype=torch.float32, device=lg.device)
     call("u3d_head_loss_bwd", lg.data_ptr(), lab.data_ptr(), rows, C, weights.data_ptr(), sums.data_ptr(),

@@ -175,12 +175,18 @@ class Tape:
                         dA2, gn2, key2, s2c = x.gn_pend.pop()
                         self.gn_bwd_one(x, ops.expand_s2(dA2, x.t.shape[:4]) if s2c else dA2, gn2, key2, G)
                     return
+                parts = None  # GroupNorm-backward partials a data-gradient pass took (head or ring epilogue)
                 if head:  # dA, bf16 dy and the bias gradient in one pass over the fp32 dlogits
                     db = self.grad_out(key + ".bias", b) if bias else None
                     if isinstance(dy, DeferredLossGrad):  # the loss gradient formed inside the head's pass
                         lg_, lab_, wt_, sums_, go_ = dy.payload
                         assert lg_.data_ptr() == y.data_ptr() and lg_.shape == y.shape, "deferred loss gradient: not this head's logits"
-                        dA, dyT = ops.head_loss_bwd(lg_, lab_, wt_, sums_, go_, pd, cin, dbias=db)
+                        if gn is not None and pair is None and ops.head_gn_parts_ok(lg_, x.t, cin, gn):
+                            # the prologue GroupNorm's backward partials in the same pass (no partial pass over dA)
+                            dA, dyT, parts = ops.head_loss_bwd(lg_, lab_, wt_, sums_, go_, pd, cin, dbias=db,
+                                                               x0=x.t, gn=gn)
+                        else:
+                            dA, dyT = ops.head_loss_bwd(lg_, lab_, wt_, sums_, go_, pd, cin, dbias=db)
                     else:
                         dA, dyT = ops.head_bwd(dy, pd, cin, dbias=db)
                     if bias:
@@ -202,7 +208,6 @@ class Tape:
                 s2c = (gn is not None and pair == "park" and k == 1 and stride == 2 and ops.S2_COMPACT
                        and ops._use_conv1x1(dyT.dtype, dyT.shape[-1], cin, 1, dyT.shape[0])
                        and ops.s2_compact_ok(x.t.shape, cin, dyT.element_size()))
-                parts = None
                 if gn is not None and not head and pair != "park" and not (pair == "finish" and x.gn_pend):
                     fused = ops.conv_dgrad_gn(dyT, pd, cin, x.t, k, stride, gn,  # GN-bwd partials in the epilogue
                                               dgb=lambda: (self.grad_out(gn_key + ".weight", gn[1]),

@@ -29,11 +29,12 @@ def test_head_loss_bwd_bitwise(gpu, cin, dims):
     assert torch.equal(db0, db1)
 
 
-def _step_grads(dev, fused, extra, monkeypatch, calls):
+def _step_grads(dev, fused, extra, monkeypatch, calls, gn_parts=False):
     import unet3D
     from loss_functions.loss_partial import EDiceLoss_partial
     from u3d import ops
     monkeypatch.setattr(ops, "HEAD_LOSS_FUSED", fused)
+    monkeypatch.setattr(ops, "HEAD_GN_PARTS", gn_parts)
     torch.manual_seed(0)
     m = unet3D.unet3D_baseline([1, 2, 2, 2, 2], num_classes=16, weight_std=True).to(dev).train()
     crit = EDiceLoss_partial(16)
@@ -110,3 +111,84 @@ def test_loss_forward_lane_pair_form(gpu, dims):
     # fp32 per-block partials of up to a few thousand terms, summed in a different order: ~1e-6 relative apart
     torch.testing.assert_close(s1, s0, rtol=2e-5, atol=1e-6)
     torch.testing.assert_close(l1, l0, rtol=2e-5, atol=1e-7)
+
+
+def _gn_case(gpu, dims, cin=32, G=8, seed=4):
+    from u3d import ops
+    g = torch.Generator().manual_seed(seed)
+    lg = (torch.randn(dims + (16,), generator=g) * 3).to(gpu)
+    lab = torch.randint(0, 16, dims, generator=g).float().to(gpu)
+    wt = (torch.rand(16, generator=g) < 0.7).float().to(gpu)
+    _, sums = ops.partial_loss_fwd(lg, lab, wt, True, True)
+    go = torch.tensor([0.61], device=gpu)
+    w = torch.randn(16, cin, 1, 1, 1, generator=g).to(gpu)
+    _, pd, _ = ops.wstd_fwd(w, torch.bfloat16, False)
+    x0 = (torch.randn(dims + (cin,), generator=g) * 1.4 + 0.3).to(gpu).to(torch.bfloat16)
+    st = ops.gn_stats(x0, G)
+    ga = (1 + 0.3 * torch.randn(cin, generator=g)).to(gpu)
+    be = (0.3 * torch.randn(cin, generator=g)).to(gpu)
+    return lg, lab, wt, sums, go, pd, x0, (st, ga, be, G)
+
+
+@pytest.mark.parametrize("dims,G", [((2, 8, 8, 16), 8), ((3, 5, 6, 32), 16), ((1, 1, 4, 8), 8), ((2, 96, 96, 96), 8),
+                                    ((1, 32, 33, 35), 4)])
+def test_head_loss_bwd_gn_parts(gpu, dims, G):
+    """u3d_head_loss_bwd_gn (round 6): the head's GN + ReLU prologue backward partials taken in the head's pass.
+    dA and the bf16 dy bitwise those of u3d_head_loss_bwd; the bias gradient, the partials (against an fp64 torch
+    restatement of gn_bwd's per-channel sums, reference: GroupNorm backward behind unet3D.py:1644-1657) and the
+    resulting dx / dgamma / dbeta (against the separate-partial-pass gn_bwd) within fp32 summation-order tolerance."""
+    from u3d import ops
+    lg, lab, wt, sums, go, pd, x0, gn = _gn_case(gpu, dims, G=G)
+    assert ops.head_gn_parts_ok(lg, x0, 32, gn)
+    db0, db1 = torch.empty(16, device=gpu), torch.empty(16, device=gpu)
+    dA0, dy0 = ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, dbias=db0)
+    dA1, dy1, parts = ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, dbias=db1, x0=x0, gn=gn)
+    assert torch.equal(dA0, dA1) and torch.equal(dy0, dy1)
+    torch.testing.assert_close(db1, db0, rtol=1e-5, atol=1e-6)
+    # fp64 restatement of the per-(sample, channel) sums
+    st, ga, be, _ = gn
+    n, c = x0.shape[0], 32
+    grp = torch.arange(c, device=gpu) // (c // G)
+    mu, rs = st[:, grp, 0].double(), st[:, grp, 1].double()
+    xf = x0.double().reshape(n, -1, c)
+    sc = rs.float() * ga[None]
+    pre = x0.float().reshape(n, -1, c) * sc[:, None] + (be[None] - st[:, grp, 0] * sc)[:, None]
+    gmask = torch.where(pre > 0, dA0.double().reshape(n, -1, c), torch.zeros((), dtype=torch.float64, device=gpu))
+    xhat = (xf - mu[:, None]) * rs[:, None]
+    ref = torch.stack([gmask.sum(1), (gmask * xhat).sum(1)], -1)  # [n, c, 2]
+    got = parts.double().sum(1)
+    scale = gmask.abs().sum(1).max().item() + 1e-30
+    assert (got - ref).abs().max().item() <= 1e-5 * scale, (got - ref).abs().max().item()
+    dg0, dbt0 = torch.empty(c, device=gpu), torch.empty(c, device=gpu)
+    dg1, dbt1 = torch.empty(c, device=gpu), torch.empty(c, device=gpu)
+    dx0 = ops.gn_bwd(dA0, x0, st, ga, be, G, dgamma=dg0, dbeta=dbt0)
+    dx1 = ops.gn_bwd_parts(dA1, x0, parts, st, ga, be, G, dgamma=dg1, dbeta=dbt1)
+    torch.testing.assert_close(dg1, dg0, rtol=1e-4, atol=1e-4 * dg0.abs().max().item())
+    torch.testing.assert_close(dbt1, dbt0, rtol=1e-4, atol=1e-4 * dbt0.abs().max().item())
+    # bf16 dx: the apply coefficients differ in the last fp32 bits -> at most one bf16 rounding step apart
+    d = (dx1.float() - dx0.float()).abs()
+    ulp = torch.maximum(dx0.float().abs(), dx1.float().abs()) * 2.0 ** -7 + 1e-6
+    assert bool((d <= ulp).all()), d.max().item()
+    # deterministic
+    _, _, parts2 = ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, x0=x0, gn=gn)
+    assert torch.equal(parts, parts2)
+
+
+def test_head_loss_bwd_gn_applicability(gpu):
+    from u3d import ops
+    lg, lab, wt, sums, go, pd, x0, gn = _gn_case(gpu, (2, 3, 5, 7))  # v = 105: blocks would straddle samples
+    assert not ops.head_gn_parts_ok(lg, x0, 32, gn)
+    with pytest.raises(AssertionError):
+        ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, x0=x0, gn=gn)
+
+
+def test_step_gradients_head_gn_parts(gpu, monkeypatch):
+    """Whole-step parameter gradients with the head's GN partials fused vs the separate partial pass: the same up to
+    fp32 summation order (the partial sums are regrouped; everything upstream inherits the last-bit differences)."""
+    calls = [0]
+    a, _, _ = _step_grads(gpu, True, None, monkeypatch, calls, gn_parts=False)
+    b, _, _ = _step_grads(gpu, True, None, monkeypatch, calls, gn_parts=True)
+    for n in a:
+        scale = a[n].abs().max().item() + 1e-12
+        err = (a[n] - b[n]).abs().max().item()
+        assert err <= 2e-2 * scale, (n, err, scale)

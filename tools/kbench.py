@@ -229,6 +229,36 @@ CASES["fwd96_plain"] = lambda: _fwd(2, 32, 32, 96, 3, 1, False, False)
 CASES["head96"] = lambda: _fwd(2, 32, 16, 96, 1, 1, True, False)
 
 
+def _hlb(n, s, mode):
+    """the head's fused loss + data-gradient backward at 2 x 96^3 (cin 32, 16 classes): "plain" alone, "gn" with the
+    prologue GN's backward partials, "sep" / "fused" plus the whole GroupNorm backward (separate partial pass or parts)"""
+    shp = (n, s, s, s)
+    lg = torch.randn(shp + (16,), device=dev) * 3
+    lab = torch.randint(0, 16, shp, device=dev).float()
+    wt = torch.ones(16, device=dev)
+    _, sums = ops.partial_loss_fwd(lg, lab, wt, True, True)
+    go = torch.ones(1, device=dev)
+    _, pd, _ = ops.wstd_fwd(torch.randn(16, 32, 1, 1, 1, device=dev), bf, False)
+    x0 = torch.randn(shp + (32,), device=dev).to(bf)
+    g = (ops.gn_stats(x0, 8), torch.ones(32, device=dev), torch.zeros(32, device=dev), 8)
+    dg, db, dbb = torch.zeros(32, device=dev), torch.zeros(32, device=dev), torch.zeros(16, device=dev)
+
+    def f():
+        if mode in ("gn", "fused"):
+            da, _, parts = ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, dbias=dbb, x0=x0, gn=g)
+            if mode == "fused":
+                ops.gn_bwd_parts(da, x0, parts, g[0], g[1], g[2], 8, dgamma=dg, dbeta=db)
+        else:
+            da, _ = ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, dbias=dbb)
+            if mode == "sep":
+                ops.gn_bwd(da, x0, g[0], g[1], g[2], 8, dgamma=dg, dbeta=db)
+    return t_(f), 0.0
+
+
+for _m in ("plain", "gn", "sep", "fused"):
+    CASES[f"hlb96{_m}"] = (lambda m=_m: _hlb(2, 96, m))
+
+
 def _queue(fn):
     def run():
         saved = ops.RING_QUEUE
