@@ -259,6 +259,19 @@ for _m in ("plain", "gn", "sep", "fused"):
     CASES[f"hlb96{_m}"] = (lambda m=_m: _hlb(2, 96, m))
 
 
+def _slabsum(ns, co, ci):
+    """the slab sum of one weight gradient [ns, 27, co, ci] fp32 (u3d_wgrad_sum_slabs): the batched end-of-step sum's
+    per-weight work (96^3: 256 slabs of 27 x 32 x 32; 48^3: 64 of 27 x 64 x 64; 24^3: 16 of 128^2; 12^3: 4 of 256^2)"""
+    part = torch.randn(ns, 27, co, ci, device=dev)
+    us = t_(lambda: ops.sum_slabs(part, ns, co, ci))
+    print(f"   ({part.numel() * 4 / us / 1e6:.2f} TB/s read)")
+    return us, 0.0
+
+
+for (_lvl, _ns, _c) in (("96", 256, 32), ("48", 64, 64), ("24", 16, 128), ("12", 4, 256)):
+    CASES[f"slabsum{_lvl}"] = (lambda ns=_ns, c=_c: _slabsum(ns, c, c))
+
+
 def _queue(fn):
     def run():
         saved = ops.RING_QUEUE
