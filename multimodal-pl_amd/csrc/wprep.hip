@@ -396,7 +396,10 @@ __global__ __launch_bounds__(WB_T) void wstd_grad_row_kernel(WBatch<WPack> bt) {
   __shared__ double red[WB_T / 64][2];
   __shared__ float fs[2];
   __shared__ float gl[NPT * WB_T];
-  const WPack& D = bt.d[find_desc(bt, blockIdx.x)];
+  // round 6: the descriptor by value (one scalar fetch, not a kernel-argument reload ahead of every load), g's (t, ci)
+  // from a fixed ci and a t stride where cin divides the block (every trunk conv: no per-element integer division —
+  // ~40 instructions between consecutive loads before), and w's loads issued with g's, ahead of the LDS stores
+  const WPack D = bt.d[find_desc(bt, blockIdx.x)];
   const int co = blockIdx.x - D.b0, tid = threadIdx.x;
   const int K3 = D.k3, K = D.cin * K3, cout_p = round_up(D.cout, 32), cin_p = round_up(D.cin, 32);
   const bool std_ = D.st != nullptr;
@@ -404,7 +407,32 @@ __global__ __launch_bounds__(WB_T) void wstd_grad_row_kernel(WBatch<WPack> bt) {
   const float rsg = std_ ? 1.f / D.st[co * 2 + 1] : 1.f;
   const float* wr = D.w + (long long)co * K;
   float wv[NPT], gv[NPT];
-  {  // g[t][co][ci], element j = t * cin + ci -> LDS slot ci * K3 + t (parameter order)
+  // buffer loads: an element past the row gets the out-of-range sentinel offset and reads 0 with no branch around the
+  // load (plain predicated loads came out as one branch + wait per element)
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)wr, 0, 0x7FFFFFF0, 0x00020000);
+  auto load_w = [&]() {
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int e = tid + i * WB_T;
+      const unsigned off = e < K && std_ ? (unsigned)e * 4u : 0xFFFFFFF0u;
+      wv[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wrs, off, 0, 0));
+    }
+  };
+  if (WB_T % D.cin == 0) {  // uniform: element j = tid + i * WB_T has ci = tid % cin, t = tid / cin + i * WB_T / cin
+    const int ci = tid % D.cin, t0 = tid / D.cin, ts = WB_T / D.cin;
+    const auto grs = __builtin_amdgcn_make_buffer_rsrc((void*)D.g, 0, 0x7FFFFFF0, 0x00020000);
+    const unsigned g0 = (unsigned)(((t0 * cout_p + co) * cin_p + ci) * 4), gs = (unsigned)(ts * cout_p * cin_p * 4);
+    float gt[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const unsigned off = tid + i * WB_T < K ? g0 + (unsigned)i * gs : 0xFFFFFFF0u;
+      gt[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, off, 0, 0));
+    }
+    load_w();
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+      if (tid + i * WB_T < K) gl[ci * K3 + t0 + i * ts] = gt[i];
+  } else {  // g[t][co][ci], element j = t * cin + ci -> LDS slot ci * K3 + t (parameter order)
     float gt[NPT];
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
@@ -412,17 +440,13 @@ __global__ __launch_bounds__(WB_T) void wstd_grad_row_kernel(WBatch<WPack> bt) {
       const int t = j / D.cin, ci = j - t * D.cin;
       gt[i] = j < K ? D.g[((long long)t * cout_p + co) * cin_p + ci] : 0.f;
     }
+    load_w();
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       const int j = tid + i * WB_T;
       const int t = j / D.cin, ci = j - t * D.cin;
       if (j < K) gl[ci * K3 + t] = gt[i];
     }
-  }
-#pragma unroll
-  for (int i = 0; i < NPT; ++i) {
-    const int e = tid + i * WB_T;
-    wv[i] = e < K && std_ ? wr[e] : 0.f;
   }
   __syncthreads();
 #pragma unroll
