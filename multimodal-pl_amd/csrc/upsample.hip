@@ -115,6 +115,17 @@ __global__ __launch_bounds__(256) void up_fwd_quad_kernel(const bf16* __restrict
     const uint32_t u = v[k >> 1];
     return __builtin_bit_cast(float, (k & 1) ? (u & 0xFFFF0000u) : (u << 16));
   };
+  // round 6: the 4 skip vectors issued with the 18 input loads (loaded inside the output loop, each was followed by a
+  // wait for every load in flight: 4 more round trips per thread; 96^3 launch 73 us = 3.3 TB/s)
+  u32x4 skr[2][2];
+  if (skip) {
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+      for (int qw = 0; qw < 2; ++qw)
+        skr[qh][qw] = *reinterpret_cast<const u32x4*>(
+            skip + ((((long long)nn * D + od) * H + 2 * ih + qh) * W + 2 * iw + qw) * c + j * 8);
+  }
 #pragma unroll
   for (int qh = 0; qh < 2; ++qh) {
     const int oh = 2 * ih + qh;
@@ -125,8 +136,6 @@ __global__ __launch_bounds__(256) void up_fwd_quad_kernel(const bf16* __restrict
       const int ow = 2 * iw + qw;
       const Lerp Lw = lerp_of(ow, w);
       const long long off = ((((long long)nn * D + od) * H + oh) * W + ow) * c + j * 8;
-      float sv[8];
-      if (skip) loadv<bf16, 8>(skip + off, sv);
       u32x4 t[2][2][2];  // [a][th][tw]
 #pragma unroll
       for (int a_ = 0; a_ < 2; ++a_)
@@ -143,7 +152,7 @@ __global__ __launch_bounds__(256) void up_fwd_quad_kernel(const bf16* __restrict
                         Lh.l1 * (Lw.l0 * un(t[1][1][0], e) + Lw.l1 * un(t[1][1][1], e)));
       if (skip)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] += sv[e];
+        for (int e = 0; e < 8; ++e) o[e] += un(skr[qh][qw], e);
       storev<bf16, 8>(y + off, o);
       if constexpr (STATS) {
 #pragma unroll
@@ -178,8 +187,7 @@ __global__ __launch_bounds__(256) void up_fwd_quad_kernel(const bf16* __restrict
     if (threadIdx.x < 32) {
       const int g = threadIdx.x >> 1, comp = threadIdx.x & 1;
       float t = 0.f;
-#pragma unroll
-      for (int wv = 0; wv < 4; ++wv) {
+      for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) {
         if constexpr (CPG >= 16) {  // chunks 2g, 2g + 1 (slot 0 each)
           t += red[wv][2 * g][comp];
           t += red[wv][2 * g + 1][comp];
@@ -418,6 +426,15 @@ __global__ __launch_bounds__(256) void up_bwd_blk_kernel(const T* __restrict__ d
 
 using namespace u3d;
 
+// the quad kernel's block: one input row's w * c / 8 threads (192 at every trunk level) in whole waves, not 256 (a
+// quarter of every block idle before round 6); longer rows: 256-thread blocks
+static void up_quad_shape(int c, int w, int& gx, int& bx) {
+  const int tpr = w * (c / 8);
+  bx = tpr <= 256 ? (tpr + 63) / 64 * 64 : 256;
+  gx = cdiv(tpr, bx);
+}
+
+
 
 extern "C" int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
                                   u3d_stream_t stream) {
@@ -430,7 +447,9 @@ extern "C" int u3d_upsample2x_add(int dtype, const void* x, int n, int c, int d,
   U3D_REQUIRE((long long)n * 2 * d < 65536 && 2 * h < 65536, "upsample: volume too large for the row grid");
   const dim3 gr(cdiv(row, 256), 2 * h, n * 2 * d), bl(256);
   if (dtype == U3D_BF16 && vect && opt(OPT_UP_QUAD) != 0) {  // UP_QUAD = 0: the one-output kernel (A/B)
-    hipLaunchKernelGGL(up_fwd_quad_kernel<0>, dim3(cdiv(w * (c / 8), 256), h, n * 2 * d), bl, 0, s, (const bf16*)x,
+    int gx, bx;
+    up_quad_shape(c, w, gx, bx);
+    hipLaunchKernelGGL(up_fwd_quad_kernel<0>, dim3(gx, h, n * 2 * d), dim3(bx), 0, s, (const bf16*)x,
                        (const bf16*)skip, (bf16*)y, n, c, d, h, w, nullptr);
     return check_launch("up_fwd_quad_kernel");
   }
@@ -452,7 +471,9 @@ static bool up_stats_ok(int n, int c, int d, int h, int w) {
 
 extern "C" long long u3d_upsample2x_stats_ws_floats(int n, int c, int d, int h, int w) {
   if (!up_stats_ok(n, c, d, h, w)) return 0;
-  return (long long)n * cdiv(w * (c / 8), 256) * h * 2 * d * 32;
+  int gx, bx;
+  up_quad_shape(c, w, gx, bx);
+  return (long long)n * gx * h * 2 * d * 32;
 }
 
 extern "C" int u3d_upsample2x_add_stats(const void* x, int n, int c, int d, int h, int w, const void* skip, void* y,
@@ -460,7 +481,9 @@ extern "C" int u3d_upsample2x_add_stats(const void* x, int n, int c, int d, int 
   U3D_REQUIRE(x && y && spart && stats && n > 0 && c > 0 && d > 0 && h > 0 && w > 0, "upsample_stats: bad args");
   U3D_REQUIRE(up_stats_ok(n, c, d, h, w), "upsample_stats: unsupported shape (c = %d)", c);
   hipStream_t s = (hipStream_t)stream;
-  const dim3 gr(cdiv(w * (c / 8), 256), h, n * 2 * d), bl(256);
+  int gx, bx;
+  up_quad_shape(c, w, gx, bx);
+  const dim3 gr(gx, h, n * 2 * d), bl(bx);
   switch (c / 16) {
     case 2: hipLaunchKernelGGL(up_fwd_quad_kernel<2>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w, spart); break;
     case 4: hipLaunchKernelGGL(up_fwd_quad_kernel<4>, gr, bl, 0, s, (const bf16*)x, (const bf16*)skip, (bf16*)y, n, c, d, h, w, spart); break;
