@@ -293,6 +293,14 @@ def _stem_plain(n=2, s=96):
     return t_(lambda: ops.stem_fwd(x, pf, 32, 1, bf)), 2.0 * n * s ** 3 * 27 * 32
 
 
+def _stem_stats(n=2, s=96):
+    """the bench's conv1: 1 -> 32 with the output GroupNorm(16) statistics from the epilogue (stem1_fwd_kernel<bf16, 1>)"""
+    x = torch.rand((n, 1, s, s, s), device=dev)
+    w = torch.randn(32, 1, 3, 3, 3, device=dev)
+    pf, _, _ = ops.wstd_fwd(w, bf, True, need_dgrad=False)
+    return t_(lambda: ops.stem_fwd_stats(x, pf, 32, 1, bf)), 2.0 * n * s ** 3 * 27 * 32
+
+
 CASES_EXTRA = {"fwd_s2_96": lambda: _fwd(2, 32, 64, 96, 3, 2, True, False),
                "fwd_s2_48": lambda: _fwd(2, 64, 128, 48, 3, 2, True, False),
                "fwd_s2_12": lambda: _fwd(2, 256, 256, 12, 3, 2, True, False),
@@ -300,7 +308,8 @@ CASES_EXTRA = {"fwd_s2_96": lambda: _fwd(2, 32, 64, 96, 3, 2, True, False),
                "fwd48_gn": lambda: _fwd(2, 64, 64, 48, 3, 1, True, False),
                "fwd48_res": lambda: _fwd(2, 64, 64, 48, 3, 1, False, True),
                "fwd24_plain": lambda: _fwd(2, 128, 128, 24, 3, 1, False, False),
-               "stem96": lambda: _stem_plain()}
+               "stem96": lambda: _stem_plain(),
+               "stem96st": lambda: _stem_stats()}
 CASES.update(CASES_EXTRA)
 
 
