@@ -20,6 +20,8 @@ done
 bash tools/pmc_sq2.sh r06_end_sq2 fwd96 dgrad96gn wgrad96 > /dev/null 2>&1 || { echo "sq2 failed"; exit 1; }
 for p in a b; do python3 tools/pmc_summary.py gpurun_out/r06_end_sq2/${p}_counter_collection.csv >> $O/sq2.txt 2>&1; done
 cat $O/pmc_*.json
+# the bench line's trace_check reads the newest profiles/*kernel_summary.txt: the trace just taken on this box
+cp $O/kernel_summary.txt profiles/r06_kernel_summary.txt
 fi
 if [ "$PART" = all ] || [ "$PART" = bench ]; then
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { echo "bench failed"; tail -5 $O/bench.log; exit 1; }
