@@ -46,6 +46,7 @@ enum Opt : int {
   OPT_LOSS_PAIR,      // loss forward, 16 classes softmax + BCE: each voxel's classes over a lane pair (0: one lane)
   OPT_HEAD_NB,        // classifier head / head backward blocks (at most)
   OPT_HEAD_GN_NB,     // head backward with the prologue GN's partials: blocks over all samples (at most)
+  OPT_STEM_MFMA,      // bf16 conv1 (1 -> 32) on the matrix cores, bf16 operands (0: the fp32 packed-FMA kernel)
   OPT_COUNT
 };
 int opt(Opt o);

@@ -179,6 +179,144 @@ __global__ __launch_bounds__(ST) void stem1_fwd_kernel(const float* __restrict__
   }
 }
 
+// Round 6: conv1 (cin 1 -> 32, stride 1, bf16 output) on the matrix cores. K = the 27 taps (padded to 32): one
+// v_mfma_f32_16x16x32_bf16 per (16 voxels, 16 output channels), A = the standardised weights [co][tap], B = the taps of
+// 16 voxels. The operands are bf16 — what the reference's autocast conv1 multiplies (the input volume and the
+// weight cast to bf16; unet3D.py:1632 under torch.autocast) — so the products are exact and only the fp32 summation
+// order differs from an fp64 conv on the same operands. The VALU form (stem1_fwd_kernel) spends 432 packed fp32 FMAs
+// per voxel on fp32 operands (57 us at 2 x 96^3, VALU-bound); here a lane loads its voxel's 27 taps, writes them as one
+// 64-B bf16 row of the wave's LDS block, and the wave runs 8 MFMAs per 64 voxels. The accumulators (lane: 4
+// channels of one voxel) go back through the same LDS block so every store instruction writes 1 KB of consecutive
+// voxels; STATS: the GroupNorm(16) partial sums of the stored bf16 values as stem1_fwd_kernel<.., true> (same spart
+// layout, another fp32 order).
+template <bool STATS>
+__global__ __launch_bounds__(ST) void stem1_mfma_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                                                        bf16* __restrict__ y, int d, int h, int w, long long nvox,
+                                                        float* __restrict__ spart = nullptr) {
+  typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+  __shared__ __attribute__((aligned(16))) char tr[ST / 64][64 * 64];  // per wave: 64 rows x 64 B
+  __shared__ float red[STATS ? ST / 64 : 1][32];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, r16 = l & 15, q = l >> 4;
+  const long long v0 = (long long)blockIdx.x * ST + wv * 64;  // the wave's first voxel
+  const long long vr = v0 + l;
+  const long long v = vr < nvox ? vr : nvox - 1;
+  const int xx = (int)(v % w);
+  const long long rr = v / w;
+  const int yy = (int)(rr % h);
+  const long long nz = rr / h;
+  const int z = (int)(nz % d);
+  const long long nn = nz / d;
+  const float* xb = x + nn * d * h * w;
+  char* const wb = tr[wv];
+  auto swz = [](int row, int c) { return 16 * (c ^ ((row >> 2) & 3)); };
+  {  // this lane's 27 taps (t = (kd * 3 + kh) * 3 + kw) as bf16, taps 27..31 zero, into row l
+    float tv[32];
+#pragma unroll
+    for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int zd = z + kd - 1, zh = yy + kh - 1, zw = xx + kw - 1;
+          const bool ok = (unsigned)zd < (unsigned)d && (unsigned)zh < (unsigned)h && (unsigned)zw < (unsigned)w;
+          tv[(kd * 3 + kh) * 3 + kw] = ok ? xb[((long long)zd * h + zh) * w + zw] : 0.f;
+        }
+#pragma unroll
+    for (int t = 27; t < 32; ++t) tv[t] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      u32x4 pk;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pk[k] = pack_bf16x2(tv[8 * c + 2 * k], tv[8 * c + 2 * k + 1]);
+      *reinterpret_cast<u32x4*>(wb + l * 64 + swz(l, c)) = pk;
+    }
+  }
+  // A fragments: lane (r16, q) holds W[co = 16 cb + r16][taps 8q .. 8q + 7] (bf16-valued fp32 table: exact)
+  bf16x8_t af[2];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    u32x4 pk;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t0 = 8 * q + 2 * k, t1 = t0 + 1;
+      pk[k] = pack_bf16x2(t0 < 27 ? wt[t0 * 32 + 16 * cb + r16] : 0.f, t1 < 27 ? wt[t1 * 32 + 16 * cb + r16] : 0.f);
+    }
+    af[cb] = __builtin_bit_cast(bf16x8_t, pk);
+  }
+  __builtin_amdgcn_wave_barrier();
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int row = 16 * g + r16;
+    const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u32x4*>(wb + row * 64 + swz(row, q)));
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+      acc[g][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cb], bf, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  }
+  __builtin_amdgcn_wave_barrier();
+  // D[co = 16 cb + 4q + i][voxel 16 g + r16] -> row (16 g + r16), channels 16 cb + 4 q .. + 3 (8 B)
+  float gs[2][2], gq[2][2];  // STATS: [cb][group 8 cb + 2 q + j] (sum, squares) of the stored values
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) gs[cb][j] = gq[cb][j] = 0.f;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int row = 16 * g + r16;
+    const bool ok = v0 + row < nvox;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const uint32_t lo = pack_bf16x2(acc[g][cb][0], acc[g][cb][1]), hi = pack_bf16x2(acc[g][cb][2], acc[g][cb][3]);
+      const int cbyte = 32 * cb + 8 * q;  // byte offset of channel 16 cb + 4 q in the 64-B row
+      *reinterpret_cast<uint2*>(wb + row * 64 + swz(row, cbyte >> 4) + (cbyte & 15)) = uint2{lo, hi};
+      if constexpr (STATS) {
+        const float a0 = __uint_as_float(lo << 16), a1 = __uint_as_float(lo & 0xffff0000u);
+        const float a2 = __uint_as_float(hi << 16), a3 = __uint_as_float(hi & 0xffff0000u);
+        gs[cb][0] += ok ? a0 + a1 : 0.f;
+        gq[cb][0] += ok ? a0 * a0 + a1 * a1 : 0.f;
+        gs[cb][1] += ok ? a2 + a3 : 0.f;
+        gq[cb][1] += ok ? a2 * a2 + a3 * a3 : 0.f;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // lane-linear 16-B chunks: each store instruction writes 1 KB of consecutive voxels
+    const int p = l + 64 * k, vx = p >> 2, c4 = p & 3;
+    const u32x4 pk = *reinterpret_cast<const u32x4*>(wb + vx * 64 + swz(vx, c4));
+    if (v0 + vx < nvox) *reinterpret_cast<u32x4*>(y + (v0 + vx) * 32 + 8 * c4) = pk;
+  }
+  if constexpr (STATS) {
+    // over the 16 lanes of each q (xor over r16), then the block's waves in order; red[wave][2 * group + k]
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          gs[cb][j] += __shfl_xor(gs[cb][j], o);
+          gq[cb][j] += __shfl_xor(gq[cb][j], o);
+        }
+    if (r16 == 0) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int grp = 8 * cb + 2 * q + j;
+          red[wv][2 * grp] = gs[cb][j];
+          red[wv][2 * grp + 1] = gq[cb][j];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      float t = 0.f;
+#pragma unroll
+      for (int w_ = 0; w_ < ST / 64; ++w_) t += red[w_][threadIdx.x];
+      spart[(long long)blockIdx.x * 32 + threadIdx.x] = t;
+    }
+  }
+}
+
 // dW[t][co][ci] partial over a voxel split: thread per (t, ci, co) output, loop over the split's voxels.
 template <typename T>
 __global__ __launch_bounds__(ST) void stem_wgrad_kernel(const T* __restrict__ dy, const float* __restrict__ x,
@@ -392,8 +530,12 @@ extern "C" int u3d_stem1_fwd_stats(const float* x, int n, int d, int h, int w, c
   float* wt = static_cast<float*>(ws);
   const long long nvox = (long long)n * v;
   hipLaunchKernelGGL(stem1_wtab_kernel<bf16>, dim3(1), dim3(1024), 0, s, (const bf16*)wpk, 32, wt);
-  hipLaunchKernelGGL((stem1_fwd_kernel<bf16, true>), dim3((unsigned)(nvox / ST)), dim3(ST), 0, s, x, wt, (bf16*)y, d, h, w,
-                     nvox, spart);
+  if (opt(OPT_STEM_MFMA) != 0)
+    hipLaunchKernelGGL(stem1_mfma_kernel<true>, dim3((unsigned)(nvox / ST)), dim3(ST), 0, s, x, wt, (bf16*)y, d, h, w,
+                       nvox, spart);
+  else
+    hipLaunchKernelGGL((stem1_fwd_kernel<bf16, true>), dim3((unsigned)(nvox / ST)), dim3(ST), 0, s, x, wt, (bf16*)y, d,
+                       h, w, nvox, spart);
   if (check_launch("stem1_fwd_kernel<stats>")) return U3D_EHIP;
   return launch_gn16_finalize(spart, n, (int)(v / ST), 2.0 * (double)v, stats, s);
 }
@@ -413,7 +555,10 @@ extern "C" int u3d_stem_fwd(int dtype, const float* x, int n, int cin, int d, in
     const dim3 g1((unsigned)((nvox + ST - 1) / ST));
     if (dtype == U3D_BF16) {
       hipLaunchKernelGGL(stem1_wtab_kernel<bf16>, dim3(1), dim3(1024), 0, s, (const bf16*)wpk, round_up(cin, 32), wt);
-      hipLaunchKernelGGL(stem1_fwd_kernel<bf16>, g1, dim3(ST), 0, s, x, wt, (bf16*)y, d, h, w, nvox);
+      if (opt(OPT_STEM_MFMA) != 0)
+        hipLaunchKernelGGL(stem1_mfma_kernel<false>, g1, dim3(ST), 0, s, x, wt, (bf16*)y, d, h, w, nvox, nullptr);
+      else
+        hipLaunchKernelGGL(stem1_fwd_kernel<bf16>, g1, dim3(ST), 0, s, x, wt, (bf16*)y, d, h, w, nvox);
     } else {
       hipLaunchKernelGGL(stem1_wtab_kernel<float>, dim3(1), dim3(1024), 0, s, (const float*)wpk, round_up(cin, 32), wt);
       hipLaunchKernelGGL(stem1_fwd_kernel<float>, g1, dim3(ST), 0, s, x, wt, (float*)y, d, h, w, nvox);

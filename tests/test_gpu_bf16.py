@@ -356,10 +356,54 @@ def test_stem1_packed_kernel_bitwise_equals_generic(gpu, dt, dims):
     x = torch.randn((2, 1) + dims, device=gpu)
     w = torch.randn(32, 1, 3, 3, 3, device=gpu)
     pf, _, _ = ops.wstd_fwd(w, dt, True, need_dgrad=False)
-    y = ops.stem_fwd(x, pf, 32, 1, dt)
+    with ops.option("STEM_MFMA", 0):  # (bf16 runs the matrix-core kernel by default: test_stem1_mfma_*)
+        y = ops.stem_fwd(x, pf, 32, 1, dt)
     with ops.option("STEM1", 0):
         y0 = ops.stem_fwd(x, pf, 32, 1, dt)
     assert torch.equal(y, y0)
+
+
+def _stem_ref_bf16_operands(x, pf):
+    """fp64 conv1 on the operands the matrix-core kernel multiplies: the input and the packed weights in bf16."""
+    wq = pf.float().cpu()[:, :32, :1].permute(1, 2, 0).reshape(32, 1, 3, 3, 3).double()
+    return wq, x.to(torch.bfloat16).double().cpu()
+
+
+@pytest.mark.parametrize("n,dims", [(2, (5, 7, 16)), (1, (3, 5, 7)), (2, (8, 8, 16)), (3, (4, 9, 33))])
+def test_stem1_mfma_vs_fp64(gpu, n, dims):
+    """bf16 conv1 (1 -> 32) on the matrix cores (round 6, stem1_mfma_kernel): bf16 operands (the reference's autocast
+    conv1), exact products, fp32 sums: every output within one bf16 rounding of the fp64 conv on the same operands
+    (+ 1e-6 of the largest output for the fp32 summation order); ragged voxel counts (partial waves) included."""
+    from u3d import ops
+    torch.manual_seed(21)
+    x = torch.randn((n, 1) + dims, device=gpu) * 1.5 + 0.3
+    w = torch.randn(32, 1, 3, 3, 3, device=gpu)
+    pf, _, _ = ops.wstd_fwd(w, torch.bfloat16, True, need_dgrad=False)
+    y = ops.stem_fwd(x, pf, 32, 1, torch.bfloat16)
+    wq, xb = _stem_ref_bf16_operands(x, pf)
+    ref = F.conv3d(xb, wq, padding=1).permute(0, 2, 3, 4, 1)
+    d = (y.double().cpu() - ref).abs()
+    assert bool((d <= ref.abs() * 2.0 ** -8 + 1e-6 * ref.abs().max()).all()), d.max().item()
+
+
+def test_stem1_mfma_bench_size(gpu):
+    """the bench's conv1 (2 x 96^3, with the epilogue statistics): sampled planes within one bf16 rounding of the fp64
+    conv on the bf16 operands; the statistics form writes the same output as the plain form."""
+    from u3d import ops
+    torch.manual_seed(22)
+    x = torch.rand((2, 1, 96, 96, 96), device=gpu) * 2 - 1
+    w = torch.randn(32, 1, 3, 3, 3, device=gpu)
+    pf, _, _ = ops.wstd_fwd(w, torch.bfloat16, True, need_dgrad=False)
+    y, s16 = ops.stem_fwd_stats(x, pf, 32, 1, torch.bfloat16)
+    assert s16 is not None
+    assert torch.equal(y, ops.stem_fwd(x, pf, 32, 1, torch.bfloat16))
+    wq, xb = _stem_ref_bf16_operands(x, pf)
+    for n in range(2):
+        for z in (0, 47, 95):
+            lo, hi = max(0, z - 1), min(96, z + 2)
+            ref = F.conv3d(xb[n:n + 1, :, lo:hi], wq, padding=1)[0, :, z - lo].permute(1, 2, 0)
+            dd = (y[n, z].double().cpu() - ref).abs()
+            assert bool((dd <= ref.abs() * 2.0 ** -8 + 1e-6 * ref.abs().max()).all()), (n, z, dd.max().item())
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
