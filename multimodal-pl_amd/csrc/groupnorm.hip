@@ -83,6 +83,48 @@ __device__ __forceinline__ void load_da2(const T* __restrict__ da2, const RedGeo
   }
 }
 
+// Round 6: fine-voxel coordinates advanced incrementally along a loop's fixed voxel stride (no per-voxel divisions:
+// s2_index's two quotients were most of the S2 kernels' extra instructions), and da2 read by compact index
+struct Crd {
+  int z, y, x;
+};
+__device__ __forceinline__ Crd crd_of(long long v, const RedGeom& g) {
+  const int vi = (int)v, hw = g.fh * g.fw;
+  const int a = vi / hw, rem = vi - a * hw, b = rem / g.fw;
+  return Crd{a, b, rem - b * g.fw};
+}
+__device__ __forceinline__ Crd crd_add(Crd c, const Crd& s, const RedGeom& g) {  // s: a stride's (z, y, x), y < fh, x < fw
+  c.x += s.x;
+  const int cx = c.x >= g.fw;
+  c.x -= cx ? g.fw : 0;
+  c.y += s.y + cx;
+  const int cy = c.y >= g.fh;
+  c.y -= cy ? g.fh : 0;
+  c.z += s.z + cy;
+  return c;
+}
+// da2 (compact) at fine voxel c of sample n, zeros at odd voxels or past the volume (ok = false)
+template <typename T>
+__device__ __forceinline__ void load_da2_crd(const T* __restrict__ da2, const RedGeom& g, int n, const Crd& c, bool ok,
+                                             int j, float (&d2)[16 / sizeof(T)]) {
+  constexpr int VEC = 16 / sizeof(T);
+  const bool ev = ok && ((c.z | c.y | c.x) & 1) == 0;
+  const long long ci = ((long long)(c.z >> 1) * g.ch + (c.y >> 1)) * g.cw + (c.x >> 1);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)da2, 0, (int)(g.n * g.cv * g.c * (int)sizeof(T)), 0x00020000);
+  const unsigned bo = ev ? (unsigned)((((long long)n * g.cv + ci) * g.c + j * VEC) * sizeof(T)) : 0xFFFFFFF0u;
+  const u32x4 r = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, bo, 0, 0));
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d2[i] = __uint_as_float(r[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      d2[2 * i] = __uint_as_float(r[i] << 16);
+      d2[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
+    }
+  }
+}
+
 // reduction blocks over all samples
 static long long gn_max_blocks() { return std::max(1, opt(OPT_GN_MAXBLK)); }
 
@@ -520,16 +562,29 @@ __global__ __launch_bounds__(GT) void gn_bwd2_partial(const T* __restrict__ da1,
       }
     };
     constexpr int PR = U3D_GN2_PR;  // voxels per round (3 predicated loads each)
+    Crd cr{}, s1{}, sr{};  // S2: coordinates of v, the strides vlanes and PR * vlanes
+    if constexpr (S2) {
+      cr = crd_of(v0 + vl, g);
+      s1 = crd_of(g.vlanes, g);
+      sr = crd_of((long long)PR * g.vlanes, g);
+    }
     for (long long v = v0 + vl; v < v1; v += PR * g.vlanes) {
       float xv[PR][VEC], d1[PR][VEC], d2[PR][VEC];
+      Crd cu = cr;
 #pragma unroll
       for (int u = 0; u < PR; ++u) {
         const long long vv = std::min(v + u * g.vlanes, v1 - 1);
         const long long off = base + vv * g.c + j * VEC;
         load16<T>(x + off, xv[u]);
         load16<T>(da1 + off, d1[u]);
-        load_da2<T, S2>(da2, g, n, vv, j, off, d2[u]);
+        if constexpr (S2) {
+          load_da2_crd<T>(da2, g, n, cu, v + u * g.vlanes < v1, j, d2[u]);
+          cu = crd_add(cu, s1, g);
+        } else {
+          load_da2<T, S2>(da2, g, n, vv, j, off, d2[u]);
+        }
       }
+      if constexpr (S2) cr = crd_add(cr, sr, g);
 #pragma unroll
       for (int u = 0; u < PR; ++u) {
         if (v + u * g.vlanes >= v1)
@@ -604,6 +659,12 @@ __global__ __launch_bounds__(GT) void gn_bwd2_apply(const T* __restrict__ da1, c
   }
   const long long nb = (long long)n * g.v * g.c + j * VEC;
   const int vstep = stride / g.chn;
+  Crd cr{}, s1{}, s2{};  // S2: coordinates of vox, the strides vstep and 2 vstep
+  if constexpr (S2) {
+    cr = crd_of(first / g.chn, g);
+    s1 = crd_of(vstep, g);
+    s2 = crd_of(2LL * vstep, g);
+  }
   for (long long vox = first / g.chn; vox < g.v; vox += 2LL * vstep) {  // rounds of 2 voxels (up to 8 loads)
     float xv[2][VEC], d1[2][VEC], d2[2][VEC], o[2][VEC];
 #pragma unroll
@@ -612,9 +673,13 @@ __global__ __launch_bounds__(GT) void gn_bwd2_apply(const T* __restrict__ da1, c
       const long long off = nb + vv * g.c;
       load16<T>(x + off, xv[u]);
       load16<T>(da1 + off, d1[u]);
-      load_da2<T, S2>(da2, g, n, vv, j, off, d2[u]);
+      if constexpr (S2)
+        load_da2_crd<T>(da2, g, n, u ? crd_add(cr, s1, g) : cr, vox + (long long)u * vstep < g.v, j, d2[u]);
+      else
+        load_da2<T, S2>(da2, g, n, vv, j, off, d2[u]);
       if (accum) load16<T>(dx + off, o[u]);
     }
+    if constexpr (S2) cr = crd_add(cr, s2, g);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
