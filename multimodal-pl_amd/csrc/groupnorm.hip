@@ -478,10 +478,16 @@ __global__ __launch_bounds__(GPF) void gn_bwd_parts_finalize(const float* __rest
 
 // dx (+)= alpha*m*dA + bx*x + d per element; grid (blocks, n): a thread's 16-B channel chunk is fixed (the
 // grid stride is a multiple of the chunks per voxel), so its 5 x VEC coefficients load once into registers.
-template <typename T>
+// Round 6: ACC a template parameter and GA_U voxels per round with every load issued before the math: with the
+// runtime `accum` branch around the dx load the compiler waited for all loads right after it, one voxel (2-3 loads)
+// in flight per thread per round trip (5 launches of 60 us per step at 96^3). Same arithmetic per element.
+#ifndef U3D_GA_U
+#define U3D_GA_U 1  // (2, 4: measured slower, gpurun_out/r06hh)
+#endif
+template <typename T, bool ACC>
 __global__ __launch_bounds__(GT) void gn_bwd_apply(const T* __restrict__ da, const T* __restrict__ x, RedGeom g,
-                                                  const float* __restrict__ coef, T* __restrict__ dx, int accum) {
-  constexpr int VEC = 16 / sizeof(T);
+                                                  const float* __restrict__ coef, T* __restrict__ dx) {
+  constexpr int VEC = 16 / sizeof(T), U = U3D_GA_U;
   const int n = blockIdx.y;
   const int first = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;  // chn | blockDim
   const int j = first % g.chn;
@@ -494,21 +500,36 @@ __global__ __launch_bounds__(GT) void gn_bwd_apply(const T* __restrict__ da, con
   const T* xn = x + (long long)n * g.v * g.c + j * VEC;
   const T* dan = da + (long long)n * g.v * g.c + j * VEC;
   T* dxn = dx + (long long)n * g.v * g.c + j * VEC;
-  const int vstep = stride / g.chn;
-  for (long long vox = first / g.chn; vox < g.v; vox += vstep) {  // (rounds of 4 voxels measured slower here)
-    const long long off = vox * g.c;
-    float xv[VEC], dv[VEC], o[VEC];
-    load16<T>(xn + off, xv);
-    load16<T>(dan + off, dv);
-    if (accum) load16<T>(dxn + off, o);
+  const long long vstep = stride / g.chn;
+  for (long long vox = first / g.chn; vox < g.v; vox += U * vstep) {
+    float xv[U][VEC], dv[U][VEC], o[U][VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      const float gd = fmaf(xv[e], cf[0][e], cf[1][e]) > 0.f ? dv[e] : 0.f;
-      const float r = fmaf(cf[2][e], gd, fmaf(cf[3][e], xv[e], cf[4][e]));
-      o[e] = accum ? o[e] + r : r;
+    for (int u = 0; u < U; ++u) {  // clamped straight-line loads
+      const long long off = std::min(vox + u * vstep, g.v - 1) * g.c;
+      load16<T>(xn + off, xv[u]);
+      load16<T>(dan + off, dv[u]);
+      if constexpr (ACC) load16<T>(dxn + off, o[u]);
     }
-    store16<T>(dxn + off, o);
+    __builtin_amdgcn_sched_barrier(0);  // all of the round's loads ahead of its math and stores
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float gd = fmaf(xv[u][e], cf[0][e], cf[1][e]) > 0.f ? dv[u][e] : 0.f;
+        const float r = fmaf(cf[2][e], gd, fmaf(cf[3][e], xv[u][e], cf[4][e]));
+        o[u][e] = ACC ? o[u][e] + r : r;
+      }
+      if (vox + u * vstep < g.v) store16<T>(dxn + (vox + u * vstep) * g.c, o[u]);
+    }
   }
+}
+template <typename T>
+static void launch_gn_bwd_apply(dim3 grid, int thr, hipStream_t s, const T* da, const T* x, const RedGeom& g,
+                                const float* coef, T* dx, int accum) {
+  if (accum)
+    hipLaunchKernelGGL((gn_bwd_apply<T, true>), grid, dim3(thr), 0, s, da, x, g, coef, dx);
+  else
+    hipLaunchKernelGGL((gn_bwd_apply<T, false>), grid, dim3(thr), 0, s, da, x, g, coef, dx);
 }
 
 
@@ -635,10 +656,10 @@ __global__ __launch_bounds__(GT) void gn_bwd2_partial(const T* __restrict__ da1,
   }
 }
 
-template <typename T, bool S2>
+template <typename T, bool S2, bool ACC>
 __global__ __launch_bounds__(GT) void gn_bwd2_apply(const T* __restrict__ da1, const T* __restrict__ da2,
                                                    const T* __restrict__ x, RedGeom g, const float* __restrict__ coef,
-                                                   T* __restrict__ dx, int accum) {
+                                                   T* __restrict__ dx) {
   constexpr int VEC = 16 / sizeof(T);
   const int n = blockIdx.y;
   const int first = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;  // chn | blockDim
@@ -677,7 +698,7 @@ __global__ __launch_bounds__(GT) void gn_bwd2_apply(const T* __restrict__ da1, c
         load_da2_crd<T>(da2, g, n, u ? crd_add(cr, s1, g) : cr, vox + (long long)u * vstep < g.v, j, d2[u]);
       else
         load_da2<T, S2>(da2, g, n, vv, j, off, d2[u]);
-      if (accum) load16<T>(dx + off, o[u]);
+      if constexpr (ACC) load16<T>(dx + off, o[u]);  // (a template flag: no branch, no wait behind it)
     }
     if constexpr (S2) cr = crd_add(cr, s2, g);
 #pragma unroll
@@ -687,7 +708,7 @@ __global__ __launch_bounds__(GT) void gn_bwd2_apply(const T* __restrict__ da1, c
         const float g1 = fmaf(xv[u][e], sc1[e], sh1[e]) > 0.f ? d1[u][e] : 0.f;
         const float g2 = fmaf(xv[u][e], sc2[e], sh2[e]) > 0.f ? d2[u][e] : 0.f;
         const float r = fmaf(al1[e], g1, fmaf(al2[e], g2, fmaf(bx[e], xv[u][e], dd[e])));
-        o[u][e] = accum ? o[u][e] + r : r;
+        o[u][e] = ACC ? o[u][e] + r : r;
       }
       if (vox + (long long)u * vstep < g.v) store16<T>(dx + nb + (vox + (long long)u * vstep) * g.c, o[u]);
     }
@@ -777,13 +798,12 @@ extern "C" int u3d_gn_bwd(int dtype, const void* da, const void* x, int n, int c
   if (dtype == U3D_BF16) {
     hipLaunchKernelGGL(gn_bwd_partial<bf16>, dim3(g.nblk, n), dim3(GT), 0, s, (const bf16*)da, (const bf16*)x, g, stats,
                        gamma, beta, gn_part_ptr(ws), cnt, coef, dgamma, dbeta, accumulate_params);
-    hipLaunchKernelGGL(gn_bwd_apply<bf16>, dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da, (const bf16*)x, g, coef,
-                       (bf16*)dx, accumulate);
+    launch_gn_bwd_apply<bf16>(dim3(ablk, n), athr, s, (const bf16*)da, (const bf16*)x, g, coef, (bf16*)dx, accumulate);
   } else {
     hipLaunchKernelGGL(gn_bwd_partial<float>, dim3(g.nblk, n), dim3(GT), 0, s, (const float*)da, (const float*)x, g,
                        stats, gamma, beta, gn_part_ptr(ws), cnt, coef, dgamma, dbeta, accumulate_params);
-    hipLaunchKernelGGL(gn_bwd_apply<float>, dim3(ablk, n), dim3(athr), 0, s, (const float*)da, (const float*)x, g, coef,
-                       (float*)dx, accumulate);
+    launch_gn_bwd_apply<float>(dim3(ablk, n), athr, s, (const float*)da, (const float*)x, g, coef, (float*)dx,
+                               accumulate);
   }
   return check_launch("gn_bwd");
 }
@@ -803,8 +823,7 @@ extern "C" int u3d_gn_bwd_parts(const void* da, const void* x, int n, int c, lon
   const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + athr - 1) / athr);
   hipLaunchKernelGGL(gn_bwd_parts_finalize, dim3(1), dim3(GPF), 0, s, parts, nparts, g, stats, gamma, beta, coef, dgamma,
                      dbeta, accumulate_params);
-  hipLaunchKernelGGL(gn_bwd_apply<bf16>, dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da, (const bf16*)x, g, coef,
-                     (bf16*)dx, accumulate);
+  launch_gn_bwd_apply<bf16>(dim3(ablk, n), athr, s, (const bf16*)da, (const bf16*)x, g, coef, (bf16*)dx, accumulate);
   return check_launch("gn_bwd_parts");
 }
 
@@ -818,8 +837,8 @@ extern "C" int u3d_gn_bwd_apply_coef(const void* da, const void* x, int n, int c
   const long long nvec = v * g.chn;
   const int athr = GT / g.chn * g.chn;
   const int ablk = (int)std::min<long long>(std::max(1, 4096 / n), (nvec + athr - 1) / athr);
-  hipLaunchKernelGGL(gn_bwd_apply<bf16>, dim3(ablk, n), dim3(athr), 0, (hipStream_t)stream, (const bf16*)da,
-                     (const bf16*)x, g, coef, (bf16*)dx, accumulate);
+  launch_gn_bwd_apply<bf16>(dim3(ablk, n), athr, (hipStream_t)stream, (const bf16*)da, (const bf16*)x, g, coef,
+                            (bf16*)dx, accumulate);
   return check_launch("gn_bwd_apply_coef");
 }
 
@@ -882,14 +901,22 @@ static int gn_bwd2_launch(int dtype, const void* da1, const void* da2, const voi
     hipLaunchKernelGGL((gn_bwd2_partial<bf16, S2>), dim3(g.nblk, n), dim3(GT), 0, s, (const bf16*)da1,
                        (const bf16*)da2, (const bf16*)x, g, stats, gamma1, beta1, gamma2, beta2, gn_part_ptr(ws), cnt,
                        coef, dgamma1, dbeta1, dgamma2, dbeta2, accumulate_params);
-    hipLaunchKernelGGL((gn_bwd2_apply<bf16, S2>), dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da1,
-                       (const bf16*)da2, (const bf16*)x, g, coef, (bf16*)dx, accumulate);
+    if (accumulate)
+      hipLaunchKernelGGL((gn_bwd2_apply<bf16, S2, true>), dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da1,
+                         (const bf16*)da2, (const bf16*)x, g, coef, (bf16*)dx);
+    else
+      hipLaunchKernelGGL((gn_bwd2_apply<bf16, S2, false>), dim3(ablk, n), dim3(athr), 0, s, (const bf16*)da1,
+                         (const bf16*)da2, (const bf16*)x, g, coef, (bf16*)dx);
   } else {
     hipLaunchKernelGGL((gn_bwd2_partial<float, S2>), dim3(g.nblk, n), dim3(GT), 0, s, (const float*)da1,
                        (const float*)da2, (const float*)x, g, stats, gamma1, beta1, gamma2, beta2, gn_part_ptr(ws),
                        cnt, coef, dgamma1, dbeta1, dgamma2, dbeta2, accumulate_params);
-    hipLaunchKernelGGL((gn_bwd2_apply<float, S2>), dim3(ablk, n), dim3(athr), 0, s, (const float*)da1,
-                       (const float*)da2, (const float*)x, g, coef, (float*)dx, accumulate);
+    if (accumulate)
+      hipLaunchKernelGGL((gn_bwd2_apply<float, S2, true>), dim3(ablk, n), dim3(athr), 0, s, (const float*)da1,
+                         (const float*)da2, (const float*)x, g, coef, (float*)dx);
+    else
+      hipLaunchKernelGGL((gn_bwd2_apply<float, S2, false>), dim3(ablk, n), dim3(athr), 0, s, (const float*)da1,
+                         (const float*)da2, (const float*)x, g, coef, (float*)dx);
   }
   return check_launch("gn_bwd2");
 }
