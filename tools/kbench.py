@@ -294,7 +294,7 @@ def _stem_plain(n=2, s=96):
 
 
 def _stem_stats(n=2, s=96):
-    """the bench's conv1: 1 -> 32 with the output GroupNorm(16) statistics from the epilogue (stem1_fwd_kernel<bf16, 1>)"""
+    """the bench's conv1: 1 -> 32 with the output GroupNorm(16) statistics from the epilogue (stem1_mfma_kernel<true>)"""
     x = torch.rand((n, 1, s, s, s), device=dev)
     w = torch.randn(32, 1, 3, 3, 3, device=dev)
     pf, _, _ = ops.wstd_fwd(w, bf, True, need_dgrad=False)

@@ -6,7 +6,7 @@ A step starts at the launch of the stem kernel (the first libu3d kernel of every
 per-step wall times."""
 import re
 
-MARKER = r"u3d::stem1_fwd_kernel"
+MARKER = r"u3d::stem1_(fwd|mfma)_kernel"
 
 
 def _t(r, key):
