@@ -600,6 +600,23 @@ def test_no_kernel_spills_to_scratch():
         zip(KR.demangle(list(bad)), bad.values()))
 
 
+def test_trace_step_marker_names_a_shipped_conv1_kernel():
+    """tools/trace_steps.py splits a kernel trace into steps at the conv1 kernel (profile fidelity):
+    its marker must match a kernel the library ships (round 6 moved conv1 to stem1_mfma_kernel; a stale marker made
+    the steady-state summaries silently empty)."""
+    import re
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import kernel_resources as KR
+    import trace_steps
+    lib = os.path.join(REPO, "multimodal-pl_amd", "u3d", "libu3d.so")
+    if not os.path.exists(lib) or not os.path.exists(os.path.join(KR.LLVM, "llvm-readelf")):
+        pytest.skip("library or llvm tools not present")
+    names = KR.demangle(list(KR.kernels(lib)))
+    hits = [nm for nm in names if re.search(trace_steps.MARKER, nm)]
+    assert any("stem1_mfma_kernel" in nm for nm in hits), hits
+
+
 def test_stride2_dgrad_beyond_2gib_routes_to_the_64bit_kernel(monkeypatch):
     """the stride-2 data-gradient kernel addresses dy with 32-bit buffer offsets, so a dy of 2 GiB or more
     must route to the 64-bit implicit-GEMM data gradient instead of failing with EINVAL (routing only: meta tensors,
