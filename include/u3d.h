@@ -204,14 +204,15 @@ int u3d_head_loss_bwd(const float* logits, const float* labels, long long rows, 
  * GroupNorm + ReLU prologue (round 6; x0 bf16 [n][v][cin] = the prologue's input, gn_* its GroupNorm): parts
  * [n][bps][cin][2] = (sum g, sum g * xhat), g = dA where gn(x0) > 0, per block of one sample, for u3d_gn_bwd_parts
  * (nparts = bps = u3d_head_loss_bwd_gn_bps(n, v, cin); 0 = the form does not apply: needs cin = 32, v % 32 == 0).
- * dbias_partials holds n * bps rows. Replaces the pair precls_conv backward -> the GroupNorm backward of its input
+ * dbias_partials holds n * bps rows; with dbias (nullable; cnt = one zeroed unsigned, left zeroed) the launch's last
+ * workgroup sums them into dbias[C] (fixed order). Replaces the pair precls_conv backward -> the GroupNorm backward of its input
  * (unet3D.py:1653-1657 behind the decoder's last GN + ReLU, :1644-1650) as one pass over dA instead of two. */
 int u3d_head_loss_bwd_gn_bps(int n, long long v, int cin);
 int u3d_head_loss_bwd_gn(const float* logits, const float* labels, int n, long long v, int C, const float* weights,
                          const double* sums, const float* grad_out, const void* wpk_dgrad, int cin, void* dA,
                          void* dy_bf16, float* dbias_partials, const void* x0, const float* gn_stats,
-                         const float* gn_gamma, const float* gn_beta, int gn_groups, float* parts,
-                         u3d_stream_t stream);
+                         const float* gn_gamma, const float* gn_beta, int gn_groups, float* parts, float* dbias,
+                         unsigned* cnt, u3d_stream_t stream);
 
 /* bf16 32->32 3^3 stride-1 conv (cin = cout = 32; the full-resolution layers) in halo-brick form with the
  * weights held in registers: flip=0 forward (wpk = forward pack, optional GN+ReLU prologue and residual),

@@ -304,7 +304,9 @@ __global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __rest
                                                             const float* __restrict__ gga = nullptr,
                                                             const float* __restrict__ gbe = nullptr, int ggroups = 0,
                                                             long long v = 0, int bps = 1,
-                                                            float* __restrict__ gparts = nullptr) {
+                                                            float* __restrict__ gparts = nullptr,
+                                                            float* __restrict__ dbias = nullptr,
+                                                            unsigned* __restrict__ cnt = nullptr) {
   constexpr int cout = 16, cout_p = 32;
   __shared__ float red[HD_T / 64][32];
   __shared__ f32x4 gtb[GN ? 64 : 1];  // per channel (scale, shift, rstd, mean) of the block's sample
@@ -500,7 +502,32 @@ __global__ __launch_bounds__(HD_T) void head_loss_bwd_kernel(const float* __rest
   if (threadIdx.x < 32) {
     float t = 0.f;
     for (int w = 0; w < HD_T / 64; ++w) t += red[w][threadIdx.x];
-    if (threadIdx.x < cout) dbp[(long long)blockIdx.x * cout + threadIdx.x] = t;
+    if (threadIdx.x < cout) {
+      if (GN && dbias)  // agent-scope (sc1) store: read by the last-arriving block below
+        __hip_atomic_store(dbp + (long long)blockIdx.x * cout + threadIdx.x, t, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        dbp[(long long)blockIdx.x * cout + threadIdx.x] = t;
+    }
+  }
+  if constexpr (GN) {
+    // round 6: the bias gradient summed by the launch's last-arriving block (fixed row order, fp64) instead of two
+    // channel-sum launches after it; the counter is left zeroed
+    if (dbias == nullptr) return;
+    __shared__ unsigned s_last;
+    __shared__ double cs[16];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == gridDim.x - 1;
+      if (s_last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    lastarriver_rowsum<HD_T>(dbp, 1, (int)gridDim.x, cout, cs);
+    __syncthreads();
+    if (threadIdx.x < cout) dbias[threadIdx.x] = (float)cs[threadIdx.x];
   }
 }
 
@@ -589,19 +616,20 @@ extern "C" int u3d_head_loss_bwd_gn_bps(int n, long long v, int cin) {
 // u3d_head_loss_bwd plus the GroupNorm-backward partials of the head's GN + ReLU prologue (x0 = its input, gn_* = its
 // GroupNorm) into parts[n][bps][cin][2] = (sum g, sum g * xhat) per block of one sample, bps =
 // u3d_head_loss_bwd_gn_bps(n, v, cin); u3d_gn_bwd_parts then finalizes and applies them. dbias_partials holds n * bps
-// rows. dA, dy and the bias partials' total are those of u3d_head_loss_bwd up to the bias partials' summation order.
+// rows; with dbias (+ cnt: one zeroed unsigned, left zeroed) the launch's last block also sums them into dbias[C].
+// dA, dy and the bias gradient are those of u3d_head_loss_bwd up to the bias partials' summation order.
 extern "C" int u3d_head_loss_bwd_gn(const float* logits, const float* labels, int n, long long v, int C,
                                     const float* weights, const double* sums, const float* grad_out,
                                     const void* wpk_dgrad, int cin, void* dA, void* dy_bf16, float* dbias_partials,
                                     const void* x0, const float* gn_stats, const float* gn_gamma, const float* gn_beta,
-                                    int gn_groups, float* parts, u3d_stream_t stream) {
+                                    int gn_groups, float* parts, float* dbias, unsigned* cnt, u3d_stream_t stream) {
   const int bps = u3d_head_loss_bwd_gn_bps(n, v, cin);
   U3D_REQUIRE(bps > 0 && C == 16, "head_loss_bwd_gn: needs C = 16, cin = 32, v %% 32 == 0");
   U3D_REQUIRE(logits && labels && weights && sums && grad_out && wpk_dgrad && dA && dy_bf16 && dbias_partials && x0 &&
-                  gn_stats && gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0 && parts,
+                  gn_stats && gn_gamma && gn_beta && gn_groups > 0 && cin % gn_groups == 0 && parts && (!dbias || cnt),
               "head_loss_bwd_gn: bad args");
   hipLaunchKernelGGL(head_loss_bwd_kernel<true>, dim3(n * bps), dim3(HD_T), 0, (hipStream_t)stream, logits, labels,
                      (long long)n * v, weights, sums, grad_out, (const bf16*)wpk_dgrad, cin, (bf16*)dA, (bf16*)dy_bf16,
-                     dbias_partials, (const bf16*)x0, gn_stats, gn_gamma, gn_beta, gn_groups, v, bps, parts);
+                     dbias_partials, (const bf16*)x0, gn_stats, gn_gamma, gn_beta, gn_groups, v, bps, parts, dbias, cnt);
   return check_launch("head_loss_bwd_kernel<GN>");
 }

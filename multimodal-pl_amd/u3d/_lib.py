@@ -33,7 +33,7 @@ _SIGS = {
     "u3d_head_loss_bwd_gn_bps": [I, L, I],
     "u3d_head_bwd": [P, L, I, P, I, P, P, P, P],
     "u3d_head_loss_bwd": [P, P, L, I, P, P, P, P, I, P, P, P, P],
-    "u3d_head_loss_bwd_gn": [P, P, I, L, I, P, P, P, P, I, P, P, P, P, P, P, P, I, P, P],
+    "u3d_head_loss_bwd_gn": [P, P, I, L, I, P, P, P, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
     "u3d_partial_target": [P, I, L, P, I, I, I, I, P, P],
     "u3d_window_accumulate": [P, I, I, I, I, I, P, P, P, F, F, P, P, I, I, I, I, I, I, I, I, P],
     "u3d_window_normalize": [P, P, I, I, L, P],

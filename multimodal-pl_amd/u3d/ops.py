@@ -794,6 +794,8 @@ HEAD_LOSS_FUSED = os.environ.get("U3D_HEAD_LOSS_FUSED", "1") != "0"
 
 
 HEAD_GN_PARTS = os.environ.get("U3D_HEAD_GN_PARTS", "1") == "1"
+HEAD_CNT_SLOT = 24  # the GN head backward's arrival counter (zeroed, left zeroed)
+HEAD_DBIAS_FUSED = os.environ.get("U3D_HEAD_DBIAS_FUSED", "1") == "1"  # 0: two channel-sum launches (A/B)
 
 
 def head_gn_parts_ok(lg, x0, cin, gn):
@@ -827,10 +829,14 @@ def head_loss_bwd(lg, lab, weights, sums, grad_out, wpk_dgrad, cin, dbias=None, 
         dbp = torch.empty((n * bps, C), dtype=torch.float32, device=lg.device)
         parts = torch.empty((n, bps, cin, 2), dtype=torch.float32, device=lg.device)
         st, ga, be, G = gn
+        # the bias gradient summed by the launch's last workgroup (zeroed counter in its own workspace slot)
+        fused = dbias is not None and HEAD_DBIAS_FUSED
         call("u3d_head_loss_bwd_gn", lg.data_ptr(), lab.data_ptr(), n, v, C, weights.data_ptr(), sums.data_ptr(),
              grad_out.data_ptr(), wpk_dgrad.data_ptr(), cin, dA.data_ptr(), dyb.data_ptr(), dbp.data_ptr(),
-             x0.data_ptr(), st.data_ptr(), ga.data_ptr(), be.data_ptr(), G, parts.data_ptr(), _stream())
-        if dbias is not None:
+             x0.data_ptr(), st.data_ptr(), ga.data_ptr(), be.data_ptr(), G, parts.data_ptr(),
+             _ptr(dbias) if fused else None, _ptr(WS.get(256, lg.device, slot=HEAD_CNT_SLOT)) if fused else None,
+             _stream())
+        if dbias is not None and not fused:
             channel_sum(dbp, out=dbias)
         return dA, dyb, parts
     nb = query("u3d_head_bwd_blocks", rows)

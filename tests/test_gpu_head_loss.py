@@ -169,9 +169,24 @@ def test_head_loss_bwd_gn_parts(gpu, dims, G):
     d = (dx1.float() - dx0.float()).abs()
     ulp = torch.maximum(dx0.float().abs(), dx1.float().abs()) * 2.0 ** -7 + 1e-6
     assert bool((d <= ulp).all()), d.max().item()
-    # deterministic
-    _, _, parts2 = ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, x0=x0, gn=gn)
-    assert torch.equal(parts, parts2)
+    # deterministic; the bias gradient's arrival counter is left zeroed (a second launch sums the same rows)
+    db2 = torch.full((16,), float("nan"), device=gpu)
+    _, _, parts2 = ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, dbias=db2, x0=x0, gn=gn)
+    assert torch.equal(parts, parts2) and torch.equal(db1, db2)
+
+
+def test_head_loss_bwd_gn_dbias_last_arriver(gpu, monkeypatch):
+    """The GN head backward's bias gradient summed in-kernel by the last-arriving workgroup (round 6) against the two
+    channel-sum launches it replaces: fp64 sums of the same partial rows, so equal to fp32 rounding."""
+    from u3d import ops
+    lg, lab, wt, sums, go, pd, x0, gn = _gn_case(gpu, (2, 64, 64, 64), G=8)
+    db0, db1 = torch.empty(16, device=gpu), torch.empty(16, device=gpu)
+    monkeypatch.setattr(ops, "HEAD_DBIAS_FUSED", False)
+    ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, dbias=db0, x0=x0, gn=gn)
+    monkeypatch.setattr(ops, "HEAD_DBIAS_FUSED", True)
+    for _ in range(3):
+        ops.head_loss_bwd(lg, lab, wt, sums, go, pd, 32, dbias=db1, x0=x0, gn=gn)
+        torch.testing.assert_close(db1, db0, rtol=1e-6, atol=1e-6 * db0.abs().max().item())
 
 
 def test_head_loss_bwd_gn_applicability(gpu):
