@@ -379,11 +379,14 @@ __global__ __launch_bounds__(ST) void stem_wgrad_kernel(const T* __restrict__ dy
 
 // MFMA weight gradient of the 1-channel stride-1 stem (conv1 1->32 of unet3D_baseline / unet3D at 96^3):
 //   dW[co][t] = sum_v dy[v][co] * x[v + off(t)]   (M = co, N = 27 taps padded to 32, K = voxels)
-// A workgroup walks 2 x 8 x 32-voxel bricks of its split; per brick the dy brick (32 KB, read transposed
+// A workgroup walks SM_BD x 8 x 32-voxel bricks of its split; per brick the dy brick (SM_BD x 16 KB, read transposed
 // with ds_read_b64_tr_b16) and the fp32 input halo (4 x 10 x 34) sit in LDS. A k-step = 16 consecutive w
 // voxels of one row, so the B fragment of tap t is 8 consecutive halo values of the shifted row. The 8
 // per-wave tiles are summed in fixed order at the end; the slab rows ci > 0 are written as zeros.
-constexpr int SM_BD = 2, SM_BH = 8, SM_BW = 32, SM_NV = SM_BD * SM_BH * SM_BW;
+#ifndef U3D_SM_BD
+#define U3D_SM_BD 4  // round 6: 4-plane bricks (64 KB of dy per brick in flight; 2 planes: 46.6 us at 2 x 96^3)
+#endif
+constexpr int SM_BD = U3D_SM_BD, SM_BH = 8, SM_BW = 32, SM_NV = SM_BD * SM_BH * SM_BW;
 constexpr int SM_HD = SM_BD + 2, SM_HH = SM_BH + 2, SM_HW = SM_BW + 2, SM_NH = SM_HD * SM_HH * SM_HW;
 
 typedef short sm_v4i16 __attribute__((ext_vector_type(4)));
@@ -469,8 +472,11 @@ __global__ __launch_bounds__(512, 1) void stem_wgrad_mfma_kernel(const bf16* __r
   for (int b = b0; b < b1; ++b) {
     const bool more = b + 1 < b1;
     prefetch(more ? b + 1 : b);
+#ifndef U3D_ABL_STEMW
+#define U3D_ABL_STEMW 0  // timing-only ablations: 1 = one MFMA step per brick, 2 = only the ci = 0 slab column stored
+#endif
 #pragma unroll
-    for (int j = 0; j < SM_NV / 16 / 8; ++j) {
+    for (int j = 0; j < ((U3D_ABL_STEMW & 1) ? 1 : SM_NV / 16 / 8); ++j) {
       const int ks = wave + 8 * j;                 // 16 voxels: row (vd, vh), w = 16 * (ks & 1) ...
       const int k0 = (ks * 16 + 8 * hq + q) * ROWB + colb;
       const sm_bf16x8 a = __builtin_bit_cast(sm_bf16x8, __builtin_shufflevector(sm_tr_read(dyt, k0),
@@ -478,12 +484,19 @@ __global__ __launch_bounds__(512, 1) void stem_wgrad_mfma_kernel(const bf16* __r
                                                                                  0, 1, 2, 3, 4, 5, 6, 7));
       const int v0 = ks * 16 + 8 * hq;             // first of this lane's 8 voxels
       const int vw = v0 % SM_BW, vh = (v0 / SM_BW) % SM_BH, vd = v0 / (SM_BW * SM_BH);
-      const float* src = hal + (vd * SM_HH + vh) * SM_HW + vw + toff;
-      typedef short v8i16 __attribute__((ext_vector_type(8)));
-      v8i16 bv;
+      const float* src = hal + (vd * SM_HH + vh) * SM_HW + vw + toff;  // in range for every lane (ttap clamped)
+      // round 6: the 8 halo reads issued unconditionally and converted in pairs (v_cvt_pk_bf16_f32, the rounding of
+      // from_f<bf16>); the padded taps 27-31 zeroed by a select. A per-element branch had made each read wait alone.
+      typedef float f32x8 __attribute__((ext_vector_type(8)));
+      typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+      f32x8 fv;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) bv[e] = tap < 27 ? (short)from_f<bf16>(src[e]) : (short)0;
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, __builtin_bit_cast(sm_bf16x8, bv), acc, 0, 0, 0);
+      for (int e = 0; e < 8; ++e) fv[e] = src[e];
+      u32x4v bw = __builtin_bit_cast(u32x4v, __builtin_convertvector(fv, sm_bf16x8));
+      const unsigned keep = tap < 27 ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bw[e] &= keep;
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, __builtin_bit_cast(sm_bf16x8, bw), acc, 0, 0, 0);
     }
     __syncthreads();
     if (more) commit();
@@ -503,7 +516,7 @@ __global__ __launch_bounds__(512, 1) void stem_wgrad_mfma_kernel(const bf16* __r
 #pragma unroll
       for (int wv = 0; wv < 8; ++wv) s += red[(wv * 32 + co) * 32 + t];
     }
-    pp[e] = s;
+    if (!(U3D_ABL_STEMW & 2) || ci == 0) pp[e] = s;
   }
 }
 }  // namespace u3d

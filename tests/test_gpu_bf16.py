@@ -226,11 +226,12 @@ def test_bf16_conv_wgrad_1x1(gpu, n, cin, cout, dims, s):
     assert err < 2e-3 * ref.abs().max().item(), err
 
 
-@pytest.mark.parametrize("dims", [(6, 10, 64), (3, 9, 32), (5, 7, 20), (33, 48, 64), (48, 64, 96)])
+@pytest.mark.parametrize("dims", [(6, 10, 64), (3, 9, 32), (5, 7, 20), (33, 48, 64), (48, 64, 96), (35, 64, 96),
+                                  (96, 96, 96)])
 def test_bf16_stem_wgrad(gpu, dims):
-    """conv1 (1 -> 32, 3^3, stride 1) weight gradient: MFMA kernel (w % 32 == 0) and the VALU kernel. The two large
-    volumes give the MFMA kernel's workgroups 2 and 5 bricks each (its two-deep register prefetch, odd brick counts,
-    a partial last d brick)."""
+    """conv1 (1 -> 32, 3^3, stride 1) weight gradient: MFMA kernel (w % 32 == 0) and the VALU kernel. The large
+    volumes give the MFMA kernel's workgroups 1-7 bricks of 4 x 8 x 32 voxels each (its register prefetch of the next
+    brick, partial last d bricks at d = 33 and 35); 96^3 is the bench's conv1."""
     from u3d import ops
     torch.manual_seed(7)
     n = 2
