@@ -47,6 +47,7 @@ enum Opt : int {
   OPT_HEAD_NB,        // classifier head / head backward blocks (at most)
   OPT_HEAD_GN_NB,     // head backward with the prologue GN's partials: blocks over all samples (at most)
   OPT_STEM_MFMA,      // bf16 conv1 (1 -> 32) on the matrix cores, bf16 operands (0: the fp32 packed-FMA kernel)
+  OPT_WB_S2BD,        // stride-2 brick weight-gradient brick depth in output planes (2 or 3)
   OPT_COUNT
 };
 int opt(Opt o);

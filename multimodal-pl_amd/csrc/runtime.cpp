@@ -44,7 +44,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"SMALL_WGS", 256},    {"GN_MAXBLK", 256},  {"HEAD_TR", 1},        {"STEM1", 1},      {"UP_BWD_BLK", -1},
     {"WGRAD_BD", 3},       {"WB_WGS", 256},     {"WR_TILE16", 0},      {"WR_WGS", 256},     {"WB_S2CO64", 1},
     {"IGEMM_BM", 128}, {"WSTD_ROW", 1}, {"UP_QUAD", 1}, {"LOSS_PAIR", 1},
-    {"HEAD_NB", 768},  {"HEAD_GN_NB", 512}, {"STEM_MFMA", 1},
+    {"HEAD_NB", 768},  {"HEAD_GN_NB", 512}, {"STEM_MFMA", 1}, {"WB_S2BD", 3},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;

@@ -86,13 +86,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
   // (2-way bank conflicts)
   constexpr int HWE = S == 2 ? (HW + 1) / 2 : 0;
   auto wpos = [&](int hw) { return S == 2 ? ((hw & 1) ? HWE + (hw >> 1) : (hw >> 1)) : hw; };
-  int tap_off[MAXT];
-#pragma unroll
-  for (int j = 0; j < MAXT; ++j) {
+  // tap j's halo row offset, formed where it is used (an array of 4 held across the loop cost 4 VGPRs)
+  auto tap_off_of = [&](int j) {
     const int t = min(wave + 8 * j, 26);
     const int td = t / 9, th = (t / 3) % 3, tw = t % 3;
-    tap_off[j] = ((td * HH + th) * HW + (S == 2 ? (tw == 1 ? HWE : tw >> 1) : tw)) * ROWB;
-  }
+    return ((td * HH + th) * HW + (S == 2 ? (tw == 1 ? HWE : tw >> 1) : tw)) * ROWB;
+  };
   const int ntap = (27 - wave + 7) / 8;  // 4 for waves 0-2, 3 for 3-7
 
   // fragment lane geometry: group gq = lane>>4, in-group lane i = lane&15 -> (q = i>>2, p = i&3)
@@ -100,7 +99,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
   const int colb = (16 * (gq & 1) + 4 * p) * 2;  // byte offset of this lane's 4 columns
 
   u32x4 pdy[DYL], phl[HLL];
-  f32x2 sc[4], sh[4];
+  // the GroupNorm coefficients of the current sample in LDS (per 8-channel chunk), read only inside commit: held in
+  // registers across the MFMA loop they pushed the 3-plane stride-2 form past 256 VGPRs
+  __shared__ f32x2 gsc[4][4], gsh[4][4];
   int gn_n = -1;
 
   auto decode = [&](long long b, int& n, int& od0, int& oh0, int& ow0) {
@@ -156,9 +157,26 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
   auto commit = [&](long long b) {
     int n, od0, oh0, ow0;
     decode(b, n, od0, oh0, ow0);
-    if (has_gn && n != gn_n) {
+    if (has_gn && n != gn_n) {  // n is uniform over the workgroup: the barrier is reached by all or none
       gn_n = n;
-      gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, n, ci0 + ch * 8, sc, sh);
+      if (tid < 4) {
+        f32x2 sc[4], sh[4];
+        gn_coef8(gstat, gamma, beta, g.gn_groups, g.cin, n, ci0 + tid * 8, sc, sh);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          gsc[tid][k] = sc[k];
+          gsh[tid][k] = sh[k];
+        }
+      }
+      __syncthreads();
+    }
+    f32x2 sc[4], sh[4];
+    if (has_gn) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sc[k] = gsc[ch][k];
+        sh[k] = gsh[ch][k];
+      }
     }
 #pragma unroll
     for (int i = 0; i < DYL; ++i) {
@@ -212,7 +230,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
         for (int c = 0; c < NCO; ++c) a[c] = frag_from(tr_read(dyt, ar[0] + 64 * c), tr_read(dyt, ar[1] + 64 * c));
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          bb[j] = frag_from(tr_read(hal, hr[0] + tap_off[j]), tr_read(hal, hr[1] + tap_off[j]));
+          bb[j] = frag_from(tr_read(hal, hr[0] + tap_off_of(j)), tr_read(hal, hr[1] + tap_off_of(j)));
       };
       auto mfmas = [&](const bf16x8 (&a)[NCO], const bf16x8 (&bb)[NT]) {
 #pragma unroll
@@ -234,9 +252,19 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
       } else {  // twice the accumulators: no fragment lookahead (the other wave of the SIMD covers the LDS reads)
 #pragma unroll 1
         for (int ks = 0; ks < NKS; ++ks) {
-          bf16x8 a0[NCO], b0[NT];
-          frags(ks, a0, b0);
-          mfmas(a0, b0);
+          int ar[2], hr[2];
+          rows(ks, ar, hr);
+          bf16x8 a0[NCO];
+#pragma unroll
+          for (int c = 0; c < NCO; ++c) a0[c] = frag_from(tr_read(dyt, ar[0] + 64 * c), tr_read(dyt, ar[1] + 64 * c));
+          // one tap's halo fragment at a time (4 VGPRs live instead of 16: the 3-plane stride-2 form fits 256)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            const bf16x8 bj = frag_from(tr_read(hal, hr[0] + tap_off_of(j)), tr_read(hal, hr[1] + tap_off_of(j)));
+#pragma unroll
+            for (int c = 0; c < NCO; ++c)
+              acc[j][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[c], bj, acc[j][c], 0, 0, 0);
+          }
         }
       }
     };
@@ -442,7 +470,7 @@ static int wb_nco(int stride, int cout) { return stride == 2 && opt(OPT_WB_S2CO6
 
 static void brick_dims(int stride, int* bd, int* bh, int* bw) {
   if (stride == 1) { *bd = wgrad_bd(); *bh = 8; *bw = 16; }
-  else { *bd = 2; *bh = 4; *bw = 8; }
+  else { *bd = opt(OPT_WB_S2BD) == 2 ? 2 : 3; *bh = 4; *bw = 8; }
 }
 
 extern "C" int u3d_conv_wgrad_brick_splits(int n, int cin, int d, int h, int w, int cout, int stride) {
@@ -498,7 +526,9 @@ extern "C" int u3d_conv_wgrad_brick(const void* dy, const void* x, int n, int ci
       hipLaunchKernelGGL((wgrad_brick_kernel<BD_, BH_, BW_, S_, NCO_, false>), grid, dim3(512), 0, s,              \
                          (const bf16*)dy, (const bf16*)x, gn_stats, gn_gamma, gn_beta, partials, g);               \
   } while (0)
-  if (stride == 2 && nco == 2) U3D_WB(2, 4, 8, 2, 2);
+  if (stride == 2 && bd == 3 && nco == 2) U3D_WB(3, 4, 8, 2, 2);
+  else if (stride == 2 && bd == 3) U3D_WB(3, 4, 8, 2, 1);
+  else if (stride == 2 && nco == 2) U3D_WB(2, 4, 8, 2, 2);
   else if (stride == 1 && bd == 2) U3D_WB(2, 8, 16, 1, 1);
   else if (stride == 1) U3D_WB(3, 8, 16, 1, 1);
   else U3D_WB(2, 4, 8, 2, 1);
