@@ -310,7 +310,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_brick_kernel(const bf16* __restr
 // 32 k16 steps of a chunk are spread over the 8 waves; the 8 per-wave partial tiles are summed in LDS in
 // fixed order at the end (deterministic). Memory-bound by design (16-32 flop/B): the next chunk is
 // prefetched into registers while the current one is consumed.
-constexpr int W1_NV = 512;
+#ifndef U3D_W1_NV
+#define U3D_W1_NV 512
+#endif
+constexpr int W1_NV = U3D_W1_NV;  // output voxels per chunk
 
 struct W1Geom {
   int cin, cout, cin_p, cout_p;
