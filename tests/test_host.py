@@ -186,24 +186,39 @@ def _ddp_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_ddp_bucketer_gloo_world2():
+def _run_ranks(target, world, timeout=120):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=60) for _ in procs]
+    out = sorted((q.get(timeout=timeout) for _ in procs), key=lambda o: o[0])
     for p in procs:
-        p.join(timeout=60)
+        p.join(timeout=timeout)
         assert p.exitcode == 0
-    out.sort()
+    return out
+
+
+def _check_bucketer(world):
+    out = _run_ranks(_ddp_worker, world)
     for rank, vals, w, _ in out:
         for n, v in vals.items():
             i = int(n[1:])
-            expect = 0.0 if n == "p2" else (1 + 2) / 2 * (1 + i)  # mean over ranks of (rank+1)*(1+i)
+            expect = 0.0 if n == "p2" else (world + 1) / 2 * (1 + i)  # mean over ranks of (rank+1)*(1+i)
             assert np.allclose(v, expect), (n, v[:3], expect)
-    assert np.allclose(out[0][2], out[1][2])  # init broadcast: identical weights on both ranks
+    for o in out[1:]:
+        assert np.allclose(out[0][2], o[2])  # init broadcast: identical weights on every rank
+
+
+def test_ddp_bucketer_gloo_world2():
+    _check_bucketer(2)
+
+
+def test_ddp_bucketer_gloo_world8():
+    """BASELINE configs[2]'s rank count (8 x 2 patches = global batch 16) rehearsed on the CPU: the same buckets, the
+    AVG over 8 ranks and the initial broadcast, through gloo (the RCCL path itself never ran beyond world 1 here)."""
+    _check_bucketer(8)
 
 
 def _used_flags_worker(rank, world, port, q):
@@ -223,7 +238,7 @@ def _used_flags_worker(rank, world, port, q):
             p.grad = None
         b.begin()
         for n, p in reversed(params):
-            if n == "p4" or (n == "p2" and rank == 1):
+            if n == "p4" or (n == "p2" and rank != 0):
                 continue
             b.out(n).fill_(float(rank + 1) * (1 + int(n[1:])))
             b.done(n)
@@ -234,24 +249,25 @@ def _used_flags_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_ddp_used_flags_gloo_world2():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_used_flags_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    out = sorted(q.get(timeout=60) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+def _check_used_flags(world):
+    out = _run_ranks(_used_flags_worker, world)
     for rank, steps, assigned in out:
         assert assigned == (["p0", "p1", "p2", "p3"] if rank == 0 else ["p0", "p1", "p3"])
         for grads in steps:
             assert grads["p4"] is None, (rank, "a parameter no rank produced must keep grad None")
-            assert np.allclose(grads["p2"], 0.5 * 1 * 3), (rank, grads["p2"][:3])  # rank 0's (0+1)*3 over 2 ranks
+            assert np.allclose(grads["p2"], 3.0 / world), (rank, grads["p2"][:3])  # rank 0's (0+1)*3 over the ranks
             for i in (0, 1, 3):
-                assert np.allclose(grads[f"p{i}"], 1.5 * (1 + i)), (rank, i)
+                assert np.allclose(grads[f"p{i}"], (world + 1) / 2 * (1 + i)), (rank, i)
+
+
+def test_ddp_used_flags_gloo_world2():
+    _check_used_flags(2)
+
+
+def test_ddp_used_flags_gloo_world8():
+    """p2 produced on rank 0 of 8 only, p4 on none: the used flags ride the last bucket's AVG at configs[2]'s rank
+    count."""
+    _check_used_flags(8)
 
 
 def _fallback_worker(rank, world, port, q):
